@@ -1,0 +1,301 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json metric: GiB/s CRC32 verify of device-resident 64 KiB files.
+
+Workload (BASELINE.json configs[1]): per GPU, a resident set of 1,024 TFS blocks x
+1,024 files x 64 KiB payload (1 M files, 64 GiB of payload), laid out as block
+images: each file is a 36-byte FileInfo followed by its payload
+(LogicBlock::close_write_file, logic_block.cpp:171-178,295-300), so payloads sit
+at 65,572*k + 36 -- 4-byte aligned only, as on disk.  One step = one verify pass
+over the whole resident set (recompute Func::crc(0, payload) and compare with
+the stored crc_ carried in the descriptor).  16 steps = the 1 TiB of config 2.
+
+Multi-GPU: one process per GPU, blocks partitioned by block id (each rank owns
+its own 1,024 blocks); no collective on the data path (torch.distributed is
+used only for the barrier and the max-over-ranks of the timing).  Weak scaling.
+
+Timing: W warmup steps, then K steps bracketed by barrier + synchronize; HIP
+events on the launch stream give the per-launch kernel time for the roofline.
+cpu_baseline: the reference Func::crc text (oracle/_ref, kind "reference") or the
+oracle restatement (kind "port"), single thread, on a bounded sample of the same
+resident bytes, rank 0 at N=1 only.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FILE_SIZE = 65536
+FILES_PER_BLOCK = 1024
+FILEINFO = 36
+HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (8.0 TB/s)
+ALGO_BYTES_PER_FILE = FILE_SIZE + 16 + 4 + 1  # payload + descriptor + crc out + verdict
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=16)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--blocks", type=int, default=1024, help="resident blocks per GPU (1024 = 1 M files)")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--e2e", action="store_true", help="also measure the pinned H2D-inclusive rate (stderr)")
+    p.add_argument("--membench", action="store_true", help="also time raw streaming reads (stderr)")
+    return p.parse_args()
+
+
+def cpu_baseline(sample_u8, offs, lens, expected, seconds):
+    """Single-thread reference CRC over a bounded sample (test infrastructure)."""
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "libref_crc.so")
+    ora_so = os.path.join(ROOT, "oracle", "liboracle_crc.so")
+    if os.path.exists(ref_so):
+        L = ctypes.CDLL(ref_so)
+        f = L.ref_func_crc
+        kind = "reference"
+    else:
+        L = ctypes.CDLL(ora_so)
+        f = L.oracle_crc
+        kind = "port"
+    f.restype = ctypes.c_uint32
+    f.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int32]
+    base = sample_u8.ctypes.data
+    nbytes = 0
+    passes = 0
+    t0 = time.perf_counter()
+    while True:
+        for i in range(len(offs)):
+            c = f(0, base + int(offs[i]), int(lens[i]))
+            if c != int(expected[i]):
+                raise SystemExit("cpu baseline disagrees with GPU expected crc at file %d" % i)
+            nbytes += int(lens[i])
+        passes += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    # all-core variant through the oracle's pthread batch (one file per task)
+    allcore = None
+    try:
+        O = ctypes.CDLL(ora_so)
+        O.oracle_crc_batch_mt.restype = ctypes.c_int
+        O.oracle_crc_batch_mt.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_int]
+        import tfs_amd.crc as crc
+        d = np.zeros(len(offs), crc.DESC_DTYPE)
+        d["offset"] = offs
+        d["len"] = lens
+        out = np.zeros(len(offs), np.uint32)
+        threads = min(16, os.cpu_count() or 1)
+        t1 = time.perf_counter()
+        reps = 0
+        while True:
+            O.oracle_crc_batch_mt(d.ctypes.data, len(offs), base, out.ctypes.data, threads)
+            reps += 1
+            if time.perf_counter() - t1 >= min(3.0, seconds):
+                break
+        ad = time.perf_counter() - t1
+        assert (out == expected).all()
+        allcore = {"value": reps * float(np.sum(lens)) / ad / 2**30, "cores": threads}
+    except Exception as e:  # reported, never fatal
+        allcore = {"error": str(e)}
+    return {
+        "value": nbytes / dt / 2**30,
+        "unit": "GiB/s",
+        "cores": 1,
+        "kind": kind,
+        "sample": "%d passes over %d x 64 KiB payloads (%.0f MiB) copied from the GPU-resident batch; "
+                  "Func::crc(0, payload) vs stored crc, single thread, %.1f s" % (
+                      passes, len(offs), float(np.sum(lens)) / 2**20, dt),
+        "allcore": allcore,
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    import tfs_amd.crc as crc
+    from tfs_amd.synth import synth_bytes
+    ctx = crc.Context(local)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    nblocks = args.blocks
+    nfiles = nblocks * FILES_PER_BLOCK
+    rec = FILEINFO + FILE_SIZE
+    block_bytes = FILES_PER_BLOCK * rec
+    total = nblocks * block_bytes
+    total_al = (total + 4095) // 4096 * 4096
+    # Blocks owned by this rank: global block ids rank, rank+world, ... (partition by block id).
+    img = torch.empty(total_al, dtype=torch.uint8, device=dev)
+    ctx.synth_fill_device(img, total_al, 0x9E3779B97F4A7C15 + rank, 0, stream=sp)
+    rec_off = np.arange(nfiles, dtype=np.uint64) * rec
+    desc = np.zeros(nfiles, crc.DESC_DTYPE)
+    desc["offset"] = rec_off + FILEINFO
+    desc["len"] = FILE_SIZE
+    d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+    d_crc = torch.zeros(nfiles, dtype=torch.int32, device=dev)
+    # write path: checksum-on-write of every payload, then persist FileInfo{crc_} headers
+    ctx.batch_device(d_desc, nfiles, img, d_crc, stream=sp)
+    d_off = torch.from_numpy(rec_off.view(np.int64)).to(dev)
+    d_len = torch.full((nfiles,), FILE_SIZE, dtype=torch.int32, device=dev)
+    ctx.write_headers_device(img, d_off, d_len, d_crc, 1 + rank * nfiles, nfiles, stream=sp)
+    torch.cuda.synchronize(dev)
+    expected = d_crc.cpu().numpy().view(np.uint32).copy()
+    desc["aux"] = expected
+    d_vdesc = torch.from_numpy(desc.view(np.uint8)).to(dev)
+    d_ok = torch.zeros(nfiles, dtype=torch.uint8, device=dev)
+    d_bad = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    # parity spot check of the resident bytes against the oracle (test infrastructure)
+    sample_idx = np.linspace(0, nfiles - 1, 48).astype(np.int64)
+    ora = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle_crc.so"))
+    ora.oracle_crc.restype = ctypes.c_uint32
+    ora.oracle_crc.argtypes = [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_int32]
+    for i in sample_idx:
+        o = int(desc["offset"][i])
+        host = img[o:o + FILE_SIZE].cpu().numpy().tobytes()
+        assert host == synth_bytes(0x9E3779B97F4A7C15 + rank, FILE_SIZE, o).tobytes()
+        if ora.oracle_crc(0, host, FILE_SIZE) != int(expected[i]):
+            raise SystemExit("GPU CRC disagrees with oracle at file %d" % i)
+
+    def step():
+        ctx.verify_device(d_vdesc, nfiles, img, None, d_ok, d_bad, stream=sp)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    d_bad.zero_()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        step()
+        ev[k][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    nbad = int(d_bad.item())
+    if nbad:
+        raise SystemExit("verify reported %d mismatches on clean data" % nbad)
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    payload_bytes = float(world) * args.steps * nfiles * FILE_SIZE
+    value = payload_bytes / elapsed / 2**30
+    avg_kern_s = float(np.mean(kern_ms)) / 1e3
+    achieved = nfiles * ALGO_BYTES_PER_FILE / avg_kern_s / 1e9
+
+    extra = {}
+    if args.membench:
+        out = torch.zeros(4, dtype=torch.int32, device=dev)
+        for pat in (0, 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ctx.membench_device(pat, img, d_vdesc, nfiles, total, out, stream=sp)
+            e0.record(stream)
+            for _ in range(5):
+                ctx.membench_device(pat, img, d_vdesc, nfiles, total, out, stream=sp)
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            ms = e0.elapsed_time(e1) / 5
+            nb = total if pat == 0 else nfiles * FILE_SIZE
+            extra["membench_pattern%d_GBs" % pat] = nb / (ms / 1e3) / 1e9
+        print(json.dumps({"membench": extra}), file=sys.stderr)
+
+    result = {
+        "metric": "GiB/s CRC32 verify, device-resident 64 KiB files; 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (splitmix64 payloads, FileInfo-headed block images, generated on device)",
+        "config": {
+            "workload": "device-resident CRC32 verify: %d blocks x %d files x 64 KiB per GPU (%d files, %.1f GiB "
+                        "payload); 16 steps = 1 TiB per GPU (BASELINE configs[1])" % (
+                            nblocks, FILES_PER_BLOCK, nfiles, nfiles * FILE_SIZE / 2**30),
+            "files_per_gpu": nfiles,
+            "file_size": FILE_SIZE,
+            "layout": "block image, FileInfo(36 B)|payload, payload 4-byte aligned",
+            "partition": "by block id across ranks, no collective",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "kernel": "crc_files_kernel<1> (verify)",
+            "kernel_ms_avg": avg_kern_s * 1e3,
+            "algorithmic_bytes_per_launch": nfiles * ALGO_BYTES_PER_FILE,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        ns = min(2048, nfiles)
+        idx = np.linspace(0, nfiles - 1, ns).astype(np.int64)
+        # copy the sampled records (identical bytes) to host
+        sample = np.zeros(ns * FILE_SIZE, np.uint8)
+        for j, i in enumerate(idx):
+            o = int(desc["offset"][i])
+            sample[j * FILE_SIZE:(j + 1) * FILE_SIZE] = img[o:o + FILE_SIZE].cpu().numpy()
+        result["cpu_baseline"] = cpu_baseline(sample, np.arange(ns) * FILE_SIZE, np.full(ns, FILE_SIZE),
+                                              expected[idx], args.cpu_seconds)
+    if args.e2e:
+        print(json.dumps({"e2e": e2e_rate(ctx, torch, dev)}), file=sys.stderr)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+def e2e_rate(ctx, torch, dev):
+    """Host block image -> pinned -> GPU verify -> verdicts back: the PCIe-inclusive rate."""
+    import tfs_amd.crc as crc
+    nfiles = 4096
+    rec = FILEINFO + FILE_SIZE
+    host = torch.empty(nfiles * rec, dtype=torch.uint8).pin_memory()
+    from tfs_amd.synth import synth_bytes
+    host.numpy()[:] = synth_bytes(5, nfiles * rec)
+    offs = np.arange(nfiles) * rec + FILEINFO
+    exp = ctx.batch(host.numpy(), offs, [FILE_SIZE] * nfiles)
+    t0 = time.perf_counter()
+    reps = 4
+    for _ in range(reps):
+        c, ok, nbad, rc = ctx.verify(host.numpy(), offs, [FILE_SIZE] * nfiles, exp)
+        assert nbad == 0
+    dt = time.perf_counter() - t0
+    return {"GiBps_incl_pinned_h2d": reps * nfiles * FILE_SIZE / dt / 2**30, "files": nfiles}
+
+
+if __name__ == "__main__":
+    main()

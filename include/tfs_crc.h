@@ -1,0 +1,222 @@
+/*
+ * tfs_crc.h -- C ABI of the MI355X-native per-file CRC32 integrity path.
+ *
+ * Drop-in boundary for TFS's dataserver CRC call sites (reference =
+ * simonsysu/tfs @ TFS 2.3.0, /root/reference).  Every entry point below names
+ * the reference interface it replaces.  Plain C types only (no torch, no HIP
+ * types): device pointers and streams are passed as `void*`.
+ *
+ * Arithmetic: reflected CRC-32, polynomial 0xEDB88320, caller-supplied seed,
+ * no pre/post inversion, len <= 0 returns the seed -- bit-identical to
+ * tfs::common::Func::crc (src/common/func.cpp:426-435, table
+ * src/common/func.h:128-154).  The computation runs on the GPU (hand-written
+ * gfx950 kernels in tfs_amd/csrc/); there is no CPU fallback: without a usable
+ * device every entry point returns TFS_CRC_EXIT_NO_DEVICE.
+ *
+ * Return convention (reference src/common/error_msg.h, src/common/cdefine.h):
+ *   TFS_SUCCESS (0) on success, negative TFS codes on failure.
+ */
+#ifndef TFS_CRC_H_
+#define TFS_CRC_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------- */
+#define TFS_SUCCESS 0                      /* cdefine.h:26 */
+#define TFS_EXIT_CHECK_CRC_ERROR (-1010)   /* error_msg.h:35  verify: crc mismatch */
+#define TFS_EXIT_PARAMETER_ERROR (-1016)   /* error_msg.h:41  bad argument */
+#define TFS_EXIT_DATA_FILE_ERROR (-8013)   /* error_msg.h:149 close: client crc != data crc */
+#define TFS_EXIT_FILE_INFO_ERROR (-8016)   /* error_msg.h:152 FileInfo id/flag mismatch */
+#define TFS_EXIT_READ_FILE_SIZE_ERROR (-8034) /* error_msg.h:170 record shorter than FileInfo */
+#define TFS_EXIT_SYNC_FILE_ERROR (-8038)   /* error_msg.h:174 verify: size mismatch */
+/* New codes (outside the reference's -1000..-16008 range): */
+#define TFS_CRC_EXIT_DEVICE_ERROR (-20001) /* a HIP call failed; see tfs_crc32_last_error() */
+#define TFS_CRC_EXIT_NO_DEVICE (-20002)    /* no usable gfx950 device / kernels not loadable */
+
+/* FileInfo flags, src/dataserver/dataserver_define.h:54-59 */
+#define TFS_FI_DELETED 1
+#define TFS_FI_INVALID 2
+#define TFS_FI_CONCEAL 4
+
+#define TFS_FILEINFO_SIZE 36          /* sizeof(FileInfo), internal.h:432-446, pack(4) */
+#define TFS_BLOCK_RESERVER_LENGTH 512 /* physical_block.h:31 */
+
+/* ---- data layouts ---------------------------------------------------- */
+
+/* One file to checksum: `len` bytes at base + offset, starting CRC `seed`
+ * (Func::crc's first argument; 0 at every per-file call site,
+ * data_file.cpp:190).  16 bytes, naturally aligned. */
+typedef struct tfs_crc_desc {
+  uint64_t offset;
+  uint32_t len;
+  uint32_t seed;
+} tfs_crc_desc;
+
+/* One file to verify: recomputed Func::crc(0, base+offset, len) must equal
+ * `expected` (the stored FileInfo.crc_, sync_backup.cpp:429). 16 bytes. */
+typedef struct tfs_crc_vdesc {
+  uint64_t offset;
+  uint32_t len;
+  uint32_t expected;
+} tfs_crc_vdesc;
+
+/* FileInfo exactly as stored in a block (src/common/internal.h:432-446). */
+#pragma pack(push, 4)
+typedef struct tfs_file_info {
+  uint64_t id_;
+  int32_t offset_;
+  int32_t size_;   /* payload + 36 on disk */
+  int32_t usize_;
+  int32_t modify_time_;
+  int32_t create_time_;
+  int32_t flag_;
+  uint32_t crc_;
+} tfs_file_info;
+#pragma pack(pop)
+
+/* One index entry of a block (RawMeta, internal.h:535-645): file id, logical
+ * data offset of its FileInfo, size incl. the 36-byte header. */
+typedef struct tfs_raw_meta {
+  uint64_t file_id;
+  int32_t offset;
+  int32_t size;
+} tfs_raw_meta;
+
+typedef struct tfs_crc_ctx tfs_crc_ctx;
+
+/* ---- context ---------------------------------------------------------- */
+
+/* Create a context bound to HIP device `device` (one per GPU; the dataserver
+ * owns one per local GPU).  Loads the CRC tables into device memory.
+ * Thread-safe to use from many threads (calls are serialised per ctx). */
+int tfs_crc32_ctx_create(int device, tfs_crc_ctx** out);
+int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx);
+/* Message of the last failure on this ctx (or of the process-wide default ctx
+ * when ctx == NULL).  Never NULL. */
+const char* tfs_crc32_last_error(const tfs_crc_ctx* ctx);
+/* Number of HIP devices visible to this process (0 when none). */
+int tfs_crc32_device_count(void);
+
+/* ---- scalar drop-in --------------------------------------------------- */
+
+/* Replaces `static uint32_t Func::crc(uint32_t crc, const char* data,
+ * const int32_t len)` (src/common/func.h:90, func.cpp:426-435).  Host buffer,
+ * result by value, len <= 0 returns crc.  Runs on the process-wide default
+ * context (device 0).  On device failure returns `crc` and sets *err (when
+ * err != NULL) -- use the batch API when errors must be observed. */
+uint32_t tfs_crc32(uint32_t crc, const char* data, int32_t len);
+uint32_t tfs_crc32_e(uint32_t crc, const char* data, int32_t len, int* err);
+
+/* Replaces DataFile::get_crc() (src/dataserver/data_file.cpp:168-194):
+ * Func::crc(0, data, length).  The reference re-reads payloads > 2 MiB in
+ * 2 MiB chunks with a running seed (:183-186); that equals one pass over the
+ * whole payload, which is what this computes. */
+int tfs_datafile_get_crc(tfs_crc_ctx* ctx, const char* data, int32_t length, uint32_t* out_crc);
+
+/* ---- batch, host memory ----------------------------------------------- */
+
+/* Batched Func::crc over `n` files of a host buffer [base, base+base_len):
+ * out_crc[i] = Func::crc(d[i].seed, base + d[i].offset, d[i].len).  The
+ * touched bytes are staged through pinned memory (hipMemcpyAsync) to the GPU.
+ * Call sites: data_file.cpp:190 via data_management.cpp:197 (write), batched
+ * across concurrent leases. */
+int tfs_crc32_batch(tfs_crc_ctx* ctx, const tfs_crc_desc* d, uint32_t n, const void* base, uint64_t base_len,
+                    uint32_t* out_crc);
+
+/* Batched verify-on-read: out_crc[i] = Func::crc(0, base+d[i].offset, d[i].len),
+ * out_ok[i] = (out_crc[i] == d[i].expected), *n_bad = number of mismatches.
+ * Returns TFS_SUCCESS when all match, TFS_EXIT_CHECK_CRC_ERROR when any does
+ * not (sync_backup.cpp:429), other negatives on error.  out_crc / out_ok /
+ * n_bad may be NULL.  Call sites: sync_backup.cpp:383/412, file_repair.cpp:142,
+ * block_console.cpp:570. */
+int tfs_crc32_verify(tfs_crc_ctx* ctx, const tfs_crc_vdesc* d, uint32_t n, const void* base, uint64_t base_len,
+                     uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad);
+
+/* ---- batch, device-resident ------------------------------------------- */
+
+/* Same as tfs_crc32_batch with every pointer in device memory of ctx's GPU;
+ * enqueued on `stream` (a hipStream_t, NULL = ctx's stream); asynchronous:
+ * results are valid once the stream reaches this point. */
+int tfs_crc32_batch_device(tfs_crc_ctx* ctx, const tfs_crc_desc* d_desc, uint32_t n, const void* d_base,
+                           uint32_t* d_out_crc, void* stream);
+/* Device-resident verify. d_n_bad (may be NULL) is accumulated into (atomic
+ * add), so zero it first.  d_out_crc / d_out_ok may be NULL. */
+int tfs_crc32_verify_device(tfs_crc_ctx* ctx, const tfs_crc_vdesc* d_desc, uint32_t n, const void* d_base,
+                            uint32_t* d_out_crc, uint8_t* d_out_ok, uint32_t* d_n_bad, void* stream);
+
+/* ---- async host API ---------------------------------------------------- */
+
+typedef struct tfs_crc_ticket {
+  uint64_t id;
+} tfs_crc_ticket;
+
+/* Enqueue a host-memory verify (as tfs_crc32_verify) and return immediately;
+ * the caller keeps d/base/outputs alive and unmodified until tfs_crc32_wait.
+ * H2D copy, kernel and D2H copy run on the ctx stream, double-buffered against
+ * other in-flight submissions. */
+int tfs_crc32_submit_verify(tfs_crc_ctx* ctx, const tfs_crc_vdesc* d, uint32_t n, const void* base,
+                            uint64_t base_len, uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad,
+                            tfs_crc_ticket* ticket);
+/* Block until the ticket's results are in the caller's buffers; returns the
+ * status the synchronous call would have returned. */
+int tfs_crc32_wait(tfs_crc_ctx* ctx, tfs_crc_ticket ticket);
+
+/* ---- block images ----------------------------------------------------- */
+
+/* Verify-on-read of files stored in a block image (logical data area: offset 0
+ * = first FileInfo, i.e. the bytes after the 512-byte BlockPrefix,
+ * physical_block.cpp:30-35).  For each meta: read the FileInfo at
+ * image+meta.offset, recompute Func::crc(0, payload, meta.size-36) and report
+ * per file status[i] in {TFS_SUCCESS, TFS_EXIT_FILE_INFO_ERROR (header id !=
+ * meta id), TFS_EXIT_READ_FILE_SIZE_ERROR (meta.size <= 36),
+ * TFS_EXIT_SYNC_FILE_ERROR (FileInfo.size_ != meta.size), TFS_EXIT_CHECK_CRC_ERROR}
+ * -- the checks of sync_backup.cpp:345-435 / block_console.cpp:543-577 in that
+ * order.  d_* variants take device pointers; the host variant copies the image. */
+int tfs_block_verify(tfs_crc_ctx* ctx, const void* image, uint64_t image_len, const tfs_raw_meta* metas, uint32_t n,
+                     uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad);
+int tfs_block_verify_device(tfs_crc_ctx* ctx, const void* d_image, uint64_t image_len, const tfs_raw_meta* d_metas,
+                            uint32_t n, uint32_t* d_out_crc, int32_t* d_out_status, uint32_t* d_n_bad, void* stream);
+
+/* Compaction with re-CRC (CompactTask::real_compact, src/dataserver/task.cpp:713-836):
+ * walk `metas` (sorted by offset, traverse_sorted_segment_meta), skip files
+ * whose real flag (flags[i], logic_block.cpp:1273) has FI_DELETED|FI_INVALID,
+ * and pack each live file as FileInfo{offset_=w, size_=usize_=payload+36,
+ * other fields and crc_ copied} | payload into `dest` (task.cpp:753-798).
+ * Adds the verify the reference does not do: recomputed payload CRC ==
+ * stored crc_ (crc_ok[i] = 1 ok, 0 mismatch, 2 skipped).  dest_metas receives
+ * the RawMeta list of the new block (task.cpp:764-768); *dest_len and
+ * *n_live the new data size and file count.  Host buffers; the source block is
+ * copied to the GPU, verified and repacked there, and the new block copied
+ * back (H<->D included, BASELINE config 4). */
+int tfs_block_compact(tfs_crc_ctx* ctx, const void* src_image, uint64_t src_len, const tfs_raw_meta* metas,
+                      const int32_t* flags, uint32_t n, void* dest_image, uint64_t dest_cap, tfs_raw_meta* dest_metas,
+                      uint8_t* crc_ok, uint64_t* dest_len, uint32_t* n_live);
+
+/* ---- test / bench helpers (not part of the dataserver boundary) -------- */
+
+/* Fill nbytes (multiple of 8) of device memory with the splitmix64 synthetic
+ * stream of tfs_amd/synth.py: word i = splitmix64(seed + (first_word+i+1)*GOLDEN). */
+int tfs_crc32_synth_fill_device(tfs_crc_ctx* ctx, void* d_dst, uint64_t nbytes, uint64_t seed, uint64_t first_word,
+                                void* stream);
+/* Write FileInfo{id=first_id+f, offset_=rec_off[f], size_=usize_=len[f]+36, crc_=crc[f]}
+ * at d_image + d_rec_off[f] for f < n (device pointers). */
+int tfs_crc32_write_headers_device(tfs_crc_ctx* ctx, void* d_image, const uint64_t* d_rec_off, const uint32_t* d_len,
+                                   const uint32_t* d_crc, uint64_t first_id, uint32_t n, void* stream);
+/* Calibration: stream the bytes without CRC arithmetic.  pattern 0 = coalesced
+ * grid-stride over [d_base, d_base+nbytes); pattern 1 = the CRC kernel's
+ * per-file lane-segment access pattern over d_desc (len multiple of 1 KiB). */
+int tfs_crc32_membench_device(tfs_crc_ctx* ctx, int pattern, const void* d_base, const tfs_crc_desc* d_desc,
+                              uint32_t n, uint64_t nbytes, uint32_t* d_out, unsigned grid, void* stream);
+/* The ctx's HIP stream (as void*) and a synchronize on it. */
+void* tfs_crc32_stream(tfs_crc_ctx* ctx);
+int tfs_crc32_sync(tfs_crc_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TFS_CRC_H_ */

@@ -1,0 +1,223 @@
+"""GPU parity: the HIP path (through the C ABI) vs the oracle and the golden
+vectors.  Integer/byte work, so the bar is bit-exact everywhere."""
+import numpy as np
+import pytest
+
+from conftest import ocrc, vector_input
+from tfs_amd.synth import synth_bytes
+
+pytestmark = pytest.mark.gpu
+
+
+def _pack(items, align_pad=7):
+    """items: list of bytes -> (buffer, offsets) with odd gaps between payloads."""
+    offs, chunks, o = [], [], 0
+    for i, d in enumerate(items):
+        gap = (i * 5 + 3) % align_pad
+        chunks.append(bytes(gap))
+        o += gap
+        offs.append(o)
+        chunks.append(d)
+        o += len(d)
+    chunks.append(bytes(16))
+    return np.frombuffer(b"".join(chunks), np.uint8), offs
+
+
+def test_golden_vectors_gpu(gpu_ctx, golden):
+    vs = golden["vectors"]
+    datas = [vector_input(v) for v in vs]
+    lens = [max(v.get("len_arg", len(d)), 0) for v, d in zip(vs, datas)]
+    buf, offs = _pack(datas)
+    got = gpu_ctx.batch(buf, offs, lens, [v["seed"] for v in vs])
+    for v, g in zip(vs, got):
+        assert int(g) == v["expected"], v["name"]
+
+
+def test_continuation_and_datafile_gpu(gpu_ctx, golden):
+    for v in golden["continuation"]:
+        d = vector_input(v)
+        cut = v["cut"]
+        buf = np.frombuffer(d, np.uint8)
+        c1 = gpu_ctx.batch(buf, [0], [cut], [v["seed"]])[0]
+        assert int(c1) == v["expected_first"], v["name"]
+        c2 = gpu_ctx.batch(buf, [cut], [len(d) - cut], [int(c1)])[0]
+        assert int(c2) == v["expected"], v["name"]
+    for v in golden["datafile_big"]:
+        assert gpu_ctx.datafile_get_crc(vector_input(v)) == v["expected"], v["name"]
+
+
+def test_scalar_func_crc_kats():
+    import tfs_amd.crc as crc
+    assert crc.func_crc(0, b"123456789") == 0x2DFD2D88
+    assert crc.func_crc(0xFFFFFFFF, b"123456789") ^ 0xFFFFFFFF == 0xCBF43926
+    assert crc.func_crc(0x4E534654, b"123456789") == 0xCADE6EAE
+    assert crc.func_crc(0, b"\x80") == 0xEDB88320
+    assert crc.func_crc(0x1234, b"") == 0x1234
+    assert crc.func_crc(7, b"abcde", -5) == 7
+    assert crc.func_crc(0, b"1" + bytes(31)) == 0xD631B691
+
+
+@pytest.mark.parametrize("seed_mode", ["zero", "random"])
+def test_all_small_lengths_and_alignments(gpu_ctx, oracle, seed_mode):
+    rng = np.random.default_rng(11 if seed_mode == "zero" else 12)
+    lens = list(range(0, 600)) + [int(x) for x in rng.integers(600, 20000, 150)]
+    buf = synth_bytes(99, sum(lens) + 32 * len(lens) + 64)
+    raw = buf.tobytes()
+    offs, o = [], 0
+    for i, n in enumerate(lens):
+        o += i % 16 + 1
+        offs.append(o)
+        o += n
+    seeds = [0] * len(lens) if seed_mode == "zero" else [int(x) for x in rng.integers(0, 2**32, len(lens))]
+    got = gpu_ctx.batch(buf, offs, lens, seeds)
+    for i, n in enumerate(lens):
+        assert int(got[i]) == ocrc(oracle, seeds[i], raw[offs[i]:offs[i] + n]), (i, n, offs[i] % 16)
+
+
+def test_large_sizes(gpu_ctx, oracle):
+    sizes = [65535, 65536, 65537, 65536 * 64 - 5, (1 << 20) + 1, 3 * (1 << 20) + 17, 9 * (1 << 20) + 3]
+    for k, n in enumerate(sizes):
+        for off in (0, 4, 13):
+            buf = synth_bytes(300 + k, n + off + 8)
+            raw = buf.tobytes()
+            s = [0, 0x4E534654, 0xFFFFFFFF][k % 3]
+            got = gpu_ctx.batch(buf, [off], [n], [s])[0]
+            assert int(got) == ocrc(oracle, s, raw[off:off + n]), (n, off)
+
+
+def test_verify_detects_every_single_byte_corruption(gpu_ctx, oracle):
+    n, ln = 96, 65536
+    stride = ln + 36
+    buf = synth_bytes(5, n * stride + 64)
+    raw = bytearray(buf.tobytes())
+    offs = [36 + i * stride for i in range(n)]
+    exp = [ocrc(oracle, 0, raw[o:o + ln]) for o in offs]
+    rng = np.random.default_rng(3)
+    bad_files = sorted(rng.choice(n, 17, replace=False).tolist())
+    for f in bad_files:
+        pos = offs[f] + int(rng.integers(0, ln))
+        raw[pos] ^= 1 << int(rng.integers(0, 8))
+    crc, ok, nbad, rc = gpu_ctx.verify(np.frombuffer(bytes(raw), np.uint8), offs, [ln] * n, exp)
+    assert nbad == len(bad_files) and rc == -1010
+    assert [i for i in range(n) if not ok[i]] == bad_files
+    for i in range(n):
+        assert int(crc[i]) == ocrc(oracle, 0, raw[offs[i]:offs[i] + ln])
+
+
+def test_async_submit_wait(gpu_ctx, oracle):
+    hs, exps = [], []
+    for k in range(3):
+        buf = synth_bytes(700 + k, 10 * 4096 + 8)
+        offs = [i * 4096 + 4 for i in range(10)]
+        exp = [ocrc(oracle, 0, buf[o:o + 4000].tobytes()) for o in offs]
+        if k == 1:
+            exp[4] ^= 0x10
+        hs.append(gpu_ctx.submit_verify(buf, offs, [4000] * 10, exp))
+    for k, h in enumerate(hs):
+        crc, ok, nbad, rc = gpu_ctx.wait(h)
+        assert nbad == (1 if k == 1 else 0)
+
+
+def test_device_resident_torch(gpu_ctx, oracle):
+    import torch
+    import tfs_amd.crc as crc
+    n, ln = 512, 65536
+    stride = ln + 36
+    nbytes = (n * stride + 4095) // 4096 * 4096
+    dev = torch.device("cuda:0")
+    img = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    gpu_ctx.synth_fill_device(img, nbytes, 1234, 0, stream=stream)
+    d = np.zeros(n, crc.DESC_DTYPE)
+    d["offset"] = 36 + np.arange(n) * stride
+    d["len"] = ln
+    dd = torch.from_numpy(d.view(np.uint8)).to(dev)
+    out = torch.zeros(n, dtype=torch.int32, device=dev)
+    gpu_ctx.batch_device(dd, n, img, out, stream=stream)
+    torch.cuda.synchronize()
+    host = synth_bytes(1234, nbytes)
+    assert (img.cpu().numpy() == host).all()
+    got = out.cpu().numpy().view(np.uint32)
+    for i in range(0, n, 37):
+        o = int(d["offset"][i])
+        assert int(got[i]) == ocrc(oracle, 0, host[o:o + ln].tobytes())
+    # verify on device against the computed CRCs, with two corrupted expectations
+    v = d.copy()
+    v["aux"] = got
+    v["aux"][[3, 300]] ^= 1
+    vd = torch.from_numpy(v.view(np.uint8)).to(dev)
+    okd = torch.zeros(n, dtype=torch.uint8, device=dev)
+    nb = torch.zeros(1, dtype=torch.int32, device=dev)
+    gpu_ctx.verify_device(vd, n, img, None, okd, nb, stream=stream)
+    torch.cuda.synchronize()
+    assert int(nb.item()) == 2
+    assert sorted(np.nonzero(okd.cpu().numpy() == 0)[0].tolist()) == [3, 300]
+
+
+def _block_image(oracle, sizes, seed=21):
+    """Pack FileInfo|payload records like LogicBlock::close_write_file does."""
+    import tfs_amd.crc as crc
+    total = sum(36 + s for s in sizes)
+    img = np.zeros(total + 64, np.uint8)
+    metas = np.zeros(len(sizes), crc.META_DTYPE)
+    o = 0
+    for i, s in enumerate(sizes):
+        pay = synth_bytes(seed * 1000 + i, s)
+        fi = np.zeros(1, crc.FILEINFO_DTYPE)
+        fi["id_"] = 1000 + i
+        fi["offset_"] = o
+        fi["size_"] = s + 36
+        fi["usize_"] = s + 36
+        fi["crc_"] = ocrc(oracle, 0, pay.tobytes())
+        img[o:o + 36] = fi.view(np.uint8)
+        img[o + 36:o + 36 + s] = pay
+        metas[i] = (1000 + i, o, s + 36)
+        o += 36 + s
+    return img, metas
+
+
+def test_block_verify_statuses(gpu_ctx, oracle):
+    sizes = [65536] * 20 + [1, 100, 4097, 70001]
+    img, metas = _block_image(oracle, sizes)
+    crc_, st, nbad, rc = gpu_ctx.block_verify(img, metas)
+    assert nbad == 0 and (st == 0).all()
+    img[int(metas[5]["offset"]) + 36 + 777] ^= 0x40            # payload corruption
+    metas2 = metas.copy()
+    metas2[7]["file_id"] = 999999                               # header id mismatch
+    img[int(metas[9]["offset"]) + 12] ^= 0x01                   # FileInfo.size_ mismatch
+    metas2[11]["size"] = 36                                     # too short
+    crc_, st, nbad, rc = gpu_ctx.block_verify(img, metas2)
+    assert rc == -1010 and nbad == 4
+    assert st[5] == -1010 and st[7] == -8016 and st[9] == -8038 and st[11] == -8034
+    for i in (0, 21, 23):
+        o = int(metas[i]["offset"])
+        code = oracle.oracle_verify_file(img.ctypes.data, img.size, o, int(metas[i]["size"]), None)
+        assert code == st[i] == 0
+
+
+def test_block_compact_matches_oracle(gpu_ctx, oracle):
+    rng = np.random.default_rng(8)
+    sizes = [65536] * 30 + [int(x) for x in rng.integers(1, 9000, 30)]
+    img, metas = _block_image(oracle, sizes, seed=33)
+    flags = np.zeros(len(sizes), np.int32)
+    flags[::2] |= 1                 # delete every even file (test_logic_block_and_compact.cpp:946-975)
+    flags[1::6] |= 2                # and invalidate some
+    flags[3::10] |= 4               # concealed files survive
+    img[int(metas[5]["offset"]) + 40] ^= 1   # a live file with a bad payload
+    dest, dmetas, ok, rc = gpu_ctx.block_compact(img, metas, flags)
+    n = len(sizes)
+    mo = metas["offset"].astype(np.int64)
+    ms = metas["size"].astype(np.int32)
+    odest = np.zeros(dest.size + 64, np.uint8)
+    doff = np.zeros(n, np.int64)
+    dsz = np.zeros(n, np.int32)
+    ook = np.zeros(n, np.uint8)
+    w = oracle.oracle_compact(img.ctypes.data, mo.ctypes.data, ms.ctypes.data, flags.ctypes.data, n,
+                              odest.ctypes.data, doff.ctypes.data, dsz.ctypes.data, ook.ctypes.data)
+    assert w == dest.size
+    assert (odest[:w] == dest).all()
+    assert (ook == ok).all()
+    assert rc == -1010 and ok[5] == 0
+    live = [i for i in range(n) if not flags[i] & 3]
+    assert [int(x) for x in dmetas["file_id"]] == [int(metas[i]["file_id"]) for i in live]
+    assert [int(x) for x in dmetas["offset"]] == [int(doff[i]) for i in live]

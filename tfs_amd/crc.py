@@ -1,0 +1,290 @@
+"""ctypes binding of the C ABI in include/tfs_crc.h (libtfs_crc.so, built in-tree).
+
+The native library is the product: every function here calls into the gfx950
+kernels through the C ABI.  There is no Python or CPU fallback -- if the
+library is missing this module raises on import, and if no gfx950 device is
+present the calls return TFS_CRC_EXIT_NO_DEVICE and raise TfsCrcError.
+
+Names mirror the reference interface they replace:
+  func_crc(seed, data)        tfs::common::Func::crc   src/common/func.h:90, func.cpp:426-435
+  Context.batch / verify      the per-file call sites   data_file.cpp:190, sync_backup.cpp:383/429
+  Context.block_verify        verify-on-read of a block sync_backup.cpp:345-435, block_console.cpp:543-577
+  Context.block_compact       CompactTask::real_compact task.cpp:713-836 (+ re-CRC verify)
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libtfs_crc.so")
+
+TFS_SUCCESS = 0
+TFS_EXIT_CHECK_CRC_ERROR = -1010
+TFS_EXIT_PARAMETER_ERROR = -1016
+TFS_EXIT_DATA_FILE_ERROR = -8013
+TFS_EXIT_FILE_INFO_ERROR = -8016
+TFS_EXIT_READ_FILE_SIZE_ERROR = -8034
+TFS_EXIT_SYNC_FILE_ERROR = -8038
+TFS_CRC_EXIT_DEVICE_ERROR = -20001
+TFS_CRC_EXIT_NO_DEVICE = -20002
+
+FI_DELETED, FI_INVALID, FI_CONCEAL = 1, 2, 4
+FILEINFO_SIZE = 36
+
+DESC_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("aux", "<u4")])  # tfs_crc_desc / tfs_crc_vdesc
+META_DTYPE = np.dtype([("file_id", "<u8"), ("offset", "<i4"), ("size", "<i4")])  # tfs_raw_meta
+FILEINFO_DTYPE = np.dtype([("id_", "<u8"), ("offset_", "<i4"), ("size_", "<i4"), ("usize_", "<i4"),
+                           ("modify_time_", "<i4"), ("create_time_", "<i4"), ("flag_", "<i4"),
+                           ("crc_", "<u4")], align=False)
+assert DESC_DTYPE.itemsize == 16 and META_DTYPE.itemsize == 16 and FILEINFO_DTYPE.itemsize == 36
+
+# Every symbol include/tfs_crc.h declares (checked by tests/test_abi.py).
+EXPORTED = [
+    "tfs_crc32_ctx_create", "tfs_crc32_ctx_destroy", "tfs_crc32_last_error", "tfs_crc32_device_count",
+    "tfs_crc32", "tfs_crc32_e", "tfs_datafile_get_crc", "tfs_crc32_batch", "tfs_crc32_verify",
+    "tfs_crc32_batch_device", "tfs_crc32_verify_device", "tfs_crc32_submit_verify", "tfs_crc32_wait",
+    "tfs_block_verify", "tfs_block_verify_device", "tfs_block_compact",
+    "tfs_crc32_synth_fill_device", "tfs_crc32_write_headers_device", "tfs_crc32_membench_device",
+    "tfs_crc32_stream", "tfs_crc32_sync",
+]
+
+
+class TfsCrcError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s (code %d)" % (msg, code))
+        self.code = code
+
+
+_LIB = None
+
+
+def lib():
+    """Load libtfs_crc.so; raise loudly when it is missing (no fallback)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("tfs_amd native library not built: %s (run __graft_entry__.build())" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u32, i32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64
+        sig = {
+            "tfs_crc32_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(vp)]),
+            "tfs_crc32_ctx_destroy": (ctypes.c_int, [vp]),
+            "tfs_crc32_last_error": (ctypes.c_char_p, [vp]),
+            "tfs_crc32_device_count": (ctypes.c_int, []),
+            "tfs_crc32": (u32, [u32, ctypes.c_char_p, i32]),
+            "tfs_crc32_e": (u32, [u32, ctypes.c_char_p, i32, ctypes.POINTER(ctypes.c_int)]),
+            "tfs_datafile_get_crc": (ctypes.c_int, [vp, ctypes.c_char_p, i32, ctypes.POINTER(u32)]),
+            "tfs_crc32_batch": (ctypes.c_int, [vp, vp, u32, vp, u64, vp]),
+            "tfs_crc32_verify": (ctypes.c_int, [vp, vp, u32, vp, u64, vp, vp, vp]),
+            "tfs_crc32_batch_device": (ctypes.c_int, [vp, vp, u32, vp, vp, vp]),
+            "tfs_crc32_verify_device": (ctypes.c_int, [vp, vp, u32, vp, vp, vp, vp, vp]),
+            "tfs_crc32_submit_verify": (ctypes.c_int, [vp, vp, u32, vp, u64, vp, vp, vp, vp]),
+            "tfs_crc32_wait": (ctypes.c_int, [vp, u64]),
+            "tfs_block_verify": (ctypes.c_int, [vp, vp, u64, vp, u32, vp, vp, vp]),
+            "tfs_block_verify_device": (ctypes.c_int, [vp, vp, u64, vp, u32, vp, vp, vp, vp]),
+            "tfs_block_compact": (ctypes.c_int, [vp, vp, u64, vp, vp, u32, vp, u64, vp, vp, vp, vp]),
+            "tfs_crc32_synth_fill_device": (ctypes.c_int, [vp, vp, u64, u64, u64, vp]),
+            "tfs_crc32_write_headers_device": (ctypes.c_int, [vp, vp, vp, vp, vp, u64, u32, vp]),
+            "tfs_crc32_membench_device": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, u32, u64, vp, ctypes.c_uint, vp]),
+            "tfs_crc32_stream": (vp, [vp]),
+            "tfs_crc32_sync": (ctypes.c_int, [vp]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def device_count():
+    return lib().tfs_crc32_device_count()
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    if isinstance(a, int):
+        return a
+    if hasattr(a, "data_ptr"):  # torch tensor (device memory plumbing only)
+        return a.data_ptr()
+    if isinstance(a, (bytes, bytearray, memoryview)):
+        return ctypes.cast(ctypes.c_char_p(bytes(a)), ctypes.c_void_p).value
+    raise TypeError("unsupported buffer %r" % type(a))
+
+
+def _as_u8(data):
+    if isinstance(data, np.ndarray):
+        return np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+    return np.frombuffer(bytes(data), dtype=np.uint8)
+
+
+class Context:
+    """One per GPU: wraps tfs_crc_ctx (device tables, stream, staging pools)."""
+
+    def __init__(self, device=0):
+        h = ctypes.c_void_p()
+        rc = lib().tfs_crc32_ctx_create(device, ctypes.byref(h))
+        if rc != TFS_SUCCESS:
+            msg = lib().tfs_crc32_last_error(h).decode() if h.value else "ctx_create failed"
+            if h.value:
+                lib().tfs_crc32_ctx_destroy(h)
+            raise TfsCrcError(rc, "tfs_crc32_ctx_create(%d): %s" % (device, msg))
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if self.handle is not None and self.handle.value:
+            lib().tfs_crc32_ctx_destroy(self.handle)
+        self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc, what, ok=(TFS_SUCCESS,)):
+        if rc not in ok:
+            raise TfsCrcError(rc, "%s: %s" % (what, lib().tfs_crc32_last_error(self.handle).decode()))
+        return rc
+
+    @property
+    def stream(self):
+        return lib().tfs_crc32_stream(self.handle)
+
+    def sync(self):
+        self._check(lib().tfs_crc32_sync(self.handle), "sync")
+
+    # ---- host-memory batches -------------------------------------------------
+    def batch(self, base, offsets, lens, seeds=0):
+        """out[i] = Func::crc(seeds[i], base+offsets[i], lens[i]) for a host buffer."""
+        buf = _as_u8(base)
+        n = len(offsets)
+        d = np.zeros(n, DESC_DTYPE)
+        d["offset"] = offsets
+        d["len"] = lens
+        d["aux"] = seeds
+        out = np.zeros(n, np.uint32)
+        self._check(lib().tfs_crc32_batch(self.handle, _ptr(d), n, _ptr(buf), buf.size, _ptr(out)), "batch")
+        return out
+
+    def verify(self, base, offsets, lens, expected):
+        """Verify-on-read: returns (crc, ok, n_bad, rc) with rc TFS_SUCCESS or TFS_EXIT_CHECK_CRC_ERROR."""
+        buf = _as_u8(base)
+        n = len(offsets)
+        d = np.zeros(n, DESC_DTYPE)
+        d["offset"] = offsets
+        d["len"] = lens
+        d["aux"] = expected
+        crc = np.zeros(n, np.uint32)
+        ok = np.zeros(n, np.uint8)
+        nbad = np.zeros(1, np.uint32)
+        rc = lib().tfs_crc32_verify(self.handle, _ptr(d), n, _ptr(buf), buf.size, _ptr(crc), _ptr(ok), _ptr(nbad))
+        self._check(rc, "verify", ok=(TFS_SUCCESS, TFS_EXIT_CHECK_CRC_ERROR))
+        return crc, ok, int(nbad[0]), rc
+
+    def submit_verify(self, base, offsets, lens, expected):
+        """Async verify; returns a handle to pass to wait()."""
+        buf = _as_u8(base)
+        n = len(offsets)
+        d = np.zeros(n, DESC_DTYPE)
+        d["offset"] = offsets
+        d["len"] = lens
+        d["aux"] = expected
+        crc = np.zeros(n, np.uint32)
+        ok = np.zeros(n, np.uint8)
+        nbad = np.zeros(1, np.uint32)
+        t = ctypes.c_uint64()
+        rc = lib().tfs_crc32_submit_verify(self.handle, _ptr(d), n, _ptr(buf), buf.size, _ptr(crc), _ptr(ok),
+                                           _ptr(nbad), ctypes.byref(t))
+        self._check(rc, "submit_verify")
+        return {"ticket": t.value, "keep": (buf, d), "crc": crc, "ok": ok, "nbad": nbad}
+
+    def wait(self, h):
+        rc = lib().tfs_crc32_wait(self.handle, h["ticket"])
+        self._check(rc, "wait", ok=(TFS_SUCCESS, TFS_EXIT_CHECK_CRC_ERROR))
+        return h["crc"], h["ok"], int(h["nbad"][0]), rc
+
+    def datafile_get_crc(self, data):
+        b = bytes(data)
+        out = ctypes.c_uint32()
+        self._check(lib().tfs_datafile_get_crc(self.handle, b, len(b), ctypes.byref(out)), "datafile_get_crc")
+        return out.value
+
+    # ---- device-resident (pointers are device addresses, e.g. torch tensors) -
+    def batch_device(self, d_desc, n, d_base, d_out, stream=None):
+        self._check(lib().tfs_crc32_batch_device(self.handle, _ptr(d_desc), n, _ptr(d_base), _ptr(d_out), stream),
+                    "batch_device")
+
+    def verify_device(self, d_desc, n, d_base, d_crc=None, d_ok=None, d_nbad=None, stream=None):
+        self._check(lib().tfs_crc32_verify_device(self.handle, _ptr(d_desc), n, _ptr(d_base), _ptr(d_crc),
+                                                  _ptr(d_ok), _ptr(d_nbad), stream), "verify_device")
+
+    def synth_fill_device(self, d_dst, nbytes, seed, first_word=0, stream=None):
+        self._check(lib().tfs_crc32_synth_fill_device(self.handle, _ptr(d_dst), nbytes, seed, first_word, stream),
+                    "synth_fill_device")
+
+    def write_headers_device(self, d_image, d_rec_off, d_len, d_crc, first_id, n, stream=None):
+        self._check(lib().tfs_crc32_write_headers_device(self.handle, _ptr(d_image), _ptr(d_rec_off), _ptr(d_len),
+                                                         _ptr(d_crc), first_id, n, stream), "write_headers_device")
+
+    def membench_device(self, pattern, d_base, d_desc, n, nbytes, d_out, grid=0, stream=None):
+        self._check(lib().tfs_crc32_membench_device(self.handle, pattern, _ptr(d_base), _ptr(d_desc), n, nbytes,
+                                                    _ptr(d_out), grid, stream), "membench_device")
+
+    def block_verify_device(self, d_image, image_len, d_metas, n, d_crc=None, d_status=None, d_nbad=None,
+                            stream=None):
+        self._check(lib().tfs_block_verify_device(self.handle, _ptr(d_image), image_len, _ptr(d_metas), n,
+                                                  _ptr(d_crc), _ptr(d_status), _ptr(d_nbad), stream),
+                    "block_verify_device")
+
+    # ---- block images (host) -------------------------------------------------
+    def block_verify(self, image, metas):
+        img = _as_u8(image)
+        m = np.ascontiguousarray(metas, dtype=META_DTYPE)
+        n = len(m)
+        crc = np.zeros(n, np.uint32)
+        st = np.zeros(n, np.int32)
+        nbad = np.zeros(1, np.uint32)
+        rc = lib().tfs_block_verify(self.handle, _ptr(img), img.size, _ptr(m), n, _ptr(crc), _ptr(st), _ptr(nbad))
+        self._check(rc, "block_verify", ok=(TFS_SUCCESS, TFS_EXIT_CHECK_CRC_ERROR))
+        return crc, st, int(nbad[0]), rc
+
+    def block_compact(self, image, metas, flags):
+        img = _as_u8(image)
+        m = np.ascontiguousarray(metas, dtype=META_DTYPE)
+        fl = np.ascontiguousarray(flags, dtype=np.int32)
+        n = len(m)
+        cap = int(m["size"].astype(np.int64).sum()) + 16
+        dest = np.zeros(cap, np.uint8)
+        dmetas = np.zeros(n, META_DTYPE)
+        ok = np.zeros(n, np.uint8)
+        dlen = ctypes.c_uint64()
+        nlive = ctypes.c_uint32()
+        rc = lib().tfs_block_compact(self.handle, _ptr(img), img.size, _ptr(m), _ptr(fl), n, _ptr(dest), cap,
+                                     _ptr(dmetas), _ptr(ok), ctypes.byref(dlen), ctypes.byref(nlive))
+        self._check(rc, "block_compact", ok=(TFS_SUCCESS, TFS_EXIT_CHECK_CRC_ERROR))
+        return dest[:dlen.value], dmetas[:nlive.value], ok, rc
+
+
+def func_crc(crc, data, length=None):
+    """Drop-in for Func::crc(uint32_t crc, const char* data, const int32_t len) (GPU, default context)."""
+    b = bytes(data)
+    n = len(b) if length is None else int(length)
+    if n > len(b):
+        raise ValueError("length exceeds buffer")
+    err = ctypes.c_int(0)
+    v = lib().tfs_crc32_e(crc & 0xFFFFFFFF, b, n, ctypes.byref(err))
+    if err.value != TFS_SUCCESS:
+        raise TfsCrcError(err.value, "tfs_crc32: %s" % lib().tfs_crc32_last_error(None).decode())
+    return v

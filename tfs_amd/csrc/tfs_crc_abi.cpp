@@ -1,0 +1,614 @@
+// tfs_crc_abi.cpp -- host side of the C ABI declared in include/tfs_crc.h.
+//
+// Owns per-GPU contexts (stream, device-resident tables, device scratch and
+// pinned staging pools) and drives the gfx950 kernels in tfs_crc_kernels.hip.
+// There is deliberately no CPU CRC here: if a device call fails the error is
+// returned (TFS_CRC_EXIT_DEVICE_ERROR / TFS_CRC_EXIT_NO_DEVICE), never computed
+// on the host instead.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/tfs_crc.h"
+#include "crc_math.h"
+#include "tfs_crc_device.h"
+
+namespace tfscrc {
+hipError_t launch_crc_files(int mode, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
+                            uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, hipStream_t stream);
+hipError_t launch_block_verify(const uint8_t* image, uint64_t image_len, const RawMeta* metas, uint32_t n,
+                               const Tables* tg, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
+                               hipStream_t stream);
+hipError_t launch_compact_copy(const uint8_t* src, const RawMeta* metas, const int32_t* flags, const int64_t* dest_off,
+                               uint32_t n, uint8_t* dst, hipStream_t stream);
+hipError_t launch_synth_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, uint64_t first_word, hipStream_t stream);
+hipError_t launch_write_headers(uint8_t* image, const uint64_t* rec_off, const uint32_t* len, const uint32_t* crc,
+                                uint64_t first_id, uint32_t n, hipStream_t stream);
+hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, uint32_t n, uint64_t nbytes,
+                           uint32_t* out, unsigned grid, hipStream_t stream);
+}  // namespace tfscrc
+
+static_assert(sizeof(tfs_crc_desc) == 16 && sizeof(tfs_crc_vdesc) == 16, "descriptor ABI");
+static_assert(sizeof(tfs_raw_meta) == sizeof(tfscrc::RawMeta), "RawMeta ABI");
+static_assert(sizeof(tfs_file_info) == 36, "FileInfo ABI");
+
+namespace {
+
+using namespace tfscrc;
+
+// Growable device allocation.
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t reserve(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes, 4096);
+    want = (want + 0xFFFF) & ~size_t(0xFFFF);
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+// Growable pinned host allocation.
+struct PinBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t reserve(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes, 4096);
+    want = (want + 0xFFFF) & ~size_t(0xFFFF);
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+// One in-flight host-memory submission (async API) or the scratch of a sync call.
+struct Slot {
+  DevBuf d_data, d_desc, d_crc, d_ok, d_bad, d_aux;
+  PinBuf h_data, h_crc, h_ok, h_bad;
+  hipEvent_t done = nullptr;
+  bool busy = false;
+  uint64_t ticket = 0;
+  int status = TFS_SUCCESS;
+  // user outputs for the async path
+  uint32_t n = 0;
+  uint32_t* out_crc = nullptr;
+  uint8_t* out_ok = nullptr;
+  uint32_t* n_bad = nullptr;
+  void release() {
+    d_data.release(); d_desc.release(); d_crc.release(); d_ok.release(); d_bad.release(); d_aux.release();
+    h_data.release(); h_crc.release(); h_ok.release(); h_bad.release();
+    if (done) (void)hipEventDestroy(done);
+    done = nullptr;
+  }
+};
+
+constexpr int kSlots = 4;
+
+}  // namespace
+
+struct tfs_crc_ctx {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  Tables* d_tables = nullptr;
+  std::mutex mu;
+  std::string last_error = "no error";
+  Slot slots[kSlots];
+  uint64_t next_ticket = 1;
+};
+
+namespace {
+
+int set_err(tfs_crc_ctx* ctx, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (ctx) ctx->last_error = buf;
+  return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                                   \
+  do {                                                                                                       \
+    hipError_t e_ = (expr);                                                                                  \
+    if (e_ != hipSuccess)                                                                                    \
+      return set_err((ctx), TFS_CRC_EXIT_DEVICE_ERROR, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                     __FILE__, __LINE__);                                                                    \
+  } while (0)
+
+void build_tables(Tables* t) {
+  make_slice_tables(t->slice, 4);
+  for (int li = 0; li < kNumSegLog; ++li) {
+    const uint64_t L = uint64_t(kMinSeg) << li;
+    for (int j = 0; j < kLevels; ++j) make_shift_table(t->shift[li][j], L << j);
+    make_shift_table(t->shift[li][kStripeShift], 63 * L);
+  }
+}
+
+bool is_pinned_host(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+// Range of base actually touched by n descriptors (offset, len pairs).
+template <typename D>
+bool span_of(const D* d, uint32_t n, uint64_t base_len, uint64_t* lo, uint64_t* hi) {
+  uint64_t a = UINT64_MAX, b = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t e = d[i].offset + d[i].len;
+    if (e < d[i].offset || e > base_len) return false;
+    if (d[i].len == 0) continue;
+    a = std::min(a, d[i].offset);
+    b = std::max(b, e);
+  }
+  if (a == UINT64_MAX) a = b = 0;
+  *lo = a & ~uint64_t(255);  // keep the device copy 256-aligned modulo the host offset
+  *hi = b;
+  return true;
+}
+
+// Stage the touched span of a host buffer onto the device in slot s.  Returns
+// the device pointer that corresponds to host `base` (may point before the
+// allocation; only [lo, hi) is valid).
+int stage_span(tfs_crc_ctx* ctx, Slot& s, const void* base, uint64_t lo, uint64_t hi, const uint8_t** d_base) {
+  const uint64_t bytes = hi - lo;
+  HIP_TRY(ctx, s.d_data.reserve(bytes + 16));
+  const uint8_t* src = static_cast<const uint8_t*>(base) + lo;
+  if (bytes) {
+    if (is_pinned_host(base)) {
+      HIP_TRY(ctx, hipMemcpyAsync(s.d_data.p, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    } else {
+      HIP_TRY(ctx, s.h_data.reserve(bytes));
+      memcpy(s.h_data.p, src, bytes);
+      HIP_TRY(ctx, hipMemcpyAsync(s.d_data.p, s.h_data.p, bytes, hipMemcpyHostToDevice, ctx->stream));
+    }
+  }
+  *d_base = static_cast<const uint8_t*>(s.d_data.p) - lo;
+  return TFS_SUCCESS;
+}
+
+Slot* free_slot(tfs_crc_ctx* ctx) {
+  for (auto& s : ctx->slots)
+    if (!s.busy) return &s;
+  return nullptr;
+}
+
+// Enqueue a host-memory batch on slot s (mode 0 compute, 1 verify).  Outputs
+// land in the slot's pinned buffers when s.done fires.
+int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint32_t n, const void* base,
+                       uint64_t base_len) {
+  uint64_t lo = 0, hi = 0;
+  const Desc* dd = static_cast<const Desc*>(d);
+  if (!span_of(dd, n, base_len, &lo, &hi))
+    return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "descriptor range exceeds base_len %llu",
+                   (unsigned long long)base_len);
+  const uint8_t* d_base = nullptr;
+  int rc = stage_span(ctx, s, base, lo, hi, &d_base);
+  if (rc) return rc;
+  HIP_TRY(ctx, s.d_desc.reserve(size_t(n) * sizeof(Desc)));
+  HIP_TRY(ctx, s.d_crc.reserve(size_t(n) * 4));
+  HIP_TRY(ctx, s.d_ok.reserve(n));
+  HIP_TRY(ctx, s.d_bad.reserve(4));
+  HIP_TRY(ctx, s.h_crc.reserve(size_t(n) * 4));
+  HIP_TRY(ctx, s.h_ok.reserve(n));
+  HIP_TRY(ctx, s.h_bad.reserve(4));
+  // descriptors go through pinned memory too (h_ok doubles as nothing here; use d_aux staging)
+  HIP_TRY(ctx, s.d_aux.reserve(16));
+  HIP_TRY(ctx, hipMemcpyAsync(s.d_desc.p, d, size_t(n) * sizeof(Desc), hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(ctx, hipMemsetAsync(s.d_bad.p, 0, 4, ctx->stream));
+  HIP_TRY(ctx, launch_crc_files(mode, d_base, static_cast<const Desc*>(s.d_desc.p), n, ctx->d_tables,
+                                static_cast<uint32_t*>(s.d_crc.p), static_cast<uint8_t*>(s.d_ok.p),
+                                static_cast<uint32_t*>(s.d_bad.p), ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(s.h_crc.p, s.d_crc.p, size_t(n) * 4, hipMemcpyDeviceToHost, ctx->stream));
+  if (mode == 1) {
+    HIP_TRY(ctx, hipMemcpyAsync(s.h_ok.p, s.d_ok.p, n, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(s.h_bad.p, s.d_bad.p, 4, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  if (!s.done) HIP_TRY(ctx, hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+  HIP_TRY(ctx, hipEventRecord(s.done, ctx->stream));
+  return TFS_SUCCESS;
+}
+
+int finish_slot(tfs_crc_ctx* ctx, Slot& s, int mode, uint32_t n, uint32_t* out_crc, uint8_t* out_ok,
+                uint32_t* n_bad) {
+  HIP_TRY(ctx, hipEventSynchronize(s.done));
+  if (out_crc && n) memcpy(out_crc, s.h_crc.p, size_t(n) * 4);
+  if (mode == 1) {
+    if (out_ok && n) memcpy(out_ok, s.h_ok.p, n);
+    const uint32_t bad = n ? *static_cast<uint32_t*>(s.h_bad.p) : 0u;
+    if (n_bad) *n_bad = bad;
+    return bad ? TFS_EXIT_CHECK_CRC_ERROR : TFS_SUCCESS;
+  }
+  return TFS_SUCCESS;
+}
+
+std::once_flag g_default_once;
+tfs_crc_ctx* g_default = nullptr;
+int g_default_rc = TFS_CRC_EXIT_NO_DEVICE;
+std::string g_default_err = "default context not created";
+
+tfs_crc_ctx* default_ctx(int* rc) {
+  std::call_once(g_default_once, [] {
+    tfs_crc_ctx* c = nullptr;
+    g_default_rc = tfs_crc32_ctx_create(0, &c);
+    if (g_default_rc == TFS_SUCCESS) g_default = c;
+    else g_default_err = c ? c->last_error : "tfs_crc32_ctx_create(0) failed";
+  });
+  if (rc) *rc = g_default_rc;
+  return g_default;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tfs_crc32_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+int tfs_crc32_ctx_create(int device, tfs_crc_ctx** out) {
+  if (!out) return TFS_EXIT_PARAMETER_ERROR;
+  *out = nullptr;
+  int ndev = tfs_crc32_device_count();
+  if (ndev <= 0) return TFS_CRC_EXIT_NO_DEVICE;
+  if (device < 0 || device >= ndev) return TFS_EXIT_PARAMETER_ERROR;
+  auto* ctx = new tfs_crc_ctx();
+  ctx->device = device;
+  int rc = TFS_SUCCESS;
+  do {
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) { rc = set_err(ctx, TFS_CRC_EXIT_NO_DEVICE, "hipSetDevice(%d): %s", device, hipGetErrorString(e)); break; }
+    hipDeviceProp_t prop;
+    e = hipGetDeviceProperties(&prop, device);
+    if (e != hipSuccess) { rc = set_err(ctx, TFS_CRC_EXIT_NO_DEVICE, "hipGetDeviceProperties: %s", hipGetErrorString(e)); break; }
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+      rc = set_err(ctx, TFS_CRC_EXIT_NO_DEVICE, "device %d is %s; kernels are built for gfx950 only", device, prop.gcnArchName);
+      break;
+    }
+    e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) { rc = set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "hipStreamCreate: %s", hipGetErrorString(e)); break; }
+    std::vector<Tables> host(1);
+    build_tables(host.data());
+    e = hipMalloc(reinterpret_cast<void**>(&ctx->d_tables), sizeof(Tables));
+    if (e != hipSuccess) { rc = set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "hipMalloc(tables): %s", hipGetErrorString(e)); break; }
+    e = hipMemcpy(ctx->d_tables, host.data(), sizeof(Tables), hipMemcpyHostToDevice);
+    if (e != hipSuccess) { rc = set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "hipMemcpy(tables): %s", hipGetErrorString(e)); break; }
+  } while (0);
+  *out = ctx;  // returned even on failure so the caller can read last_error; destroy it
+  return rc;
+}
+
+int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx) {
+  if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
+  if (ctx->device >= 0) (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  for (auto& s : ctx->slots) s.release();
+  if (ctx->d_tables) (void)hipFree(ctx->d_tables);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return TFS_SUCCESS;
+}
+
+const char* tfs_crc32_last_error(const tfs_crc_ctx* ctx) {
+  if (!ctx) {
+    if (g_default) return g_default->last_error.c_str();
+    return g_default_err.c_str();
+  }
+  return ctx->last_error.c_str();
+}
+
+int tfs_crc32_batch(tfs_crc_ctx* ctx, const tfs_crc_desc* d, uint32_t n, const void* base, uint64_t base_len,
+                    uint32_t* out_crc) {
+  if (!ctx || (n && (!d || !out_crc || !base))) return TFS_EXIT_PARAMETER_ERROR;
+  if (n == 0) return TFS_SUCCESS;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  Slot* s = free_slot(ctx);
+  if (!s) return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "all %d slots busy with async submissions", kSlots);
+  int rc = enqueue_host_batch(ctx, *s, 0, d, n, base, base_len);
+  if (rc) return rc;
+  return finish_slot(ctx, *s, 0, n, out_crc, nullptr, nullptr);
+}
+
+int tfs_crc32_verify(tfs_crc_ctx* ctx, const tfs_crc_vdesc* d, uint32_t n, const void* base, uint64_t base_len,
+                     uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad) {
+  if (!ctx || (n && (!d || !base))) return TFS_EXIT_PARAMETER_ERROR;
+  if (n == 0) {
+    if (n_bad) *n_bad = 0;
+    return TFS_SUCCESS;
+  }
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  Slot* s = free_slot(ctx);
+  if (!s) return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "all %d slots busy with async submissions", kSlots);
+  int rc = enqueue_host_batch(ctx, *s, 1, d, n, base, base_len);
+  if (rc) return rc;
+  return finish_slot(ctx, *s, 1, n, out_crc, out_ok, n_bad);
+}
+
+int tfs_crc32_submit_verify(tfs_crc_ctx* ctx, const tfs_crc_vdesc* d, uint32_t n, const void* base,
+                            uint64_t base_len, uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad,
+                            tfs_crc_ticket* ticket) {
+  if (!ctx || !ticket || (n && (!d || !base))) return TFS_EXIT_PARAMETER_ERROR;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  Slot* s = free_slot(ctx);
+  if (!s) return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "all %d slots busy; wait on a ticket first", kSlots);
+  if (n) {
+    int rc = enqueue_host_batch(ctx, *s, 1, d, n, base, base_len);
+    if (rc) return rc;
+  } else {
+    if (!s->done) HIP_TRY(ctx, hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
+    HIP_TRY(ctx, hipEventRecord(s->done, ctx->stream));
+  }
+  s->busy = true;
+  s->ticket = ctx->next_ticket++;
+  s->n = n;
+  s->out_crc = out_crc;
+  s->out_ok = out_ok;
+  s->n_bad = n_bad;
+  ticket->id = s->ticket;
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_wait(tfs_crc_ctx* ctx, tfs_crc_ticket ticket) {
+  if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  for (auto& s : ctx->slots) {
+    if (s.busy && s.ticket == ticket.id) {
+      HIP_TRY(ctx, hipSetDevice(ctx->device));
+      int rc = finish_slot(ctx, s, 1, s.n, s.out_crc, s.out_ok, s.n_bad);
+      s.busy = false;
+      return rc;
+    }
+  }
+  return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "unknown ticket %llu", (unsigned long long)ticket.id);
+}
+
+int tfs_crc32_batch_device(tfs_crc_ctx* ctx, const tfs_crc_desc* d_desc, uint32_t n, const void* d_base,
+                           uint32_t* d_out_crc, void* stream) {
+  if (!ctx || (n && (!d_desc || !d_base || !d_out_crc))) return TFS_EXIT_PARAMETER_ERROR;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  HIP_TRY(ctx, launch_crc_files(0, static_cast<const uint8_t*>(d_base), reinterpret_cast<const Desc*>(d_desc), n,
+                                ctx->d_tables, d_out_crc, nullptr, nullptr, st));
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_verify_device(tfs_crc_ctx* ctx, const tfs_crc_vdesc* d_desc, uint32_t n, const void* d_base,
+                            uint32_t* d_out_crc, uint8_t* d_out_ok, uint32_t* d_n_bad, void* stream) {
+  if (!ctx || (n && (!d_desc || !d_base))) return TFS_EXIT_PARAMETER_ERROR;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  HIP_TRY(ctx, launch_crc_files(1, static_cast<const uint8_t*>(d_base), reinterpret_cast<const Desc*>(d_desc), n,
+                                ctx->d_tables, d_out_crc, d_out_ok, d_n_bad, st));
+  return TFS_SUCCESS;
+}
+
+uint32_t tfs_crc32_e(uint32_t crc, const char* data, int32_t len, int* err) {
+  if (err) *err = TFS_SUCCESS;
+  if (len <= 0) return crc;  // func.cpp:429: the loop does not run
+  if (!data) {
+    if (err) *err = TFS_EXIT_PARAMETER_ERROR;
+    return crc;
+  }
+  int rc = 0;
+  tfs_crc_ctx* ctx = default_ctx(&rc);
+  if (!ctx) {
+    if (err) *err = rc;
+    return crc;
+  }
+  tfs_crc_desc d{0, uint32_t(len), crc};
+  uint32_t out = crc;
+  rc = tfs_crc32_batch(ctx, &d, 1, data, uint64_t(len), &out);
+  if (rc) {
+    if (err) *err = rc;
+    return crc;
+  }
+  return out;
+}
+
+uint32_t tfs_crc32(uint32_t crc, const char* data, int32_t len) { return tfs_crc32_e(crc, data, len, nullptr); }
+
+int tfs_datafile_get_crc(tfs_crc_ctx* ctx, const char* data, int32_t length, uint32_t* out_crc) {
+  if (!out_crc) return TFS_EXIT_PARAMETER_ERROR;
+  if (length <= 0) {
+    *out_crc = 0;
+    return TFS_SUCCESS;
+  }
+  if (!ctx) {
+    int rc = 0;
+    ctx = default_ctx(&rc);
+    if (!ctx) return rc;
+  }
+  tfs_crc_desc d{0, uint32_t(length), 0u};
+  return tfs_crc32_batch(ctx, &d, 1, data, uint64_t(length), out_crc);
+}
+
+int tfs_block_verify_device(tfs_crc_ctx* ctx, const void* d_image, uint64_t image_len, const tfs_raw_meta* d_metas,
+                            uint32_t n, uint32_t* d_out_crc, int32_t* d_out_status, uint32_t* d_n_bad, void* stream) {
+  if (!ctx || (n && (!d_image || !d_metas))) return TFS_EXIT_PARAMETER_ERROR;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  HIP_TRY(ctx, launch_block_verify(static_cast<const uint8_t*>(d_image), image_len,
+                                   reinterpret_cast<const RawMeta*>(d_metas), n, ctx->d_tables, d_out_crc,
+                                   d_out_status, d_n_bad, st));
+  return TFS_SUCCESS;
+}
+
+int tfs_block_verify(tfs_crc_ctx* ctx, const void* image, uint64_t image_len, const tfs_raw_meta* metas, uint32_t n,
+                     uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad) {
+  if (!ctx || (n && (!image || !metas))) return TFS_EXIT_PARAMETER_ERROR;
+  if (n == 0) {
+    if (n_bad) *n_bad = 0;
+    return TFS_SUCCESS;
+  }
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  Slot* s = free_slot(ctx);
+  if (!s) return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "all %d slots busy", kSlots);
+  const uint8_t* d_base = nullptr;
+  int rc = stage_span(ctx, *s, image, 0, image_len, &d_base);
+  if (rc) return rc;
+  HIP_TRY(ctx, s->d_desc.reserve(size_t(n) * sizeof(RawMeta)));
+  HIP_TRY(ctx, s->d_crc.reserve(size_t(n) * 4));
+  HIP_TRY(ctx, s->d_ok.reserve(size_t(n) * 4));
+  HIP_TRY(ctx, s->d_bad.reserve(4));
+  HIP_TRY(ctx, s->h_crc.reserve(size_t(n) * 4));
+  HIP_TRY(ctx, s->h_ok.reserve(size_t(n) * 4));
+  HIP_TRY(ctx, s->h_bad.reserve(4));
+  HIP_TRY(ctx, hipMemcpyAsync(s->d_desc.p, metas, size_t(n) * sizeof(RawMeta), hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(ctx, hipMemsetAsync(s->d_bad.p, 0, 4, ctx->stream));
+  HIP_TRY(ctx, launch_block_verify(d_base, image_len, static_cast<const RawMeta*>(s->d_desc.p), n, ctx->d_tables,
+                                   static_cast<uint32_t*>(s->d_crc.p), static_cast<int32_t*>(s->d_ok.p),
+                                   static_cast<uint32_t*>(s->d_bad.p), ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(s->h_crc.p, s->d_crc.p, size_t(n) * 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(s->h_ok.p, s->d_ok.p, size_t(n) * 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(s->h_bad.p, s->d_bad.p, 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  if (out_crc) memcpy(out_crc, s->h_crc.p, size_t(n) * 4);
+  if (out_status) memcpy(out_status, s->h_ok.p, size_t(n) * 4);
+  const uint32_t bad = *static_cast<uint32_t*>(s->h_bad.p);
+  if (n_bad) *n_bad = bad;
+  return bad ? TFS_EXIT_CHECK_CRC_ERROR : TFS_SUCCESS;
+}
+
+int tfs_block_compact(tfs_crc_ctx* ctx, const void* src_image, uint64_t src_len, const tfs_raw_meta* metas,
+                      const int32_t* flags, uint32_t n, void* dest_image, uint64_t dest_cap, tfs_raw_meta* dest_metas,
+                      uint8_t* crc_ok, uint64_t* dest_len, uint32_t* n_live) {
+  if (!ctx || (n && (!src_image || !metas || !flags || !dest_image))) return TFS_EXIT_PARAMETER_ERROR;
+  // Host: new offsets in iteration order (task.cpp:753-768).
+  std::vector<int64_t> doff(n, -1);
+  std::vector<tfs_raw_meta> live;
+  live.reserve(n);
+  int64_t w = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (metas[i].size <= TFS_FILEINFO_SIZE || metas[i].offset < 0 ||
+        uint64_t(metas[i].offset) + uint64_t(metas[i].size) > src_len)
+      return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "meta %u out of range", i);
+    if (flags[i] & (TFS_FI_DELETED | TFS_FI_INVALID)) continue;
+    doff[i] = w;
+    live.push_back(tfs_raw_meta{metas[i].file_id, int32_t(w), metas[i].size});
+    w += metas[i].size;
+  }
+  if (uint64_t(w) > dest_cap) return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "dest_cap %llu < %lld", (unsigned long long)dest_cap, (long long)w);
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  Slot* s = free_slot(ctx);
+  if (!s) return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "all %d slots busy", kSlots);
+  const uint8_t* d_src = nullptr;
+  int rc = stage_span(ctx, *s, src_image, 0, src_len, &d_src);
+  if (rc) return rc;
+  // aux: metas | flags | doff | crc | status ; dest in d_crc (reuse name loosely: separate buffers)
+  const size_t mb = size_t(n) * sizeof(RawMeta), fb = size_t(n) * 4, ob = size_t(n) * 8;
+  HIP_TRY(ctx, s->d_desc.reserve(mb + fb + ob + 2 * fb + 16));
+  uint8_t* aux = static_cast<uint8_t*>(s->d_desc.p);
+  RawMeta* d_metas = reinterpret_cast<RawMeta*>(aux);
+  int32_t* d_flags = reinterpret_cast<int32_t*>(aux + mb);
+  int64_t* d_doff = reinterpret_cast<int64_t*>(aux + ((mb + fb + 7) & ~size_t(7)));
+  uint32_t* d_crc = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(d_doff) + ob);
+  int32_t* d_status = reinterpret_cast<int32_t*>(d_crc + n);
+  HIP_TRY(ctx, s->d_aux.reserve(std::max<uint64_t>(uint64_t(w), 16)));
+  HIP_TRY(ctx, s->d_bad.reserve(4));
+  HIP_TRY(ctx, hipMemcpyAsync(d_metas, metas, mb, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(d_flags, flags, fb, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(d_doff, doff.data(), ob, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(ctx, hipMemsetAsync(s->d_bad.p, 0, 4, ctx->stream));
+  // Verify every file (skipped ones included; their verdict is overwritten below).
+  HIP_TRY(ctx, launch_block_verify(d_src, src_len, d_metas, n, ctx->d_tables, d_crc, d_status,
+                                   static_cast<uint32_t*>(s->d_bad.p), ctx->stream));
+  HIP_TRY(ctx, launch_compact_copy(d_src, d_metas, d_flags, d_doff, n, static_cast<uint8_t*>(s->d_aux.p), ctx->stream));
+  HIP_TRY(ctx, s->h_ok.reserve(size_t(n) * 4));
+  HIP_TRY(ctx, hipMemcpyAsync(s->h_ok.p, d_status, size_t(n) * 4, hipMemcpyDeviceToHost, ctx->stream));
+  if (w) HIP_TRY(ctx, hipMemcpyAsync(dest_image, s->d_aux.p, size_t(w), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  const int32_t* st = static_cast<const int32_t*>(s->h_ok.p);
+  uint32_t bad = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    uint8_t v;
+    if (doff[i] < 0) v = 2;
+    else v = st[i] == TFS_SUCCESS ? 1 : 0;
+    if (v == 0) ++bad;
+    if (crc_ok) crc_ok[i] = v;
+  }
+  if (dest_metas && !live.empty()) memcpy(dest_metas, live.data(), live.size() * sizeof(tfs_raw_meta));
+  if (dest_len) *dest_len = uint64_t(w);
+  if (n_live) *n_live = uint32_t(live.size());
+  return bad ? TFS_EXIT_CHECK_CRC_ERROR : TFS_SUCCESS;
+}
+
+// ---- test / bench helpers (not part of the dataserver boundary) ----------
+
+int tfs_crc32_synth_fill_device(tfs_crc_ctx* ctx, void* d_dst, uint64_t nbytes, uint64_t seed, uint64_t first_word,
+                                void* stream) {
+  if (!ctx || !d_dst || (nbytes & 7)) return TFS_EXIT_PARAMETER_ERROR;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  HIP_TRY(ctx, launch_synth_fill(static_cast<uint64_t*>(d_dst), nbytes / 8, seed, first_word, st));
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_write_headers_device(tfs_crc_ctx* ctx, void* d_image, const uint64_t* d_rec_off, const uint32_t* d_len,
+                                   const uint32_t* d_crc, uint64_t first_id, uint32_t n, void* stream) {
+  if (!ctx || !d_image) return TFS_EXIT_PARAMETER_ERROR;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  HIP_TRY(ctx, launch_write_headers(static_cast<uint8_t*>(d_image), d_rec_off, d_len, d_crc, first_id, n, st));
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_membench_device(tfs_crc_ctx* ctx, int pattern, const void* d_base, const tfs_crc_desc* d_desc,
+                              uint32_t n, uint64_t nbytes, uint32_t* d_out, unsigned grid, void* stream) {
+  if (!ctx || !d_base || !d_out) return TFS_EXIT_PARAMETER_ERROR;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  HIP_TRY(ctx, launch_membench(pattern, static_cast<const uint8_t*>(d_base), reinterpret_cast<const Desc*>(d_desc), n,
+                               nbytes, d_out, grid, st));
+  return TFS_SUCCESS;
+}
+
+void* tfs_crc32_stream(tfs_crc_ctx* ctx) { return ctx ? static_cast<void*>(ctx->stream) : nullptr; }
+
+int tfs_crc32_sync(tfs_crc_ctx* ctx) {
+  if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return TFS_SUCCESS;
+}
+
+}  // extern "C"
