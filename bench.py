@@ -118,23 +118,19 @@ def cpu_baseline(sample_u8, offs, lens, expected, seconds):
 
 def main():
     args = parse()
-    import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
+        # Rendezvous/barrier/max-of-times only: the data path has no collective,
+        # so a CPU (gloo) group is enough and keeps torch's own HIP runtime out
+        # of this process (the product library brings /opt/rocm's).
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        dist.init_process_group(backend="gloo")
     import tfs_amd.crc as crc
     from tfs_amd.synth import synth_bytes
     ctx = crc.Context(local)
-    stream = torch.cuda.current_stream(dev)
-    sp = stream.cuda_stream
 
     nblocks = args.blocks
     nfiles = nblocks * FILES_PER_BLOCK
@@ -142,26 +138,27 @@ def main():
     block_bytes = FILES_PER_BLOCK * rec
     total = nblocks * block_bytes
     total_al = (total + 4095) // 4096 * 4096
-    # Blocks owned by this rank: global block ids rank, rank+world, ... (partition by block id).
-    img = torch.empty(total_al, dtype=torch.uint8, device=dev)
-    ctx.synth_fill_device(img, total_al, 0x9E3779B97F4A7C15 + rank, 0, stream=sp)
+    data_seed = (0x9E3779B97F4A7C15 + rank) & 0xFFFFFFFFFFFFFFFF
+    # This rank's blocks (global block ids rank, rank+world, ...: partition by block id).
+    img = crc.DeviceBuffer(ctx, total_al)
+    ctx.synth_fill_device(img, total_al, data_seed, 0)
     rec_off = np.arange(nfiles, dtype=np.uint64) * rec
     desc = np.zeros(nfiles, crc.DESC_DTYPE)
     desc["offset"] = rec_off + FILEINFO
     desc["len"] = FILE_SIZE
-    d_desc = torch.from_numpy(desc.view(np.uint8)).to(dev)
-    d_crc = torch.zeros(nfiles, dtype=torch.int32, device=dev)
+    d_desc = crc.DeviceBuffer(ctx, desc.nbytes).upload(desc)
+    d_crc = crc.DeviceBuffer(ctx, 4 * nfiles)
     # write path: checksum-on-write of every payload, then persist FileInfo{crc_} headers
-    ctx.batch_device(d_desc, nfiles, img, d_crc, stream=sp)
-    d_off = torch.from_numpy(rec_off.view(np.int64)).to(dev)
-    d_len = torch.full((nfiles,), FILE_SIZE, dtype=torch.int32, device=dev)
-    ctx.write_headers_device(img, d_off, d_len, d_crc, 1 + rank * nfiles, nfiles, stream=sp)
-    torch.cuda.synchronize(dev)
-    expected = d_crc.cpu().numpy().view(np.uint32).copy()
+    ctx.batch_device(d_desc, nfiles, img, d_crc)
+    d_off = crc.DeviceBuffer(ctx, 8 * nfiles).upload(rec_off)
+    d_len = crc.DeviceBuffer(ctx, 4 * nfiles).upload(np.full(nfiles, FILE_SIZE, np.uint32))
+    ctx.write_headers_device(img, d_off, d_len, d_crc, 1 + rank * nfiles, nfiles)
+    ctx.sync()
+    expected = d_crc.download(np.uint32)
     desc["aux"] = expected
-    d_vdesc = torch.from_numpy(desc.view(np.uint8)).to(dev)
-    d_ok = torch.zeros(nfiles, dtype=torch.uint8, device=dev)
-    d_bad = torch.zeros(1, dtype=torch.int32, device=dev)
+    d_vdesc = crc.DeviceBuffer(ctx, desc.nbytes).upload(desc)
+    d_ok = crc.DeviceBuffer(ctx, nfiles)
+    d_bad = crc.DeviceBuffer(ctx, 4)
 
     # parity spot check of the resident bytes against the oracle (test infrastructure)
     sample_idx = np.linspace(0, nfiles - 1, 48).astype(np.int64)
@@ -170,38 +167,39 @@ def main():
     ora.oracle_crc.argtypes = [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_int32]
     for i in sample_idx:
         o = int(desc["offset"][i])
-        host = img[o:o + FILE_SIZE].cpu().numpy().tobytes()
-        assert host == synth_bytes(0x9E3779B97F4A7C15 + rank, FILE_SIZE, o).tobytes()
+        host = img.download(np.uint8, FILE_SIZE, o).tobytes()
+        assert host == synth_bytes(data_seed, FILE_SIZE, o).tobytes()
         if ora.oracle_crc(0, host, FILE_SIZE) != int(expected[i]):
             raise SystemExit("GPU CRC disagrees with oracle at file %d" % i)
 
     def step():
-        ctx.verify_device(d_vdesc, nfiles, img, None, d_ok, d_bad, stream=sp)
+        ctx.verify_device(d_vdesc, nfiles, img, None, d_ok, d_bad)
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
-    d_bad.zero_()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    ctx.sync()
+    d_bad.zero()
+    ev = [(crc.Event(ctx), crc.Event(ctx)) for _ in range(args.steps)]
     if dist:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    ctx.sync()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        ev[k][0].record(stream)
+        ev[k][0].record()
         step()
-        ev[k][1].record(stream)
-    torch.cuda.synchronize(dev)
+        ev[k][1].record()
+    ctx.sync()
     if dist:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
-    nbad = int(d_bad.item())
+    kern_ms = [a.elapsed_ms(b) for a, b in ev]
+    nbad = int(d_bad.download(np.uint32)[0])
     if nbad:
         raise SystemExit("verify reported %d mismatches on clean data" % nbad)
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     payload_bytes = float(world) * args.steps * nfiles * FILE_SIZE
@@ -211,16 +209,15 @@ def main():
 
     extra = {}
     if args.membench:
-        out = torch.zeros(4, dtype=torch.int32, device=dev)
+        out = crc.DeviceBuffer(ctx, 16)
         for pat in (0, 1):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            ctx.membench_device(pat, img, d_vdesc, nfiles, total, out, stream=sp)
-            e0.record(stream)
+            e0, e1 = crc.Event(ctx), crc.Event(ctx)
+            ctx.membench_device(pat, img, d_vdesc, nfiles, total, out)
+            e0.record()
             for _ in range(5):
-                ctx.membench_device(pat, img, d_vdesc, nfiles, total, out, stream=sp)
-            e1.record(stream)
-            torch.cuda.synchronize(dev)
-            ms = e0.elapsed_time(e1) / 5
+                ctx.membench_device(pat, img, d_vdesc, nfiles, total, out)
+            e1.record()
+            ms = e0.elapsed_ms(e1) / 5
             nb = total if pat == 0 else nfiles * FILE_SIZE
             extra["membench_pattern%d_GBs" % pat] = nb / (ms / 1e3) / 1e9
         print(json.dumps({"membench": extra}), file=sys.stderr)
@@ -262,38 +259,42 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         ns = min(2048, nfiles)
         idx = np.linspace(0, nfiles - 1, ns).astype(np.int64)
-        # copy the sampled records (identical bytes) to host
+        # copy the sampled payloads (identical bytes) to host
         sample = np.zeros(ns * FILE_SIZE, np.uint8)
         for j, i in enumerate(idx):
             o = int(desc["offset"][i])
-            sample[j * FILE_SIZE:(j + 1) * FILE_SIZE] = img[o:o + FILE_SIZE].cpu().numpy()
+            sample[j * FILE_SIZE:(j + 1) * FILE_SIZE] = img.download(np.uint8, FILE_SIZE, o)
         result["cpu_baseline"] = cpu_baseline(sample, np.arange(ns) * FILE_SIZE, np.full(ns, FILE_SIZE),
                                               expected[idx], args.cpu_seconds)
     if args.e2e:
-        print(json.dumps({"e2e": e2e_rate(ctx, torch, dev)}), file=sys.stderr)
+        print(json.dumps({"e2e": e2e_rate(ctx)}), file=sys.stderr)
     if rank == 0:
         print(json.dumps(result), flush=True)
+    del ev
+    for b in (img, d_desc, d_crc, d_off, d_len, d_vdesc, d_ok, d_bad):
+        b.free()
     ctx.close()
     if dist:
         dist.destroy_process_group()
 
 
-def e2e_rate(ctx, torch, dev):
-    """Host block image -> pinned -> GPU verify -> verdicts back: the PCIe-inclusive rate."""
+def e2e_rate(ctx):
+    """Host block image (pinned) -> GPU verify -> verdicts back: the PCIe-inclusive rate."""
     import tfs_amd.crc as crc
+    from tfs_amd.synth import synth_bytes
     nfiles = 4096
     rec = FILEINFO + FILE_SIZE
-    host = torch.empty(nfiles * rec, dtype=torch.uint8).pin_memory()
-    from tfs_amd.synth import synth_bytes
-    host.numpy()[:] = synth_bytes(5, nfiles * rec)
+    host = crc.PinnedBuffer(ctx, nfiles * rec)
+    host.array[:] = synth_bytes(5, nfiles * rec)
     offs = np.arange(nfiles) * rec + FILEINFO
-    exp = ctx.batch(host.numpy(), offs, [FILE_SIZE] * nfiles)
-    t0 = time.perf_counter()
+    exp = ctx.batch(host.array, offs, [FILE_SIZE] * nfiles)
     reps = 4
+    t0 = time.perf_counter()
     for _ in range(reps):
-        c, ok, nbad, rc = ctx.verify(host.numpy(), offs, [FILE_SIZE] * nfiles, exp)
+        c, ok, nbad, rc = ctx.verify(host.array, offs, [FILE_SIZE] * nfiles, exp)
         assert nbad == 0
     dt = time.perf_counter() - t0
+    host.free()
     return {"GiBps_incl_pinned_h2d": reps * nfiles * FILE_SIZE / dt / 2**30, "files": nfiles}
 
 

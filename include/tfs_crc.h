@@ -212,6 +212,20 @@ int tfs_crc32_write_headers_device(tfs_crc_ctx* ctx, void* d_image, const uint64
  * per-file lane-segment access pattern over d_desc (len multiple of 1 KiB). */
 int tfs_crc32_membench_device(tfs_crc_ctx* ctx, int pattern, const void* d_base, const tfs_crc_desc* d_desc,
                               uint32_t n, uint64_t nbytes, uint32_t* d_out, unsigned grid, void* stream);
+/* Device / pinned memory and event plumbing for callers that hold no HIP
+ * runtime of their own (tests, bench, a dataserver without HIP code).
+ * tfs_crc32_memcpy: hipMemcpyDefault direction; stream NULL = ctx stream and
+ * synchronous, otherwise asynchronous on `stream`. */
+int tfs_crc32_dev_malloc(tfs_crc_ctx* ctx, uint64_t bytes, void** d_ptr);
+int tfs_crc32_dev_free(tfs_crc_ctx* ctx, void* d_ptr);
+int tfs_crc32_host_malloc_pinned(tfs_crc_ctx* ctx, uint64_t bytes, void** h_ptr);
+int tfs_crc32_host_free_pinned(tfs_crc_ctx* ctx, void* h_ptr);
+int tfs_crc32_memcpy(tfs_crc_ctx* ctx, void* dst, const void* src, uint64_t bytes, void* stream);
+int tfs_crc32_memset_device(tfs_crc_ctx* ctx, void* d_ptr, int value, uint64_t bytes, void* stream);
+int tfs_crc32_event_create(tfs_crc_ctx* ctx, void** ev);
+int tfs_crc32_event_record(tfs_crc_ctx* ctx, void* ev, void* stream);
+int tfs_crc32_event_elapsed_ms(tfs_crc_ctx* ctx, void* ev_start, void* ev_end, float* ms);
+int tfs_crc32_event_destroy(tfs_crc_ctx* ctx, void* ev);
 /* The ctx's HIP stream (as void*) and a synchronize on it. */
 void* tfs_crc32_stream(tfs_crc_ctx* ctx);
 int tfs_crc32_sync(tfs_crc_ctx* ctx);

@@ -118,26 +118,23 @@ def test_async_submit_wait(gpu_ctx, oracle):
         assert nbad == (1 if k == 1 else 0)
 
 
-def test_device_resident_torch(gpu_ctx, oracle):
-    import torch
+def test_device_resident(gpu_ctx, oracle):
     import tfs_amd.crc as crc
     n, ln = 512, 65536
     stride = ln + 36
     nbytes = (n * stride + 4095) // 4096 * 4096
-    dev = torch.device("cuda:0")
-    img = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream().cuda_stream
-    gpu_ctx.synth_fill_device(img, nbytes, 1234, 0, stream=stream)
+    img = crc.DeviceBuffer(gpu_ctx, nbytes)
+    gpu_ctx.synth_fill_device(img, nbytes, 1234, 0)
     d = np.zeros(n, crc.DESC_DTYPE)
     d["offset"] = 36 + np.arange(n) * stride
     d["len"] = ln
-    dd = torch.from_numpy(d.view(np.uint8)).to(dev)
-    out = torch.zeros(n, dtype=torch.int32, device=dev)
-    gpu_ctx.batch_device(dd, n, img, out, stream=stream)
-    torch.cuda.synchronize()
+    dd = crc.DeviceBuffer(gpu_ctx, d.nbytes).upload(d)
+    out = crc.DeviceBuffer(gpu_ctx, 4 * n)
+    gpu_ctx.batch_device(dd, n, img, out)
+    gpu_ctx.sync()
     host = synth_bytes(1234, nbytes)
-    assert (img.cpu().numpy() == host).all()
-    got = out.cpu().numpy().view(np.uint32)
+    assert (img.download() == host).all()
+    got = out.download(np.uint32)
     for i in range(0, n, 37):
         o = int(d["offset"][i])
         assert int(got[i]) == ocrc(oracle, 0, host[o:o + ln].tobytes())
@@ -145,13 +142,14 @@ def test_device_resident_torch(gpu_ctx, oracle):
     v = d.copy()
     v["aux"] = got
     v["aux"][[3, 300]] ^= 1
-    vd = torch.from_numpy(v.view(np.uint8)).to(dev)
-    okd = torch.zeros(n, dtype=torch.uint8, device=dev)
-    nb = torch.zeros(1, dtype=torch.int32, device=dev)
-    gpu_ctx.verify_device(vd, n, img, None, okd, nb, stream=stream)
-    torch.cuda.synchronize()
-    assert int(nb.item()) == 2
-    assert sorted(np.nonzero(okd.cpu().numpy() == 0)[0].tolist()) == [3, 300]
+    vd = crc.DeviceBuffer(gpu_ctx, v.nbytes).upload(v)
+    okd = crc.DeviceBuffer(gpu_ctx, n)
+    nb = crc.DeviceBuffer(gpu_ctx, 4)
+    nb.zero()
+    gpu_ctx.verify_device(vd, n, img, None, okd, nb)
+    gpu_ctx.sync()
+    assert int(nb.download(np.uint32)[0]) == 2
+    assert sorted(np.nonzero(okd.download() == 0)[0].tolist()) == [3, 300]
 
 
 def _block_image(oracle, sizes, seed=21):

@@ -46,6 +46,9 @@ EXPORTED = [
     "tfs_crc32_batch_device", "tfs_crc32_verify_device", "tfs_crc32_submit_verify", "tfs_crc32_wait",
     "tfs_block_verify", "tfs_block_verify_device", "tfs_block_compact",
     "tfs_crc32_synth_fill_device", "tfs_crc32_write_headers_device", "tfs_crc32_membench_device",
+    "tfs_crc32_dev_malloc", "tfs_crc32_dev_free", "tfs_crc32_host_malloc_pinned", "tfs_crc32_host_free_pinned",
+    "tfs_crc32_memcpy", "tfs_crc32_memset_device", "tfs_crc32_event_create", "tfs_crc32_event_record",
+    "tfs_crc32_event_elapsed_ms", "tfs_crc32_event_destroy",
     "tfs_crc32_stream", "tfs_crc32_sync",
 ]
 
@@ -87,6 +90,16 @@ def lib():
             "tfs_crc32_synth_fill_device": (ctypes.c_int, [vp, vp, u64, u64, u64, vp]),
             "tfs_crc32_write_headers_device": (ctypes.c_int, [vp, vp, vp, vp, vp, u64, u32, vp]),
             "tfs_crc32_membench_device": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, u32, u64, vp, ctypes.c_uint, vp]),
+            "tfs_crc32_dev_malloc": (ctypes.c_int, [vp, u64, ctypes.POINTER(vp)]),
+            "tfs_crc32_dev_free": (ctypes.c_int, [vp, vp]),
+            "tfs_crc32_host_malloc_pinned": (ctypes.c_int, [vp, u64, ctypes.POINTER(vp)]),
+            "tfs_crc32_host_free_pinned": (ctypes.c_int, [vp, vp]),
+            "tfs_crc32_memcpy": (ctypes.c_int, [vp, vp, vp, u64, vp]),
+            "tfs_crc32_memset_device": (ctypes.c_int, [vp, vp, ctypes.c_int, u64, vp]),
+            "tfs_crc32_event_create": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
+            "tfs_crc32_event_record": (ctypes.c_int, [vp, vp, vp]),
+            "tfs_crc32_event_elapsed_ms": (ctypes.c_int, [vp, vp, vp, ctypes.POINTER(ctypes.c_float)]),
+            "tfs_crc32_event_destroy": (ctypes.c_int, [vp, vp]),
             "tfs_crc32_stream": (vp, [vp]),
             "tfs_crc32_sync": (ctypes.c_int, [vp]),
         }
@@ -109,8 +122,8 @@ def _ptr(a):
         return a.ctypes.data
     if isinstance(a, int):
         return a
-    if hasattr(a, "data_ptr"):  # torch tensor (device memory plumbing only)
-        return a.data_ptr()
+    if isinstance(a, (DeviceBuffer, PinnedBuffer)):
+        return a.ptr
     if isinstance(a, (bytes, bytearray, memoryview)):
         return ctypes.cast(ctypes.c_char_p(bytes(a)), ctypes.c_void_p).value
     raise TypeError("unsupported buffer %r" % type(a))
@@ -221,7 +234,7 @@ class Context:
         self._check(lib().tfs_datafile_get_crc(self.handle, b, len(b), ctypes.byref(out)), "datafile_get_crc")
         return out.value
 
-    # ---- device-resident (pointers are device addresses, e.g. torch tensors) -
+    # ---- device-resident (pointers are device addresses: DeviceBuffer or int) ---
     def batch_device(self, d_desc, n, d_base, d_out, stream=None):
         self._check(lib().tfs_crc32_batch_device(self.handle, _ptr(d_desc), n, _ptr(d_base), _ptr(d_out), stream),
                     "batch_device")
@@ -275,6 +288,82 @@ class Context:
                                      _ptr(dmetas), _ptr(ok), ctypes.byref(dlen), ctypes.byref(nlive))
         self._check(rc, "block_compact", ok=(TFS_SUCCESS, TFS_EXIT_CHECK_CRC_ERROR))
         return dest[:dlen.value], dmetas[:nlive.value], ok, rc
+
+
+class DeviceBuffer:
+    """Device memory owned through the C ABI (tfs_crc32_dev_malloc)."""
+
+    def __init__(self, ctx, nbytes):
+        p = ctypes.c_void_p()
+        ctx._check(lib().tfs_crc32_dev_malloc(ctx.handle, nbytes, ctypes.byref(p)), "dev_malloc(%d)" % nbytes)
+        self.ctx, self.ptr, self.nbytes = ctx, p.value, nbytes
+
+    def free(self):
+        if self.ptr:
+            lib().tfs_crc32_dev_free(self.ctx.handle, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def upload(self, arr, offset=0):
+        a = np.ascontiguousarray(arr)
+        self.ctx._check(lib().tfs_crc32_memcpy(self.ctx.handle, self.ptr + offset, a.ctypes.data, a.nbytes, None),
+                        "memcpy h2d")
+        return self
+
+    def download(self, dtype=np.uint8, count=None, offset=0):
+        dt = np.dtype(dtype)
+        if count is None:
+            count = (self.nbytes - offset) // dt.itemsize
+        out = np.empty(count, dt)
+        self.ctx._check(lib().tfs_crc32_memcpy(self.ctx.handle, out.ctypes.data, self.ptr + offset, out.nbytes,
+                                               None), "memcpy d2h")
+        return out
+
+    def zero(self, stream=None):
+        self.ctx._check(lib().tfs_crc32_memset_device(self.ctx.handle, self.ptr, 0, self.nbytes, stream), "memset")
+
+
+class PinnedBuffer:
+    """Page-locked host memory (hipHostMalloc) viewed as a numpy uint8 array."""
+
+    def __init__(self, ctx, nbytes):
+        p = ctypes.c_void_p()
+        ctx._check(lib().tfs_crc32_host_malloc_pinned(ctx.handle, nbytes, ctypes.byref(p)), "host_malloc_pinned")
+        self.ctx, self.ptr, self.nbytes = ctx, p.value, nbytes
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p.value))
+
+    def free(self):
+        if self.ptr:
+            self.array = None
+            lib().tfs_crc32_host_free_pinned(self.ctx.handle, self.ptr)
+            self.ptr = None
+
+
+class Event:
+    def __init__(self, ctx):
+        p = ctypes.c_void_p()
+        ctx._check(lib().tfs_crc32_event_create(ctx.handle, ctypes.byref(p)), "event_create")
+        self.ctx, self.ptr = ctx, p.value
+
+    def record(self, stream=None):
+        self.ctx._check(lib().tfs_crc32_event_record(self.ctx.handle, self.ptr, stream), "event_record")
+
+    def elapsed_ms(self, end):
+        ms = ctypes.c_float()
+        self.ctx._check(lib().tfs_crc32_event_elapsed_ms(self.ctx.handle, self.ptr, end.ptr, ctypes.byref(ms)),
+                        "event_elapsed")
+        return ms.value
+
+    def __del__(self):
+        try:
+            lib().tfs_crc32_event_destroy(self.ctx.handle, self.ptr)
+        except Exception:
+            pass
 
 
 def func_crc(crc, data, length=None):

@@ -602,6 +602,83 @@ int tfs_crc32_membench_device(tfs_crc_ctx* ctx, int pattern, const void* d_base,
   return TFS_SUCCESS;
 }
 
+int tfs_crc32_dev_malloc(tfs_crc_ctx* ctx, uint64_t bytes, void** d_ptr) {
+  if (!ctx || !d_ptr) return TFS_EXIT_PARAMETER_ERROR;
+  *d_ptr = nullptr;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  HIP_TRY(ctx, hipMalloc(d_ptr, bytes ? bytes : 1));
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_dev_free(tfs_crc_ctx* ctx, void* d_ptr) {
+  if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
+  if (!d_ptr) return TFS_SUCCESS;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  HIP_TRY(ctx, hipFree(d_ptr));
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_host_malloc_pinned(tfs_crc_ctx* ctx, uint64_t bytes, void** h_ptr) {
+  if (!ctx || !h_ptr) return TFS_EXIT_PARAMETER_ERROR;
+  *h_ptr = nullptr;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  HIP_TRY(ctx, hipHostMalloc(h_ptr, bytes ? bytes : 1, hipHostMallocDefault));
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_host_free_pinned(tfs_crc_ctx* ctx, void* h_ptr) {
+  if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
+  if (!h_ptr) return TFS_SUCCESS;
+  HIP_TRY(ctx, hipHostFree(h_ptr));
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_memcpy(tfs_crc_ctx* ctx, void* dst, const void* src, uint64_t bytes, void* stream) {
+  if (!ctx || (bytes && (!dst || !src))) return TFS_EXIT_PARAMETER_ERROR;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  if (bytes) HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, st));
+  if (!stream) HIP_TRY(ctx, hipStreamSynchronize(st));
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_memset_device(tfs_crc_ctx* ctx, void* d_ptr, int value, uint64_t bytes, void* stream) {
+  if (!ctx || (bytes && !d_ptr)) return TFS_EXIT_PARAMETER_ERROR;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  if (bytes) HIP_TRY(ctx, hipMemsetAsync(d_ptr, value, bytes, st));
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_event_create(tfs_crc_ctx* ctx, void** ev) {
+  if (!ctx || !ev) return TFS_EXIT_PARAMETER_ERROR;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  hipEvent_t e;
+  HIP_TRY(ctx, hipEventCreate(&e));
+  *ev = e;
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_event_record(tfs_crc_ctx* ctx, void* ev, void* stream) {
+  if (!ctx || !ev) return TFS_EXIT_PARAMETER_ERROR;
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  HIP_TRY(ctx, hipEventRecord(static_cast<hipEvent_t>(ev), st));
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_event_elapsed_ms(tfs_crc_ctx* ctx, void* ev_start, void* ev_end, float* ms) {
+  if (!ctx || !ev_start || !ev_end || !ms) return TFS_EXIT_PARAMETER_ERROR;
+  HIP_TRY(ctx, hipEventSynchronize(static_cast<hipEvent_t>(ev_end)));
+  HIP_TRY(ctx, hipEventElapsedTime(ms, static_cast<hipEvent_t>(ev_start), static_cast<hipEvent_t>(ev_end)));
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_event_destroy(tfs_crc_ctx* ctx, void* ev) {
+  if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
+  if (ev) HIP_TRY(ctx, hipEventDestroy(static_cast<hipEvent_t>(ev)));
+  return TFS_SUCCESS;
+}
+
 void* tfs_crc32_stream(tfs_crc_ctx* ctx) { return ctx ? static_cast<void*>(ctx->stream) : nullptr; }
 
 int tfs_crc32_sync(tfs_crc_ctx* ctx) {
