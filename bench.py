@@ -210,7 +210,7 @@ def main():
     extra = {}
     if args.membench:
         out = crc.DeviceBuffer(ctx, 16)
-        for pat in (0, 1):
+        for pat in (0, 16, 32, 64, 1024):
             e0, e1 = crc.Event(ctx), crc.Event(ctx)
             ctx.membench_device(pat, img, d_vdesc, nfiles, total, out)
             e0.record()
@@ -218,8 +218,8 @@ def main():
                 ctx.membench_device(pat, img, d_vdesc, nfiles, total, out)
             e1.record()
             ms = e0.elapsed_ms(e1) / 5
-            nb = total if pat == 0 else nfiles * FILE_SIZE
-            extra["membench_pattern%d_GBs" % pat] = nb / (ms / 1e3) / 1e9
+            nb = total if pat == 0 else nfiles * (FILE_SIZE // (64 * pat)) * 64 * pat
+            extra["membench_run%d_GBs" % pat] = nb / (ms / 1e3) / 1e9
         print(json.dumps({"membench": extra}), file=sys.stderr)
 
     result = {

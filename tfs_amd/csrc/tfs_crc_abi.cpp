@@ -11,6 +11,7 @@
 #include <atomic>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -22,7 +23,7 @@
 
 namespace tfscrc {
 hipError_t launch_crc_files(int mode, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
-                            uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, hipStream_t stream);
+                            uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, hipStream_t stream, int variant);
 hipError_t launch_block_verify(const uint8_t* image, uint64_t image_len, const RawMeta* metas, uint32_t n,
                                const Tables* tg, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
                                hipStream_t stream);
@@ -120,6 +121,7 @@ struct tfs_crc_ctx {
   std::string last_error = "no error";
   Slot slots[kSlots];
   uint64_t next_ticket = 1;
+  int variant = 0;  // kernel variant (TFS_CRC_VARIANT, measurement knob; 0 = product default)
 };
 
 namespace {
@@ -144,10 +146,10 @@ int set_err(tfs_crc_ctx* ctx, int code, const char* fmt, ...) {
 
 void build_tables(Tables* t) {
   make_slice_tables(t->slice, 4);
-  for (int li = 0; li < kNumSegLog; ++li) {
-    const uint64_t L = uint64_t(kMinSeg) << li;
-    for (int j = 0; j < kLevels; ++j) make_shift_table(t->shift[li][j], L << j);
-    make_shift_table(t->shift[li][kStripeShift], 63 * L);
+  for (int ri = 0; ri < kNumRuns; ++ri) {
+    const uint64_t run = uint64_t(16) << ri;
+    make_shift_table(t->stripe[ri], 63 * run);
+    for (int j = 0; j < kLevels; ++j) make_shift_table(t->level[ri][j], run << j);
   }
 }
 
@@ -228,7 +230,7 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
   HIP_TRY(ctx, hipMemsetAsync(s.d_bad.p, 0, 4, ctx->stream));
   HIP_TRY(ctx, launch_crc_files(mode, d_base, static_cast<const Desc*>(s.d_desc.p), n, ctx->d_tables,
                                 static_cast<uint32_t*>(s.d_crc.p), static_cast<uint8_t*>(s.d_ok.p),
-                                static_cast<uint32_t*>(s.d_bad.p), ctx->stream));
+                                static_cast<uint32_t*>(s.d_bad.p), ctx->stream, ctx->variant));
   HIP_TRY(ctx, hipMemcpyAsync(s.h_crc.p, s.d_crc.p, size_t(n) * 4, hipMemcpyDeviceToHost, ctx->stream));
   if (mode == 1) {
     HIP_TRY(ctx, hipMemcpyAsync(s.h_ok.p, s.d_ok.p, n, hipMemcpyDeviceToHost, ctx->stream));
@@ -289,6 +291,7 @@ int tfs_crc32_ctx_create(int device, tfs_crc_ctx** out) {
   if (device < 0 || device >= ndev) return TFS_EXIT_PARAMETER_ERROR;
   auto* ctx = new tfs_crc_ctx();
   ctx->device = device;
+  if (const char* v = getenv("TFS_CRC_VARIANT")) ctx->variant = atoi(v);
   int rc = TFS_SUCCESS;
   do {
     hipError_t e = hipSetDevice(device);
@@ -406,7 +409,7 @@ int tfs_crc32_batch_device(tfs_crc_ctx* ctx, const tfs_crc_desc* d_desc, uint32_
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   HIP_TRY(ctx, launch_crc_files(0, static_cast<const uint8_t*>(d_base), reinterpret_cast<const Desc*>(d_desc), n,
-                                ctx->d_tables, d_out_crc, nullptr, nullptr, st));
+                                ctx->d_tables, d_out_crc, nullptr, nullptr, st, ctx->variant));
   return TFS_SUCCESS;
 }
 
@@ -416,7 +419,7 @@ int tfs_crc32_verify_device(tfs_crc_ctx* ctx, const tfs_crc_vdesc* d_desc, uint3
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   HIP_TRY(ctx, launch_crc_files(1, static_cast<const uint8_t*>(d_base), reinterpret_cast<const Desc*>(d_desc), n,
-                                ctx->d_tables, d_out_crc, d_out_ok, d_n_bad, st));
+                                ctx->d_tables, d_out_crc, d_out_ok, d_n_bad, st, ctx->variant));
   return TFS_SUCCESS;
 }
 

@@ -5,15 +5,19 @@
 
 namespace tfscrc {
 
-constexpr int kWave = 64;           // CDNA wavefront
-constexpr int kBlock = 256;         // 4 waves per workgroup, one file per wave
-constexpr unsigned kMaxGrid = 8192; // grid-stride beyond 32 workgroups/CU
+constexpr int kWave = 64;            // CDNA wavefront
+constexpr int kBlock = 1024;         // 16 waves per workgroup, one file per wave, 1 workgroup per CU
+constexpr unsigned kMaxGrid = 256;   // persistent: one workgroup per CU (LDS-bound)
 constexpr uint32_t kMinParallelLen = 32;  // shorter payloads: byte loop in every lane
-constexpr uint32_t kMinSeg = 64;          // lane segment L = kMinSeg << li
-constexpr int kNumSegLog = 5;             // li = 0..4 -> L = 64..1024 bytes
-constexpr int kLevels = 6;                // shift tables for L*2^j, j = 0..5
-constexpr int kStripeShift = 6;           // shift table for 63*L (between stripes)
-constexpr int kShiftTabs = 7;
+// Lane runs: each lane owns RUN contiguous bytes of every 64*RUN-byte stripe.
+constexpr int kNumRuns = 4;               // RUN = 16 << ri, ri = 0..3 -> 16, 32, 64, 128 bytes
+constexpr int kLevels = 6;                // shift tables for RUN*2^j, j = 0..5 (final lane combine)
+// LDS layout (bytes): 4 slice tables replicated 32x (lane & 31 owns bank lane & 31),
+// then the stripe-shift byte tables and the six level-shift byte tables (not replicated).
+constexpr uint32_t kRepTableBytes = 256u * 32u * 4u;      // 32 KiB per slice table
+constexpr uint32_t kLdsStripeOff = 4u * kRepTableBytes;   // 128 KiB
+constexpr uint32_t kLdsLevelOff = kLdsStripeOff + 4096u;          // + 4 KiB stripe-shift tables
+constexpr uint32_t kLdsBytes = kLdsLevelOff + 6u * 4096u;          // + 24 KiB level tables = 156 KiB
 
 constexpr int kFileInfoSize = 36;  // sizeof(FileInfo), internal.h:432-446
 
@@ -56,15 +60,11 @@ static_assert(sizeof(FileInfoHdr) == kFileInfoSize, "FileInfo must be 36 bytes")
 
 // Device-resident constant tables (built on the host by crc_math.h).
 struct Tables {
-  uint32_t slice[4][256];                                // slice-by-4, LDS-staged per workgroup
-  uint32_t shift[kNumSegLog][kShiftTabs][4][256];        // byte tables of shift(c, L*2^j) and shift(c, 63*L)
+  uint32_t slice[4][256];                          // slice-by-4 (slice k: byte then k zero bytes)
+  uint32_t stripe[kNumRuns][4][256];               // byte tables of shift(c, 63*RUN)
+  uint32_t level[kNumRuns][kLevels][4][256];       // byte tables of shift(c, RUN*2^j)
 };
 
-// Segment size for a body of `body` bytes: the largest L in 64..1024 with
-// 64 * L <= body (so a wave's 64 lanes are busy), at least 64.
-__host__ __device__ inline uint32_t pick_segment_log(uint32_t body) {
-  const uint32_t q = body >> 6;
-  return q >= 1024u ? 4u : q >= 512u ? 3u : q >= 256u ? 2u : q >= 128u ? 1u : 0u;
-}
+constexpr int run_index(int run) { return run == 16 ? 0 : run == 32 ? 1 : run == 64 ? 2 : 3; }
 
 }  // namespace tfscrc

@@ -6,19 +6,25 @@
 // Bit-identical arithmetic: reflected CRC-32 (0xEDB88320), caller seed, no
 // inversion.
 //
-// Execution model: one wavefront per file.  The file's aligned
-// body is cut into lane segments of L bytes (L = 64..1024, chosen per file),
-// laid out so the LAST segment ends at the last 16-byte boundary of the file
-// (leading bytes of a seed-0 CRC that are zero do not change it, so the body is
-// zero-extended at the front).  Each lane runs the slice-by-4 table recurrence
-// (LDS tables) over its segments; segments of later 64-segment stripes continue
-// the same lane chain after a shift over the 63 foreign segments in between.
-// Lane results are moved to their position by shift(c, (63-lane)*L) -- a
-// product of level shifts looked up in byte tables -- and XOR-reduced across
-// the wave with __shfl_xor (the CRC is linear over GF(2)).  The <=15 tail bytes
-// after the last 16-byte boundary are folded in by every lane redundantly.
-// The seed is injected by XOR into the first four message bytes, which is
-// exactly what Func::crc does with its initial register.
+// Execution model: one wavefront per file, 16 waves per
+// workgroup, one workgroup per CU (persistent grid-stride over files).
+//
+// Byte -> lane mapping ("stripes"): the file's aligned body is cut, from its
+// last 16-byte boundary backwards, into stripes of 64*RUN bytes; lane l owns
+// bytes [l*RUN, (l+1)*RUN) of every stripe.  A stripe is therefore one
+// coalesced sweep of the wave (RUN/16 dwordx4 loads per lane, contiguous across
+// lanes), so the HBM stream is read in whole cache lines straight into VGPRs.
+// Each lane runs one CRC chain over its runs: slice-by-4 steps whose four
+// 1 KiB tables are replicated 32x in LDS so that lane (l & 31) always hits
+// bank (l & 31) -- a random-byte table lookup never bank-conflicts -- and, at
+// every stripe boundary, a jump over the 63 foreign runs (shift(c, 63*RUN), one
+// byte-table lookup per state byte).  Finally lane chains are moved to their
+// place with shift(c, (63-lane)*RUN) (level tables) and XOR-reduced across the
+// wave with __shfl_xor -- the CRC is linear over GF(2).  The body starts zero-
+// extended in front (leading zero bytes do not change a seed-0 CRC register);
+// the seed is injected by XOR into the first four message bytes, which is
+// exactly Func::crc's initial register; the <=15 tail bytes after the last
+// 16-byte boundary are folded in by every lane redundantly.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -27,33 +33,100 @@
 namespace tfscrc {
 
 // ---------------------------------------------------------------------------
-// Table helpers.  T points at 4x256 slice tables in LDS (slice k = byte followed
-// by k zero bytes); shift tables live in global memory (L2-resident, touched a
-// few times per file).
+// LDS table access.  Replicated slice table k (k zero bytes follow the byte)
+// lives at k*32 KiB; entry b of copy j at b*128 + j*4.  `lb` = this lane's
+// copy offset ((lane & 31) * 4); it has no bits in 7..14, so OR == ADD.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t step4(const uint32_t* T, uint32_t c, uint32_t w) {
+// Payload loads through explicit global (addrspace 1) pointers: flat loads would
+// also count on lgkmcnt and serialise against the LDS table lookups.
+typedef const __attribute__((address_space(1))) uint32_t* gu32p;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4* gu128p;
+typedef const __attribute__((address_space(1))) uint8_t* gu8p;
+__device__ __forceinline__ uint32_t ld32(uintptr_t a) { return *reinterpret_cast<gu32p>(a); }
+__device__ __forceinline__ uint4 ld128(uintptr_t a) {
+  const u32x4 v = *reinterpret_cast<gu128p>(a);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+// Streaming payload load: read once, never re-used -> non-temporal (nt) policy.
+template <bool NT>
+__device__ __forceinline__ uint4 ld128s(uintptr_t a) {
+  if (NT) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<gu128p>(a));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+  return ld128(a);
+}
+__device__ __forceinline__ uint32_t ld8(uintptr_t a) { return *reinterpret_cast<gu8p>(a); }
+
+// `T` is the workgroup's __shared__ table array (LDS address 0 in practice).
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t* T, uint32_t byte_addr) {
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(T) + byte_addr);
+}
+
+__device__ __forceinline__ uint32_t step4(const uint32_t* T, uint32_t lb, uint32_t c, uint32_t w) {
   const uint32_t x = c ^ w;
-  return T[768 + (x & 0xffu)] ^ T[512 + ((x >> 8) & 0xffu)] ^ T[256 + ((x >> 16) & 0xffu)] ^ T[x >> 24];
+  const uint32_t a0 = ((x << 7) & 0x7F80u) | lb;   // byte 0 -> slice 3
+  const uint32_t a1 = ((x >> 1) & 0x7F80u) | lb;   // byte 1 -> slice 2
+  const uint32_t a2 = ((x >> 9) & 0x7F80u) | lb;   // byte 2 -> slice 1
+  const uint32_t a3 = ((x >> 17) & 0x7F80u) | lb;  // byte 3 -> slice 0
+  return lds_ld(T, a0 + 3 * kRepTableBytes) ^ lds_ld(T, a1 + 2 * kRepTableBytes) ^
+         lds_ld(T, a2 + kRepTableBytes) ^ lds_ld(T, a3);
 }
 
-__device__ __forceinline__ uint32_t step1(const uint32_t* T, uint32_t c, uint32_t b) {
-  return (c >> 8) ^ T[(c ^ b) & 0xffu];
+__device__ __forceinline__ uint32_t step1(const uint32_t* T, uint32_t lb, uint32_t c, uint32_t b) {
+  return (c >> 8) ^ lds_ld(T, (((c ^ b) << 7) & 0x7F80u) | lb);
 }
 
-__device__ __forceinline__ uint32_t shift_tab(const uint32_t* __restrict__ S, uint32_t c) {
+// shift(c, d) from a (non-replicated) 4x256 byte table at LDS offset `off`.
+__device__ __forceinline__ uint32_t shift_lds(const uint32_t* T, uint32_t off, uint32_t c) {
+  return lds_ld(T, off + ((c << 2) & 0x3FCu)) ^ lds_ld(T, off + 1024u + ((c >> 6) & 0x3FCu)) ^
+         lds_ld(T, off + 2048u + ((c >> 14) & 0x3FCu)) ^ lds_ld(T, off + 3072u + ((c >> 22) & 0x3FCu));
+}
+// shift(c, 63*RUN): the jump over the 63 foreign runs between two stripes.
+__device__ __forceinline__ uint32_t shift_stripe(const uint32_t* T, uint32_t c) { return shift_lds(T, kLdsStripeOff, c); }
+
+// shift by a byte-table in global memory (L2-resident; a few lookups per file).
+__device__ __forceinline__ uint32_t shift_glb(const uint32_t* __restrict__ S0, uint32_t c) {
+  const gu32p S = reinterpret_cast<gu32p>(reinterpret_cast<uintptr_t>(S0));
   return S[c & 0xffu] ^ S[256 + ((c >> 8) & 0xffu)] ^ S[512 + ((c >> 16) & 0xffu)] ^ S[768 + (c >> 24)];
 }
 
-__device__ __forceinline__ uint32_t ld32(uintptr_t a) { return *reinterpret_cast<const uint32_t*>(a); }
-__device__ __forceinline__ uint4 ld128(uintptr_t a) { return *reinterpret_cast<const uint4*>(a); }
+
+
+__device__ __forceinline__ uint32_t steps16(const uint32_t* T, uint32_t lb, uint32_t c, const uint4& v) {
+  c = step4(T, lb, c, v.x);
+  c = step4(T, lb, c, v.y);
+  c = step4(T, lb, c, v.z);
+  return step4(T, lb, c, v.w);
+}
+
+// Stage the tables: 32 copies of each slice table (conflict-free lookups) and
+// the stripe-shift tables for RUN.  Every thread of the workgroup takes part.
+template <int RUN>
+__device__ __forceinline__ void load_tables(uint32_t* T, const Tables* __restrict__ tg) {
+  for (uint32_t i = threadIdx.x; i < 4u * 256u * 32u; i += blockDim.x) {
+    const uint32_t k = i >> 13, b = (i >> 5) & 255u;
+    T[i] = tg->slice[k][b];
+  }
+  const uint32_t* st = tg->stripe[run_index(RUN)][0];
+  for (uint32_t i = threadIdx.x; i < 1024u; i += blockDim.x) T[kLdsStripeOff / 4 + i] = st[i];
+  const uint32_t* lv = tg->level[run_index(RUN)][0][0];
+  for (uint32_t i = threadIdx.x; i < 6u * 1024u; i += blockDim.x) T[kLdsLevelOff / 4 + i] = lv[i];
+  __syncthreads();
+}
 
 // CRC of `len` bytes at p with initial register `seed`, computed by the whole
-// wave; the result is returned in every lane.  `lane` = threadIdx.x & 63.
-__device__ uint32_t wave_crc(const uint8_t* p, uint32_t len, uint32_t seed, const uint32_t* T,
+// wave; the result is returned in every lane.
+template <int RUN, int PF, bool NT>
+__device__ __forceinline__ uint32_t wave_crc(const uint32_t* T, const uint8_t* p, uint32_t len, uint32_t seed,
                              const Tables* __restrict__ tg, int lane) {
-  if (len < kMinParallelLen) {  // tiny: every lane runs the byte loop of func.cpp:429-433
+  constexpr uint32_t kStripe = 64u * RUN;
+  constexpr int kVec = RUN / 16;  // dwordx4 loads per lane per stripe
+  const uint32_t lb = uint32_t(lane & 31) * 4u;
+  if (len < kMinParallelLen) {  // tiny: the byte loop of func.cpp:429-433 in every lane
     uint32_t c = seed;
-    for (uint32_t i = 0; i < len; ++i) c = step1(T, c, p[i]);
+    for (uint32_t i = 0; i < len; ++i) c = step1(T, lb, c, ld8(reinterpret_cast<uintptr_t>(p) + i));
     return c;
   }
   const uintptr_t start = reinterpret_cast<uintptr_t>(p);
@@ -61,92 +134,116 @@ __device__ uint32_t wave_crc(const uint8_t* p, uint32_t len, uint32_t seed, cons
   const uintptr_t A = start & ~uintptr_t(3);
   const uintptr_t B16 = end & ~uintptr_t(15);
   const uint32_t s = uint32_t(start - A);
-  const uint32_t body = uint32_t(B16 - A);  // >= 20 because len >= kMinParallelLen
+  const uint32_t body = uint32_t(B16 - A);  // > 8 because len >= kMinParallelLen
+  const uint32_t nstripes = (body + kStripe - 1) / kStripe;
+  const uintptr_t sb0 = B16 - uintptr_t(nstripes) * kStripe;  // stripe 0 base (<= A)
 
-  const uint32_t li = pick_segment_log(body);
-  const uint32_t L = kMinSeg << li;
-  const uint32_t nseg = (body + L - 1) / L;
-  const uint32_t nstripes = (nseg + kWave - 1) / kWave;
-  const uint32_t vsegs = nstripes * kWave;
-
-  const uint32_t* __restrict__ Sstripe = tg->shift[li][kStripeShift][0];
-  const uint32_t headmask = 0xffffffffu << (8 * s);
-  const uint32_t seed_lo = seed << (8 * s);
-  const uint32_t seed_hi = s ? (seed >> (32 - 8 * s)) : 0u;
-
+  // Stripe 0: may begin before the payload (zero extension) and holds the
+  // seed-injected first bytes.  Dword by dword with guards.  When the payload
+  // starts inside the last dword of stripe 0, the high seed bytes belong to the
+  // first dword of stripe 1 (lane 0): `inj` carries them there.
   uint32_t c = 0;
-  for (uint32_t r = 0; r < nstripes; ++r) {
-    if (r) c = shift_tab(Sstripe, c);
-    const uint32_t v = r * kWave + lane;
-    const uint64_t dist_hi = uint64_t(vsegs - 1 - v) * L;  // bytes between segment end and B16
-    if (dist_hi >= body) continue;                          // segment wholly in the zero extension
-    const uintptr_t hi = B16 - dist_hi;
-    uintptr_t q = (dist_hi + L >= body) ? A : hi - L;
-    if (q == A) {
-      c = step4(T, c, (ld32(q) & headmask) ^ seed_lo);
-      q += 4;
-    }
-    if (q == A + 4 && q < hi) {
-      c = step4(T, c, ld32(q) ^ seed_hi);
-      q += 4;
-    }
-    while ((q & 15) && q < hi) {
-      c = step4(T, c, ld32(q));
-      q += 4;
-    }
-    for (; q + 64 <= hi; q += 64) {
-      const uint4 a = ld128(q), b = ld128(q + 16), d = ld128(q + 32), e = ld128(q + 48);
-      c = step4(T, c, a.x); c = step4(T, c, a.y); c = step4(T, c, a.z); c = step4(T, c, a.w);
-      c = step4(T, c, b.x); c = step4(T, c, b.y); c = step4(T, c, b.z); c = step4(T, c, b.w);
-      c = step4(T, c, d.x); c = step4(T, c, d.y); c = step4(T, c, d.z); c = step4(T, c, d.w);
-      c = step4(T, c, e.x); c = step4(T, c, e.y); c = step4(T, c, e.z); c = step4(T, c, e.w);
-    }
-    for (; q < hi; q += 16) {
-      const uint4 a = ld128(q);
-      c = step4(T, c, a.x); c = step4(T, c, a.y); c = step4(T, c, a.z); c = step4(T, c, a.w);
+  const uint32_t seed_hi = s ? (seed >> (32 - 8 * s)) : 0u;
+  uint32_t inj = (lane == 0 && A + 4 == sb0 + kStripe) ? seed_hi : 0u;
+  {
+    const uint32_t headmask = 0xffffffffu << (8 * s);
+    const uint32_t seed_lo = seed << (8 * s);
+    const uintptr_t lo = sb0 + uintptr_t(lane) * RUN;
+#pragma unroll
+    for (int i = 0; i < RUN / 4; ++i) {
+      const uintptr_t q = lo + 4u * i;
+      uint32_t w = q >= A ? ld32(q) : 0u;
+      w = q == A ? ((w & headmask) ^ seed_lo) : w;
+      w = q == A + 4 ? (w ^ seed_hi) : w;
+      c = step4(T, lb, c, w);
     }
   }
-  // Move the lane's chain to its place in the body: shift by (63-lane)*L.
+  // Stripes 1.. : coalesced dwordx4 sweeps, PF stripes in flight.  Loads past
+  // the last stripe are clamped to it (an L2 re-read, never out of bounds) so
+  // the steady state is branch-free and the compiler's vmcnt waits stay counted.
+  if (nstripes > 1) {
+    const uintptr_t lane_base = sb0 + uintptr_t(lane) * RUN;
+    const uint32_t last = nstripes - 1;
+    uint4 buf[PF][kVec];
+#pragma unroll
+    for (int f = 0; f < PF; ++f) {
+      const uint32_t st = (1u + f) < last ? (1u + f) : last;
+#pragma unroll
+      for (int v = 0; v < kVec; ++v) buf[f][v] = ld128s<NT>(lane_base + uintptr_t(st) * kStripe + 16u * v);
+    }
+    // Full groups of PF stripes: straight-line, every buffer consumed then refilled.
+    uint32_t r = 1;
+    for (; r + PF <= nstripes; r += PF) {
+#pragma unroll
+      for (int f = 0; f < PF; ++f) {
+        c = shift_stripe(T, c);
+        if (f == 0) {
+          c ^= inj;  // XOR into the stripe's first dword == XOR into the register before its step
+          inj = 0;
+        }
+#pragma unroll
+        for (int v = 0; v < kVec; ++v) c = steps16(T, lb, c, buf[f][v]);
+        const uint32_t nx = r + f + PF;
+        const uint32_t st = nx < last ? nx : last;
+#pragma unroll
+        for (int v = 0; v < kVec; ++v) buf[f][v] = ld128s<NT>(lane_base + uintptr_t(st) * kStripe + 16u * v);
+      }
+    }
+    // Remaining 0..PF-1 stripes are already in buf[0..].
+#pragma unroll
+    for (int f = 0; f < PF - 1; ++f) {
+      if (r + f < nstripes) {
+        c = shift_stripe(T, c);
+        if (f == 0) c ^= inj;
+#pragma unroll
+        for (int v = 0; v < kVec; ++v) c = steps16(T, lb, c, buf[f][v]);
+      }
+    }
+  }
+  // Move each lane's chain to its place in the body: shift by (63-lane)*RUN.
   const uint32_t k = uint32_t(kWave - 1 - lane);
 #pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    const uint32_t sh = shift_tab(tg->shift[li][j][0], c);
+  for (int j = 0; j < kLevels; ++j) {
+    const uint32_t sh = shift_lds(T, kLdsLevelOff + 4096u * j, c);
     c = ((k >> j) & 1u) ? sh : c;
   }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) c ^= __shfl_xor(c, m, kWave);
   // Tail after the last 16-byte boundary (same in every lane).
   uintptr_t q = B16;
-  for (; q + 4 <= end; q += 4) c = step4(T, c, ld32(q));
-  for (; q < end; ++q) c = step1(T, c, *reinterpret_cast<const uint8_t*>(q));
+  for (; q + 4 <= end; q += 4) c = step4(T, lb, c, ld32(q));
+  for (; q < end; ++q) c = step1(T, lb, c, ld8(q));
   return c;
 }
 
-__device__ __forceinline__ void load_slice_tables(uint32_t* T, const Tables* __restrict__ tg) {
-  for (int i = threadIdx.x; i < 1024; i += blockDim.x) T[i] = tg->slice[0][i];
-  __syncthreads();
-}
+constexpr int kRun = 16;  // product configuration (see DESIGN.md §4 for the sweep)
+constexpr int kPF = 8;
+constexpr bool kNT = true;
 
 // MODE 0: compute (aux = seed) -> out_crc.  MODE 1: verify (aux = expected, seed 0).
-template <int MODE>
+template <int MODE, int RUN, int PF, bool NT>
 __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __restrict__ base,
                                                            const Desc* __restrict__ desc, uint32_t n,
                                                            const Tables* __restrict__ tg, uint32_t* out_crc,
                                                            uint8_t* out_ok, uint32_t* n_bad) {
-  __shared__ uint32_t T[1024];
-  load_slice_tables(T, tg);
+  __shared__ uint32_t lds_tables[kLdsBytes / 4];
+  load_tables<RUN>(lds_tables, tg);
   const int lane = threadIdx.x & (kWave - 1);
   const uint32_t wpb = kBlock / kWave;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   uint32_t bad = 0;
-  for (uint32_t f = blockIdx.x * wpb + wave; f < n; f += gridDim.x * wpb) {
-    const Desc d = desc[f];
-    const uint32_t seed = MODE == 0 ? d.aux : 0u;
-    const uint32_t c = wave_crc(base + d.offset, d.len, seed, T, tg, lane);
+  const uint32_t stride = gridDim.x * wpb;
+  uint32_t f = blockIdx.x * wpb + wave;
+  Desc d = f < n ? desc[f] : Desc{0, 0, 0};
+  for (; f < n; f += stride) {
+    const Desc cur = d;
+    if (f + stride < n) d = desc[f + stride];  // next file's descriptor, loaded under this file's work
+    const uint32_t seed = MODE == 0 ? cur.aux : 0u;
+    const uint32_t c = wave_crc<RUN, PF, NT>(lds_tables, base + cur.offset, cur.len, seed, tg, lane);
     if (lane == 0) {
       if (out_crc) out_crc[f] = c;
       if (MODE == 1) {
-        const bool ok = c == d.aux;
+        const bool ok = c == cur.aux;
         if (out_ok) out_ok[f] = ok ? 1 : 0;
         bad += ok ? 0u : 1u;
       }
@@ -161,8 +258,8 @@ __global__ void __launch_bounds__(kBlock) block_verify_kernel(const uint8_t* __r
                                                               const RawMeta* __restrict__ metas, uint32_t n,
                                                               const Tables* __restrict__ tg, uint32_t* out_crc,
                                                               int32_t* out_status, uint32_t* n_bad) {
-  __shared__ uint32_t T[1024];
-  load_slice_tables(T, tg);
+  __shared__ uint32_t lds_tables[kLdsBytes / 4];
+  load_tables<kRun>(lds_tables, tg);
   const int lane = threadIdx.x & (kWave - 1);
   const uint32_t wpb = kBlock / kWave;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -181,7 +278,7 @@ __global__ void __launch_bounds__(kBlock) block_verify_kernel(const uint8_t* __r
       // 36-byte header at an arbitrary byte offset: byte-wise read, same in all lanes.
       uint8_t* hb = reinterpret_cast<uint8_t*>(&h);
       for (int i = 0; i < kFileInfoSize; ++i) hb[i] = rec[i];
-      c = wave_crc(rec + kFileInfoSize, uint32_t(m.size - kFileInfoSize), 0u, T, tg, lane);
+      c = wave_crc<kRun, kPF, kNT>(lds_tables, rec + kFileInfoSize, uint32_t(m.size - kFileInfoSize), 0u, tg, lane);
       if (h.id != m.file_id) status = kExitFileInfoError;
       else if (h.size != m.size) status = kExitSyncFileError;
       else if (c != h.crc) status = kExitCheckCrcError;
@@ -275,15 +372,15 @@ __global__ void write_headers_kernel(uint8_t* __restrict__ image, const uint64_t
   for (int i = 0; i < kFileInfoSize; ++i) d[i] = hb[i];
 }
 
-// Calibration kernels (not on the product path): how fast can this GPU stream
-// the same bytes without the CRC arithmetic?  PATTERN 0: fully coalesced
-// grid-stride 16 B/lane.  PATTERN 1: the CRC kernel's access pattern (one
-// wave per file, lane segments of L bytes, 4 x 16 B loads in flight per lane).
-template <int PATTERN>
-__global__ void __launch_bounds__(kBlock) membench_kernel(const uint8_t* __restrict__ base, const Desc* __restrict__ desc,
-                                                          uint32_t n, uint64_t nbytes, uint32_t* out) {
+// Calibration kernel (not on the product path): stream the same bytes without
+// the CRC arithmetic.  run == 0: fully coalesced grid-stride, 16 B/lane.
+// run > 0: the CRC kernel's pattern -- one wave per file, each lane reading
+// `run` contiguous bytes of every 64*run-byte stripe (len multiple of 64*run).
+__global__ void __launch_bounds__(kBlock) membench_kernel(const uint8_t* __restrict__ base,
+                                                          const Desc* __restrict__ desc, uint32_t n,
+                                                          uint64_t nbytes, uint32_t run, uint32_t* out) {
   uint32_t acc = 0;
-  if (PATTERN == 0) {
+  if (run == 0) {
     const uint4* p = reinterpret_cast<const uint4*>(base);
     const uint64_t nv = nbytes / 16;
     const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
@@ -297,14 +394,14 @@ __global__ void __launch_bounds__(kBlock) membench_kernel(const uint8_t* __restr
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     for (uint32_t f = blockIdx.x * wpb + wave; f < n; f += gridDim.x * wpb) {
       const Desc d = desc[f];
-      const uintptr_t start = reinterpret_cast<uintptr_t>(base + d.offset);
-      const uint32_t L = d.len / kWave;  // assumes len multiple of 1 KiB, 16-aligned start
-      uintptr_t q = (start + 15) & ~uintptr_t(15);
-      q += uint64_t(lane) * L;
-      const uintptr_t hi = q + L;
-      for (; q + 64 <= hi; q += 64) {
-        const uint4 a = ld128(q), b = ld128(q + 16), c = ld128(q + 32), e = ld128(q + 48);
-        acc ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ e.x ^ e.y ^ e.z ^ e.w;
+      const uintptr_t start = (reinterpret_cast<uintptr_t>(base + d.offset) + 15) & ~uintptr_t(15);
+      const uint32_t stripe = 64u * run, ns = d.len / stripe;
+      for (uint32_t r = 0; r < ns; ++r) {
+        const uintptr_t q = start + uintptr_t(r) * stripe + uintptr_t(lane) * run;
+        for (uint32_t v = 0; v < run; v += 16) {
+          const uint4 a = ld128(q + v);
+          acc ^= a.x ^ a.y ^ a.z ^ a.w;
+        }
       }
     }
   }
@@ -327,15 +424,33 @@ static unsigned grid_for(uint32_t nwork) {
   return unsigned(g);
 }
 
-hipError_t launch_crc_files(int mode, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
-                            uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, hipStream_t stream) {
-  if (n == 0) return hipSuccess;
+// Kernel variants (RUN bytes per lane per stripe, PF stripes in flight).  The
+// product default is kRun/kPF; TFS_CRC_VARIANT selects another for measurement.
+template <int MODE>
+static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
+                                 uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, hipStream_t stream) {
   const dim3 grid(grid_for(n)), block(kBlock);
-  if (mode == 0)
-    hipLaunchKernelGGL(crc_files_kernel<0>, grid, block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad);
-  else
-    hipLaunchKernelGGL(crc_files_kernel<1>, grid, block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad);
+#define TFS_LAUNCH(R, P, N)                                                                                   \
+  hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N>), grid, block, 0, stream, base, desc, n, tg, out_crc, out_ok, \
+                     n_bad)
+  switch (variant) {
+    case 1: TFS_LAUNCH(16, 8, false); break;
+    case 2: TFS_LAUNCH(32, 4, true); break;
+    case 3: TFS_LAUNCH(32, 3, true); break;
+    case 4: TFS_LAUNCH(16, 12, true); break;
+    case 5: TFS_LAUNCH(32, 6, true); break;
+    case 6: TFS_LAUNCH(16, 6, true); break;
+    default: TFS_LAUNCH(kRun, kPF, kNT); break;
+  }
+#undef TFS_LAUNCH
   return hipGetLastError();
+}
+
+hipError_t launch_crc_files(int mode, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
+                            uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, hipStream_t stream, int variant) {
+  if (n == 0) return hipSuccess;
+  if (mode == 0) return launch_variant<0>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, stream);
+  return launch_variant<1>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, stream);
 }
 
 hipError_t launch_block_verify(const uint8_t* image, uint64_t image_len, const RawMeta* metas, uint32_t n,
@@ -365,11 +480,9 @@ hipError_t launch_synth_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, uint
 
 hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, uint32_t n, uint64_t nbytes,
                            uint32_t* out, unsigned grid, hipStream_t stream) {
-  if (pattern == 0)
-    hipLaunchKernelGGL(membench_kernel<0>, dim3(grid ? grid : 4096), dim3(kBlock), 0, stream, base, desc, n, nbytes, out);
-  else
-    hipLaunchKernelGGL(membench_kernel<1>, dim3(grid ? grid : grid_for(n)), dim3(kBlock), 0, stream, base, desc, n,
-                       nbytes, out);
+  const uint32_t run = pattern <= 0 ? 0u : uint32_t(pattern);
+  hipLaunchKernelGGL(membench_kernel, dim3(grid ? grid : (run ? grid_for(n) : 2048u)), dim3(kBlock), 0, stream, base,
+                     desc, n, nbytes, run, out);
   return hipGetLastError();
 }
 
