@@ -222,6 +222,16 @@ def main():
             extra["membench_run%d_GBs" % pat] = nb / (ms / 1e3) / 1e9
         print(json.dumps({"membench": extra}), file=sys.stderr)
 
+    # HBM traffic per launch from the committed rocprofv3 PMC passes of this same
+    # command (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; profiles/pmc_latest.json).
+    pmc = {}
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_latest.json")) as fh:
+            pmc = json.load(fh)
+        if nfiles != 1048576 or os.environ.get("TFS_CRC_VARIANT", "0") != "0":
+            pmc = {}
+    except (OSError, ValueError):
+        pmc = {}
     result = {
         "metric": "GiB/s CRC32 verify, device-resident 64 KiB files; 1/2/4/8 MI355X",
         "value": value,
@@ -250,7 +260,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": pmc.get("traffic_bytes_per_launch"),
+            "traffic_source": pmc.get("source"),
             "kernel": "crc_files_kernel<1> (verify)",
             "kernel_ms_avg": avg_kern_s * 1e3,
             "algorithmic_bytes_per_launch": nfiles * ALGO_BYTES_PER_FILE,
