@@ -1,7 +1,9 @@
 set -o pipefail
-mkdir -p gpurun_out/prof
+mkdir -p gpurun_out/prof2
+timeout -k 10 400 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || exit 1
+for v in 0 1 2 3 4 5 6; do
+  TFS_CRC_VARIANT=$v timeout -k 10 200 python bench.py --steps 8 --warmup 2 --no-cpu > gpurun_out/bench_v$v.log 2> gpurun_out/bench_v$v.err || exit 3
+done
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/trace -o run --output-format csv -- python bench.py --steps 8 --warmup 2 --cpu-seconds 5 > gpurun_out/prof/bench_trace.log 2> gpurun_out/prof/bench_trace.err || exit 1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex crc_files_kernel -d gpurun_out/prof/fetch -o run --output-format csv -- python bench.py --steps 4 --warmup 1 --no-cpu > gpurun_out/prof/bench_fetch.log 2> gpurun_out/prof/bench_fetch.err || exit 2
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex crc_files_kernel -d gpurun_out/prof/write -o run --output-format csv -- python bench.py --steps 4 --warmup 1 --no-cpu > gpurun_out/prof/bench_write.log 2> gpurun_out/prof/bench_write.err || exit 3
-timeout -k 10 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --kernel-include-regex crc_files_kernel -d gpurun_out/prof/rdreq -o run --output-format csv -- python bench.py --steps 4 --warmup 1 --no-cpu > gpurun_out/prof/bench_rdreq.log 2> gpurun_out/prof/bench_rdreq.err || exit 4
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS --kernel-include-regex "crc_files_kernel<1" -d gpurun_out/prof2/sq1 -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu > /dev/null 2> gpurun_out/prof2/sq1.err || exit 4
+timeout -k 10 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE --kernel-include-regex "crc_files_kernel<1" -d gpurun_out/prof2/sq2 -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu > /dev/null 2> gpurun_out/prof2/sq2.err || exit 5

@@ -72,4 +72,11 @@ inline void make_shift_table(uint32_t t[4][256], uint64_t nbytes) {
     for (uint32_t b = 0; b < 256; ++b) t[j][b] = multmodp(k, b << (8 * j));
 }
 
+// 5-bit-chunk shift table: shift(c, n) = XOR_k t[k][(c >> 5k) & 31], k = 0..6.
+inline void make_shift_table5(uint32_t t[7][32], uint64_t nbytes) {
+  const uint32_t k = x2nmodp(nbytes, 3);
+  for (int j = 0; j < 7; ++j)
+    for (uint32_t e = 0; e < 32; ++e) t[j][e] = (j == 6 && e >= 4) ? 0u : multmodp(k, e << (5 * j));
+}
+
 }  // namespace tfscrc

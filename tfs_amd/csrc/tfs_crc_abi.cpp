@@ -148,8 +148,12 @@ void build_tables(Tables* t) {
   make_slice_tables(t->slice, 4);
   for (int ri = 0; ri < kNumRuns; ++ri) {
     const uint64_t run = uint64_t(16) << ri;
-    make_shift_table(t->stripe[ri], 63 * run);
-    for (int j = 0; j < kLevels; ++j) make_shift_table(t->level[ri][j], run << j);
+    make_shift_table5(t->stripe[ri], 63 * run);
+    make_shift_table5(t->stripe64[ri], 64 * run);
+    for (int j = 0; j < kLevels; ++j) make_shift_table5(t->level[ri][j], run << j);
+    make_shift_table(t->stripe8[ri], 63 * run);
+    make_shift_table(t->stripe64_8[ri], 64 * run);
+    for (int j = 0; j < kLevels; ++j) make_shift_table(t->level8[ri][j], run << j);
   }
 }
 

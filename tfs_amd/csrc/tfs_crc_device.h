@@ -16,8 +16,20 @@ constexpr int kLevels = 6;                // shift tables for RUN*2^j, j = 0..5 
 // then the stripe-shift byte tables and the six level-shift byte tables (not replicated).
 constexpr uint32_t kRepTableBytes = 256u * 32u * 4u;      // 32 KiB per slice table
 constexpr uint32_t kLdsStripeOff = 4u * kRepTableBytes;   // 128 KiB
-constexpr uint32_t kLdsLevelOff = kLdsStripeOff + 4096u;          // + 4 KiB stripe-shift tables
-constexpr uint32_t kLdsBytes = kLdsLevelOff + 6u * 4096u;          // + 24 KiB level tables = 156 KiB
+// Shift tables are indexed by 5-bit chunks of the CRC register (7 chunks, 32
+// entries each): 32 entries sit in 32 distinct banks, so a random-index lookup
+// never conflicts -- unlike a 256-entry byte table (~3.5x conflict cost).
+// Alternatively (S8 kernels) 4x256 byte tables: 4 lookups instead of 7, but
+// random indices conflict.  Both layouts are kept; DESIGN.md §4 has the numbers.
+constexpr int kShiftChunks = 7;
+constexpr uint32_t kShift5Stride = 1024u;                          // 896 B table, padded
+constexpr uint32_t kShift8Stride = 4096u;                          // 4 x 256 x 4 B
+template <bool S8> struct LdsLayout {
+  static constexpr uint32_t stride = S8 ? kShift8Stride : kShift5Stride;
+  static constexpr uint32_t stripe_off = kLdsStripeOff;
+  static constexpr uint32_t level_off = kLdsStripeOff + stride;
+  static constexpr uint32_t bytes = level_off + 6u * stride;        // 135 KiB (5-bit) / 156 KiB (8-bit)
+};
 
 constexpr int kFileInfoSize = 36;  // sizeof(FileInfo), internal.h:432-446
 
@@ -61,8 +73,12 @@ static_assert(sizeof(FileInfoHdr) == kFileInfoSize, "FileInfo must be 36 bytes")
 // Device-resident constant tables (built on the host by crc_math.h).
 struct Tables {
   uint32_t slice[4][256];                          // slice-by-4 (slice k: byte then k zero bytes)
-  uint32_t stripe[kNumRuns][4][256];               // byte tables of shift(c, 63*RUN)
-  uint32_t level[kNumRuns][kLevels][4][256];       // byte tables of shift(c, RUN*2^j)
+  uint32_t stripe[kNumRuns][kShiftChunks][32];          // 5-bit-chunk tables of shift(c, 63*RUN)
+  uint32_t stripe64[kNumRuns][kShiftChunks][32];        // shift(c, 64*RUN) (parallel-shift form)
+  uint32_t level[kNumRuns][kLevels][kShiftChunks][32];  // shift(c, RUN*2^j), final lane combine
+  uint32_t stripe8[kNumRuns][4][256];                   // byte-table forms of the same shifts
+  uint32_t stripe64_8[kNumRuns][4][256];
+  uint32_t level8[kNumRuns][kLevels][4][256];
 };
 
 constexpr int run_index(int run) { return run == 16 ? 0 : run == 32 ? 1 : run == 64 ? 2 : 3; }

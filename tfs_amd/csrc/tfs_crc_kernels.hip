@@ -59,71 +59,116 @@ __device__ __forceinline__ uint4 ld128s(uintptr_t a) {
 }
 __device__ __forceinline__ uint32_t ld8(uintptr_t a) { return *reinterpret_cast<gu8p>(a); }
 
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
 // `T` is the workgroup's __shared__ table array (LDS address 0 in practice).
 __device__ __forceinline__ uint32_t lds_ld(const uint32_t* T, uint32_t byte_addr) {
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(T) + byte_addr);
 }
 
-__device__ __forceinline__ uint32_t step4(const uint32_t* T, uint32_t lb, uint32_t c, uint32_t w) {
-  const uint32_t x = c ^ w;
-  const uint32_t a0 = ((x << 7) & 0x7F80u) | lb;   // byte 0 -> slice 3
-  const uint32_t a1 = ((x >> 1) & 0x7F80u) | lb;   // byte 1 -> slice 2
-  const uint32_t a2 = ((x >> 9) & 0x7F80u) | lb;   // byte 2 -> slice 1
-  const uint32_t a3 = ((x >> 17) & 0x7F80u) | lb;  // byte 3 -> slice 0
-  return lds_ld(T, a0 + 3 * kRepTableBytes) ^ lds_ld(T, a1 + 2 * kRepTableBytes) ^
-         lds_ld(T, a2 + kRepTableBytes) ^ lds_ld(T, a3);
+// Replicated slice tables, laid out for one-instruction addressing: the byte
+// address of (table t, entry b, copy j) is
+//   region(t) << 16 | b << 8 | half(t) << 7 | j << 2
+// with T3 = (region 0, half 0), T2 = (0, 1), T1 = (1, 0), T0 = (1, 1).  Bits 2..6
+// are the lane's copy, so lane (l & 31) always reads bank (l & 31): no bank
+// conflicts for any data.  The address is a byte permutation of {x, Lk}:
+// v_perm_b32 places byte k of x in bits 8..15 and keeps Lk's bytes 0 and 2.
+__device__ __forceinline__ uint32_t perm_addr(uint32_t x, uint32_t L, uint32_t sel) {
+  return __builtin_amdgcn_perm(x, L, sel);
+}
+constexpr uint32_t kSelByte0 = 0x0C020400u, kSelByte1 = 0x0C020500u, kSelByte2 = 0x0C020600u, kSelByte3 = 0x0C020700u;
+// Lane bases for the four slice tables.
+struct LaneBase {
+  uint32_t t3, t2, t1, t0;
+};
+__device__ __forceinline__ LaneBase lane_base_of(int lane) {
+  const uint32_t l4 = uint32_t(lane & 31) * 4u;
+  return LaneBase{l4, l4 | 0x80u, l4 | 0x10000u, l4 | 0x10080u};
 }
 
-__device__ __forceinline__ uint32_t step1(const uint32_t* T, uint32_t lb, uint32_t c, uint32_t b) {
-  return (c >> 8) ^ lds_ld(T, (((c ^ b) << 7) & 0x7F80u) | lb);
+// One dword of the slice-by-4 recurrence on x = c ^ w, fused with the XOR of the
+// next payload dword: returns M(x) ^ w_next.
+__device__ __forceinline__ uint32_t step4x(const uint32_t* T, const LaneBase& lb, uint32_t x, uint32_t w_next) {
+  const uint32_t a = xor3(lds_ld(T, perm_addr(x, lb.t3, kSelByte0)), lds_ld(T, perm_addr(x, lb.t2, kSelByte1)),
+                          lds_ld(T, perm_addr(x, lb.t1, kSelByte2)));
+  return xor3(a, lds_ld(T, perm_addr(x, lb.t0, kSelByte3)), w_next);
+}
+__device__ __forceinline__ uint32_t step4(const uint32_t* T, const LaneBase& lb, uint32_t c, uint32_t w) {
+  return step4x(T, lb, c ^ w, 0u);
 }
 
-// shift(c, d) from a (non-replicated) 4x256 byte table at LDS offset `off`.
+__device__ __forceinline__ uint32_t step1(const uint32_t* T, const LaneBase& lb, uint32_t c, uint32_t b) {
+  return (c >> 8) ^ lds_ld(T, perm_addr(c ^ b, lb.t0, kSelByte0));
+}
+
+// shift(c, d) from a 7x32 chunk table at LDS offset `off`: conflict-free lookups.
+__device__ __forceinline__ uint32_t shift5(const uint32_t* T, uint32_t off, uint32_t c) {
+  const uint32_t a = xor3(lds_ld(T, off + ((c << 2) & 0x7Cu)), lds_ld(T, off + 128u + ((c >> 3) & 0x7Cu)),
+                          lds_ld(T, off + 256u + ((c >> 8) & 0x7Cu)));
+  const uint32_t b = xor3(lds_ld(T, off + 384u + ((c >> 13) & 0x7Cu)), lds_ld(T, off + 512u + ((c >> 18) & 0x7Cu)),
+                          lds_ld(T, off + 640u + ((c >> 23) & 0x7Cu)));
+  return xor3(a, b, lds_ld(T, off + 768u + ((c >> 28) & 0x0Cu)));
+}
+// shift(c, d) from 4x256 byte tables at `off` (fewer lookups, random bank conflicts).
+__device__ __forceinline__ uint32_t shift8(const uint32_t* T, uint32_t off, uint32_t c) {
+  const uint32_t a = xor3(lds_ld(T, off + ((c << 2) & 0x3FCu)), lds_ld(T, off + 1024u + ((c >> 6) & 0x3FCu)),
+                          lds_ld(T, off + 2048u + ((c >> 14) & 0x3FCu)));
+  return a ^ lds_ld(T, off + 3072u + ((c >> 22) & 0x3FCu));
+}
+template <bool S8>
 __device__ __forceinline__ uint32_t shift_lds(const uint32_t* T, uint32_t off, uint32_t c) {
-  return lds_ld(T, off + ((c << 2) & 0x3FCu)) ^ lds_ld(T, off + 1024u + ((c >> 6) & 0x3FCu)) ^
-         lds_ld(T, off + 2048u + ((c >> 14) & 0x3FCu)) ^ lds_ld(T, off + 3072u + ((c >> 22) & 0x3FCu));
+  return S8 ? shift8(T, off, c) : shift5(T, off, c);
 }
-// shift(c, 63*RUN): the jump over the 63 foreign runs between two stripes.
-__device__ __forceinline__ uint32_t shift_stripe(const uint32_t* T, uint32_t c) { return shift_lds(T, kLdsStripeOff, c); }
-
-// shift by a byte-table in global memory (L2-resident; a few lookups per file).
-__device__ __forceinline__ uint32_t shift_glb(const uint32_t* __restrict__ S0, uint32_t c) {
-  const gu32p S = reinterpret_cast<gu32p>(reinterpret_cast<uintptr_t>(S0));
-  return S[c & 0xffu] ^ S[256 + ((c >> 8) & 0xffu)] ^ S[512 + ((c >> 16) & 0xffu)] ^ S[768 + (c >> 24)];
+// shift(c, 63*RUN) (or 64*RUN in PAR form): the jump between two stripes of a lane.
+template <bool S8>
+__device__ __forceinline__ uint32_t shift_stripe(const uint32_t* T, uint32_t c) {
+  return shift_lds<S8>(T, LdsLayout<S8>::stripe_off, c);
 }
 
-
-
-__device__ __forceinline__ uint32_t steps16(const uint32_t* T, uint32_t lb, uint32_t c, const uint4& v) {
-  c = step4(T, lb, c, v.x);
-  c = step4(T, lb, c, v.y);
-  c = step4(T, lb, c, v.z);
-  return step4(T, lb, c, v.w);
+__device__ __forceinline__ uint32_t steps16(const uint32_t* T, const LaneBase& lb, uint32_t c, const uint4& v) {
+  uint32_t x = c ^ v.x;
+  x = step4x(T, lb, x, v.y);
+  x = step4x(T, lb, x, v.z);
+  x = step4x(T, lb, x, v.w);
+  return step4x(T, lb, x, 0u);
 }
 
 // Stage the tables: 32 copies of each slice table (conflict-free lookups) and
 // the stripe-shift tables for RUN.  Every thread of the workgroup takes part.
-template <int RUN>
+template <int RUN, bool PAR, bool S8>
 __device__ __forceinline__ void load_tables(uint32_t* T, const Tables* __restrict__ tg) {
+  // dword index i = region<<14 | b<<6 | half<<5 | j  (see the address layout above)
   for (uint32_t i = threadIdx.x; i < 4u * 256u * 32u; i += blockDim.x) {
-    const uint32_t k = i >> 13, b = (i >> 5) & 255u;
-    T[i] = tg->slice[k][b];
+    const uint32_t region = i >> 14, b = (i >> 6) & 255u, half = (i >> 5) & 1u;
+    const uint32_t t = 3u - (region * 2u + half);  // T3, T2, T1, T0
+    T[i] = tg->slice[t][b];
   }
-  const uint32_t* st = tg->stripe[run_index(RUN)][0];
-  for (uint32_t i = threadIdx.x; i < 1024u; i += blockDim.x) T[kLdsStripeOff / 4 + i] = st[i];
-  const uint32_t* lv = tg->level[run_index(RUN)][0][0];
-  for (uint32_t i = threadIdx.x; i < 6u * 1024u; i += blockDim.x) T[kLdsLevelOff / 4 + i] = lv[i];
+  using LL = LdsLayout<S8>;
+  const uint32_t ri = run_index(RUN);
+  const uint32_t nent = S8 ? 1024u : kShiftChunks * 32u;
+  const uint32_t* st = S8 ? (PAR ? tg->stripe64_8[ri][0] : tg->stripe8[ri][0])
+                          : (PAR ? tg->stripe64[ri][0] : tg->stripe[ri][0]);
+  for (uint32_t i = threadIdx.x; i < nent; i += blockDim.x) T[LL::stripe_off / 4 + i] = st[i];
+  const uint32_t* lv = S8 ? tg->level8[ri][0][0] : tg->level[ri][0][0];
+  for (uint32_t i = threadIdx.x; i < 6u * nent; i += blockDim.x) {
+    const uint32_t j = i / nent, r = i % nent;
+    T[(LL::level_off + LL::stride * j) / 4 + r] = lv[i];
+  }
   __syncthreads();
 }
 
 // CRC of `len` bytes at p with initial register `seed`, computed by the whole
 // wave; the result is returned in every lane.
-template <int RUN, int PF, bool NT>
+// PAR: per stripe, c' = shift(c, 64*RUN) ^ crc(0, run) -- the shift lookups run in
+// parallel with the run's own chain instead of in front of it (same lookup count).
+template <int RUN, int PF, bool NT, bool PAR, bool S8>
 __device__ __forceinline__ uint32_t wave_crc(const uint32_t* T, const uint8_t* p, uint32_t len, uint32_t seed,
                              const Tables* __restrict__ tg, int lane) {
   constexpr uint32_t kStripe = 64u * RUN;
   constexpr int kVec = RUN / 16;  // dwordx4 loads per lane per stripe
-  const uint32_t lb = uint32_t(lane & 31) * 4u;
+  const LaneBase lb = lane_base_of(lane);
   if (len < kMinParallelLen) {  // tiny: the byte loop of func.cpp:429-433 in every lane
     uint32_t c = seed;
     for (uint32_t i = 0; i < len; ++i) c = step1(T, lb, c, ld8(reinterpret_cast<uintptr_t>(p) + i));
@@ -176,13 +221,22 @@ __device__ __forceinline__ uint32_t wave_crc(const uint32_t* T, const uint8_t* p
     for (; r + PF <= nstripes; r += PF) {
 #pragma unroll
       for (int f = 0; f < PF; ++f) {
-        c = shift_stripe(T, c);
-        if (f == 0) {
-          c ^= inj;  // XOR into the stripe's first dword == XOR into the register before its step
-          inj = 0;
-        }
+        if (PAR) {
+          const uint32_t sh = shift_stripe<S8>(T, c);
+          uint32_t g = inj;
+          if (f == 0) inj = 0;
 #pragma unroll
-        for (int v = 0; v < kVec; ++v) c = steps16(T, lb, c, buf[f][v]);
+          for (int v = 0; v < kVec; ++v) g = steps16(T, lb, g, buf[f][v]);
+          c = sh ^ g;
+        } else {
+          c = shift_stripe<S8>(T, c);
+          if (f == 0) {
+            c ^= inj;  // XOR into the stripe's first dword == XOR into the register before its step
+            inj = 0;
+          }
+#pragma unroll
+          for (int v = 0; v < kVec; ++v) c = steps16(T, lb, c, buf[f][v]);
+        }
         const uint32_t nx = r + f + PF;
         const uint32_t st = nx < last ? nx : last;
 #pragma unroll
@@ -193,10 +247,18 @@ __device__ __forceinline__ uint32_t wave_crc(const uint32_t* T, const uint8_t* p
 #pragma unroll
     for (int f = 0; f < PF - 1; ++f) {
       if (r + f < nstripes) {
-        c = shift_stripe(T, c);
-        if (f == 0) c ^= inj;
+        if (PAR) {
+          const uint32_t sh = shift_stripe<S8>(T, c);
+          uint32_t g = f == 0 ? inj : 0u;
 #pragma unroll
-        for (int v = 0; v < kVec; ++v) c = steps16(T, lb, c, buf[f][v]);
+          for (int v = 0; v < kVec; ++v) g = steps16(T, lb, g, buf[f][v]);
+          c = sh ^ g;
+        } else {
+          c = shift_stripe<S8>(T, c);
+          if (f == 0) c ^= inj;
+#pragma unroll
+          for (int v = 0; v < kVec; ++v) c = steps16(T, lb, c, buf[f][v]);
+        }
       }
     }
   }
@@ -204,7 +266,7 @@ __device__ __forceinline__ uint32_t wave_crc(const uint32_t* T, const uint8_t* p
   const uint32_t k = uint32_t(kWave - 1 - lane);
 #pragma unroll
   for (int j = 0; j < kLevels; ++j) {
-    const uint32_t sh = shift_lds(T, kLdsLevelOff + 4096u * j, c);
+    const uint32_t sh = shift_lds<S8>(T, LdsLayout<S8>::level_off + LdsLayout<S8>::stride * j, c);
     c = ((k >> j) & 1u) ? sh : c;
   }
 #pragma unroll
@@ -219,15 +281,17 @@ __device__ __forceinline__ uint32_t wave_crc(const uint32_t* T, const uint8_t* p
 constexpr int kRun = 16;  // product configuration (see DESIGN.md §4 for the sweep)
 constexpr int kPF = 8;
 constexpr bool kNT = true;
+constexpr bool kPAR = false;
+constexpr bool kS8 = true;
 
 // MODE 0: compute (aux = seed) -> out_crc.  MODE 1: verify (aux = expected, seed 0).
-template <int MODE, int RUN, int PF, bool NT>
+template <int MODE, int RUN, int PF, bool NT, bool PAR, bool S8>
 __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __restrict__ base,
                                                            const Desc* __restrict__ desc, uint32_t n,
                                                            const Tables* __restrict__ tg, uint32_t* out_crc,
                                                            uint8_t* out_ok, uint32_t* n_bad) {
-  __shared__ uint32_t lds_tables[kLdsBytes / 4];
-  load_tables<RUN>(lds_tables, tg);
+  __shared__ uint32_t lds_tables[LdsLayout<S8>::bytes / 4];
+  load_tables<RUN, PAR, S8>(lds_tables, tg);
   const int lane = threadIdx.x & (kWave - 1);
   const uint32_t wpb = kBlock / kWave;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -239,7 +303,7 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
     const Desc cur = d;
     if (f + stride < n) d = desc[f + stride];  // next file's descriptor, loaded under this file's work
     const uint32_t seed = MODE == 0 ? cur.aux : 0u;
-    const uint32_t c = wave_crc<RUN, PF, NT>(lds_tables, base + cur.offset, cur.len, seed, tg, lane);
+    const uint32_t c = wave_crc<RUN, PF, NT, PAR, S8>(lds_tables, base + cur.offset, cur.len, seed, tg, lane);
     if (lane == 0) {
       if (out_crc) out_crc[f] = c;
       if (MODE == 1) {
@@ -258,8 +322,8 @@ __global__ void __launch_bounds__(kBlock) block_verify_kernel(const uint8_t* __r
                                                               const RawMeta* __restrict__ metas, uint32_t n,
                                                               const Tables* __restrict__ tg, uint32_t* out_crc,
                                                               int32_t* out_status, uint32_t* n_bad) {
-  __shared__ uint32_t lds_tables[kLdsBytes / 4];
-  load_tables<kRun>(lds_tables, tg);
+  __shared__ uint32_t lds_tables[LdsLayout<kS8>::bytes / 4];
+  load_tables<kRun, kPAR, kS8>(lds_tables, tg);
   const int lane = threadIdx.x & (kWave - 1);
   const uint32_t wpb = kBlock / kWave;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -278,7 +342,7 @@ __global__ void __launch_bounds__(kBlock) block_verify_kernel(const uint8_t* __r
       // 36-byte header at an arbitrary byte offset: byte-wise read, same in all lanes.
       uint8_t* hb = reinterpret_cast<uint8_t*>(&h);
       for (int i = 0; i < kFileInfoSize; ++i) hb[i] = rec[i];
-      c = wave_crc<kRun, kPF, kNT>(lds_tables, rec + kFileInfoSize, uint32_t(m.size - kFileInfoSize), 0u, tg, lane);
+      c = wave_crc<kRun, kPF, kNT, kPAR, kS8>(lds_tables, rec + kFileInfoSize, uint32_t(m.size - kFileInfoSize), 0u, tg, lane);
       if (h.id != m.file_id) status = kExitFileInfoError;
       else if (h.size != m.size) status = kExitSyncFileError;
       else if (c != h.crc) status = kExitCheckCrcError;
@@ -430,17 +494,17 @@ template <int MODE>
 static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
                                  uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, hipStream_t stream) {
   const dim3 grid(grid_for(n)), block(kBlock);
-#define TFS_LAUNCH(R, P, N)                                                                                   \
-  hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N>), grid, block, 0, stream, base, desc, n, tg, out_crc, out_ok, \
-                     n_bad)
+#define TFS_LAUNCH(R, P, N, Q, S)                                                                          \
+  hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N, Q, S>), grid, block, 0, stream, base, desc, n, tg, out_crc, \
+                     out_ok, n_bad)
   switch (variant) {
-    case 1: TFS_LAUNCH(16, 8, false); break;
-    case 2: TFS_LAUNCH(32, 4, true); break;
-    case 3: TFS_LAUNCH(32, 3, true); break;
-    case 4: TFS_LAUNCH(16, 12, true); break;
-    case 5: TFS_LAUNCH(32, 6, true); break;
-    case 6: TFS_LAUNCH(16, 6, true); break;
-    default: TFS_LAUNCH(kRun, kPF, kNT); break;
+    case 1: TFS_LAUNCH(16, 8, true, false, false); break;
+    case 2: TFS_LAUNCH(16, 8, true, true, true); break;
+    case 3: TFS_LAUNCH(16, 8, true, true, false); break;
+    case 4: TFS_LAUNCH(32, 4, false, false, true); break;
+    case 5: TFS_LAUNCH(32, 4, false, true, false); break;
+    case 6: TFS_LAUNCH(16, 12, true, false, true); break;
+    default: TFS_LAUNCH(kRun, kPF, kNT, kPAR, kS8); break;
   }
 #undef TFS_LAUNCH
   return hipGetLastError();
