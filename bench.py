@@ -48,6 +48,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--e2e", action="store_true", help="also measure the pinned H2D-inclusive rate (stderr)")
     p.add_argument("--membench", action="store_true", help="also time raw streaming reads (stderr)")
+    p.add_argument("--ab", default="", help="comma list of TFS_CRC_VARIANT ids: interleaved A/B timing (stderr)")
+    p.add_argument("--ab-rounds", type=int, default=6)
     return p.parse_args()
 
 
@@ -207,19 +209,23 @@ def main():
     avg_kern_s = float(np.mean(kern_ms)) / 1e3
     achieved = nfiles * ALGO_BYTES_PER_FILE / avg_kern_s / 1e9
 
+    if args.ab:
+        ab_compare(args, crc, img, d_vdesc, nfiles, d_ok, d_bad)
+
     extra = {}
     if args.membench:
         out = crc.DeviceBuffer(ctx, 16)
-        for pat in (0, 16, 32, 64, 1024):
+        for pat, grid in ((0, 0), (1000, 0), (0, 256), (1000, 256), (0, 1024), (1000, 1024), (16, 0), (1016, 0)):
             e0, e1 = crc.Event(ctx), crc.Event(ctx)
-            ctx.membench_device(pat, img, d_vdesc, nfiles, total, out)
+            ctx.membench_device(pat, img, d_vdesc, nfiles, total, out, grid=grid)
             e0.record()
             for _ in range(5):
-                ctx.membench_device(pat, img, d_vdesc, nfiles, total, out)
+                ctx.membench_device(pat, img, d_vdesc, nfiles, total, out, grid=grid)
             e1.record()
             ms = e0.elapsed_ms(e1) / 5
-            nb = total if pat == 0 else nfiles * (FILE_SIZE // (64 * pat)) * 64 * pat
-            extra["membench_run%d_GBs" % pat] = nb / (ms / 1e3) / 1e9
+            run = pat % 1000
+            nb = total if run == 0 else nfiles * (FILE_SIZE // (64 * run)) * 64 * run
+            extra["membench_p%d_g%d_GBs" % (pat, grid)] = nb / (ms / 1e3) / 1e9
         print(json.dumps({"membench": extra}), file=sys.stderr)
 
     # HBM traffic per launch from the committed rocprofv3 PMC passes of this same
@@ -287,6 +293,34 @@ def main():
     ctx.close()
     if dist:
         dist.destroy_process_group()
+
+
+def ab_compare(args, crc, img, d_vdesc, nfiles, d_ok, d_bad):
+    """Rule: perf deltas come from interleaved rounds in one process on one device."""
+    variants = [int(v) for v in args.ab.split(",") if v != ""]
+    ctxs = {}
+    for v in variants:
+        os.environ["TFS_CRC_VARIANT"] = str(v)
+        ctxs[v] = crc.Context(img.ctx.device)
+    os.environ["TFS_CRC_VARIANT"] = "0"
+    times = {v: [] for v in variants}
+    for _ in range(args.ab_rounds):
+        for v in variants:
+            c = ctxs[v]
+            e0, e1 = crc.Event(c), crc.Event(c)
+            c.verify_device(d_vdesc, nfiles, img, None, d_ok, d_bad)
+            e0.record()
+            for _ in range(3):
+                c.verify_device(d_vdesc, nfiles, img, None, d_ok, d_bad)
+            e1.record()
+            times[v].append(e0.elapsed_ms(e1) / 3)
+    out = {}
+    for v in variants:
+        ms = sorted(times[v])
+        out[v] = {"median_ms": ms[len(ms) // 2], "min_ms": ms[0],
+                  "frac_at_median": nfiles * ALGO_BYTES_PER_FILE / (ms[len(ms) // 2] / 1e3) / 1e9 / HBM_PEAK_GBS}
+        ctxs[v].close()
+    print(json.dumps({"ab": out}), file=sys.stderr)
 
 
 def e2e_rate(ctx):

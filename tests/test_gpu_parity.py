@@ -262,3 +262,34 @@ def test_kernel_variants_parity(oracle, variant, monkeypatch):
             assert int(g) == ocrc(oracle, sd, raw[o:o + n]), (variant, o, n)
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_cross_file_pipeline_many_files(oracle, variant, monkeypatch):
+    """> 4096 files so every wave runs a sequence of files of mixed geometry
+    (tiny / single-stripe / multi-stripe, any alignment, any seed): exercises
+    the next-file prefetch of the persistent kernel."""
+    import tfs_amd.crc as crc
+    monkeypatch.setenv("TFS_CRC_VARIANT", str(variant))
+    ctx = crc.Context(0)
+    try:
+        rng = np.random.default_rng(777 + variant)
+        n = 3 * 4096 + 517
+        kind = rng.integers(0, 4, n)
+        lens = np.where(kind == 0, rng.integers(0, 32, n),
+                        np.where(kind == 1, rng.integers(32, 1100, n),
+                                 np.where(kind == 2, rng.integers(1100, 9000, n), rng.integers(9000, 70000, n))))
+        gaps = rng.integers(0, 16, n)
+        offs = np.cumsum(gaps + np.concatenate([[0], lens[:-1]])).astype(np.uint64)
+        total = int(offs[-1] + lens[-1] + 64)
+        buf = synth_bytes(31337 + variant, total)
+        seeds = np.where(rng.integers(0, 2, n) == 0, 0, rng.integers(0, 2**32, n)).astype(np.uint32)
+        got = ctx.batch(buf, offs, lens, seeds)
+        d = np.zeros(n, crc.DESC_DTYPE)
+        d["offset"], d["len"], d["aux"] = offs, lens, seeds
+        exp = np.zeros(n, np.uint32)
+        oracle.oracle_crc_batch(d.ctypes.data, n, buf.ctypes.data, exp.ctypes.data)
+        bad = np.nonzero(got != exp)[0]
+        assert bad.size == 0, [(int(i), int(lens[i]), int(offs[i]) % 16, int(seeds[i])) for i in bad[:10]]
+    finally:
+        ctx.close()

@@ -161,82 +161,120 @@ __device__ __forceinline__ void load_tables(uint32_t* T, const Tables* __restric
 
 // CRC of `len` bytes at p with initial register `seed`, computed by the whole
 // wave; the result is returned in every lane.
-// PAR: per stripe, c' = shift(c, 64*RUN) ^ crc(0, run) -- the shift lookups run in
-// parallel with the run's own chain instead of in front of it (same lookup count).
-template <int RUN, int PF, bool NT, bool PAR, bool S8>
-__device__ __forceinline__ uint32_t wave_crc(const uint32_t* T, const uint8_t* p, uint32_t len, uint32_t seed,
-                             const Tables* __restrict__ tg, int lane) {
-  constexpr uint32_t kStripe = 64u * RUN;
-  constexpr int kVec = RUN / 16;  // dwordx4 loads per lane per stripe
-  const LaneBase lb = lane_base_of(lane);
-  if (len < kMinParallelLen) {  // tiny: the byte loop of func.cpp:429-433 in every lane
-    uint32_t c = seed;
-    for (uint32_t i = 0; i < len; ++i) c = step1(T, lb, c, ld8(reinterpret_cast<uintptr_t>(p) + i));
-    return c;
-  }
-  const uintptr_t start = reinterpret_cast<uintptr_t>(p);
-  const uintptr_t end = start + len;
-  const uintptr_t A = start & ~uintptr_t(3);
-  const uintptr_t B16 = end & ~uintptr_t(15);
-  const uint32_t s = uint32_t(start - A);
-  const uint32_t body = uint32_t(B16 - A);  // > 8 because len >= kMinParallelLen
-  const uint32_t nstripes = (body + kStripe - 1) / kStripe;
-  const uintptr_t sb0 = B16 - uintptr_t(nstripes) * kStripe;  // stripe 0 base (<= A)
+// ---------------------------------------------------------------------------
+// One file as the wave sees it.  All of this is wave-uniform (scalar) state.
+// ---------------------------------------------------------------------------
+template <int RUN>
+struct FileGeo {
+  uintptr_t start, end, A, B16, sb0;
+  uint32_t len, s, nstripes, seed;
+};
 
-  // Stripe 0: may begin before the payload (zero extension) and holds the
-  // seed-injected first bytes.  Dword by dword with guards.  When the payload
-  // starts inside the last dword of stripe 0, the high seed bytes belong to the
-  // first dword of stripe 1 (lane 0): `inj` carries them there.
+template <int RUN>
+__device__ __forceinline__ FileGeo<RUN> make_geo(const uint8_t* p, uint32_t len, uint32_t seed) {
+  constexpr uint32_t kStripe = 64u * RUN;
+  FileGeo<RUN> g;
+  g.start = reinterpret_cast<uintptr_t>(p);
+  g.len = len;
+  g.seed = seed;
+  g.end = g.start + len;
+  g.A = g.start & ~uintptr_t(3);
+  g.B16 = g.end & ~uintptr_t(15);
+  g.s = uint32_t(g.start - g.A);
+  const uint32_t body = len >= kMinParallelLen ? uint32_t(g.B16 - g.A) : 0u;
+  g.nstripes = (body + kStripe - 1) / kStripe;
+  g.sb0 = g.B16 - uintptr_t(g.nstripes) * kStripe;
+  return g;
+}
+
+// Per-lane registers loaded ahead of a file's compute: the lane's run of
+// stripe 0 (zero in front of the payload, masked and seed-injected at A) and
+// the <= 15 tail bytes after the last 16-byte boundary (same in every lane).
+template <int RUN>
+struct Head {
+  uint32_t w[RUN / 4];
+  uint32_t tw[3];
+  uint32_t tb[3];
+};
+
+template <int RUN>
+__device__ __forceinline__ Head<RUN> load_head(const FileGeo<RUN>& g, int lane) {
+  Head<RUN> h;
+  const uintptr_t lo = g.sb0 + uintptr_t(lane) * RUN;
+#pragma unroll
+  for (int i = 0; i < RUN / 4; ++i) {
+    const uintptr_t q = lo + 4u * i;
+    h.w[i] = (g.nstripes && q >= g.A) ? ld32(q) : 0u;
+  }
+  const uintptr_t tq = g.nstripes ? g.B16 : g.start;  // tiny files: everything is "tail"
+#pragma unroll
+  for (int i = 0; i < 3; ++i) h.tw[i] = (g.nstripes && g.B16 + 4u * i + 4u <= g.end) ? ld32(g.B16 + 4u * i) : 0u;
+  const uintptr_t B = g.nstripes ? (g.end & ~uintptr_t(3)) : tq;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) h.tb[i] = (g.nstripes && B + i < g.end) ? ld8(B + i) : 0u;
+  return h;
+}
+
+// Stripes 1.. of a file: PF stripes in flight per lane.
+template <int RUN, int PF, bool NT>
+__device__ __forceinline__ void load_ring(const FileGeo<RUN>& g, int lane, uint4 (&buf)[PF][RUN / 16]) {
+  constexpr uint32_t kStripe = 64u * RUN;
+  const uintptr_t lane_base = g.sb0 + uintptr_t(lane) * RUN;
+  const uint32_t last = g.nstripes > 1 ? g.nstripes - 1 : 0u;
+  // files with <= 1 stripe point the (unused) ring at the file start: in bounds
+  const uintptr_t base = g.nstripes > 1 ? lane_base : (g.start & ~uintptr_t(15));
+#pragma unroll
+  for (int f = 0; f < PF; ++f) {
+    const uint32_t st = (1u + f) < last ? (1u + f) : last;
+#pragma unroll
+    for (int v = 0; v < RUN / 16; ++v)
+      buf[f][v] = ld128s<NT>(g.nstripes > 1 ? base + uintptr_t(st) * kStripe + 16u * v : base);
+  }
+}
+
+// The lane's chain over stripes 0..nstripes-1 (before the final combine).
+template <int RUN, int PF, bool NT, bool S8>
+__device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase& lb, const FileGeo<RUN>& g,
+                                               const Head<RUN>& h, uint4 (&buf)[PF][RUN / 16], int lane) {
+  constexpr uint32_t kStripe = 64u * RUN;
+  constexpr int kVec = RUN / 16;
+  // Stripe 0: mask the bytes before `start` in the dword at A and inject the
+  // seed into the first four message bytes (that is Func::crc's initial
+  // register).  When A is the last dword of stripe 0, the high seed bytes
+  // belong to lane 0's first dword of stripe 1: `inj` carries them there.
+  const uint32_t headmask = 0xffffffffu << (8 * g.s);
+  const uint32_t seed_lo = g.seed << (8 * g.s);
+  const uint32_t seed_hi = g.s ? (g.seed >> (32 - 8 * g.s)) : 0u;
+  uint32_t inj = (lane == 0 && g.A + 4 == g.sb0 + kStripe) ? seed_hi : 0u;
   uint32_t c = 0;
-  const uint32_t seed_hi = s ? (seed >> (32 - 8 * s)) : 0u;
-  uint32_t inj = (lane == 0 && A + 4 == sb0 + kStripe) ? seed_hi : 0u;
   {
-    const uint32_t headmask = 0xffffffffu << (8 * s);
-    const uint32_t seed_lo = seed << (8 * s);
-    const uintptr_t lo = sb0 + uintptr_t(lane) * RUN;
+    const uintptr_t lo = g.sb0 + uintptr_t(lane) * RUN;
 #pragma unroll
     for (int i = 0; i < RUN / 4; ++i) {
       const uintptr_t q = lo + 4u * i;
-      uint32_t w = q >= A ? ld32(q) : 0u;
-      w = q == A ? ((w & headmask) ^ seed_lo) : w;
-      w = q == A + 4 ? (w ^ seed_hi) : w;
+      uint32_t w = h.w[i];
+      w = q == g.A ? ((w & headmask) ^ seed_lo) : w;
+      w = q == g.A + 4 ? (w ^ seed_hi) : w;
       c = step4(T, lb, c, w);
     }
   }
-  // Stripes 1.. : coalesced dwordx4 sweeps, PF stripes in flight.  Loads past
-  // the last stripe are clamped to it (an L2 re-read, never out of bounds) so
-  // the steady state is branch-free and the compiler's vmcnt waits stay counted.
-  if (nstripes > 1) {
-    const uintptr_t lane_base = sb0 + uintptr_t(lane) * RUN;
-    const uint32_t last = nstripes - 1;
-    uint4 buf[PF][kVec];
-#pragma unroll
-    for (int f = 0; f < PF; ++f) {
-      const uint32_t st = (1u + f) < last ? (1u + f) : last;
-#pragma unroll
-      for (int v = 0; v < kVec; ++v) buf[f][v] = ld128s<NT>(lane_base + uintptr_t(st) * kStripe + 16u * v);
-    }
-    // Full groups of PF stripes: straight-line, every buffer consumed then refilled.
+  if (g.nstripes > 1) {
+    const uintptr_t lane_base = g.sb0 + uintptr_t(lane) * RUN;
+    const uint32_t last = g.nstripes - 1;
+    // Full groups of PF stripes: straight-line, every buffer consumed then
+    // refilled (loads past the last stripe are clamped to it: an L2 re-read,
+    // never out of bounds, and the compiler's vmcnt waits stay counted).
     uint32_t r = 1;
-    for (; r + PF <= nstripes; r += PF) {
+    for (; r + PF <= g.nstripes; r += PF) {
 #pragma unroll
       for (int f = 0; f < PF; ++f) {
-        if (PAR) {
-          const uint32_t sh = shift_stripe<S8>(T, c);
-          uint32_t g = inj;
-          if (f == 0) inj = 0;
-#pragma unroll
-          for (int v = 0; v < kVec; ++v) g = steps16(T, lb, g, buf[f][v]);
-          c = sh ^ g;
-        } else {
-          c = shift_stripe<S8>(T, c);
-          if (f == 0) {
-            c ^= inj;  // XOR into the stripe's first dword == XOR into the register before its step
-            inj = 0;
-          }
-#pragma unroll
-          for (int v = 0; v < kVec; ++v) c = steps16(T, lb, c, buf[f][v]);
+        c = shift_stripe<S8>(T, c);
+        if (f == 0) {
+          c ^= inj;  // XOR into the stripe's first dword == XOR into the register before its step
+          inj = 0;
         }
+#pragma unroll
+        for (int v = 0; v < kVec; ++v) c = steps16(T, lb, c, buf[f][v]);
         const uint32_t nx = r + f + PF;
         const uint32_t st = nx < last ? nx : last;
 #pragma unroll
@@ -246,21 +284,25 @@ __device__ __forceinline__ uint32_t wave_crc(const uint32_t* T, const uint8_t* p
     // Remaining 0..PF-1 stripes are already in buf[0..].
 #pragma unroll
     for (int f = 0; f < PF - 1; ++f) {
-      if (r + f < nstripes) {
-        if (PAR) {
-          const uint32_t sh = shift_stripe<S8>(T, c);
-          uint32_t g = f == 0 ? inj : 0u;
+      if (r + f < g.nstripes) {
+        c = shift_stripe<S8>(T, c);
+        if (f == 0) c ^= inj;
 #pragma unroll
-          for (int v = 0; v < kVec; ++v) g = steps16(T, lb, g, buf[f][v]);
-          c = sh ^ g;
-        } else {
-          c = shift_stripe<S8>(T, c);
-          if (f == 0) c ^= inj;
-#pragma unroll
-          for (int v = 0; v < kVec; ++v) c = steps16(T, lb, c, buf[f][v]);
-        }
+        for (int v = 0; v < kVec; ++v) c = steps16(T, lb, c, buf[f][v]);
       }
     }
+  }
+  return c;
+}
+
+// Combine the lane chains into the file CRC and fold in the tail.
+template <int RUN, bool S8>
+__device__ __forceinline__ uint32_t finish_file(const uint32_t* T, const LaneBase& lb, const FileGeo<RUN>& g,
+                                                const Head<RUN>& h, uint32_t c, int lane) {
+  if (g.nstripes == 0) {  // tiny (< kMinParallelLen): the byte loop of func.cpp:429-433 in every lane
+    uint32_t t = g.seed;
+    for (uint32_t i = 0; i < g.len; ++i) t = step1(T, lb, t, ld8(g.start + i));
+    return t;
   }
   // Move each lane's chain to its place in the body: shift by (63-lane)*RUN.
   const uint32_t k = uint32_t(kWave - 1 - lane);
@@ -272,46 +314,89 @@ __device__ __forceinline__ uint32_t wave_crc(const uint32_t* T, const uint8_t* p
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) c ^= __shfl_xor(c, m, kWave);
   // Tail after the last 16-byte boundary (same in every lane).
-  uintptr_t q = B16;
-  for (; q + 4 <= end; q += 4) c = step4(T, lb, c, ld32(q));
-  for (; q < end; ++q) c = step1(T, lb, c, ld8(q));
+  const uint32_t ntw = uint32_t((g.end & ~uintptr_t(3)) - g.B16) / 4u;
+  const uint32_t ntb = uint32_t(g.end & 3u);
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    if (uint32_t(i) < ntw) c = step4(T, lb, c, h.tw[i]);
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    if (uint32_t(i) < ntb) c = step1(T, lb, c, h.tb[i]);
   return c;
 }
 
+// Single-file form (used by the block-verify kernel).
+template <int RUN, int PF, bool NT, bool S8>
+__device__ __forceinline__ uint32_t wave_crc(const uint32_t* T, const uint8_t* p, uint32_t len, uint32_t seed,
+                                             int lane) {
+  const LaneBase lb = lane_base_of(lane);
+  const FileGeo<RUN> g = make_geo<RUN>(p, len, seed);
+  const Head<RUN> h = load_head<RUN>(g, lane);
+  uint4 buf[PF][RUN / 16];
+  load_ring<RUN, PF, NT>(g, lane, buf);
+  const uint32_t c = g.nstripes ? lane_chain<RUN, PF, NT, S8>(T, lb, g, h, buf, lane) : 0u;
+  return finish_file<RUN, S8>(T, lb, g, h, c, lane);
+}
+
 constexpr int kRun = 16;  // product configuration (see DESIGN.md §4 for the sweep)
-constexpr int kPF = 8;
+constexpr int kPF = 5;
 constexpr bool kNT = true;
 constexpr bool kPAR = false;
 constexpr bool kS8 = true;
 
 // MODE 0: compute (aux = seed) -> out_crc.  MODE 1: verify (aux = expected, seed 0).
+// Files are software-pipelined per wave: the next file's stripe-0/tail words
+// and its first PF stripes are in flight while this file's lane chains are
+// combined, so HBM never waits on a file boundary.
 template <int MODE, int RUN, int PF, bool NT, bool PAR, bool S8>
 __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __restrict__ base,
                                                            const Desc* __restrict__ desc, uint32_t n,
                                                            const Tables* __restrict__ tg, uint32_t* out_crc,
                                                            uint8_t* out_ok, uint32_t* n_bad) {
+  static_assert(!PAR, "parallel-shift form retired (DESIGN.md §4)");
   __shared__ uint32_t lds_tables[LdsLayout<S8>::bytes / 4];
   load_tables<RUN, PAR, S8>(lds_tables, tg);
   const int lane = threadIdx.x & (kWave - 1);
+  const LaneBase lb = lane_base_of(lane);
   const uint32_t wpb = kBlock / kWave;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  uint32_t bad = 0;
   const uint32_t stride = gridDim.x * wpb;
   uint32_t f = blockIdx.x * wpb + wave;
-  Desc d = f < n ? desc[f] : Desc{0, 0, 0};
-  for (; f < n; f += stride) {
-    const Desc cur = d;
-    if (f + stride < n) d = desc[f + stride];  // next file's descriptor, loaded under this file's work
-    const uint32_t seed = MODE == 0 ? cur.aux : 0u;
-    const uint32_t c = wave_crc<RUN, PF, NT, PAR, S8>(lds_tables, base + cur.offset, cur.len, seed, tg, lane);
+  if (f >= n) return;
+  Desc cur = desc[f];
+  FileGeo<RUN> g = make_geo<RUN>(base + cur.offset, cur.len, MODE == 0 ? cur.aux : 0u);
+  Head<RUN> h = load_head<RUN>(g, lane);
+  uint4 buf[PF][RUN / 16];
+  load_ring<RUN, PF, NT>(g, lane, buf);
+  Desc nxt = f + stride < n ? desc[f + stride] : Desc{0, 0, 0};
+  uint32_t bad = 0;
+  for (;;) {
+    const uint32_t c = g.nstripes ? lane_chain<RUN, PF, NT, S8>(lds_tables, lb, g, h, buf, lane) : 0u;
+    // Start the next file's loads before combining this one.
+    const bool more = f + stride < n;
+    FileGeo<RUN> ng = g;
+    Head<RUN> nh = h;
+    const Desc ncur = nxt;
+    if (more) {
+      ng = make_geo<RUN>(base + ncur.offset, ncur.len, MODE == 0 ? ncur.aux : 0u);
+      nh = load_head<RUN>(ng, lane);
+      load_ring<RUN, PF, NT>(ng, lane, buf);
+      if (f + 2 * stride < n) nxt = desc[f + 2 * stride];
+    }
+    const uint32_t crc = finish_file<RUN, S8>(lds_tables, lb, g, h, c, lane);
     if (lane == 0) {
-      if (out_crc) out_crc[f] = c;
+      if (out_crc) out_crc[f] = crc;
       if (MODE == 1) {
-        const bool ok = c == cur.aux;
+        const bool ok = crc == cur.aux;
         if (out_ok) out_ok[f] = ok ? 1 : 0;
         bad += ok ? 0u : 1u;
       }
     }
+    if (!more) break;
+    f += stride;
+    cur = ncur;
+    g = ng;
+    h = nh;
   }
   if (MODE == 1 && lane == 0 && bad && n_bad) atomicAdd(n_bad, bad);
 }
@@ -342,7 +427,7 @@ __global__ void __launch_bounds__(kBlock) block_verify_kernel(const uint8_t* __r
       // 36-byte header at an arbitrary byte offset: byte-wise read, same in all lanes.
       uint8_t* hb = reinterpret_cast<uint8_t*>(&h);
       for (int i = 0; i < kFileInfoSize; ++i) hb[i] = rec[i];
-      c = wave_crc<kRun, kPF, kNT, kPAR, kS8>(lds_tables, rec + kFileInfoSize, uint32_t(m.size - kFileInfoSize), 0u, tg, lane);
+      c = wave_crc<kRun, kPF, kNT, kS8>(lds_tables, rec + kFileInfoSize, uint32_t(m.size - kFileInfoSize), 0u, lane);
       if (h.id != m.file_id) status = kExitFileInfoError;
       else if (h.size != m.size) status = kExitSyncFileError;
       else if (c != h.crc) status = kExitCheckCrcError;
@@ -440,16 +525,18 @@ __global__ void write_headers_kernel(uint8_t* __restrict__ image, const uint64_t
 // the CRC arithmetic.  run == 0: fully coalesced grid-stride, 16 B/lane.
 // run > 0: the CRC kernel's pattern -- one wave per file, each lane reading
 // `run` contiguous bytes of every 64*run-byte stripe (len multiple of 64*run).
+// NT: non-temporal loads.
+template <bool NT>
 __global__ void __launch_bounds__(kBlock) membench_kernel(const uint8_t* __restrict__ base,
                                                           const Desc* __restrict__ desc, uint32_t n,
                                                           uint64_t nbytes, uint32_t run, uint32_t* out) {
   uint32_t acc = 0;
   if (run == 0) {
-    const uint4* p = reinterpret_cast<const uint4*>(base);
+    const uintptr_t p = reinterpret_cast<uintptr_t>(base);
     const uint64_t nv = nbytes / 16;
     const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
     for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nv; i += stride) {
-      const uint4 v = p[i];
+      const uint4 v = ld128s<NT>(p + 16 * i);
       acc ^= v.x ^ v.y ^ v.z ^ v.w;
     }
   } else {
@@ -460,12 +547,17 @@ __global__ void __launch_bounds__(kBlock) membench_kernel(const uint8_t* __restr
       const Desc d = desc[f];
       const uintptr_t start = (reinterpret_cast<uintptr_t>(base + d.offset) + 15) & ~uintptr_t(15);
       const uint32_t stripe = 64u * run, ns = d.len / stripe;
-      for (uint32_t r = 0; r < ns; ++r) {
-        const uintptr_t q = start + uintptr_t(r) * stripe + uintptr_t(lane) * run;
-        for (uint32_t v = 0; v < run; v += 16) {
-          const uint4 a = ld128(q + v);
-          acc ^= a.x ^ a.y ^ a.z ^ a.w;
-        }
+      uint32_t r = 0;
+      for (; r + 8 <= ns; r += 8) {
+        uint4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = ld128s<NT>(start + uintptr_t(r + k) * stripe + uintptr_t(lane) * 16u);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+      }
+      for (; r < ns; ++r) {
+        const uint4 a = ld128s<NT>(start + uintptr_t(r) * stripe + uintptr_t(lane) * 16u);
+        acc ^= a.x ^ a.y ^ a.z ^ a.w;
       }
     }
   }
@@ -498,12 +590,12 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
   hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N, Q, S>), grid, block, 0, stream, base, desc, n, tg, out_crc, \
                      out_ok, n_bad)
   switch (variant) {
-    case 1: TFS_LAUNCH(16, 8, true, false, false); break;
-    case 2: TFS_LAUNCH(16, 8, true, true, true); break;
-    case 3: TFS_LAUNCH(16, 8, true, true, false); break;
-    case 4: TFS_LAUNCH(32, 4, false, false, true); break;
-    case 5: TFS_LAUNCH(32, 4, false, true, false); break;
-    case 6: TFS_LAUNCH(16, 12, true, false, true); break;
+    case 1: TFS_LAUNCH(16, 8, true, false, true); break;
+    case 2: TFS_LAUNCH(16, 4, true, false, true); break;
+    case 3: TFS_LAUNCH(16, 5, true, false, true); break;
+    case 4: TFS_LAUNCH(16, 7, true, false, true); break;
+    case 5: TFS_LAUNCH(16, 6, true, false, false); break;
+    case 6: TFS_LAUNCH(16, 3, true, false, true); break;
     default: TFS_LAUNCH(kRun, kPF, kNT, kPAR, kS8); break;
   }
 #undef TFS_LAUNCH
@@ -544,9 +636,14 @@ hipError_t launch_synth_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, uint
 
 hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, uint32_t n, uint64_t nbytes,
                            uint32_t* out, unsigned grid, hipStream_t stream) {
-  const uint32_t run = pattern <= 0 ? 0u : uint32_t(pattern);
-  hipLaunchKernelGGL(membench_kernel, dim3(grid ? grid : (run ? grid_for(n) : 2048u)), dim3(kBlock), 0, stream, base,
-                     desc, n, nbytes, run, out);
+  // pattern: 0 = coalesced, 16 = stripe pattern (run 16); +1000 = non-temporal loads
+  const bool nt = pattern >= 1000;
+  const uint32_t run = uint32_t(pattern % 1000);
+  const dim3 g(grid ? grid : (run ? grid_for(n) : 2048u));
+  if (nt)
+    hipLaunchKernelGGL(membench_kernel<true>, g, dim3(kBlock), 0, stream, base, desc, n, nbytes, run, out);
+  else
+    hipLaunchKernelGGL(membench_kernel<false>, g, dim3(kBlock), 0, stream, base, desc, n, nbytes, run, out);
   return hipGetLastError();
 }
 
