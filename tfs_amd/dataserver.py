@@ -1,0 +1,184 @@
+"""ctypes binding of the dataserver-shaped C++ harness (tfs_amd/ds/, libtfs_ds.so).
+
+The harness is plain host C++ that reaches the CRC only through the C ABI of
+include/tfs_crc.h -- the shape of TFS's own dataserver after the drop-in:
+DataFile (data_file.cpp), close_write_file (data_management.cpp:173-236),
+LogicBlock records (logic_block.cpp:156-372), verify-on-read
+(sync_backup.cpp:315-472), BlockChecker CRC-error accounting
+(block_checker.cpp:58-182) and compaction (task.cpp:713-836).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import crc as _crc
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "ds", "libtfs_ds.so")
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("dataserver harness not built: %s (run __graft_entry__.build())" % LIB_PATH)
+        _crc.lib()  # load libtfs_crc.so first (same process-wide instance)
+        L = ctypes.CDLL(LIB_PATH)
+        vp, u32, i32, u64, i64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_int64
+        sig = {
+            "tfs_ds_datafile_new": (vp, [vp, u64, ctypes.c_char_p]),
+            "tfs_ds_datafile_free": (None, [vp]),
+            "tfs_ds_datafile_set_data": (ctypes.c_int, [vp, vp, i32, i32]),
+            "tfs_ds_datafile_length": (i32, [vp]),
+            "tfs_ds_datafile_get_crc": (u32, [vp, ctypes.POINTER(ctypes.c_int)]),
+            "tfs_ds_block_new": (vp, [u32, i64]),
+            "tfs_ds_block_free": (None, [vp]),
+            "tfs_ds_block_size": (i64, [vp]),
+            "tfs_ds_block_data": (vp, [vp]),
+            "tfs_ds_block_set_flag": (ctypes.c_int, [vp, u64, i32]),
+            "tfs_ds_block_corrupt": (ctypes.c_int, [vp, i64, ctypes.c_uint8]),
+            "tfs_ds_block_metas": (ctypes.c_int, [vp, vp, vp, u32]),
+            "tfs_ds_close_write_file": (ctypes.c_int, [vp, u64, u32, vp]),
+            "tfs_ds_batcher_new": (vp, [vp, u32, ctypes.c_int]),
+            "tfs_ds_batcher_free": (None, [vp]),
+            "tfs_ds_batcher_batches": (u64, [vp]),
+            "tfs_ds_batcher_close": (ctypes.c_int, [vp, vp, u64, u32, vp]),
+            "tfs_ds_checker_new": (vp, [ctypes.c_int]),
+            "tfs_ds_checker_free": (None, [vp]),
+            "tfs_ds_checker_errors": (ctypes.c_int, [vp, u32]),
+            "tfs_ds_checker_needs_repair": (ctypes.c_int, [vp, u32]),
+            "tfs_ds_verify_block": (ctypes.c_int, [vp, vp, vp, u32, vp]),
+            "tfs_ds_compact_block": (ctypes.c_int, [vp, vp, vp, vp, u32]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+class DataFile:
+    """DataFile (src/dataserver/data_file.h:33-96)."""
+
+    def __init__(self, ctx, fn, tmp_dir="/tmp"):
+        self.h = lib().tfs_ds_datafile_new(ctx.handle, fn, tmp_dir.encode())
+
+    def set_data(self, data, offset):
+        b = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8))
+        return lib().tfs_ds_datafile_set_data(self.h, b.ctypes.data, b.size, offset)
+
+    def get_length(self):
+        return lib().tfs_ds_datafile_length(self.h)
+
+    def get_crc(self):
+        st = ctypes.c_int(0)
+        c = lib().tfs_ds_datafile_get_crc(self.h, ctypes.byref(st))
+        if st.value != 0:
+            raise _crc.TfsCrcError(st.value, "DataFile::get_crc")
+        return c
+
+    def free(self):
+        if self.h:
+            lib().tfs_ds_datafile_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class LogicBlock:
+    """One logical block: FileInfo|payload records + index (logic_block.cpp)."""
+
+    def __init__(self, block_id, capacity=1 << 40):
+        self.block_id = block_id
+        self.h = lib().tfs_ds_block_new(block_id, capacity)
+
+    def close_write_file(self, file_id, client_crc, df):
+        """DataManagement::close_write_file: 0, or EXIT_DATA_FILE_ERROR (-8013) on crc mismatch."""
+        return lib().tfs_ds_close_write_file(self.h, file_id, client_crc, df.h)
+
+    def raw(self):
+        n = lib().tfs_ds_block_size(self.h)
+        if n == 0:
+            return np.zeros(0, np.uint8)
+        p = lib().tfs_ds_block_data(self.h)
+        return np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(p)).copy()
+
+    def set_flag(self, file_id, flag):
+        return lib().tfs_ds_block_set_flag(self.h, file_id, flag)
+
+    def corrupt(self, offset, mask=1):
+        return lib().tfs_ds_block_corrupt(self.h, offset, mask)
+
+    def metas(self):
+        n = lib().tfs_ds_block_metas(self.h, None, None, 0)
+        m = np.zeros(n, _crc.META_DTYPE)
+        f = np.zeros(n, np.int32)
+        lib().tfs_ds_block_metas(self.h, m.ctypes.data, f.ctypes.data, n)
+        return m, f
+
+    def free(self):
+        if self.h:
+            lib().tfs_ds_block_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class CloseBatcher:
+    """Batches close_write_file CRC checks from many threads into one GPU verify."""
+
+    def __init__(self, ctx, max_batch=64, max_wait_us=200):
+        self.h = lib().tfs_ds_batcher_new(ctx.handle, max_batch, max_wait_us)
+
+    def close(self, block, file_id, client_crc, df):
+        return lib().tfs_ds_batcher_close(self.h, block.h, file_id, client_crc, df.h)
+
+    def batches(self):
+        return lib().tfs_ds_batcher_batches(self.h)
+
+    def free(self):
+        if self.h:
+            lib().tfs_ds_batcher_free(self.h)
+            self.h = None
+
+
+class BlockCrcChecker:
+    def __init__(self, max_crc_error_nums=4):
+        self.h = lib().tfs_ds_checker_new(max_crc_error_nums)
+
+    def errors(self, block_id):
+        return lib().tfs_ds_checker_errors(self.h, block_id)
+
+    def needs_repair(self, block_id):
+        return bool(lib().tfs_ds_checker_needs_repair(self.h, block_id))
+
+    def free(self):
+        if self.h:
+            lib().tfs_ds_checker_free(self.h)
+            self.h = None
+
+
+def verify_block(ctx, block, checker=None):
+    m, f = block.metas()
+    st = np.zeros(max(len(m), 1), np.int32)
+    nbad = lib().tfs_ds_verify_block(ctx.handle, block.h, st.ctypes.data, st.size, checker.h if checker else None)
+    live = (f & (_crc.FI_DELETED | _crc.FI_INVALID)) == 0
+    return nbad, st[:int(live.sum())]
+
+
+def compact_block(ctx, src, dest):
+    m, _ = src.metas()
+    ok = np.zeros(max(len(m), 1), np.uint8)
+    rc = lib().tfs_ds_compact_block(ctx.handle, src.h, dest.h, ok.ctypes.data, ok.size)
+    return rc, ok[:len(m)]

@@ -1,0 +1,337 @@
+// ds_harness.cpp -- see ds_harness.h.  Everything CRC goes through the C ABI.
+#include "ds_harness.h"
+
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <ctime>
+
+namespace tfs {
+namespace dataserver {
+
+namespace {
+constexpr int32_t kFileInfoSize = TFS_FILEINFO_SIZE;
+
+void put_file_info(char* dst, const tfs_file_info& fi) { memcpy(dst, &fi, kFileInfoSize); }
+}  // namespace
+
+// ---------------- DataFile (data_file.cpp) ----------------
+
+DataFile::DataFile(uint64_t fn, const std::string& tmp_dir, tfs_crc_ctx* ctx)
+    : data_(WRITE_DATA_TMPBUF_SIZE), ctx_(ctx) {
+  char name[512];
+  snprintf(name, sizeof name, "%s/%llu.dat", tmp_dir.c_str(), static_cast<unsigned long long>(fn));
+  tmp_file_name_ = name;
+}
+
+DataFile::~DataFile() { set_over(); }
+
+void DataFile::set_over() {
+  length_ = 0;
+  if (fd_ != -1) {
+    close(fd_);
+    unlink(tmp_file_name_.c_str());
+    fd_ = -1;
+  }
+}
+
+int DataFile::set_data(const char* data, int32_t len, int32_t offset) {
+  if (len <= 0) return TFS_SUCCESS;
+  const int32_t length = offset + len;
+  if (length > WRITE_DATA_TMPBUF_SIZE || length_ > WRITE_DATA_TMPBUF_SIZE) {  // spill (data_file.cpp:73-101)
+    if (fd_ == -1) {
+      fd_ = open(tmp_file_name_.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0600);
+      if (fd_ == -1) return -1;
+      if (write(fd_, data_.data(), length_) != length_) return -1;
+    }
+    if (lseek(fd_, offset, SEEK_SET) == -1) return -1;
+    if (write(fd_, data, len) != len) return -1;
+  } else {
+    memcpy(data_.data() + offset, data, len);
+  }
+  if (length > length_) length_ = length;
+  return len;
+}
+
+char* DataFile::get_data(char* data, int32_t* len, int32_t offset) {
+  if (offset >= length_) {
+    *len = -1;
+    return nullptr;
+  }
+  if (length_ > WRITE_DATA_TMPBUF_SIZE) {
+    if (fd_ == -1 || lseek(fd_, offset, SEEK_SET) == -1) {
+      *len = -1;
+      return nullptr;
+    }
+    if (data == nullptr) {
+      data = data_.data();
+      *len = WRITE_DATA_TMPBUF_SIZE;
+    }
+    const ssize_t r = read(fd_, data, *len);
+    if (r < 0) {
+      *len = -1;
+      return nullptr;
+    }
+    *len = int32_t(r);
+    return data;
+  }
+  if (data == nullptr) {
+    data = data_.data() + offset;
+    *len = length_ - offset;
+  } else {
+    if (*len > length_ - offset) *len = length_ - offset;
+    memcpy(data, data_.data() + offset, *len);
+  }
+  return data;
+}
+
+uint32_t DataFile::get_crc() {
+  status_ = TFS_SUCCESS;
+  if (crc_ == 0) {
+    if (length_ > WRITE_DATA_TMPBUF_SIZE) {  // data_file.cpp:172-187: re-read in 2 MiB chunks, running seed
+      if (fd_ == -1 || lseek(fd_, 0, SEEK_SET) == -1) return crc_;
+      ssize_t rlen;
+      while ((rlen = read(fd_, data_.data(), WRITE_DATA_TMPBUF_SIZE)) > 0) {
+        tfs_crc_desc d{0, uint32_t(rlen), crc_};
+        uint32_t out = 0;
+        status_ = tfs_crc32_batch(ctx_, &d, 1, data_.data(), uint64_t(rlen), &out);
+        if (status_ != TFS_SUCCESS) return 0;
+        crc_ = out;
+      }
+    } else {
+      status_ = tfs_datafile_get_crc(ctx_, data_.data(), length_, &crc_);
+      if (status_ != TFS_SUCCESS) crc_ = 0;
+    }
+  }
+  return crc_;
+}
+
+// ---------------- LogicBlockImage (logic_block.cpp) ----------------
+
+LogicBlockImage::LogicBlockImage(uint32_t block_id, int64_t capacity) : block_id_(block_id), capacity_(capacity) {}
+
+int LogicBlockImage::append_record(uint64_t file_id, const char* payload, int32_t len, uint32_t crc) {
+  if (len < 0) return TFS_EXIT_PARAMETER_ERROR;
+  const int64_t off = int64_t(data_.size());
+  tfs_file_info fi;
+  memset(&fi, 0, sizeof fi);
+  fi.id_ = file_id;
+  fi.offset_ = int32_t(off);
+  fi.size_ = len + kFileInfoSize;   // logic_block.cpp:173
+  fi.usize_ = fi.size_;             // :235
+  fi.modify_time_ = int32_t(time(nullptr));
+  fi.create_time_ = fi.modify_time_;
+  fi.flag_ = 0;
+  fi.crc_ = crc;                    // :177
+  data_.resize(size_t(off + fi.size_));
+  put_file_info(data_.data() + off, fi);
+  if (len) memcpy(data_.data() + off + kFileInfoSize, payload, size_t(len));
+  index_[file_id] = tfs_raw_meta{file_id, int32_t(off), fi.size_};
+  flags_[file_id] = 0;
+  return TFS_SUCCESS;
+}
+
+int LogicBlockImage::close_write_file(uint64_t file_id, DataFile& df, uint32_t crc) {
+  const int32_t file_size = df.get_length();
+  if (int64_t(data_.size()) + file_size + kFileInfoSize > capacity_) return TFS_EXIT_PARAMETER_ERROR;
+  std::vector<char> payload(static_cast<size_t>(file_size));
+  int32_t off = 0;
+  while (off < file_size) {  // logic_block.cpp:258-306: drain the DataFile
+    int32_t rl = file_size - off;
+    if (!df.get_data(payload.data() + off, &rl, off) || rl <= 0) return -1;
+    off += rl;
+  }
+  return append_record(file_id, payload.data(), file_size, crc);
+}
+
+int LogicBlockImage::read_file(uint64_t file_id, std::vector<char>& out) const {
+  auto it = index_.find(file_id);
+  if (it == index_.end()) return TFS_EXIT_FILE_INFO_ERROR;
+  out.assign(data_.begin() + it->second.offset, data_.begin() + it->second.offset + it->second.size);
+  return TFS_SUCCESS;
+}
+
+int LogicBlockImage::set_flag(uint64_t file_id, int32_t flag) {
+  auto it = flags_.find(file_id);
+  if (it == flags_.end()) return TFS_EXIT_FILE_INFO_ERROR;
+  it->second = flag;
+  return TFS_SUCCESS;
+}
+
+int32_t LogicBlockImage::flag_of(uint64_t file_id) const {
+  auto it = flags_.find(file_id);
+  return it == flags_.end() ? TFS_FI_INVALID : it->second;
+}
+
+std::vector<tfs_raw_meta> LogicBlockImage::sorted_metas() const {
+  std::vector<tfs_raw_meta> v;
+  v.reserve(index_.size());
+  for (auto& kv : index_) v.push_back(kv.second);
+  std::sort(v.begin(), v.end(), [](const tfs_raw_meta& a, const tfs_raw_meta& b) { return a.offset < b.offset; });
+  return v;
+}
+
+std::vector<int32_t> LogicBlockImage::sorted_flags() const {
+  std::vector<int32_t> f;
+  for (auto& m : sorted_metas()) f.push_back(flag_of(m.file_id));
+  return f;
+}
+
+void LogicBlockImage::replace(std::vector<char>&& data, const std::vector<tfs_raw_meta>& metas,
+                              const std::vector<int32_t>& flags) {
+  data_ = std::move(data);
+  index_.clear();
+  flags_.clear();
+  for (size_t i = 0; i < metas.size(); ++i) {
+    index_[metas[i].file_id] = metas[i];
+    flags_[metas[i].file_id] = i < flags.size() ? flags[i] : 0;
+  }
+}
+
+// ---------------- close path (data_management.cpp:173-236) ----------------
+
+int close_write_file(const CloseFileInfo& info, DataFile& df, LogicBlockImage& block) {
+  const uint32_t datafile_crc = df.get_crc();
+  if (df.last_status() != TFS_SUCCESS) return df.last_status();
+  if (info.crc_ != datafile_crc) return TFS_EXIT_DATA_FILE_ERROR;  // :197-198
+  return block.close_write_file(info.file_id_, df, datafile_crc);
+}
+
+CloseBatcher::CloseBatcher(tfs_crc_ctx* ctx, size_t max_batch, int max_wait_us)
+    : ctx_(ctx), max_batch_(max_batch ? max_batch : 1), max_wait_us_(max_wait_us), worker_([this] { run(); }) {}
+
+CloseBatcher::~CloseBatcher() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  worker_.join();
+}
+
+int CloseBatcher::close(const CloseFileInfo& info, DataFile& df, LogicBlockImage& block) {
+  Req r;
+  r.info = &info;
+  r.df = &df;
+  r.block = &block;
+  std::unique_lock<std::mutex> lk(mu_);
+  queue_.push_back(&r);
+  if (queue_.size() >= max_batch_) cv_.notify_all();
+  done_cv_.wait(lk, [&] { return r.done; });
+  return r.status;
+}
+
+void CloseBatcher::run() {
+  std::unique_lock<std::mutex> lk(mu_);
+  for (;;) {
+    cv_.wait_for(lk, std::chrono::microseconds(max_wait_us_), [&] { return stop_ || queue_.size() >= max_batch_; });
+    if (queue_.empty()) {
+      if (stop_) return;
+      continue;
+    }
+    std::vector<Req*> reqs;
+    reqs.swap(queue_);
+    lk.unlock();
+    flush(reqs);
+    lk.lock();
+    for (Req* r : reqs) r->done = true;
+    ++batches_;
+    done_cv_.notify_all();
+  }
+}
+
+void CloseBatcher::flush(std::vector<Req*>& reqs) {
+  // Gather every payload into one buffer, one GPU verify for the whole batch
+  // (expected = the client's CloseFileInfo.crc_).
+  std::vector<tfs_crc_vdesc> d(reqs.size());
+  uint64_t total = 0;
+  for (size_t i = 0; i < reqs.size(); ++i) total += uint64_t(reqs[i]->df->get_length());
+  std::vector<char> gathered(size_t(total) + 16);
+  uint64_t off = 0;
+  for (size_t i = 0; i < reqs.size(); ++i) {
+    DataFile& df = *reqs[i]->df;
+    const int32_t n = df.get_length();
+    int32_t got = 0;
+    while (got < n) {
+      int32_t rl = n - got;
+      if (!df.get_data(gathered.data() + off + got, &rl, got) || rl <= 0) break;
+      got += rl;
+    }
+    d[i] = tfs_crc_vdesc{off, uint32_t(n), reqs[i]->info->crc_};
+    off += uint64_t(n);
+  }
+  std::vector<uint32_t> crc(reqs.size());
+  std::vector<uint8_t> ok(reqs.size());
+  uint32_t nbad = 0;
+  const int rc = tfs_crc32_verify(ctx_, d.data(), uint32_t(reqs.size()), gathered.data(), total, crc.data(), ok.data(),
+                                  &nbad);
+  for (size_t i = 0; i < reqs.size(); ++i) {
+    Req& r = *reqs[i];
+    if (rc != TFS_SUCCESS && rc != TFS_EXIT_CHECK_CRC_ERROR) {
+      r.status = rc;
+    } else if (!ok[i]) {
+      r.status = TFS_EXIT_DATA_FILE_ERROR;  // data_management.cpp:198
+    } else {
+      r.status = r.block->append_record(r.info->file_id_, gathered.data() + d[i].offset, int32_t(d[i].len), crc[i]);
+    }
+  }
+}
+
+// ---------------- verify / checker / compact ----------------
+
+void BlockCrcChecker::add_crc_error(uint32_t block_id, uint64_t file_id) {
+  ++errors_[block_id];
+  repair_.emplace_back(block_id, file_id);
+}
+
+int BlockCrcChecker::crc_errors(uint32_t block_id) const {
+  auto it = errors_.find(block_id);
+  return it == errors_.end() ? 0 : it->second;
+}
+
+int verify_block(tfs_crc_ctx* ctx, const LogicBlockImage& block, std::vector<int32_t>* status,
+                 BlockCrcChecker* checker) {
+  std::vector<tfs_raw_meta> metas;
+  for (auto& m : block.sorted_metas())
+    if (!(block.flag_of(m.file_id) & (TFS_FI_DELETED | TFS_FI_INVALID))) metas.push_back(m);
+  std::vector<uint32_t> crc(metas.size());
+  std::vector<int32_t> st(metas.size());
+  uint32_t nbad = 0;
+  const int rc = tfs_block_verify(ctx, block.data().data(), uint64_t(block.data_size()), metas.data(),
+                                  uint32_t(metas.size()), crc.data(), st.data(), &nbad);
+  if (rc != TFS_SUCCESS && rc != TFS_EXIT_CHECK_CRC_ERROR) return rc;
+  if (checker)
+    for (size_t i = 0; i < metas.size(); ++i)
+      if (st[i] == TFS_EXIT_CHECK_CRC_ERROR) checker->add_crc_error(block.block_id(), metas[i].file_id);
+  if (status) *status = st;
+  return int(nbad);
+}
+
+int compact_block(tfs_crc_ctx* ctx, const LogicBlockImage& src, LogicBlockImage& dest, std::vector<uint8_t>* crc_ok) {
+  const std::vector<tfs_raw_meta> metas = src.sorted_metas();
+  const std::vector<int32_t> flags = src.sorted_flags();
+  uint64_t cap = 16;
+  for (auto& m : metas) cap += uint64_t(m.size);
+  std::vector<char> out(static_cast<size_t>(cap));
+  std::vector<tfs_raw_meta> dmetas(metas.size());
+  std::vector<uint8_t> ok(metas.size());
+  uint64_t dlen = 0;
+  uint32_t nlive = 0;
+  const int rc = tfs_block_compact(ctx, src.data().data(), uint64_t(src.data_size()), metas.data(), flags.data(),
+                                   uint32_t(metas.size()), out.data(), cap, dmetas.data(), ok.data(), &dlen, &nlive);
+  if (rc != TFS_SUCCESS && rc != TFS_EXIT_CHECK_CRC_ERROR) return rc;
+  out.resize(size_t(dlen));
+  dmetas.resize(nlive);
+  std::vector<int32_t> dflags;
+  for (size_t i = 0; i < metas.size(); ++i)
+    if (!(flags[i] & (TFS_FI_DELETED | TFS_FI_INVALID))) dflags.push_back(flags[i]);
+  dest.replace(std::move(out), dmetas, dflags);
+  if (crc_ok) *crc_ok = ok;
+  return rc;
+}
+
+}  // namespace dataserver
+}  // namespace tfs

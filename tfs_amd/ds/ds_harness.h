@@ -1,0 +1,165 @@
+// ds_harness.h -- dataserver-shaped host code that calls the CRC path only
+// through the C ABI (include/tfs_crc.h), exactly as TFS's dataserver call sites
+// would after the drop-in.  Host C++ only (no HIP): this is what a dataserver
+// links.  Names and semantics mirror the reference (simonsysu/tfs, TFS 2.3.0):
+//
+//   DataFile              src/dataserver/data_file.{h,cpp}        (write staging, get_crc)
+//   CloseFileInfo         src/common/internal.h:716-726
+//   LogicBlockImage       src/dataserver/logic_block.cpp:156-372  (FileInfo|payload records, index)
+//   close_write_file      src/dataserver/data_management.cpp:173-236 (crc compare, persist)
+//   CloseBatcher          the async batching queue across leases (SURVEY §7 "Batching vs. latency")
+//   verify_file/_block    src/dataserver/sync_backup.cpp:315-472, block_console.cpp:502-613
+//   BlockCrcChecker       src/dataserver/block_checker.cpp:58-182, block_status.h:40-52
+//   compact_block         src/dataserver/task.cpp:713-836 (+ re-CRC verify)
+#pragma once
+#include <condition_variable>
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/tfs_crc.h"
+
+namespace tfs {
+namespace dataserver {
+
+// DataFile (data_file.h:33-96): per-lease payload buffer, 2 MiB in memory,
+// spilled to work_dir/tmp/<fn>.dat beyond that (data_file.cpp:73-101).
+class DataFile {
+ public:
+  static const int32_t WRITE_DATA_TMPBUF_SIZE = 2 * 1024 * 1024;  // data_file.h:78
+
+  DataFile(uint64_t fn, const std::string& tmp_dir, tfs_crc_ctx* ctx);
+  ~DataFile();
+  DataFile(const DataFile&) = delete;
+  DataFile& operator=(const DataFile&) = delete;
+
+  // data_file.cpp:65-113: returns len on success, TFS_SUCCESS for len <= 0, <0 on error.
+  int set_data(const char* data, int32_t len, int32_t offset);
+  // data_file.cpp:115-166 (data == NULL: return the inner buffer).
+  char* get_data(char* data, int32_t* len, int32_t offset);
+  int32_t get_length() const { return length_; }
+  // data_file.cpp:168-194 on the GPU: seed 0; > 2 MiB re-read in 2 MiB chunks
+  // with the running crc as seed (each chunk one C-ABI call).  0 = "not
+  // computed" and is recomputed on the next call, as in the reference (:170).
+  uint32_t get_crc();
+  int last_status() const { return status_; }
+  void set_over();
+  const char* buffer() const { return data_.data(); }
+
+ private:
+  int32_t length_ = 0;
+  std::vector<char> data_;
+  uint32_t crc_ = 0;
+  int fd_ = -1;
+  std::string tmp_file_name_;
+  tfs_crc_ctx* ctx_;
+  int status_ = TFS_SUCCESS;
+};
+
+struct CloseFileInfo {  // internal.h:716-726
+  uint32_t block_id_ = 0;
+  uint64_t file_id_ = 0;
+  int32_t mode_ = 0;
+  uint32_t crc_ = 0;
+  uint64_t file_number_ = 0;
+};
+
+// The logical data area of one block (main + extension blocks stitched, as
+// DataHandle presents them: data_handle.cpp:103-141) plus its index.
+class LogicBlockImage {
+ public:
+  explicit LogicBlockImage(uint32_t block_id, int64_t capacity = 64LL * 1024 * 1024);
+  uint32_t block_id() const { return block_id_; }
+  // LogicBlock::close_write_file (logic_block.cpp:156-372), insert path:
+  // FileInfo{id, offset=data_offset, size=len+36, usize, mtime, ctime, flag=0, crc}|payload.
+  int close_write_file(uint64_t file_id, DataFile& df, uint32_t crc);
+  int append_record(uint64_t file_id, const char* payload, int32_t len, uint32_t crc);
+  // LogicBlock::read_file at offset 0 (logic_block.cpp:374-440): FileInfo|payload.
+  int read_file(uint64_t file_id, std::vector<char>& out) const;
+  int set_flag(uint64_t file_id, int32_t flag);
+  int32_t flag_of(uint64_t file_id) const;
+  // index in offset order (traverse_sorted_segment_meta, index_handle.cpp:870-878)
+  std::vector<tfs_raw_meta> sorted_metas() const;
+  std::vector<int32_t> sorted_flags() const;
+  const std::vector<char>& data() const { return data_; }
+  std::vector<char>& data() { return data_; }
+  int64_t data_size() const { return int64_t(data_.size()); }
+  void replace(std::vector<char>&& data, const std::vector<tfs_raw_meta>& metas, const std::vector<int32_t>& flags);
+
+ private:
+  uint32_t block_id_;
+  int64_t capacity_;
+  std::vector<char> data_;
+  std::map<uint64_t, tfs_raw_meta> index_;
+  std::map<uint64_t, int32_t> flags_;
+};
+
+// DataManagement::close_write_file (data_management.cpp:173-236): CRC compare
+// then persist with the computed crc.  EXIT_DATA_FILE_ERROR on mismatch.
+int close_write_file(const CloseFileInfo& info, DataFile& df, LogicBlockImage& block);
+
+// Batched closes across leases: many worker threads submit, one GPU batch
+// verifies all client CRCs (tfs_crc32_verify over the gathered payloads), then
+// each waiter gets the status close_write_file would have returned.
+class CloseBatcher {
+ public:
+  CloseBatcher(tfs_crc_ctx* ctx, size_t max_batch, int max_wait_us);
+  ~CloseBatcher();
+  // Blocks until this close has been checked (and persisted on success).
+  int close(const CloseFileInfo& info, DataFile& df, LogicBlockImage& block);
+  uint64_t batches() const { return batches_; }
+
+ private:
+  struct Req {
+    const CloseFileInfo* info;
+    DataFile* df;
+    LogicBlockImage* block;
+    int status = 1;
+    bool done = false;
+  };
+  void run();
+  void flush(std::vector<Req*>& reqs);
+  tfs_crc_ctx* ctx_;
+  size_t max_batch_;
+  int max_wait_us_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<Req*> queue_;
+  bool stop_ = false;
+  uint64_t batches_ = 0;
+  std::thread worker_;
+};
+
+// BlockChecker's CRC-error accounting (block_checker.cpp:58-182, block_status.h:40-52):
+// per-block crc_error_ counter; >= max_crc_error_nums_ (parameter.cpp:256, default 4)
+// marks the block for repair.
+class BlockCrcChecker {
+ public:
+  explicit BlockCrcChecker(int max_crc_error_nums = 4) : max_(max_crc_error_nums) {}
+  void add_crc_error(uint32_t block_id, uint64_t file_id);
+  int crc_errors(uint32_t block_id) const;
+  bool needs_repair(uint32_t block_id) const { return crc_errors(block_id) >= max_; }
+  std::vector<std::pair<uint32_t, uint64_t>> repair_queue() const { return repair_; }
+
+ private:
+  int max_;
+  std::map<uint32_t, int> errors_;
+  std::vector<std::pair<uint32_t, uint64_t>> repair_;
+};
+
+// Verify-on-read of every live file of a block (one GPU batch); per-file status
+// as sync_backup.cpp:419-435 / block_console.cpp:543-577.  Mismatches are
+// reported to `checker` (may be NULL).  Returns the number of bad files or <0.
+int verify_block(tfs_crc_ctx* ctx, const LogicBlockImage& block, std::vector<int32_t>* status,
+                 BlockCrcChecker* checker);
+
+// CompactTask::real_compact with re-CRC (task.cpp:713-836): dest receives the
+// live files repacked; crc_ok per source file (1 ok / 0 mismatch / 2 skipped).
+int compact_block(tfs_crc_ctx* ctx, const LogicBlockImage& src, LogicBlockImage& dest, std::vector<uint8_t>* crc_ok);
+
+}  // namespace dataserver
+}  // namespace tfs
