@@ -197,6 +197,29 @@ int tfs_block_compact(tfs_crc_ctx* ctx, const void* src_image, uint64_t src_len,
                       const int32_t* flags, uint32_t n, void* dest_image, uint64_t dest_cap, tfs_raw_meta* dest_metas,
                       uint8_t* crc_ok, uint64_t* dest_len, uint32_t* n_live);
 
+/* Many blocks in one call (the compaction task thread's queue): each job is
+ * tfs_block_compact's arguments plus its outputs.  Jobs are pipelined over
+ * several streams so the H2D copy of one block, the verify/repack kernels of
+ * the next and the D2H copy of another overlap.  Page-locked source/dest
+ * images (tfs_crc32_host_malloc_pinned) are copied directly; pageable ones are
+ * staged.  Returns the worst job status (TFS_EXIT_CHECK_CRC_ERROR if only CRC
+ * mismatches were found). */
+typedef struct tfs_block_job {
+  const void* src_image;
+  uint64_t src_len;
+  const tfs_raw_meta* metas;
+  const int32_t* flags;
+  uint32_t n;
+  void* dest_image;
+  uint64_t dest_cap;
+  tfs_raw_meta* dest_metas; /* out, n_live entries (may be NULL) */
+  uint8_t* crc_ok;          /* out, n entries (may be NULL) */
+  uint64_t dest_len;        /* out */
+  uint32_t n_live;          /* out */
+  int status;               /* out */
+} tfs_block_job;
+int tfs_blocks_compact(tfs_crc_ctx* ctx, tfs_block_job* jobs, uint32_t njobs);
+
 /* ---- test / bench helpers (not part of the dataserver boundary) -------- */
 
 /* Fill nbytes (multiple of 8) of device memory with the splitmix64 synthetic

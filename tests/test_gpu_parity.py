@@ -293,3 +293,60 @@ def test_cross_file_pipeline_many_files(oracle, variant, monkeypatch):
         assert bad.size == 0, [(int(i), int(lens[i]), int(offs[i]) % 16, int(seeds[i])) for i in bad[:10]]
     finally:
         ctx.close()
+
+
+def test_blocks_compact_pipelined_matches_oracle(gpu_ctx, oracle):
+    """Many blocks through the 3-stream compaction pipeline; every block's output
+    equals the oracle's real_compact restatement; pinned and pageable images."""
+    import ctypes
+    import tfs_amd.crc as crc
+    rng = np.random.default_rng(44)
+    nblk = 7
+    keep = []
+    jobs = (crc.BlockJob * nblk)()
+    expect = []
+    for b in range(nblk):
+        sizes = [65536] * 40 + [int(x) for x in rng.integers(1, 20000, 25)]
+        img, metas = _block_image(oracle, sizes, seed=60 + b)
+        flags = np.zeros(len(sizes), np.int32)
+        flags[b % 2::2] |= 1
+        flags[1::3] |= 2 if b % 3 == 0 else 0
+        if b == 4:
+            img[int(metas[3]["offset"]) + 50] ^= 4   # one corrupted live file (flags[3] live for b even)
+        if b % 2 == 0:
+            pin = crc.PinnedBuffer(gpu_ctx, img.size)
+            pin.array[:] = img
+            src = pin
+            src_ptr, src_arr = pin.ptr, pin.array
+        else:
+            src, src_ptr, src_arr = img, img.ctypes.data, img
+        cap = int(metas["size"].sum()) + 64
+        dest = np.zeros(cap, np.uint8)
+        dm = np.zeros(len(sizes), crc.META_DTYPE)
+        ok = np.zeros(len(sizes), np.uint8)
+        keep.append((src, img, metas, flags, dest, dm, ok))
+        j = jobs[b]
+        j.src_image, j.src_len, j.metas, j.flags, j.n = src_ptr, img.size, metas.ctypes.data, flags.ctypes.data, len(sizes)
+        j.dest_image, j.dest_cap, j.dest_metas, j.crc_ok = dest.ctypes.data, cap, dm.ctypes.data, ok.ctypes.data
+        n = len(sizes)
+        mo = metas["offset"].astype(np.int64)
+        ms = metas["size"].astype(np.int32)
+        odest = np.zeros(cap, np.uint8)
+        doff = np.zeros(n, np.int64)
+        dsz = np.zeros(n, np.int32)
+        ook = np.zeros(n, np.uint8)
+        w = oracle.oracle_compact(src_arr.ctypes.data, mo.ctypes.data, ms.ctypes.data, flags.ctypes.data, n,
+                                  odest.ctypes.data, doff.ctypes.data, dsz.ctypes.data, ook.ctypes.data)
+        expect.append((w, odest[:w].copy(), ook))
+    rc = gpu_ctx.blocks_compact(jobs)
+    assert rc == -1010
+    for b in range(nblk):
+        src, img, metas, flags, dest, dm, ok = keep[b]
+        w, odest, ook = expect[b]
+        assert jobs[b].dest_len == w
+        assert (dest[:w] == odest).all(), b
+        assert (ok == ook).all(), b
+        assert jobs[b].status == (-1010 if b == 4 else 0)
+    for k in keep:
+        if isinstance(k[0], crc.PinnedBuffer):
+            k[0].free()

@@ -44,13 +44,21 @@ EXPORTED = [
     "tfs_crc32_ctx_create", "tfs_crc32_ctx_destroy", "tfs_crc32_last_error", "tfs_crc32_device_count",
     "tfs_crc32", "tfs_crc32_e", "tfs_datafile_get_crc", "tfs_crc32_batch", "tfs_crc32_verify",
     "tfs_crc32_batch_device", "tfs_crc32_verify_device", "tfs_crc32_submit_verify", "tfs_crc32_wait",
-    "tfs_block_verify", "tfs_block_verify_device", "tfs_block_compact",
+    "tfs_block_verify", "tfs_block_verify_device", "tfs_block_compact", "tfs_blocks_compact",
     "tfs_crc32_synth_fill_device", "tfs_crc32_write_headers_device", "tfs_crc32_membench_device",
     "tfs_crc32_dev_malloc", "tfs_crc32_dev_free", "tfs_crc32_host_malloc_pinned", "tfs_crc32_host_free_pinned",
     "tfs_crc32_memcpy", "tfs_crc32_memset_device", "tfs_crc32_event_create", "tfs_crc32_event_record",
     "tfs_crc32_event_elapsed_ms", "tfs_crc32_event_destroy",
     "tfs_crc32_stream", "tfs_crc32_sync",
 ]
+
+
+class BlockJob(ctypes.Structure):
+    """tfs_block_job (include/tfs_crc.h)."""
+    _fields_ = [("src_image", ctypes.c_void_p), ("src_len", ctypes.c_uint64), ("metas", ctypes.c_void_p),
+                ("flags", ctypes.c_void_p), ("n", ctypes.c_uint32), ("dest_image", ctypes.c_void_p),
+                ("dest_cap", ctypes.c_uint64), ("dest_metas", ctypes.c_void_p), ("crc_ok", ctypes.c_void_p),
+                ("dest_len", ctypes.c_uint64), ("n_live", ctypes.c_uint32), ("status", ctypes.c_int)]
 
 
 class TfsCrcError(RuntimeError):
@@ -87,6 +95,7 @@ def lib():
             "tfs_block_verify": (ctypes.c_int, [vp, vp, u64, vp, u32, vp, vp, vp]),
             "tfs_block_verify_device": (ctypes.c_int, [vp, vp, u64, vp, u32, vp, vp, vp, vp]),
             "tfs_block_compact": (ctypes.c_int, [vp, vp, u64, vp, vp, u32, vp, u64, vp, vp, vp, vp]),
+            "tfs_blocks_compact": (ctypes.c_int, [vp, vp, u32]),
             "tfs_crc32_synth_fill_device": (ctypes.c_int, [vp, vp, u64, u64, u64, vp]),
             "tfs_crc32_write_headers_device": (ctypes.c_int, [vp, vp, vp, vp, vp, u64, u32, vp]),
             "tfs_crc32_membench_device": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, u32, u64, vp, ctypes.c_uint, vp]),
@@ -260,6 +269,12 @@ class Context:
         self._check(lib().tfs_block_verify_device(self.handle, _ptr(d_image), image_len, _ptr(d_metas), n,
                                                   _ptr(d_crc), _ptr(d_status), _ptr(d_nbad), stream),
                     "block_verify_device")
+
+    def blocks_compact(self, jobs):
+        """Pipelined compaction of many blocks; `jobs` is a ctypes array of BlockJob."""
+        rc = lib().tfs_blocks_compact(self.handle, ctypes.cast(jobs, ctypes.c_void_p), len(jobs))
+        self._check(rc, "blocks_compact", ok=(TFS_SUCCESS, TFS_EXIT_CHECK_CRC_ERROR))
+        return rc
 
     # ---- block images (host) -------------------------------------------------
     def block_verify(self, image, metas):

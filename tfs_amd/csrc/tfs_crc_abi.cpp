@@ -111,6 +111,25 @@ struct Slot {
 
 constexpr int kSlots = 4;
 
+struct CompactSlot {
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  DevBuf d_src, d_dst, d_aux;
+  PinBuf h_aux, h_status, h_stage;
+  std::vector<uint32_t> live_idx;
+  tfs_block_job* job = nullptr;
+  bool busy = false;
+  void release() {
+    d_src.release(); d_dst.release(); d_aux.release();
+    h_aux.release(); h_status.release(); h_stage.release();
+    if (done) (void)hipEventDestroy(done);
+    if (stream) (void)hipStreamDestroy(stream);
+    done = nullptr;
+    stream = nullptr;
+  }
+};
+constexpr int kCompactSlots = 3;
+
 }  // namespace
 
 struct tfs_crc_ctx {
@@ -120,6 +139,7 @@ struct tfs_crc_ctx {
   std::mutex mu;
   std::string last_error = "no error";
   Slot slots[kSlots];
+  CompactSlot cslots[kCompactSlots];
   uint64_t next_ticket = 1;
   int variant = 0;  // kernel variant (TFS_CRC_VARIANT, measurement knob; 0 = product default)
 };
@@ -325,6 +345,10 @@ int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx) {
   if (ctx->device >= 0) (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   for (auto& s : ctx->slots) s.release();
+  for (auto& cs : ctx->cslots) {
+    if (cs.stream) (void)hipStreamSynchronize(cs.stream);
+    cs.release();
+  }
   if (ctx->d_tables) (void)hipFree(ctx->d_tables);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -515,68 +539,149 @@ int tfs_block_verify(tfs_crc_ctx* ctx, const void* image, uint64_t image_len, co
   return bad ? TFS_EXIT_CHECK_CRC_ERROR : TFS_SUCCESS;
 }
 
+// ---- compaction pipeline --------------------------------------------------
+// Each block goes through its own slot/stream: H2D of the source image, verify
+// of the live files, repack kernel, D2H of the new image.  With kCompactSlots
+// slots the H2D of block i+1, the kernels of block i and the D2H of block i-1
+// overlap (PCIe is full duplex; the copy engines run beside the kernels).
+
+static int compact_enqueue(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job) {
+  const uint32_t n = job->n;
+  cs.job = job;
+  cs.live_idx.clear();
+  job->status = TFS_SUCCESS;
+  job->dest_len = 0;
+  job->n_live = 0;
+  if (n && (!job->src_image || !job->metas || !job->flags || !job->dest_image))
+    return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "null block job pointer");
+  // Host: new offsets in iteration order (task.cpp:753-768).
+  int64_t w = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const tfs_raw_meta& m = job->metas[i];
+    if (m.size <= TFS_FILEINFO_SIZE || m.offset < 0 || uint64_t(m.offset) + uint64_t(m.size) > job->src_len)
+      return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "meta %u out of range", i);
+    if (job->flags[i] & (TFS_FI_DELETED | TFS_FI_INVALID)) continue;
+    cs.live_idx.push_back(i);
+    w += m.size;
+  }
+  if (uint64_t(w) > job->dest_cap)
+    return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "dest_cap %llu < %lld", (unsigned long long)job->dest_cap,
+                   (long long)w);
+  const uint32_t nl = uint32_t(cs.live_idx.size());
+  const size_t mb = size_t(nl) * sizeof(RawMeta), fb = size_t(nl) * 4, ob = size_t(nl) * 8;
+  const size_t aux_bytes = ob + mb + fb + 64;
+  HIP_TRY(ctx, cs.h_aux.reserve(aux_bytes));
+  HIP_TRY(ctx, cs.d_aux.reserve(aux_bytes + 2 * fb + 64));
+  uint8_t* ha = static_cast<uint8_t*>(cs.h_aux.p);
+  int64_t* h_doff = reinterpret_cast<int64_t*>(ha);
+  RawMeta* h_metas = reinterpret_cast<RawMeta*>(ha + ob);
+  int32_t* h_flags = reinterpret_cast<int32_t*>(ha + ob + mb);
+  int64_t off = 0;
+  for (uint32_t k = 0; k < nl; ++k) {
+    const uint32_t i = cs.live_idx[k];
+    h_doff[k] = off;
+    h_metas[k] = RawMeta{job->metas[i].file_id, job->metas[i].offset, job->metas[i].size};
+    h_flags[k] = job->flags[i];
+    if (job->dest_metas) job->dest_metas[k] = tfs_raw_meta{job->metas[i].file_id, int32_t(off), job->metas[i].size};
+    off += job->metas[i].size;
+  }
+  uint8_t* da = static_cast<uint8_t*>(cs.d_aux.p);
+  int64_t* d_doff = reinterpret_cast<int64_t*>(da);
+  RawMeta* d_metas = reinterpret_cast<RawMeta*>(da + ob);
+  int32_t* d_flags = reinterpret_cast<int32_t*>(da + ob + mb);
+  uint32_t* d_crc = reinterpret_cast<uint32_t*>(da + ((aux_bytes + 15) & ~size_t(15)));
+  int32_t* d_status = reinterpret_cast<int32_t*>(d_crc + nl);
+  HIP_TRY(ctx, cs.d_src.reserve(job->src_len + 16));
+  HIP_TRY(ctx, cs.d_dst.reserve(uint64_t(w) + 16));
+  HIP_TRY(ctx, cs.h_status.reserve(fb + 4));
+  if (job->src_len) {
+    if (is_pinned_host(job->src_image)) {
+      HIP_TRY(ctx, hipMemcpyAsync(cs.d_src.p, job->src_image, job->src_len, hipMemcpyHostToDevice, cs.stream));
+    } else {
+      HIP_TRY(ctx, cs.h_stage.reserve(job->src_len));
+      memcpy(cs.h_stage.p, job->src_image, job->src_len);
+      HIP_TRY(ctx, hipMemcpyAsync(cs.d_src.p, cs.h_stage.p, job->src_len, hipMemcpyHostToDevice, cs.stream));
+    }
+  }
+  if (nl) {
+    HIP_TRY(ctx, hipMemcpyAsync(da, ha, ob + mb + fb, hipMemcpyHostToDevice, cs.stream));
+    const uint8_t* d_src = static_cast<const uint8_t*>(cs.d_src.p);
+    // Re-CRC of every live file (the verify the reference's real_compact does not do).
+    HIP_TRY(ctx, launch_block_verify(d_src, job->src_len, d_metas, nl, ctx->d_tables, d_crc, d_status, nullptr,
+                                     cs.stream));
+    HIP_TRY(ctx, launch_compact_copy(d_src, d_metas, d_flags, d_doff, nl, static_cast<uint8_t*>(cs.d_dst.p),
+                                     cs.stream));
+    HIP_TRY(ctx, hipMemcpyAsync(cs.h_status.p, d_status, fb, hipMemcpyDeviceToHost, cs.stream));
+    if (w) HIP_TRY(ctx, hipMemcpyAsync(job->dest_image, cs.d_dst.p, size_t(w), hipMemcpyDeviceToHost, cs.stream));
+  }
+  if (!cs.done) HIP_TRY(ctx, hipEventCreateWithFlags(&cs.done, hipEventDisableTiming));
+  HIP_TRY(ctx, hipEventRecord(cs.done, cs.stream));
+  job->dest_len = uint64_t(w);
+  job->n_live = nl;
+  cs.busy = true;
+  return TFS_SUCCESS;
+}
+
+static int compact_finish(tfs_crc_ctx* ctx, CompactSlot& cs) {
+  if (!cs.busy) return TFS_SUCCESS;
+  cs.busy = false;
+  HIP_TRY(ctx, hipEventSynchronize(cs.done));
+  tfs_block_job* job = cs.job;
+  const int32_t* st = static_cast<const int32_t*>(cs.h_status.p);
+  if (job->crc_ok)
+    for (uint32_t i = 0; i < job->n; ++i) job->crc_ok[i] = 2;  // skipped unless live
+  uint32_t bad = 0;
+  for (uint32_t k = 0; k < uint32_t(cs.live_idx.size()); ++k) {
+    const bool ok = st[k] == TFS_SUCCESS;
+    bad += ok ? 0u : 1u;
+    if (job->crc_ok) job->crc_ok[cs.live_idx[k]] = ok ? 1 : 0;
+  }
+  job->status = bad ? TFS_EXIT_CHECK_CRC_ERROR : TFS_SUCCESS;
+  return job->status;
+}
+
+int tfs_blocks_compact(tfs_crc_ctx* ctx, tfs_block_job* jobs, uint32_t njobs) {
+  if (!ctx || (njobs && !jobs)) return TFS_EXIT_PARAMETER_ERROR;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  for (auto& cs : ctx->cslots)
+    if (!cs.stream) HIP_TRY(ctx, hipStreamCreateWithFlags(&cs.stream, hipStreamNonBlocking));
+  int worst = TFS_SUCCESS;
+  auto note = [&](int rc) {
+    if (rc != TFS_SUCCESS && (worst == TFS_SUCCESS || worst == TFS_EXIT_CHECK_CRC_ERROR)) worst = rc;
+  };
+  for (uint32_t j = 0; j < njobs; ++j) {
+    CompactSlot& cs = ctx->cslots[j % kCompactSlots];
+    note(compact_finish(ctx, cs));
+    const int rc = compact_enqueue(ctx, cs, &jobs[j]);
+    if (rc != TFS_SUCCESS) {
+      jobs[j].status = rc;
+      note(rc);
+      if (rc != TFS_EXIT_PARAMETER_ERROR) break;  // device error: stop issuing
+    }
+  }
+  for (auto& cs : ctx->cslots) note(compact_finish(ctx, cs));
+  return worst;
+}
+
 int tfs_block_compact(tfs_crc_ctx* ctx, const void* src_image, uint64_t src_len, const tfs_raw_meta* metas,
                       const int32_t* flags, uint32_t n, void* dest_image, uint64_t dest_cap, tfs_raw_meta* dest_metas,
                       uint8_t* crc_ok, uint64_t* dest_len, uint32_t* n_live) {
-  if (!ctx || (n && (!src_image || !metas || !flags || !dest_image))) return TFS_EXIT_PARAMETER_ERROR;
-  // Host: new offsets in iteration order (task.cpp:753-768).
-  std::vector<int64_t> doff(n, -1);
-  std::vector<tfs_raw_meta> live;
-  live.reserve(n);
-  int64_t w = 0;
-  for (uint32_t i = 0; i < n; ++i) {
-    if (metas[i].size <= TFS_FILEINFO_SIZE || metas[i].offset < 0 ||
-        uint64_t(metas[i].offset) + uint64_t(metas[i].size) > src_len)
-      return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "meta %u out of range", i);
-    if (flags[i] & (TFS_FI_DELETED | TFS_FI_INVALID)) continue;
-    doff[i] = w;
-    live.push_back(tfs_raw_meta{metas[i].file_id, int32_t(w), metas[i].size});
-    w += metas[i].size;
-  }
-  if (uint64_t(w) > dest_cap) return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "dest_cap %llu < %lld", (unsigned long long)dest_cap, (long long)w);
-  std::lock_guard<std::mutex> g(ctx->mu);
-  HIP_TRY(ctx, hipSetDevice(ctx->device));
-  Slot* s = free_slot(ctx);
-  if (!s) return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "all %d slots busy", kSlots);
-  const uint8_t* d_src = nullptr;
-  int rc = stage_span(ctx, *s, src_image, 0, src_len, &d_src);
-  if (rc) return rc;
-  // aux: metas | flags | doff | crc | status ; dest in d_crc (reuse name loosely: separate buffers)
-  const size_t mb = size_t(n) * sizeof(RawMeta), fb = size_t(n) * 4, ob = size_t(n) * 8;
-  HIP_TRY(ctx, s->d_desc.reserve(mb + fb + ob + 2 * fb + 16));
-  uint8_t* aux = static_cast<uint8_t*>(s->d_desc.p);
-  RawMeta* d_metas = reinterpret_cast<RawMeta*>(aux);
-  int32_t* d_flags = reinterpret_cast<int32_t*>(aux + mb);
-  int64_t* d_doff = reinterpret_cast<int64_t*>(aux + ((mb + fb + 7) & ~size_t(7)));
-  uint32_t* d_crc = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(d_doff) + ob);
-  int32_t* d_status = reinterpret_cast<int32_t*>(d_crc + n);
-  HIP_TRY(ctx, s->d_aux.reserve(std::max<uint64_t>(uint64_t(w), 16)));
-  HIP_TRY(ctx, s->d_bad.reserve(4));
-  HIP_TRY(ctx, hipMemcpyAsync(d_metas, metas, mb, hipMemcpyHostToDevice, ctx->stream));
-  HIP_TRY(ctx, hipMemcpyAsync(d_flags, flags, fb, hipMemcpyHostToDevice, ctx->stream));
-  HIP_TRY(ctx, hipMemcpyAsync(d_doff, doff.data(), ob, hipMemcpyHostToDevice, ctx->stream));
-  HIP_TRY(ctx, hipMemsetAsync(s->d_bad.p, 0, 4, ctx->stream));
-  // Verify every file (skipped ones included; their verdict is overwritten below).
-  HIP_TRY(ctx, launch_block_verify(d_src, src_len, d_metas, n, ctx->d_tables, d_crc, d_status,
-                                   static_cast<uint32_t*>(s->d_bad.p), ctx->stream));
-  HIP_TRY(ctx, launch_compact_copy(d_src, d_metas, d_flags, d_doff, n, static_cast<uint8_t*>(s->d_aux.p), ctx->stream));
-  HIP_TRY(ctx, s->h_ok.reserve(size_t(n) * 4));
-  HIP_TRY(ctx, hipMemcpyAsync(s->h_ok.p, d_status, size_t(n) * 4, hipMemcpyDeviceToHost, ctx->stream));
-  if (w) HIP_TRY(ctx, hipMemcpyAsync(dest_image, s->d_aux.p, size_t(w), hipMemcpyDeviceToHost, ctx->stream));
-  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-  const int32_t* st = static_cast<const int32_t*>(s->h_ok.p);
-  uint32_t bad = 0;
-  for (uint32_t i = 0; i < n; ++i) {
-    uint8_t v;
-    if (doff[i] < 0) v = 2;
-    else v = st[i] == TFS_SUCCESS ? 1 : 0;
-    if (v == 0) ++bad;
-    if (crc_ok) crc_ok[i] = v;
-  }
-  if (dest_metas && !live.empty()) memcpy(dest_metas, live.data(), live.size() * sizeof(tfs_raw_meta));
-  if (dest_len) *dest_len = uint64_t(w);
-  if (n_live) *n_live = uint32_t(live.size());
-  return bad ? TFS_EXIT_CHECK_CRC_ERROR : TFS_SUCCESS;
+  tfs_block_job job;
+  memset(&job, 0, sizeof job);
+  job.src_image = src_image;
+  job.src_len = src_len;
+  job.metas = metas;
+  job.flags = flags;
+  job.n = n;
+  job.dest_image = dest_image;
+  job.dest_cap = dest_cap;
+  job.dest_metas = dest_metas;
+  job.crc_ok = crc_ok;
+  const int rc = tfs_blocks_compact(ctx, &job, 1);
+  if (dest_len) *dest_len = job.dest_len;
+  if (n_live) *n_live = job.n_live;
+  return rc;
 }
 
 // ---- test / bench helpers (not part of the dataserver boundary) ----------
