@@ -302,8 +302,9 @@ def main():
         dist.destroy_process_group()
 
 
-def ab_compare(args, crc, img, d_vdesc, nfiles, d_ok, d_bad):
+def ab_compare(args, crc, img, d_vdesc, nfiles, d_ok, d_bad, mode=1, algo_bytes=None, d_out=None):
     """Rule: perf deltas come from interleaved rounds in one process on one device."""
+    algo_bytes = algo_bytes if algo_bytes is not None else nfiles * ALGO_BYTES_PER_FILE
     variants = [int(v) for v in args.ab.split(",") if v != ""]
     ctxs = {}
     for v in variants:
@@ -315,17 +316,23 @@ def ab_compare(args, crc, img, d_vdesc, nfiles, d_ok, d_bad):
         for v in variants:
             c = ctxs[v]
             e0, e1 = crc.Event(c), crc.Event(c)
-            c.verify_device(d_vdesc, nfiles, img, None, d_ok, d_bad)
+
+            def run():
+                if mode == 1:
+                    c.verify_device(d_vdesc, nfiles, img, None, d_ok, d_bad)
+                else:
+                    c.batch_device(d_vdesc, nfiles, img, d_out)
+            run()
             e0.record()
             for _ in range(3):
-                c.verify_device(d_vdesc, nfiles, img, None, d_ok, d_bad)
+                run()
             e1.record()
             times[v].append(e0.elapsed_ms(e1) / 3)
     out = {}
     for v in variants:
         ms = sorted(times[v])
         out[v] = {"median_ms": ms[len(ms) // 2], "min_ms": ms[0],
-                  "frac_at_median": nfiles * ALGO_BYTES_PER_FILE / (ms[len(ms) // 2] / 1e3) / 1e9 / HBM_PEAK_GBS}
+                  "frac_at_median": algo_bytes / (ms[len(ms) // 2] / 1e3) / 1e9 / HBM_PEAK_GBS}
         ctxs[v].close()
     print(json.dumps({"ab": out}), file=sys.stderr)
 
@@ -440,6 +447,9 @@ def bench_zipf(args):
         h = img.download(np.uint8, int(lens[i]), int(offs[i])).tobytes()
         if ora.oracle_crc(0, h, len(h)) != int(got[i]):
             raise SystemExit("zipf: GPU CRC disagrees with oracle at file %d" % i)
+    if args.ab:
+        ab_compare(args, crc, img, d_desc, n, None, None, mode=0,
+                   algo_bytes=float(lens.astype(np.float64).sum()) + 21.0 * n, d_out=d_out)
     ev = [(crc.Event(ctx), crc.Event(ctx)) for _ in range(args.steps)]
     if dist:
         dist.barrier()

@@ -1,8 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out/w
-
-
-
-timeout -k 10 300 python bench.py --workload compact --compact-blocks 4096 > gpurun_out/w/compact.log 2> gpurun_out/w/compact.err || exit 4
-timeout -k 10 300 python bench.py --workload e2e --compact-blocks 1024 > gpurun_out/w/e2e.log 2> gpurun_out/w/e2e.err || exit 5
-TFS_BENCH_SHARE_DEVICE=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 8 --warmup 2 --blocks 512 > gpurun_out/w/verify_n2.log 2> gpurun_out/w/verify_n2.err || exit 6
+timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || exit 1
+timeout -k 10 300 python bench.py --steps 4 --warmup 1 --no-cpu --ab 0,1,2,3,5,6 --ab-rounds 5 > gpurun_out/w/ab_verify.log 2> gpurun_out/w/ab_verify.err || exit 2
+timeout -k 10 300 python bench.py --workload zipf --steps 4 --warmup 1 --ab 0,1,2,3,5,6 --ab-rounds 5 > gpurun_out/w/ab_zipf.log 2> gpurun_out/w/ab_zipf.err || exit 3

@@ -23,7 +23,8 @@
 
 namespace tfscrc {
 hipError_t launch_crc_files(int mode, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
-                            uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, hipStream_t stream, int variant);
+                            uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
+                            int variant);
 hipError_t launch_block_verify(const uint8_t* image, uint64_t image_len, const RawMeta* metas, uint32_t n,
                                const Tables* tg, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
                                hipStream_t stream);
@@ -129,6 +130,7 @@ struct CompactSlot {
   }
 };
 constexpr int kCompactSlots = 3;
+constexpr uint32_t kSchedSlots = 256;
 
 }  // namespace
 
@@ -141,6 +143,10 @@ struct tfs_crc_ctx {
   Slot slots[kSlots];
   CompactSlot cslots[kCompactSlots];
   uint64_t next_ticket = 1;
+  // Work-distribution counters: kSchedSlots slots of 8 counters (one 256-byte
+  // line per counter), one slot per launch, zeroed on the launch stream first.
+  uint32_t* d_sched = nullptr;
+  std::atomic<uint32_t> sched_seq{0};
   int variant = 0;  // kernel variant (TFS_CRC_VARIANT, measurement knob; 0 = product default)
 };
 
@@ -223,6 +229,13 @@ int stage_span(tfs_crc_ctx* ctx, Slot& s, const void* base, uint64_t lo, uint64_
   return TFS_SUCCESS;
 }
 
+// A zeroed scheduler slot for one launch on `st` (see tfs_crc_ctx::d_sched).
+hipError_t sched_slot(tfs_crc_ctx* ctx, hipStream_t st, uint32_t** out) {
+  const uint32_t k = ctx->sched_seq.fetch_add(1) % kSchedSlots;
+  *out = ctx->d_sched + (kSchedSlotBytes / 4u) * k;
+  return hipMemsetAsync(*out, 0, kSchedSlotBytes, st);
+}
+
 Slot* free_slot(tfs_crc_ctx* ctx) {
   for (auto& s : ctx->slots)
     if (!s.busy) return &s;
@@ -252,9 +265,11 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
   HIP_TRY(ctx, s.d_aux.reserve(16));
   HIP_TRY(ctx, hipMemcpyAsync(s.d_desc.p, d, size_t(n) * sizeof(Desc), hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(ctx, hipMemsetAsync(s.d_bad.p, 0, 4, ctx->stream));
+  uint32_t* sched = nullptr;
+  HIP_TRY(ctx, sched_slot(ctx, ctx->stream, &sched));
   HIP_TRY(ctx, launch_crc_files(mode, d_base, static_cast<const Desc*>(s.d_desc.p), n, ctx->d_tables,
                                 static_cast<uint32_t*>(s.d_crc.p), static_cast<uint8_t*>(s.d_ok.p),
-                                static_cast<uint32_t*>(s.d_bad.p), ctx->stream, ctx->variant));
+                                static_cast<uint32_t*>(s.d_bad.p), sched, ctx->stream, ctx->variant));
   HIP_TRY(ctx, hipMemcpyAsync(s.h_crc.p, s.d_crc.p, size_t(n) * 4, hipMemcpyDeviceToHost, ctx->stream));
   if (mode == 1) {
     HIP_TRY(ctx, hipMemcpyAsync(s.h_ok.p, s.d_ok.p, n, hipMemcpyDeviceToHost, ctx->stream));
@@ -335,6 +350,8 @@ int tfs_crc32_ctx_create(int device, tfs_crc_ctx** out) {
     if (e != hipSuccess) { rc = set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "hipMalloc(tables): %s", hipGetErrorString(e)); break; }
     e = hipMemcpy(ctx->d_tables, host.data(), sizeof(Tables), hipMemcpyHostToDevice);
     if (e != hipSuccess) { rc = set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "hipMemcpy(tables): %s", hipGetErrorString(e)); break; }
+    e = hipMalloc(reinterpret_cast<void**>(&ctx->d_sched), size_t(kSchedSlots) * kSchedSlotBytes);
+    if (e != hipSuccess) { rc = set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "hipMalloc(sched): %s", hipGetErrorString(e)); break; }
   } while (0);
   *out = ctx;  // returned even on failure so the caller can read last_error; destroy it
   return rc;
@@ -350,6 +367,7 @@ int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx) {
     cs.release();
   }
   if (ctx->d_tables) (void)hipFree(ctx->d_tables);
+  if (ctx->d_sched) (void)hipFree(ctx->d_sched);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return TFS_SUCCESS;
@@ -436,8 +454,10 @@ int tfs_crc32_batch_device(tfs_crc_ctx* ctx, const tfs_crc_desc* d_desc, uint32_
   if (!ctx || (n && (!d_desc || !d_base || !d_out_crc))) return TFS_EXIT_PARAMETER_ERROR;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  uint32_t* sched = nullptr;
+  HIP_TRY(ctx, sched_slot(ctx, st, &sched));
   HIP_TRY(ctx, launch_crc_files(0, static_cast<const uint8_t*>(d_base), reinterpret_cast<const Desc*>(d_desc), n,
-                                ctx->d_tables, d_out_crc, nullptr, nullptr, st, ctx->variant));
+                                ctx->d_tables, d_out_crc, nullptr, nullptr, sched, st, ctx->variant));
   return TFS_SUCCESS;
 }
 
@@ -446,8 +466,10 @@ int tfs_crc32_verify_device(tfs_crc_ctx* ctx, const tfs_crc_vdesc* d_desc, uint3
   if (!ctx || (n && (!d_desc || !d_base))) return TFS_EXIT_PARAMETER_ERROR;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  uint32_t* sched = nullptr;
+  HIP_TRY(ctx, sched_slot(ctx, st, &sched));
   HIP_TRY(ctx, launch_crc_files(1, static_cast<const uint8_t*>(d_base), reinterpret_cast<const Desc*>(d_desc), n,
-                                ctx->d_tables, d_out_crc, d_out_ok, d_n_bad, st, ctx->variant));
+                                ctx->d_tables, d_out_crc, d_out_ok, d_n_bad, sched, st, ctx->variant));
   return TFS_SUCCESS;
 }
 

@@ -33,6 +33,11 @@ template <bool S8> struct LdsLayout {
 
 constexpr int kFileInfoSize = 36;  // sizeof(FileInfo), internal.h:432-446
 
+// Dynamic work distribution: 8 ticket counters per launch, each on its own
+// 256-byte line (atomics to one line serialise: ~88 per us for the whole line).
+constexpr uint32_t kSchedStride = 64;                    // u32 between counters
+constexpr uint32_t kSchedSlotBytes = 8u * kSchedStride * 4u;  // 2 KiB per launch
+
 // TFS status codes (src/common/error_msg.h)
 constexpr int32_t kSuccess = 0;
 constexpr int32_t kExitCheckCrcError = -1010;

@@ -342,46 +342,92 @@ constexpr int kRun = 16;  // product configuration (see DESIGN.md §4 for the sw
 constexpr int kPF = 5;
 constexpr bool kNT = true;
 constexpr bool kPAR = false;
+constexpr bool kDYN = true;
 constexpr bool kS8 = true;
+
+// Work distribution.  Static: wave w takes files w, w+W, w+2W, ... (W = all
+// waves) -- ideal when every file has the same size.  Dynamic: eight ticket
+// counters (one per group of workgroups, blockIdx % 8, i.e. one per XCD under
+// round-robin placement) each own 1/8 of the files in order; a wave takes the
+// next ticket of its group and steals from the other groups once its own is
+// exhausted, so waves finish together for any size distribution (the kernel
+// ends with its slowest wave).  The ticket for the next-but-one file is taken
+// one file ahead, so the atomic's latency hides under a file's work.
+struct Tickets {
+  uint32_t* ctr;  // 8 zeroed counters for this launch, kSchedStride u32 apart (one per 256-byte line)
+  uint32_t n, group;
+  __device__ __forceinline__ uint32_t gbegin(uint32_t g) const { return uint32_t((uint64_t(n) * g) >> 3); }
+  __device__ __forceinline__ uint32_t gcount(uint32_t g) const { return gbegin(g + 1) - gbegin(g); }
+  // Issue the atomic of the home group in lane 0; the result stays in lane 0's register.
+  __device__ __forceinline__ uint32_t issue(int lane) const {
+    uint32_t j = 0;
+    if (lane == 0) j = atomicAdd(&ctr[group * kSchedStride], 1u);
+    return j;
+  }
+  // Turn an issued ticket into a file index (n = no work left).
+  __device__ __forceinline__ uint32_t resolve(uint32_t jv, int lane) {
+    uint32_t j = __builtin_amdgcn_readlane(jv, 0);
+    for (uint32_t tries = 0;; ++tries) {
+      if (j < gcount(group)) return gbegin(group) + j;
+      if (tries == 7) return n;
+      group = (group + 1) & 7u;  // steal
+      uint32_t k = 0;
+      if (lane == 0) k = atomicAdd(&ctr[group * kSchedStride], 1u);
+      j = __builtin_amdgcn_readlane(k, 0);
+    }
+  }
+};
 
 // MODE 0: compute (aux = seed) -> out_crc.  MODE 1: verify (aux = expected, seed 0).
 // Files are software-pipelined per wave: the next file's stripe-0/tail words
 // and its first PF stripes are in flight while this file's lane chains are
 // combined, so HBM never waits on a file boundary.
-template <int MODE, int RUN, int PF, bool NT, bool PAR, bool S8>
+template <int MODE, int RUN, int PF, bool NT, bool DYN, bool S8>
 __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __restrict__ base,
                                                            const Desc* __restrict__ desc, uint32_t n,
                                                            const Tables* __restrict__ tg, uint32_t* out_crc,
-                                                           uint8_t* out_ok, uint32_t* n_bad) {
-  static_assert(!PAR, "parallel-shift form retired (DESIGN.md §4)");
+                                                           uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched) {
   __shared__ uint32_t lds_tables[LdsLayout<S8>::bytes / 4];
-  load_tables<RUN, PAR, S8>(lds_tables, tg);
+  load_tables<RUN, false, S8>(lds_tables, tg);
   const int lane = threadIdx.x & (kWave - 1);
   const LaneBase lb = lane_base_of(lane);
   const uint32_t wpb = kBlock / kWave;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t stride = gridDim.x * wpb;
-  uint32_t f = blockIdx.x * wpb + wave;
-  if (f >= n) return;
+  Tickets tk{sched, n, blockIdx.x & 7u};
+  uint32_t f, fn;
+  if (DYN) {
+    f = tk.resolve(tk.issue(lane), lane);
+    if (f >= n) return;
+    fn = tk.resolve(tk.issue(lane), lane);
+  } else {
+    f = blockIdx.x * wpb + wave;
+    if (f >= n) return;
+    fn = f + stride;
+  }
   Desc cur = desc[f];
   FileGeo<RUN> g = make_geo<RUN>(base + cur.offset, cur.len, MODE == 0 ? cur.aux : 0u);
   Head<RUN> h = load_head<RUN>(g, lane);
   uint4 buf[PF][RUN / 16];
   load_ring<RUN, PF, NT>(g, lane, buf);
-  Desc nxt = f + stride < n ? desc[f + stride] : Desc{0, 0, 0};
+  Desc nxt = fn < n ? desc[fn] : Desc{0, 0, 0};
+  uint32_t jv = DYN && fn < n ? tk.issue(lane) : 0u;  // ticket of the file after next, in flight
   uint32_t bad = 0;
   for (;;) {
     const uint32_t c = g.nstripes ? lane_chain<RUN, PF, NT, S8>(lds_tables, lb, g, h, buf, lane) : 0u;
     // Start the next file's loads before combining this one.
-    const bool more = f + stride < n;
+    const bool more = fn < n;
     FileGeo<RUN> ng = g;
     Head<RUN> nh = h;
     const Desc ncur = nxt;
+    uint32_t fnn = n;
     if (more) {
       ng = make_geo<RUN>(base + ncur.offset, ncur.len, MODE == 0 ? ncur.aux : 0u);
       nh = load_head<RUN>(ng, lane);
       load_ring<RUN, PF, NT>(ng, lane, buf);
-      if (f + 2 * stride < n) nxt = desc[f + 2 * stride];
+      fnn = DYN ? tk.resolve(jv, lane) : fn + stride;
+      if (fnn < n) nxt = desc[fnn];
+      if (DYN && fnn < n) jv = tk.issue(lane);
     }
     const uint32_t crc = finish_file<RUN, S8>(lds_tables, lb, g, h, c, lane);
     if (lane == 0) {
@@ -393,7 +439,8 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
       }
     }
     if (!more) break;
-    f += stride;
+    f = fn;
+    fn = fnn;
     cur = ncur;
     g = ng;
     h = nh;
@@ -584,29 +631,31 @@ static unsigned grid_for(uint32_t nwork) {
 // product default is kRun/kPF; TFS_CRC_VARIANT selects another for measurement.
 template <int MODE>
 static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
-                                 uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, hipStream_t stream) {
+                                 uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched,
+                                 hipStream_t stream) {
   const dim3 grid(grid_for(n)), block(kBlock);
-#define TFS_LAUNCH(R, P, N, Q, S)                                                                          \
-  hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N, Q, S>), grid, block, 0, stream, base, desc, n, tg, out_crc, \
-                     out_ok, n_bad)
+#define TFS_LAUNCH(R, P, N, D, S)                                                                          \
+  hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N, D, S>), grid, block, 0, stream, base, desc, n, tg, out_crc, \
+                     out_ok, n_bad, sched)
   switch (variant) {
-    case 1: TFS_LAUNCH(16, 8, true, false, true); break;
-    case 2: TFS_LAUNCH(16, 4, true, false, true); break;
-    case 3: TFS_LAUNCH(16, 5, true, false, true); break;
-    case 4: TFS_LAUNCH(16, 7, true, false, true); break;
-    case 5: TFS_LAUNCH(16, 6, true, false, false); break;
-    case 6: TFS_LAUNCH(16, 3, true, false, true); break;
-    default: TFS_LAUNCH(kRun, kPF, kNT, kPAR, kS8); break;
+    case 1: TFS_LAUNCH(16, 5, true, false, true); break;
+    case 2: TFS_LAUNCH(16, 4, true, true, true); break;
+    case 3: TFS_LAUNCH(16, 6, true, true, true); break;
+    case 4: TFS_LAUNCH(16, 5, true, true, false); break;
+    case 5: TFS_LAUNCH(16, 8, true, true, true); break;
+    case 6: TFS_LAUNCH(16, 3, true, true, true); break;
+    default: TFS_LAUNCH(kRun, kPF, kNT, kDYN, kS8); break;
   }
 #undef TFS_LAUNCH
   return hipGetLastError();
 }
 
 hipError_t launch_crc_files(int mode, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
-                            uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, hipStream_t stream, int variant) {
+                            uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
+                            int variant) {
   if (n == 0) return hipSuccess;
-  if (mode == 0) return launch_variant<0>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, stream);
-  return launch_variant<1>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, stream);
+  if (mode == 0) return launch_variant<0>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, sched, stream);
+  return launch_variant<1>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, sched, stream);
 }
 
 hipError_t launch_block_verify(const uint8_t* image, uint64_t image_len, const RawMeta* metas, uint32_t n,
