@@ -215,27 +215,33 @@ __device__ __forceinline__ Head<RUN> load_head(const FileGeo<RUN>& g, int lane) 
   return h;
 }
 
-// Stripes 1.. of a file: PF stripes in flight per lane.
+// Stripes 1.. of a file: PF stripes in flight per lane.  Ring slots past the
+// file's last stripe load a fixed, always L2-resident 64*RUN-byte region
+// (`junk`, the global copy of the slice tables) instead: the steady state stays
+// branch-free (so the compiler's vmcnt waits stay counted) without fetching
+// anything from HBM twice.  The wave-uniform part of the address is a scalar
+// select.
+template <int RUN>
+__device__ __forceinline__ uintptr_t stripe_base(const FileGeo<RUN>& g, uint32_t st, uintptr_t junk) {
+  return (st >= 1u && st < g.nstripes) ? g.sb0 + uintptr_t(st) * (64u * RUN) : junk;
+}
+
 template <int RUN, int PF, bool NT>
-__device__ __forceinline__ void load_ring(const FileGeo<RUN>& g, int lane, uint4 (&buf)[PF][RUN / 16]) {
-  constexpr uint32_t kStripe = 64u * RUN;
-  const uintptr_t lane_base = g.sb0 + uintptr_t(lane) * RUN;
-  const uint32_t last = g.nstripes > 1 ? g.nstripes - 1 : 0u;
-  // files with <= 1 stripe point the (unused) ring at the file start: in bounds
-  const uintptr_t base = g.nstripes > 1 ? lane_base : (g.start & ~uintptr_t(15));
+__device__ __forceinline__ void load_ring(const FileGeo<RUN>& g, int lane, uint4 (&buf)[PF][RUN / 16],
+                                          uintptr_t junk) {
 #pragma unroll
   for (int f = 0; f < PF; ++f) {
-    const uint32_t st = (1u + f) < last ? (1u + f) : last;
+    const uintptr_t sb = stripe_base<RUN>(g, 1u + f, junk) + uintptr_t(lane) * RUN;
 #pragma unroll
-    for (int v = 0; v < RUN / 16; ++v)
-      buf[f][v] = ld128s<NT>(g.nstripes > 1 ? base + uintptr_t(st) * kStripe + 16u * v : base);
+    for (int v = 0; v < RUN / 16; ++v) buf[f][v] = ld128s<NT>(sb + 16u * v);
   }
 }
 
 // The lane's chain over stripes 0..nstripes-1 (before the final combine).
 template <int RUN, int PF, bool NT, bool S8>
 __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase& lb, const FileGeo<RUN>& g,
-                                               const Head<RUN>& h, uint4 (&buf)[PF][RUN / 16], int lane) {
+                                               const Head<RUN>& h, uint4 (&buf)[PF][RUN / 16], int lane,
+                                               uintptr_t junk) {
   constexpr uint32_t kStripe = 64u * RUN;
   constexpr int kVec = RUN / 16;
   // Stripe 0: mask the bytes before `start` in the dword at A and inject the
@@ -259,11 +265,8 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
     }
   }
   if (g.nstripes > 1) {
-    const uintptr_t lane_base = g.sb0 + uintptr_t(lane) * RUN;
-    const uint32_t last = g.nstripes - 1;
     // Full groups of PF stripes: straight-line, every buffer consumed then
-    // refilled (loads past the last stripe are clamped to it: an L2 re-read,
-    // never out of bounds, and the compiler's vmcnt waits stay counted).
+    // refilled (past the last stripe: the L2-resident `junk` region).
     uint32_t r = 1;
     for (; r + PF <= g.nstripes; r += PF) {
 #pragma unroll
@@ -275,10 +278,9 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
         }
 #pragma unroll
         for (int v = 0; v < kVec; ++v) c = steps16(T, lb, c, buf[f][v]);
-        const uint32_t nx = r + f + PF;
-        const uint32_t st = nx < last ? nx : last;
+        const uintptr_t sb = stripe_base<RUN>(g, r + f + PF, junk) + uintptr_t(lane) * RUN;
 #pragma unroll
-        for (int v = 0; v < kVec; ++v) buf[f][v] = ld128s<NT>(lane_base + uintptr_t(st) * kStripe + 16u * v);
+        for (int v = 0; v < kVec; ++v) buf[f][v] = ld128s<NT>(sb + 16u * v);
       }
     }
     // Remaining 0..PF-1 stripes are already in buf[0..].
@@ -328,13 +330,13 @@ __device__ __forceinline__ uint32_t finish_file(const uint32_t* T, const LaneBas
 // Single-file form (used by the block-verify kernel).
 template <int RUN, int PF, bool NT, bool S8>
 __device__ __forceinline__ uint32_t wave_crc(const uint32_t* T, const uint8_t* p, uint32_t len, uint32_t seed,
-                                             int lane) {
+                                             int lane, uintptr_t junk) {
   const LaneBase lb = lane_base_of(lane);
   const FileGeo<RUN> g = make_geo<RUN>(p, len, seed);
   const Head<RUN> h = load_head<RUN>(g, lane);
   uint4 buf[PF][RUN / 16];
-  load_ring<RUN, PF, NT>(g, lane, buf);
-  const uint32_t c = g.nstripes ? lane_chain<RUN, PF, NT, S8>(T, lb, g, h, buf, lane) : 0u;
+  load_ring<RUN, PF, NT>(g, lane, buf, junk);
+  const uint32_t c = g.nstripes ? lane_chain<RUN, PF, NT, S8>(T, lb, g, h, buf, lane, junk) : 0u;
   return finish_file<RUN, S8>(T, lb, g, h, c, lane);
 }
 
@@ -408,13 +410,14 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
   Desc cur = desc[f];
   FileGeo<RUN> g = make_geo<RUN>(base + cur.offset, cur.len, MODE == 0 ? cur.aux : 0u);
   Head<RUN> h = load_head<RUN>(g, lane);
+  const uintptr_t junk = reinterpret_cast<uintptr_t>(tg->slice);
   uint4 buf[PF][RUN / 16];
-  load_ring<RUN, PF, NT>(g, lane, buf);
+  load_ring<RUN, PF, NT>(g, lane, buf, junk);
   Desc nxt = fn < n ? desc[fn] : Desc{0, 0, 0};
   uint32_t jv = DYN && fn < n ? tk.issue(lane) : 0u;  // ticket of the file after next, in flight
   uint32_t bad = 0;
   for (;;) {
-    const uint32_t c = g.nstripes ? lane_chain<RUN, PF, NT, S8>(lds_tables, lb, g, h, buf, lane) : 0u;
+    const uint32_t c = g.nstripes ? lane_chain<RUN, PF, NT, S8>(lds_tables, lb, g, h, buf, lane, junk) : 0u;
     // Start the next file's loads before combining this one.
     const bool more = fn < n;
     FileGeo<RUN> ng = g;
@@ -424,7 +427,7 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
     if (more) {
       ng = make_geo<RUN>(base + ncur.offset, ncur.len, MODE == 0 ? ncur.aux : 0u);
       nh = load_head<RUN>(ng, lane);
-      load_ring<RUN, PF, NT>(ng, lane, buf);
+      load_ring<RUN, PF, NT>(ng, lane, buf, junk);
       fnn = DYN ? tk.resolve(jv, lane) : fn + stride;
       if (fnn < n) nxt = desc[fnn];
       if (DYN && fnn < n) jv = tk.issue(lane);
@@ -474,7 +477,8 @@ __global__ void __launch_bounds__(kBlock) block_verify_kernel(const uint8_t* __r
       // 36-byte header at an arbitrary byte offset: byte-wise read, same in all lanes.
       uint8_t* hb = reinterpret_cast<uint8_t*>(&h);
       for (int i = 0; i < kFileInfoSize; ++i) hb[i] = rec[i];
-      c = wave_crc<kRun, kPF, kNT, kS8>(lds_tables, rec + kFileInfoSize, uint32_t(m.size - kFileInfoSize), 0u, lane);
+      c = wave_crc<kRun, kPF, kNT, kS8>(lds_tables, rec + kFileInfoSize, uint32_t(m.size - kFileInfoSize), 0u, lane,
+                                        reinterpret_cast<uintptr_t>(tg->slice));
       if (h.id != m.file_id) status = kExitFileInfoError;
       else if (h.size != m.size) status = kExitSyncFileError;
       else if (c != h.crc) status = kExitCheckCrcError;
