@@ -1,0 +1,150 @@
+"""CPU emulation of the kernel's decomposition (tfs_crc_kernels.hip), lane by
+lane, against the oracle: stripes counted back from the last 16-byte boundary,
+zero-extended front, masked first dword, seed injected into the first four
+message bytes (carried to stripe 1 when A is stripe 0's last dword), per-stripe
+shift over 63 foreign runs, final (63-lane)*RUN shift + XOR-reduce, serial tail.
+Uses the same GF(2) helpers the host builds the device tables from
+(crc_math.h), restated here in Python."""
+import random
+
+import pytest
+
+from conftest import ocrc
+from tfs_amd.synth import synth_bytes
+
+POLY = 0xEDB88320
+
+
+def mult(a, b):
+    m, p = 1 << 31, 0
+    while True:
+        if a & m:
+            p ^= b
+            if (a & (m - 1)) == 0:
+                break
+        m >>= 1
+        b = (b >> 1) ^ POLY if b & 1 else b >> 1
+    return p
+
+
+def x2n(n, k):
+    p, sq = 1 << 31, 1 << 30
+    for _ in range(k):
+        sq = mult(sq, sq)
+    while n:
+        if n & 1:
+            p = mult(sq, p)
+        n >>= 1
+        sq = mult(sq, sq)
+    return p
+
+
+T = [[0] * 256 for _ in range(4)]
+for i in range(256):
+    c = i
+    for _ in range(8):
+        c = (c >> 1) ^ POLY if c & 1 else c >> 1
+    T[0][i] = c
+for k in range(1, 4):
+    for b in range(256):
+        T[k][b] = (T[k - 1][b] >> 8) ^ T[0][T[k - 1][b] & 0xFF]
+_SH = {}
+
+
+def shift(c, n):
+    if n not in _SH:
+        _SH[n] = x2n(n, 3)
+    return mult(_SH[n], c)
+
+
+def step4(c, w):
+    x = c ^ w
+    return T[3][x & 255] ^ T[2][(x >> 8) & 255] ^ T[1][(x >> 16) & 255] ^ T[0][x >> 24]
+
+
+def step1(c, b):
+    return (c >> 8) ^ T[0][(c ^ b) & 255]
+
+
+def emulate(mem, start, ln, seed, run):
+    ld = lambda a: int.from_bytes(mem[a:a + 4], "little")
+    if ln < 32:
+        c = seed
+        for i in range(ln):
+            c = step1(c, mem[start + i])
+        return c
+    S = 64 * run
+    end = start + ln
+    A, B16 = start & ~3, end & ~15
+    s, body = start - A, B16 - A
+    ns = (body + S - 1) // S
+    sb0 = B16 - ns * S
+    headmask = (0xFFFFFFFF << (8 * s)) & 0xFFFFFFFF
+    slo = (seed << (8 * s)) & 0xFFFFFFFF
+    shi = (seed >> (32 - 8 * s)) if s else 0
+    tot = 0
+    for lane in range(64):
+        c, lo = 0, sb0 + lane * run
+        inj = shi if (lane == 0 and A + 4 == sb0 + S) else 0
+        for i in range(run // 4):
+            q = lo + 4 * i
+            w = ld(q) if q >= A else 0
+            if q == A:
+                w = (w & headmask) ^ slo
+            if q == A + 4:
+                w ^= shi
+            c = step4(c, w)
+        for r in range(1, ns):
+            c = shift(c, 63 * run)
+            if r == 1:
+                c ^= inj
+            q = sb0 + r * S + lane * run
+            for i in range(run // 4):
+                c = step4(c, ld(q + 4 * i))
+        k = 63 - lane
+        for j in range(6):
+            if (k >> j) & 1:
+                c = shift(c, run << j)
+        tot ^= c
+    c, q = tot, B16
+    while q + 4 <= end:
+        c = step4(c, ld(q))
+        q += 4
+    while q < end:
+        c = step1(c, mem[q])
+        q += 1
+    return c
+
+
+def test_slice_tables_match_oracle_table(oracle):
+    import numpy as np
+    tab = np.zeros(256, np.uint32)
+    oracle.oracle_table(tab.ctypes.data)
+    assert [int(x) for x in tab] == T[0]
+
+
+@pytest.mark.parametrize("run", [16, 32])
+def test_emulated_decomposition_matches_oracle(oracle, run):
+    mem = synth_bytes(99, 12000).tobytes()
+    rnd = random.Random(run)
+    cases = [(0, 32, 0), (1, 33, 5), (3, 100, 0xDEADBEEF), (2, 1025, 0), (7, 4100, 0x4E534654)]
+    cases += [(rnd.randrange(0, 64), rnd.randrange(32, 6000), rnd.getrandbits(32)) for _ in range(10)]
+    # the stripe-0 edge: payload starts inside the last dword of stripe 0
+    S = 64 * run
+    for st in (29, 30, 31):
+        for ln in range(S, 3 * S):
+            e = st + ln
+            if (st & ~3) + 4 == (e & ~15) - (((e & ~15) - (st & ~3) + S - 1) // S) * S + S:
+                cases.append((st, ln, 0xA5A5F00D))
+                break
+    for st, ln, sd in cases:
+        assert emulate(mem, st, ln, sd, run) == ocrc(oracle, sd, mem[st:st + ln]), (run, st, ln, sd)
+
+
+def test_shift_identity(oracle):
+    """crc(A||B) = shift(crc(A), |B|) ^ crc(B) for seed 0; leading zeros are free."""
+    d = synth_bytes(5, 3000).tobytes()
+    for cut in (0, 1, 17, 1024, 2999, 3000):
+        a, b = d[:cut], d[cut:]
+        assert shift(ocrc(oracle, 0, a), len(b)) ^ ocrc(oracle, 0, b) == ocrc(oracle, 0, d)
+    assert ocrc(oracle, 0, bytes(100) + d) == ocrc(oracle, 0, d)
