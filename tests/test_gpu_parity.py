@@ -232,9 +232,10 @@ def _stripe_edge_cases(run, count=24):
         for ln in list(range(40, 200)) + list(range(S - 40, 4 * S + 40, 3)):
             end = st + ln
             A, B16 = st & ~3, end & ~15
-            body = B16 - A
+            E = (B16 + 127) & ~127 if run == 16 else B16   # the kernel's stripe anchor
+            body = E - A
             ns = (body + S - 1) // S
-            if ln >= 32 and A + 4 == B16 - ns * S + S:
+            if ln >= 32 and A + 4 == E - ns * S + S:
                 out.append((st, ln))
         if len(out) >= count:
             break

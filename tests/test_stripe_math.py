@@ -76,9 +76,11 @@ def emulate(mem, start, ln, seed, run):
     S = 64 * run
     end = start + ln
     A, B16 = start & ~3, end & ~15
-    s, body = start - A, B16 - A
+    E = (B16 + 127) & ~127 if run == 16 else B16   # stripe anchor: whole 128-byte lines
+    nvalid = 64 - (E - B16) // run
+    s, body = start - A, E - A
     ns = (body + S - 1) // S
-    sb0 = B16 - ns * S
+    sb0 = E - ns * S
     headmask = (0xFFFFFFFF << (8 * s)) & 0xFFFFFFFF
     slo = (seed << (8 * s)) & 0xFFFFFFFF
     shi = (seed >> (32 - 8 * s)) if s else 0
@@ -88,20 +90,23 @@ def emulate(mem, start, ln, seed, run):
         inj = shi if (lane == 0 and A + 4 == sb0 + S) else 0
         for i in range(run // 4):
             q = lo + 4 * i
-            w = ld(q) if q >= A else 0
+            w = ld(q) if A <= q < B16 else 0
             if q == A:
                 w = (w & headmask) ^ slo
             if q == A + 4:
                 w ^= shi
             c = step4(c, w)
         for r in range(1, ns):
+            c_old = c
             c = shift(c, 63 * run)
             if r == 1:
                 c ^= inj
             q = sb0 + r * S + lane * run
             for i in range(run // 4):
                 c = step4(c, ld(q + 4 * i))
-        k = 63 - lane
+            if r == ns - 1 and lane >= nvalid:
+                c = c_old
+        k = 63 - lane - (64 - nvalid) + (0 if lane < nvalid else 64)
         for j in range(6):
             if (k >> j) & 1:
                 c = shift(c, run << j)
@@ -128,13 +133,14 @@ def test_emulated_decomposition_matches_oracle(oracle, run):
     mem = synth_bytes(99, 12000).tobytes()
     rnd = random.Random(run)
     cases = [(0, 32, 0), (1, 33, 5), (3, 100, 0xDEADBEEF), (2, 1025, 0), (7, 4100, 0x4E534654)]
-    cases += [(rnd.randrange(0, 64), rnd.randrange(32, 6000), rnd.getrandbits(32)) for _ in range(10)]
+    cases += [(rnd.randrange(0, 64), rnd.randrange(32, 6000), rnd.getrandbits(32)) for _ in range(40)]
     # the stripe-0 edge: payload starts inside the last dword of stripe 0
     S = 64 * run
     for st in (29, 30, 31):
         for ln in range(S, 3 * S):
             e = st + ln
-            if (st & ~3) + 4 == (e & ~15) - (((e & ~15) - (st & ~3) + S - 1) // S) * S + S:
+            E = ((e & ~15) + 127) & ~127 if run == 16 else e & ~15
+            if (st & ~3) + 4 == E - ((E - (st & ~3) + S - 1) // S) * S + S:
                 cases.append((st, ln, 0xA5A5F00D))
                 break
     for st, ln, sd in cases:

@@ -166,8 +166,9 @@ __device__ __forceinline__ void load_tables(uint32_t* T, const Tables* __restric
 // ---------------------------------------------------------------------------
 template <int RUN>
 struct FileGeo {
-  uintptr_t start, end, A, B16, sb0;
+  uintptr_t start, end, A, B16, E, sb0;
   uint32_t len, s, nstripes, seed;
+  uint32_t nvalid;  // lanes whose run in the last stripe holds payload (the rest lie past B16)
 };
 
 template <int RUN>
@@ -181,9 +182,16 @@ __device__ __forceinline__ FileGeo<RUN> make_geo(const uint8_t* p, uint32_t len,
   g.A = g.start & ~uintptr_t(3);
   g.B16 = g.end & ~uintptr_t(15);
   g.s = uint32_t(g.start - g.A);
-  const uint32_t body = len >= kMinParallelLen ? uint32_t(g.B16 - g.A) : 0u;
+  // Stripe grid anchor E: B16 rounded up to a 128-byte line (RUN = 16), so every
+  // stripe is exactly eight whole lines -- with non-temporal loads a line split
+  // between two stripes was fetched twice (+2 % HBM traffic).  Runs in
+  // [B16, E) lie in the same line as payload bytes (safe to read) and are
+  // excluded from their lanes' chains (`nvalid`).
+  g.E = RUN == 16 ? ((g.B16 + 127) & ~uintptr_t(127)) : g.B16;
+  g.nvalid = 64u - uint32_t(g.E - g.B16) / RUN;
+  const uint32_t body = len >= kMinParallelLen ? uint32_t(g.E - g.A) : 0u;
   g.nstripes = (body + kStripe - 1) / kStripe;
-  g.sb0 = g.B16 - uintptr_t(g.nstripes) * kStripe;
+  g.sb0 = g.E - uintptr_t(g.nstripes) * kStripe;
   return g;
 }
 
@@ -204,7 +212,7 @@ __device__ __forceinline__ Head<RUN> load_head(const FileGeo<RUN>& g, int lane) 
 #pragma unroll
   for (int i = 0; i < RUN / 4; ++i) {
     const uintptr_t q = lo + 4u * i;
-    h.w[i] = (g.nstripes && q >= g.A) ? ld32(q) : 0u;
+    h.w[i] = (g.nstripes && q >= g.A && q < g.B16) ? ld32(q) : 0u;  // zero chain stays zero
   }
   const uintptr_t tq = g.nstripes ? g.B16 : g.start;  // tiny files: everything is "tail"
 #pragma unroll
@@ -267,10 +275,13 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
   if (g.nstripes > 1) {
     // Full groups of PF stripes: straight-line, every buffer consumed then
     // refilled (past the last stripe: the L2-resident `junk` region).
+    const uint32_t last = g.nstripes - 1;
+    const bool lane_in_last = uint32_t(lane) < g.nvalid;
     uint32_t r = 1;
     for (; r + PF <= g.nstripes; r += PF) {
 #pragma unroll
       for (int f = 0; f < PF; ++f) {
+        const uint32_t c_old = c;
         c = shift_stripe<S8>(T, c);
         if (f == 0) {
           c ^= inj;  // XOR into the stripe's first dword == XOR into the register before its step
@@ -278,6 +289,7 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
         }
 #pragma unroll
         for (int v = 0; v < kVec; ++v) c = steps16(T, lb, c, buf[f][v]);
+        c = (r + f == last && !lane_in_last) ? c_old : c;  // run past B16: not part of the chain
         const uintptr_t sb = stripe_base<RUN>(g, r + f + PF, junk) + uintptr_t(lane) * RUN;
 #pragma unroll
         for (int v = 0; v < kVec; ++v) buf[f][v] = ld128s<NT>(sb + 16u * v);
@@ -287,10 +299,12 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
 #pragma unroll
     for (int f = 0; f < PF - 1; ++f) {
       if (r + f < g.nstripes) {
+        const uint32_t c_old = c;
         c = shift_stripe<S8>(T, c);
         if (f == 0) c ^= inj;
 #pragma unroll
         for (int v = 0; v < kVec; ++v) c = steps16(T, lb, c, buf[f][v]);
+        c = (r + f == last && !lane_in_last) ? c_old : c;
       }
     }
   }
@@ -306,8 +320,11 @@ __device__ __forceinline__ uint32_t finish_file(const uint32_t* T, const LaneBas
     for (uint32_t i = 0; i < g.len; ++i) t = step1(T, lb, t, ld8(g.start + i));
     return t;
   }
-  // Move each lane's chain to its place in the body: shift by (63-lane)*RUN.
-  const uint32_t k = uint32_t(kWave - 1 - lane);
+  // Move each lane's chain to its place: the distance from the end of its last
+  // run to B16, in runs: (63-lane) - (E-B16)/RUN, plus a whole stripe for lanes
+  // whose run in the last stripe lies past B16 (their chain ended a stripe earlier).
+  const uint32_t e_runs = 64u - g.nvalid;
+  const uint32_t k = uint32_t(kWave - 1 - lane) - e_runs + (uint32_t(lane) < g.nvalid ? 0u : 64u);
 #pragma unroll
   for (int j = 0; j < kLevels; ++j) {
     const uint32_t sh = shift_lds<S8>(T, LdsLayout<S8>::level_off + LdsLayout<S8>::stride * j, c);
@@ -580,7 +597,8 @@ __global__ void write_headers_kernel(uint8_t* __restrict__ image, const uint64_t
 template <bool NT>
 __global__ void __launch_bounds__(kBlock) membench_kernel(const uint8_t* __restrict__ base,
                                                           const Desc* __restrict__ desc, uint32_t n,
-                                                          uint64_t nbytes, uint32_t run, uint32_t* out) {
+                                                          uint64_t nbytes, uint32_t run, uint32_t* out,
+                                                          uint32_t align) {
   uint32_t acc = 0;
   if (run == 0) {
     const uintptr_t p = reinterpret_cast<uintptr_t>(base);
@@ -596,8 +614,8 @@ __global__ void __launch_bounds__(kBlock) membench_kernel(const uint8_t* __restr
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     for (uint32_t f = blockIdx.x * wpb + wave; f < n; f += gridDim.x * wpb) {
       const Desc d = desc[f];
-      const uintptr_t start = (reinterpret_cast<uintptr_t>(base + d.offset) + 15) & ~uintptr_t(15);
-      const uint32_t stripe = 64u * run, ns = d.len / stripe;
+      const uintptr_t start = (reinterpret_cast<uintptr_t>(base + d.offset) + align - 1) & ~uintptr_t(align - 1);
+      const uint32_t stripe = 64u * run, ns = (d.len - (align - 1)) / stripe;
       uint32_t r = 0;
       for (; r + 8 <= ns; r += 8) {
         uint4 v[8];
@@ -689,14 +707,17 @@ hipError_t launch_synth_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, uint
 
 hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, uint32_t n, uint64_t nbytes,
                            uint32_t* out, unsigned grid, hipStream_t stream) {
-  // pattern: 0 = coalesced, 16 = stripe pattern (run 16); +1000 = non-temporal loads
+  // pattern: 0 = coalesced, 16 = stripe pattern (run 16); +1000 = non-temporal loads;
+  // +10000 = stripes anchored at 128-byte boundaries (else 16)
+  const uint32_t align = pattern >= 10000 ? 128u : 16u;
+  pattern %= 10000;
   const bool nt = pattern >= 1000;
   const uint32_t run = uint32_t(pattern % 1000);
   const dim3 g(grid ? grid : (run ? grid_for(n) : 2048u));
   if (nt)
-    hipLaunchKernelGGL(membench_kernel<true>, g, dim3(kBlock), 0, stream, base, desc, n, nbytes, run, out);
+    hipLaunchKernelGGL(membench_kernel<true>, g, dim3(kBlock), 0, stream, base, desc, n, nbytes, run, out, align);
   else
-    hipLaunchKernelGGL(membench_kernel<false>, g, dim3(kBlock), 0, stream, base, desc, n, nbytes, run, out);
+    hipLaunchKernelGGL(membench_kernel<false>, g, dim3(kBlock), 0, stream, base, desc, n, nbytes, run, out, align);
   return hipGetLastError();
 }
 
