@@ -220,6 +220,58 @@ typedef struct tfs_block_job {
 } tfs_block_job;
 int tfs_blocks_compact(tfs_crc_ctx* ctx, tfs_block_job* jobs, uint32_t njobs);
 
+/* ---- packet CRC (BasePacket, src/common/base_packet.{h,cpp}) ------------ */
+
+/* Every V1 RPC frame carries Func::crc(TFS_PACKET_FLAG_V1, body, length) in its
+ * header: the send side computes it (BasePacket::copy / reply,
+ * base_packet.cpp:74,208; serialized by BasePacketStreamer::encode,
+ * base_packet_streamer.cpp:159-200), the receive side checks it
+ * (BasePacket::decode, base_packet.cpp:117-148) -- for every 64 KiB write and
+ * each of its forwarded replica copies.  A frame is the serialized header
+ * (TfsPacketNewHeaderV1, base_packet.h:92-162, little-endian: flag u32,
+ * length i32, type i16, version i16, id u64, crc u32 = 24 bytes; a V0 frame
+ * has only flag/length/type/check = 12 bytes) followed by `length` body bytes. */
+#define TFS_PACKET_FLAG_V0 0x4d534654u /* "TFSM", base_packet.h:347 */
+#define TFS_PACKET_FLAG_V1 0x4e534654u /* "TFSN", base_packet.h:348; also the CRC seed */
+#define TFS_PACKET_HEADER_V0_SIZE 12
+#define TFS_PACKET_HEADER_V1_SIZE 24
+#define TFS_ERROR (-1)            /* cdefine.h: broken stream */
+#define TFS_PACKET_INCOMPLETE 1   /* frame shorter than its header/body: the streamer waits */
+
+/* One frame: `len` bytes available at base + offset, starting at its header. 16 bytes. */
+typedef struct tfs_packet_desc {
+  uint64_t offset;
+  uint32_t len;
+  uint32_t reserved;
+} tfs_packet_desc;
+
+/* Receive side, batched.  Per frame, in the reference's order
+ * (getPacketInfo, base_packet_streamer.cpp:43-124; decode, base_packet.cpp:100-170):
+ *   TFS_PACKET_INCOMPLETE   fewer than 12 bytes, a V1 flag with fewer than 24, or
+ *                           the body not all there;
+ *   TFS_ERROR               flag neither V0 nor V1, or length <= 0 or > 64 MiB (:78-87);
+ *   TFS_EXIT_CHECK_CRC_ERROR  decode's CRC check failed (:141-148);
+ *   TFS_SUCCESS             decoded: CRC matched, or the frame carries none
+ *                           (V0 flag / version 0; decode checks when
+ *                           ((pcode >> 16) & 0xFFFF) >= 1, pcode = type | check << 16).
+ * out_crc[i] = the computed body CRC for checked frames, else 0.  out_status /
+ * out_crc / n_bad may be NULL.  Returns TFS_SUCCESS when every frame decoded,
+ * TFS_EXIT_CHECK_CRC_ERROR otherwise (see out_status), other negatives on error. */
+int tfs_packet_verify(tfs_crc_ctx* ctx, const tfs_packet_desc* d, uint32_t n, const void* base, uint64_t base_len,
+                      uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad);
+/* Device-resident form (asynchronous on `stream`; d_n_bad accumulated into). */
+int tfs_packet_verify_device(tfs_crc_ctx* ctx, const tfs_packet_desc* d_desc, uint32_t n, const void* d_base,
+                             uint32_t* d_out_crc, int32_t* d_out_status, uint32_t* d_n_bad, void* stream);
+/* Send side, batched: for every V1 frame whose version is >= 1, compute the body
+ * CRC and store it in the header's crc field (bytes 20..23) -- what
+ * BasePacket::copy/reply + BasePacketStreamer::encode produce.  Other frames are
+ * left as they are.  out_status as tfs_packet_verify (never a CRC error);
+ * out_crc[i] = the stored CRC or 0.  Host form writes into `base`. */
+int tfs_packet_seal(tfs_crc_ctx* ctx, const tfs_packet_desc* d, uint32_t n, void* base, uint64_t base_len,
+                    uint32_t* out_crc, int32_t* out_status);
+int tfs_packet_seal_device(tfs_crc_ctx* ctx, const tfs_packet_desc* d_desc, uint32_t n, void* d_base,
+                           uint32_t* d_out_crc, int32_t* d_out_status, void* stream);
+
 /* ---- test / bench helpers (not part of the dataserver boundary) -------- */
 
 /* Fill nbytes (multiple of 8) of device memory with the splitmix64 synthetic

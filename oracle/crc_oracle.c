@@ -30,6 +30,10 @@
  *   - CompactTask::real_compact      src/dataserver/task.cpp:713-836
  *       skip FI_DELETED|FI_INVALID (:747-751), rewrite offset/size/usize
  *       (:753-759), copy crc_ verbatim, pack FileInfo|payload (:795-798).
+ *   - packet frames                  src/common/base_packet_streamer.cpp:43-124
+ *       (getPacketInfo), src/common/base_packet.cpp:100-170 (decode),
+ *       :74,208 (copy/reply compute), header layout base_packet.h:33-162,
+ *       little-endian Serialization (serialization.h:100-140).
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -267,4 +271,96 @@ int64_t oracle_compact(const char* src, const int64_t* meta_off, const int32_t* 
     w += d.size_;
   }
   return w;
+}
+
+/* ---- packet frames ------------------------------------------------------ */
+#define ORACLE_PACKET_FLAG_V0 0x4d534654u /* base_packet.h:347 */
+#define ORACLE_PACKET_FLAG_V1 0x4e534654u /* base_packet.h:348 */
+#define ORACLE_TFS_ERROR (-1)
+#define ORACLE_PACKET_INCOMPLETE 1
+#define ORACLE_PACKET_CHECKED 2 /* internal: decode's CRC check applies */
+
+static uint32_t le32(const unsigned char* p) {
+  return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+}
+
+/* Classify one frame of `avail` bytes the way getPacketInfo + decode would.
+ * Returns ORACLE_PACKET_CHECKED with *body/*body_len/*stored set when decode
+ * checks a CRC, else the final status. */
+static int32_t packet_classify(const unsigned char* p, uint32_t avail, uint32_t* body_off, int32_t* body_len,
+                               uint32_t* stored) {
+  uint32_t flag;
+  int32_t length;
+  int16_t type, check;
+  int64_t data_len;
+  uint32_t version;
+  if (avail < 12) return ORACLE_PACKET_INCOMPLETE;             /* getPacketInfo:49 */
+  flag = le32(p);
+  length = (int32_t)le32(p + 4);
+  type = (int16_t)(p[8] | p[9] << 8);
+  check = (int16_t)(p[10] | p[11] << 8);
+  if (flag == ORACLE_PACKET_FLAG_V1 && avail < 24) return ORACLE_PACKET_INCOMPLETE;  /* :65-69 */
+  if ((flag != ORACLE_PACKET_FLAG_V0 && flag != ORACLE_PACKET_FLAG_V1) || length <= 0 || length > 0x4000000)
+    return ORACLE_TFS_ERROR;                                   /* :78-87 */
+  {
+    /* header->_pcode = type_ (int16 -> int, sign-extended); V1: |= check_ << 16 (:89) */
+    int32_t pcode = (int32_t)type;
+    data_len = length;
+    if (flag == ORACLE_PACKET_FLAG_V1) {
+      pcode |= (int32_t)((uint32_t)(int32_t)check << 16);
+      data_len += 12;                                          /* :93 */
+    }
+    version = ((uint32_t)pcode >> 16) & 0xFFFFu;               /* base_packet.cpp:104 */
+  }
+  if (12 + (uint64_t)data_len > avail) return ORACLE_PACKET_INCOMPLETE;
+  if (version < 1) return ORACLE_TFS_SUCCESS;
+  if (data_len < 12) return ORACLE_TFS_ERROR;
+  *stored = le32(p + 12 + 8);                                  /* id (8) then crc (4): :117-129 */
+  *body_off = 24;
+  *body_len = (int32_t)(data_len - 12);                        /* :137 */
+  return ORACLE_PACKET_CHECKED;
+}
+
+/* tfs_packet_verify's semantics: status per frame, computed crc (0 if none). */
+uint32_t oracle_packet_verify(const char* base, const uint64_t* offset, const uint32_t* avail, uint32_t n,
+                              uint32_t* out_crc, int32_t* out_status) {
+  uint32_t i, bad = 0;
+  for (i = 0; i < n; ++i) {
+    const unsigned char* p = (const unsigned char*)base + offset[i];
+    uint32_t body_off = 0, stored = 0;
+    int32_t body_len = 0;
+    int32_t st = packet_classify(p, avail[i], &body_off, &body_len, &stored);
+    uint32_t c = 0;
+    if (st == ORACLE_PACKET_CHECKED) {
+      c = oracle_crc(ORACLE_PACKET_FLAG_V1, (const char*)p + body_off, body_len); /* :141 */
+      st = c == stored ? ORACLE_TFS_SUCCESS : ORACLE_EXIT_CHECK_CRC_ERROR;
+    }
+    if (out_crc) out_crc[i] = c;
+    if (out_status) out_status[i] = st;
+    bad += st != ORACLE_TFS_SUCCESS;
+  }
+  return bad;
+}
+
+/* tfs_packet_seal's semantics: V1 frames that decode would check get their
+ * header crc_ set to the body CRC (copy/reply :74,208 + streamer encode). */
+void oracle_packet_seal(char* base, const uint64_t* offset, const uint32_t* avail, uint32_t n, uint32_t* out_crc,
+                        int32_t* out_status) {
+  uint32_t i;
+  for (i = 0; i < n; ++i) {
+    unsigned char* p = (unsigned char*)base + offset[i];
+    uint32_t body_off = 0, stored = 0, c = 0;
+    int32_t body_len = 0;
+    int32_t st = packet_classify(p, avail[i], &body_off, &body_len, &stored);
+    if (st == ORACLE_PACKET_CHECKED) {
+      c = oracle_crc(ORACLE_PACKET_FLAG_V1, (const char*)p + body_off, body_len);
+      if (le32(p) == ORACLE_PACKET_FLAG_V1) {
+        p[20] = (unsigned char)c; p[21] = (unsigned char)(c >> 8);
+        p[22] = (unsigned char)(c >> 16); p[23] = (unsigned char)(c >> 24);
+      }
+      st = ORACLE_TFS_SUCCESS;
+    }
+    if (out_crc) out_crc[i] = c;
+    if (out_status) out_status[i] = st;
+  }
 }

@@ -45,6 +45,10 @@ def oracle():
     L.oracle_loopback_block.restype = ctypes.c_int32
     L.oracle_loopback_block.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    L.oracle_packet_verify.restype = ctypes.c_uint32
+    L.oracle_packet_verify.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint32] + [ctypes.c_void_p] * 2
+    L.oracle_packet_seal.restype = None
+    L.oracle_packet_seal.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint32] + [ctypes.c_void_p] * 2
     L.oracle_table.restype = None
     L.oracle_table.argtypes = [ctypes.c_void_p]
     return L

@@ -10,6 +10,7 @@ Names mirror the reference interface they replace:
   Context.batch / verify      the per-file call sites   data_file.cpp:190, sync_backup.cpp:383/429
   Context.block_verify        verify-on-read of a block sync_backup.cpp:345-435, block_console.cpp:543-577
   Context.block_compact       CompactTask::real_compact task.cpp:713-836 (+ re-CRC verify)
+  Context.packet_verify/seal  BasePacket::decode / copy+reply  base_packet.cpp:74,141,208
 """
 import ctypes
 import os
@@ -29,10 +30,17 @@ TFS_EXIT_SYNC_FILE_ERROR = -8038
 TFS_CRC_EXIT_DEVICE_ERROR = -20001
 TFS_CRC_EXIT_NO_DEVICE = -20002
 
+TFS_ERROR = -1
+TFS_PACKET_INCOMPLETE = 1
+TFS_PACKET_FLAG_V0 = 0x4D534654
+TFS_PACKET_FLAG_V1 = 0x4E534654
+PACKET_HEADER_V0_SIZE, PACKET_HEADER_V1_SIZE = 12, 24
+
 FI_DELETED, FI_INVALID, FI_CONCEAL = 1, 2, 4
 FILEINFO_SIZE = 36
 
 DESC_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("aux", "<u4")])  # tfs_crc_desc / tfs_crc_vdesc
+PACKET_DESC_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("reserved", "<u4")])  # tfs_packet_desc
 META_DTYPE = np.dtype([("file_id", "<u8"), ("offset", "<i4"), ("size", "<i4")])  # tfs_raw_meta
 FILEINFO_DTYPE = np.dtype([("id_", "<u8"), ("offset_", "<i4"), ("size_", "<i4"), ("usize_", "<i4"),
                            ("modify_time_", "<i4"), ("create_time_", "<i4"), ("flag_", "<i4"),
@@ -50,6 +58,7 @@ EXPORTED = [
     "tfs_crc32_memcpy", "tfs_crc32_memset_device", "tfs_crc32_event_create", "tfs_crc32_event_record",
     "tfs_crc32_event_elapsed_ms", "tfs_crc32_event_destroy",
     "tfs_crc32_stream", "tfs_crc32_sync",
+    "tfs_packet_verify", "tfs_packet_verify_device", "tfs_packet_seal", "tfs_packet_seal_device",
 ]
 
 
@@ -111,6 +120,10 @@ def lib():
             "tfs_crc32_event_destroy": (ctypes.c_int, [vp, vp]),
             "tfs_crc32_stream": (vp, [vp]),
             "tfs_crc32_sync": (ctypes.c_int, [vp]),
+            "tfs_packet_verify": (ctypes.c_int, [vp, vp, u32, vp, u64, vp, vp, vp]),
+            "tfs_packet_verify_device": (ctypes.c_int, [vp, vp, u32, vp, vp, vp, vp, vp]),
+            "tfs_packet_seal": (ctypes.c_int, [vp, vp, u32, vp, u64, vp, vp]),
+            "tfs_packet_seal_device": (ctypes.c_int, [vp, vp, u32, vp, vp, vp, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -275,6 +288,45 @@ class Context:
         rc = lib().tfs_blocks_compact(self.handle, ctypes.cast(jobs, ctypes.c_void_p), len(jobs))
         self._check(rc, "blocks_compact", ok=(TFS_SUCCESS, TFS_EXIT_CHECK_CRC_ERROR))
         return rc
+
+    # ---- packet frames (BasePacket) ------------------------------------------
+    @staticmethod
+    def _packet_desc(offsets, lens):
+        d = np.zeros(len(offsets), PACKET_DESC_DTYPE)
+        d["offset"] = offsets
+        d["len"] = lens
+        return d
+
+    def packet_verify(self, base, offsets, lens):
+        """Receive side (BasePacket::decode): returns (crc, status, n_bad, rc)."""
+        buf = _as_u8(base)
+        d = self._packet_desc(offsets, lens)
+        n = len(d)
+        crc = np.zeros(n, np.uint32)
+        st = np.zeros(n, np.int32)
+        nbad = np.zeros(1, np.uint32)
+        rc = lib().tfs_packet_verify(self.handle, _ptr(d), n, _ptr(buf), buf.size, _ptr(crc), _ptr(st), _ptr(nbad))
+        self._check(rc, "packet_verify", ok=(TFS_SUCCESS, TFS_EXIT_CHECK_CRC_ERROR))
+        return crc, st, int(nbad[0]), rc
+
+    def packet_seal(self, buf, offsets, lens):
+        """Send side: writes the body CRC into each V1 header of `buf` (a writable uint8 array)."""
+        assert isinstance(buf, np.ndarray) and buf.dtype == np.uint8 and buf.flags.c_contiguous
+        d = self._packet_desc(offsets, lens)
+        n = len(d)
+        crc = np.zeros(n, np.uint32)
+        st = np.zeros(n, np.int32)
+        self._check(lib().tfs_packet_seal(self.handle, _ptr(d), n, _ptr(buf), buf.size, _ptr(crc), _ptr(st)),
+                    "packet_seal")
+        return crc, st
+
+    def packet_verify_device(self, d_desc, n, d_base, d_crc, d_status, d_nbad=None, stream=None):
+        self._check(lib().tfs_packet_verify_device(self.handle, _ptr(d_desc), n, _ptr(d_base), _ptr(d_crc),
+                                                   _ptr(d_status), _ptr(d_nbad), stream), "packet_verify_device")
+
+    def packet_seal_device(self, d_desc, n, d_base, d_crc, d_status, stream=None):
+        self._check(lib().tfs_packet_seal_device(self.handle, _ptr(d_desc), n, _ptr(d_base), _ptr(d_crc),
+                                                 _ptr(d_status), stream), "packet_seal_device")
 
     # ---- block images (host) -------------------------------------------------
     def block_verify(self, image, metas):

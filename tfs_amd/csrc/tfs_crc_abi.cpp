@@ -24,7 +24,12 @@
 namespace tfscrc {
 hipError_t launch_crc_files(int mode, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
                             uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
-                            int variant);
+                            int variant, uint32_t vseed);
+hipError_t launch_packet_parse(const uint8_t* base, const PacketDesc* pd, uint32_t n, int mode, Desc* desc,
+                               int32_t* pre, hipStream_t stream);
+hipError_t launch_packet_finish(uint8_t* base, const PacketDesc* pd, const Desc* desc, uint32_t n, int mode,
+                                const int32_t* pre, const uint8_t* ok, uint32_t* crc, int32_t* status,
+                                uint32_t* n_bad, hipStream_t stream);
 hipError_t launch_block_verify(const uint8_t* image, uint64_t image_len, const RawMeta* metas, uint32_t n,
                                const Tables* tg, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
                                hipStream_t stream);
@@ -40,6 +45,7 @@ hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, u
 static_assert(sizeof(tfs_crc_desc) == 16 && sizeof(tfs_crc_vdesc) == 16, "descriptor ABI");
 static_assert(sizeof(tfs_raw_meta) == sizeof(tfscrc::RawMeta), "RawMeta ABI");
 static_assert(sizeof(tfs_file_info) == 36, "FileInfo ABI");
+static_assert(sizeof(tfs_packet_desc) == sizeof(tfscrc::PacketDesc), "packet descriptor ABI");
 
 namespace {
 
@@ -148,6 +154,8 @@ struct tfs_crc_ctx {
   uint32_t* d_sched = nullptr;
   std::atomic<uint32_t> sched_seq{0};
   int variant = 0;  // kernel variant (TFS_CRC_VARIANT, measurement knob; 0 = product default)
+  DevBuf packet_scratch;  // device-resident packet calls (parse descriptors, verdicts)
+  hipStream_t packet_scratch_stream = nullptr;
 };
 
 namespace {
@@ -269,7 +277,7 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
   HIP_TRY(ctx, sched_slot(ctx, ctx->stream, &sched));
   HIP_TRY(ctx, launch_crc_files(mode, d_base, static_cast<const Desc*>(s.d_desc.p), n, ctx->d_tables,
                                 static_cast<uint32_t*>(s.d_crc.p), static_cast<uint8_t*>(s.d_ok.p),
-                                static_cast<uint32_t*>(s.d_bad.p), sched, ctx->stream, ctx->variant));
+                                static_cast<uint32_t*>(s.d_bad.p), sched, ctx->stream, ctx->variant, 0u));
   HIP_TRY(ctx, hipMemcpyAsync(s.h_crc.p, s.d_crc.p, size_t(n) * 4, hipMemcpyDeviceToHost, ctx->stream));
   if (mode == 1) {
     HIP_TRY(ctx, hipMemcpyAsync(s.h_ok.p, s.d_ok.p, n, hipMemcpyDeviceToHost, ctx->stream));
@@ -366,6 +374,7 @@ int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx) {
     if (cs.stream) (void)hipStreamSynchronize(cs.stream);
     cs.release();
   }
+  ctx->packet_scratch.release();
   if (ctx->d_tables) (void)hipFree(ctx->d_tables);
   if (ctx->d_sched) (void)hipFree(ctx->d_sched);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -457,7 +466,7 @@ int tfs_crc32_batch_device(tfs_crc_ctx* ctx, const tfs_crc_desc* d_desc, uint32_
   uint32_t* sched = nullptr;
   HIP_TRY(ctx, sched_slot(ctx, st, &sched));
   HIP_TRY(ctx, launch_crc_files(0, static_cast<const uint8_t*>(d_base), reinterpret_cast<const Desc*>(d_desc), n,
-                                ctx->d_tables, d_out_crc, nullptr, nullptr, sched, st, ctx->variant));
+                                ctx->d_tables, d_out_crc, nullptr, nullptr, sched, st, ctx->variant, 0u));
   return TFS_SUCCESS;
 }
 
@@ -469,7 +478,7 @@ int tfs_crc32_verify_device(tfs_crc_ctx* ctx, const tfs_crc_vdesc* d_desc, uint3
   uint32_t* sched = nullptr;
   HIP_TRY(ctx, sched_slot(ctx, st, &sched));
   HIP_TRY(ctx, launch_crc_files(1, static_cast<const uint8_t*>(d_base), reinterpret_cast<const Desc*>(d_desc), n,
-                                ctx->d_tables, d_out_crc, d_out_ok, d_n_bad, sched, st, ctx->variant));
+                                ctx->d_tables, d_out_crc, d_out_ok, d_n_bad, sched, st, ctx->variant, 0u));
   return TFS_SUCCESS;
 }
 
@@ -704,6 +713,131 @@ int tfs_block_compact(tfs_crc_ctx* ctx, const void* src_image, uint64_t src_len,
   if (dest_len) *dest_len = job.dest_len;
   if (n_live) *n_live = job.n_live;
   return rc;
+}
+
+// ---- packet CRC ------------------------------------------------------------
+// parse (frame -> body descriptor + pre-status) -> CRC kernel over the bodies
+// (verify: seed TFS_PACKET_FLAG_V1 vs the header crc; seal: compute) ->
+// finish (statuses, seal writes the header crc).  `scratch` holds n Desc, n
+// pre-status and n ok bytes.
+
+static size_t packet_scratch_bytes(uint32_t n) { return size_t(n) * (sizeof(Desc) + 4 + 4 + 1) + 64; }
+
+static int packet_enqueue(tfs_crc_ctx* ctx, int mode, const PacketDesc* d_pd, uint32_t n, uint8_t* d_base,
+                          void* scratch, uint32_t* d_crc, int32_t* d_status, uint32_t* d_n_bad, hipStream_t st) {
+  uint8_t* sp = static_cast<uint8_t*>(scratch);
+  Desc* d_desc = reinterpret_cast<Desc*>(sp);
+  int32_t* d_pre = reinterpret_cast<int32_t*>(sp + size_t(n) * sizeof(Desc));
+  uint32_t* d_tmp_crc = reinterpret_cast<uint32_t*>(sp + size_t(n) * (sizeof(Desc) + 4));
+  uint8_t* d_ok = sp + size_t(n) * (sizeof(Desc) + 8);
+  uint32_t* crc = d_crc ? d_crc : d_tmp_crc;
+  HIP_TRY(ctx, launch_packet_parse(d_base, d_pd, n, mode, d_desc, d_pre, st));
+  uint32_t* sched = nullptr;
+  HIP_TRY(ctx, sched_slot(ctx, st, &sched));
+  HIP_TRY(ctx, launch_crc_files(mode, d_base, d_desc, n, ctx->d_tables, crc, mode == 1 ? d_ok : nullptr, nullptr,
+                                sched, st, ctx->variant, kPacketFlagV1));
+  HIP_TRY(ctx, launch_packet_finish(d_base, d_pd, d_desc, n, mode, d_pre, d_ok, crc, d_status, d_n_bad, st));
+  return TFS_SUCCESS;
+}
+
+// Device-resident: scratch comes from slot 0's d_aux under the ctx mutex.
+static int packet_device(tfs_crc_ctx* ctx, int mode, const tfs_packet_desc* d_desc, uint32_t n, void* d_base,
+                         uint32_t* d_out_crc, int32_t* d_out_status, uint32_t* d_n_bad, void* stream) {
+  if (!ctx || (n && (!d_desc || !d_base || !d_out_status))) return TFS_EXIT_PARAMETER_ERROR;
+  if (n == 0) return TFS_SUCCESS;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  // The scratch buffer is shared by device-resident packet calls: calls on one
+  // stream are ordered by the stream; switching streams waits for the last one.
+  if (ctx->packet_scratch_stream && ctx->packet_scratch_stream != st)
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->packet_scratch_stream));
+  if (packet_scratch_bytes(n) > ctx->packet_scratch.cap && ctx->packet_scratch_stream)
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->packet_scratch_stream));  // growing frees the old buffer
+  HIP_TRY(ctx, ctx->packet_scratch.reserve(packet_scratch_bytes(n)));
+  ctx->packet_scratch_stream = st;
+  return packet_enqueue(ctx, mode, reinterpret_cast<const PacketDesc*>(d_desc), n, static_cast<uint8_t*>(d_base),
+                        ctx->packet_scratch.p, d_out_crc, d_out_status, d_n_bad, st);
+}
+
+static int packet_host(tfs_crc_ctx* ctx, int mode, const tfs_packet_desc* d, uint32_t n, void* base,
+                       uint64_t base_len, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad) {
+  if (!ctx || (n && (!d || !base))) return TFS_EXIT_PARAMETER_ERROR;
+  if (n_bad) *n_bad = 0;
+  if (n == 0) return TFS_SUCCESS;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  Slot* s = free_slot(ctx);
+  if (!s) return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "all %d slots busy with async submissions", kSlots);
+  uint64_t lo = 0, hi = 0;
+  if (!span_of(d, n, base_len, &lo, &hi))
+    return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "frame range exceeds base_len %llu", (unsigned long long)base_len);
+  const uint8_t* d_base = nullptr;
+  int rc = stage_span(ctx, *s, base, lo, hi, &d_base);
+  if (rc) return rc;
+  HIP_TRY(ctx, s->d_desc.reserve(size_t(n) * sizeof(PacketDesc)));
+  HIP_TRY(ctx, s->d_aux.reserve(packet_scratch_bytes(n)));
+  HIP_TRY(ctx, s->d_crc.reserve(size_t(n) * 4));
+  HIP_TRY(ctx, s->d_ok.reserve(size_t(n) * 4));  // statuses
+  HIP_TRY(ctx, s->d_bad.reserve(4));
+  HIP_TRY(ctx, s->h_crc.reserve(size_t(n) * 4));
+  HIP_TRY(ctx, s->h_ok.reserve(size_t(n) * 8));  // statuses, then (seal) the parse pre-statuses
+  HIP_TRY(ctx, s->h_bad.reserve(4));
+  HIP_TRY(ctx, hipMemcpyAsync(s->d_desc.p, d, size_t(n) * sizeof(PacketDesc), hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(ctx, hipMemsetAsync(s->d_bad.p, 0, 4, ctx->stream));
+  rc = packet_enqueue(ctx, mode, static_cast<const PacketDesc*>(s->d_desc.p), n, const_cast<uint8_t*>(d_base),
+                      s->d_aux.p, static_cast<uint32_t*>(s->d_crc.p), static_cast<int32_t*>(s->d_ok.p),
+                      static_cast<uint32_t*>(s->d_bad.p), ctx->stream);
+  if (rc) return rc;
+  HIP_TRY(ctx, hipMemcpyAsync(s->h_crc.p, s->d_crc.p, size_t(n) * 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(s->h_ok.p, s->d_ok.p, size_t(n) * 4, hipMemcpyDeviceToHost, ctx->stream));
+  if (mode == 0)
+    HIP_TRY(ctx, hipMemcpyAsync(static_cast<int32_t*>(s->h_ok.p) + n,
+                                static_cast<uint8_t*>(s->d_aux.p) + size_t(n) * sizeof(Desc), size_t(n) * 4,
+                                hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipMemcpyAsync(s->h_bad.p, s->d_bad.p, 4, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  const uint32_t* hc = static_cast<const uint32_t*>(s->h_crc.p);
+  const int32_t* hs = static_cast<const int32_t*>(s->h_ok.p);
+  if (out_crc) memcpy(out_crc, hc, size_t(n) * 4);
+  if (out_status) memcpy(out_status, hs, size_t(n) * 4);
+  const uint32_t bad = *static_cast<const uint32_t*>(s->h_bad.p);
+  if (n_bad) *n_bad = bad;
+  if (mode == 0) {
+    // Seal: the device wrote the crc into its copy of each checked V1 header;
+    // store the same four bytes into the caller's frames.
+    const int32_t* pre = hs + n;
+    uint8_t* hb = static_cast<uint8_t*>(base);
+    for (uint32_t i = 0; i < n; ++i) {
+      if (pre[i] != kPacketPending) continue;
+      uint8_t* p = hb + d[i].offset;
+      const uint32_t flag = uint32_t(p[0]) | uint32_t(p[1]) << 8 | uint32_t(p[2]) << 16 | uint32_t(p[3]) << 24;
+      if (flag != TFS_PACKET_FLAG_V1) continue;
+      for (int b = 0; b < 4; ++b) p[TFS_PACKET_HEADER_V0_SIZE + 8 + b] = uint8_t(hc[i] >> (8 * b));
+    }
+    return TFS_SUCCESS;
+  }
+  return bad ? TFS_EXIT_CHECK_CRC_ERROR : TFS_SUCCESS;
+}
+
+int tfs_packet_verify(tfs_crc_ctx* ctx, const tfs_packet_desc* d, uint32_t n, const void* base, uint64_t base_len,
+                      uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad) {
+  return packet_host(ctx, 1, d, n, const_cast<void*>(base), base_len, out_crc, out_status, n_bad);
+}
+
+int tfs_packet_seal(tfs_crc_ctx* ctx, const tfs_packet_desc* d, uint32_t n, void* base, uint64_t base_len,
+                    uint32_t* out_crc, int32_t* out_status) {
+  return packet_host(ctx, 0, d, n, base, base_len, out_crc, out_status, nullptr);
+}
+
+int tfs_packet_verify_device(tfs_crc_ctx* ctx, const tfs_packet_desc* d_desc, uint32_t n, const void* d_base,
+                             uint32_t* d_out_crc, int32_t* d_out_status, uint32_t* d_n_bad, void* stream) {
+  return packet_device(ctx, 1, d_desc, n, const_cast<void*>(d_base), d_out_crc, d_out_status, d_n_bad, stream);
+}
+
+int tfs_packet_seal_device(tfs_crc_ctx* ctx, const tfs_packet_desc* d_desc, uint32_t n, void* d_base,
+                           uint32_t* d_out_crc, int32_t* d_out_status, void* stream) {
+  return packet_device(ctx, 0, d_desc, n, d_base, d_out_crc, d_out_status, nullptr, stream);
 }
 
 // ---- test / bench helpers (not part of the dataserver boundary) ----------

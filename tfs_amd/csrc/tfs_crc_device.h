@@ -61,6 +61,22 @@ struct RawMeta {
   int32_t size;
 };
 
+// Packet frames (BasePacket / BasePacketStreamer, src/common/base_packet*.{h,cpp}).
+// Same bytes as tfs_packet_desc in include/tfs_crc.h.
+struct PacketDesc {
+  uint64_t offset;  // frame start (the TfsPacketNewHeaderV0/V1 header)
+  uint32_t len;     // bytes of the frame available at offset
+  uint32_t reserved;
+};
+constexpr uint32_t kPacketFlagV0 = 0x4d534654u;  // "TFSM", base_packet.h:347
+constexpr uint32_t kPacketFlagV1 = 0x4e534654u;  // "TFSN", base_packet.h:348 (also the CRC seed)
+constexpr int32_t kPacketHeaderV0Size = 12;      // sizeof(TfsPacketNewHeaderV0), pack(4)
+constexpr int32_t kPacketHeaderDiffSize = 12;    // V1 - V0: id_ (8) + crc_ (4)
+constexpr int32_t kPacketMaxDataLen = 0x4000000; // base_packet_streamer.cpp:81 (64 MiB)
+constexpr int32_t kTfsError = -1;                // cdefine.h TFS_ERROR: broken stream
+constexpr int32_t kPacketIncomplete = 1;         // streamer waits for more bytes
+constexpr int32_t kPacketPending = 0x7fffffff;   // internal: CRC check outstanding
+
 #pragma pack(push, 4)
 struct FileInfoHdr {  // FileInfo, internal.h:432-446
   uint64_t id;

@@ -397,7 +397,8 @@ struct Tickets {
   }
 };
 
-// MODE 0: compute (aux = seed) -> out_crc.  MODE 1: verify (aux = expected, seed 0).
+// MODE 0: compute (aux = seed) -> out_crc.  MODE 1: verify (aux = expected, seed
+// `vseed`: 0 for files, TFS_PACKET_FLAG_V1 for packet bodies).
 // Files are software-pipelined per wave: the next file's stripe-0/tail words
 // and its first PF stripes are in flight while this file's lane chains are
 // combined, so HBM never waits on a file boundary.
@@ -405,7 +406,8 @@ template <int MODE, int RUN, int PF, bool NT, bool DYN, bool S8>
 __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __restrict__ base,
                                                            const Desc* __restrict__ desc, uint32_t n,
                                                            const Tables* __restrict__ tg, uint32_t* out_crc,
-                                                           uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched) {
+                                                           uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched,
+                                                           uint32_t vseed) {
   __shared__ uint32_t lds_tables[LdsLayout<S8>::bytes / 4];
   load_tables<RUN, false, S8>(lds_tables, tg);
   const int lane = threadIdx.x & (kWave - 1);
@@ -425,7 +427,7 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
     fn = f + stride;
   }
   Desc cur = desc[f];
-  FileGeo<RUN> g = make_geo<RUN>(base + cur.offset, cur.len, MODE == 0 ? cur.aux : 0u);
+  FileGeo<RUN> g = make_geo<RUN>(base + cur.offset, cur.len, MODE == 0 ? cur.aux : vseed);
   Head<RUN> h = load_head<RUN>(g, lane);
   const uintptr_t junk = reinterpret_cast<uintptr_t>(tg->slice);
   uint4 buf[PF][RUN / 16];
@@ -442,7 +444,7 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
     const Desc ncur = nxt;
     uint32_t fnn = n;
     if (more) {
-      ng = make_geo<RUN>(base + ncur.offset, ncur.len, MODE == 0 ? ncur.aux : 0u);
+      ng = make_geo<RUN>(base + ncur.offset, ncur.len, MODE == 0 ? ncur.aux : vseed);
       nh = load_head<RUN>(ng, lane);
       load_ring<RUN, PF, NT>(ng, lane, buf, junk);
       fnn = DYN ? tk.resolve(jv, lane) : fn + stride;
@@ -507,6 +509,105 @@ __global__ void __launch_bounds__(kBlock) block_verify_kernel(const uint8_t* __r
     }
   }
   if (lane == 0 && bad && n_bad) atomicAdd(n_bad, bad);
+}
+
+// ---------------------------------------------------------------------------
+// Packet CRC (BasePacket, src/common/base_packet.cpp).  A wire frame is the
+// serialized TfsPacketNewHeaderV1 (base_packet.h:92-162, little-endian:
+// flag u32, length i32, type i16, version i16, id u64, crc u32 = 24 B) and
+// `length` body bytes; a V0 frame has only the first 12 header bytes.  The
+// receive side (BasePacketStreamer::getPacketInfo, base_packet_streamer.cpp:
+// 43-124, then BasePacket::decode, base_packet.cpp:100-170) checks
+// Func::crc(TFS_PACKET_FLAG_V1, body) == header crc; the send side
+// (BasePacket::copy/reply, base_packet.cpp:74,208) computes it.
+//
+// packet_parse_kernel turns frames into CRC descriptors (one thread per
+// frame); crc_files_kernel computes the bodies; packet_finish_kernel folds in
+// the verdicts (verify) or writes the CRC into the header (seal).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t ld_le32(const uint8_t* p) {
+  return uint32_t(p[0]) | uint32_t(p[1]) << 8 | uint32_t(p[2]) << 16 | uint32_t(p[3]) << 24;
+}
+__device__ __forceinline__ int32_t ld_le16s(const uint8_t* p) { return int16_t(uint16_t(p[0] | p[1] << 8)); }
+
+// mode 1 = verify (desc.aux = stored crc), 0 = seal (desc.aux = seed).
+__global__ void packet_parse_kernel(const uint8_t* __restrict__ base, const PacketDesc* __restrict__ pd, uint32_t n,
+                                    int mode, Desc* __restrict__ desc, int32_t* __restrict__ pre) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const PacketDesc f = pd[i];
+  Desc d{f.offset, 0u, kPacketFlagV1};  // len 0: Func::crc returns the seed, which then "matches"
+  int32_t st = kSuccess;
+  const uint8_t* p = base + f.offset;
+  if (f.len < uint32_t(kPacketHeaderV0Size)) {
+    st = kPacketIncomplete;  // getPacketInfo:49
+  } else {
+    const uint32_t flag = ld_le32(p);
+    const int32_t length = int32_t(ld_le32(p + 4));
+    const int32_t type = ld_le16s(p + 8), check = ld_le16s(p + 10);
+    const bool v1 = flag == kPacketFlagV1;
+    if (v1 && f.len < uint32_t(kPacketHeaderV0Size + kPacketHeaderDiffSize)) {
+      st = kPacketIncomplete;  // :65-69, the V1 header's last 12 bytes are not there yet
+    } else if ((flag != kPacketFlagV0 && !v1) || length <= 0 || length > kPacketMaxDataLen) {
+      st = kTfsError;  // :78-87 "stream error": broken
+    } else {
+      // _dataLen (:73,93) and the version decode() sees: _pcode = type (sign-
+      // extended) | check << 16 for V1 (:89), version = (_pcode >> 16) & 0xFFFF (base_packet.cpp:104).
+      const int64_t data_len = int64_t(length) + (v1 ? kPacketHeaderDiffSize : 0);
+      const uint32_t version = ((type < 0) ? 0xFFFFu : 0u) | (v1 ? uint32_t(uint16_t(check)) : 0u);
+      if (uint64_t(kPacketHeaderV0Size) + uint64_t(data_len) > f.len) {
+        st = kPacketIncomplete;
+      } else if (version >= 1u) {
+        if (data_len < kPacketHeaderDiffSize) {
+          st = kTfsError;  // id/crc would be read past the packet
+        } else {
+          // decode: id (8) and crc (4) follow the V0 header, the body after them (:117-141).
+          d.offset = f.offset + kPacketHeaderV0Size + kPacketHeaderDiffSize;
+          d.len = uint32_t(data_len - kPacketHeaderDiffSize);
+          d.aux = mode == 1 ? ld_le32(p + kPacketHeaderV0Size + 8) : kPacketFlagV1;
+          st = kPacketPending;
+        }
+      }
+    }
+  }
+  desc[i] = d;
+  pre[i] = st;
+}
+
+__global__ void packet_finish_kernel(uint8_t* __restrict__ base, const PacketDesc* __restrict__ pd,
+                                     const Desc* __restrict__ desc, uint32_t n, int mode,
+                                     const int32_t* __restrict__ pre, const uint8_t* __restrict__ ok,
+                                     uint32_t* __restrict__ crc, int32_t* __restrict__ status,
+                                     uint32_t* __restrict__ n_bad) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t bad = 0;
+  if (i < n) {
+    int32_t st = pre[i];
+    const bool checked = st == kPacketPending;
+    if (checked) {
+      if (mode == 1) {
+        st = ok[i] ? kSuccess : kExitCheckCrcError;  // decode returns false on mismatch (:142-148)
+      } else {
+        st = kSuccess;
+        // Seal: store the body CRC into the V1 header's crc_ (serialized at +20).
+        // (base_packet_streamer.cpp:166-175 writes only V1 headers; a V0-flag
+        // frame keeps its bytes.)
+        uint8_t* p = base + pd[i].offset;
+        if (ld_le32(p) == kPacketFlagV1) {
+          const uint32_t c = crc[i];
+          for (int b = 0; b < 4; ++b) p[kPacketHeaderV0Size + 8 + b] = uint8_t(c >> (8 * b));
+        }
+      }
+    } else if (crc) {
+      crc[i] = 0u;  // not checked
+    }
+    status[i] = st;
+    bad = st != kSuccess ? 1u : 0u;
+  }
+  // One atomic per wave.
+  const uint64_t m = __ballot(bad != 0);
+  if (n_bad && m && (threadIdx.x & (kWave - 1)) == 0) atomicAdd(n_bad, uint32_t(__popcll(m)));
+  (void)desc;
 }
 
 // Compaction repack (task.cpp:753-798): copy each live record (FileInfo|payload)
@@ -654,11 +755,11 @@ static unsigned grid_for(uint32_t nwork) {
 template <int MODE>
 static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
                                  uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched,
-                                 hipStream_t stream) {
+                                 hipStream_t stream, uint32_t vseed) {
   const dim3 grid(grid_for(n)), block(kBlock);
 #define TFS_LAUNCH(R, P, N, D, S)                                                                          \
   hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N, D, S>), grid, block, 0, stream, base, desc, n, tg, out_crc, \
-                     out_ok, n_bad, sched)
+                     out_ok, n_bad, sched, vseed)
   switch (variant) {
     case 1: TFS_LAUNCH(16, 5, true, false, true); break;
     case 2: TFS_LAUNCH(16, 4, true, true, true); break;
@@ -674,10 +775,26 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
 
 hipError_t launch_crc_files(int mode, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
                             uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
-                            int variant) {
+                            int variant, uint32_t vseed) {
   if (n == 0) return hipSuccess;
-  if (mode == 0) return launch_variant<0>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, sched, stream);
-  return launch_variant<1>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, sched, stream);
+  if (mode == 0) return launch_variant<0>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, sched, stream, vseed);
+  return launch_variant<1>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, sched, stream, vseed);
+}
+
+hipError_t launch_packet_parse(const uint8_t* base, const PacketDesc* pd, uint32_t n, int mode, Desc* desc,
+                               int32_t* pre, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(packet_parse_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, base, pd, n, mode, desc, pre);
+  return hipGetLastError();
+}
+
+hipError_t launch_packet_finish(uint8_t* base, const PacketDesc* pd, const Desc* desc, uint32_t n, int mode,
+                                const int32_t* pre, const uint8_t* ok, uint32_t* crc, int32_t* status,
+                                uint32_t* n_bad, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(packet_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, base, pd, desc, n, mode, pre,
+                     ok, crc, status, n_bad);
+  return hipGetLastError();
 }
 
 hipError_t launch_block_verify(const uint8_t* image, uint64_t image_len, const RawMeta* metas, uint32_t n,
