@@ -282,6 +282,11 @@ int tfs_crc32_synth_fill_device(tfs_crc_ctx* ctx, void* d_dst, uint64_t nbytes, 
  * at d_image + d_rec_off[f] for f < n (device pointers). */
 int tfs_crc32_write_headers_device(tfs_crc_ctx* ctx, void* d_image, const uint64_t* d_rec_off, const uint32_t* d_len,
                                    const uint32_t* d_crc, uint64_t first_id, uint32_t n, void* stream);
+/* Write unsealed V1 frame headers {flag V1, length = d_body_len[f], type =
+ * pcode, version, id = first_id + f, crc 0} at d_base + d_frame_off[f]. */
+int tfs_crc32_write_packet_headers_device(tfs_crc_ctx* ctx, void* d_base, const uint64_t* d_frame_off,
+                                          const uint32_t* d_body_len, uint32_t n, int32_t pcode, int32_t version,
+                                          uint64_t first_id, void* stream);
 /* Calibration: stream the bytes without CRC arithmetic.  pattern 0 = coalesced
  * grid-stride over [d_base, d_base+nbytes); pattern 1 = the CRC kernel's
  * per-file lane-segment access pattern over d_desc (len multiple of 1 KiB). */

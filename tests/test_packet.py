@@ -200,3 +200,35 @@ def test_gpu_packet_device_resident(gpu_ctx, oracle):
     gpu_ctx.sync()
     ob, _, _ = o_seal(oracle, buf, frames)
     assert np.array_equal(d_base.download(np.uint8, len(b)), ob)
+
+
+@pytest.mark.gpu
+def test_ds_packet_codec_roundtrip(gpu_ctx, oracle):
+    """The C++ codec (tfs_amd/ds/packet_codec.cpp): a send batch sealed on the GPU
+    decodes cleanly; a flipped body byte fails that frame only; a cut stream
+    leaves the incomplete tail unconsumed (getPacketInfo waits for it)."""
+    from tfs_amd import dataserver as ds
+    enc = ds.PacketEncoder(gpu_ctx)
+    bodies = []
+    for i in range(40):
+        body = pk.write_data_body(100 + i, 5000 + i, i * 65536, synth_bytes(77 + i, 1 + 1733 * i).tobytes(),
+                                  ds=[1, 2, 3], lease=(2, 900 + i))
+        bodies.append(body)
+        enc.add(pk.WRITE_DATA_MESSAGE, pk.TFS_PACKET_VERSION_V2, 1000 + i, body)
+    assert enc.flush() == 0
+    out = enc.output()
+    # identical to building the frames in Python and sealing with the oracle
+    ref = b"".join(pk.frame_v1(b, version=2, pid=1000 + i) for i, b in enumerate(bodies))
+    frames = pk.split_frames(ref)
+    ob, _, _ = o_seal(oracle, ref, frames)
+    assert out == ob.tobytes()
+    rc, off, st, crc, consumed = ds.decode_stream(gpu_ctx, out)
+    assert rc == 0 and len(st) == 40 and (st == 0).all() and consumed == len(out)
+    bad = bytearray(out)
+    bad[off[7] + 24 + 50] ^= 0x40
+    rc, off2, st2, _, consumed = ds.decode_stream(gpu_ctx, bytes(bad))
+    assert rc == -1010 and st2[7] == -1010 and (np.delete(st2, 7) == 0).all()
+    cut = out[:off[30] + 100]
+    rc, off3, st3, _, consumed = ds.decode_stream(gpu_ctx, cut)
+    assert rc == 0 and consumed == off[30] and st3[-1] == 1 and len(st3) == 31
+    enc.free()

@@ -59,6 +59,7 @@ EXPORTED = [
     "tfs_crc32_event_elapsed_ms", "tfs_crc32_event_destroy",
     "tfs_crc32_stream", "tfs_crc32_sync",
     "tfs_packet_verify", "tfs_packet_verify_device", "tfs_packet_seal", "tfs_packet_seal_device",
+    "tfs_crc32_write_packet_headers_device",
 ]
 
 
@@ -124,6 +125,7 @@ def lib():
             "tfs_packet_verify_device": (ctypes.c_int, [vp, vp, u32, vp, vp, vp, vp, vp]),
             "tfs_packet_seal": (ctypes.c_int, [vp, vp, u32, vp, u64, vp, vp]),
             "tfs_packet_seal_device": (ctypes.c_int, [vp, vp, u32, vp, vp, vp, vp]),
+            "tfs_crc32_write_packet_headers_device": (ctypes.c_int, [vp, vp, vp, vp, u32, i32, i32, u64, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -319,6 +321,12 @@ class Context:
         self._check(lib().tfs_packet_seal(self.handle, _ptr(d), n, _ptr(buf), buf.size, _ptr(crc), _ptr(st)),
                     "packet_seal")
         return crc, st
+
+    def write_packet_headers_device(self, d_base, d_frame_off, d_body_len, n, pcode=9, version=2, first_id=1,
+                                    stream=None):
+        self._check(lib().tfs_crc32_write_packet_headers_device(self.handle, _ptr(d_base), _ptr(d_frame_off),
+                                                                _ptr(d_body_len), n, pcode, version, first_id,
+                                                                stream), "write_packet_headers_device")
 
     def packet_verify_device(self, d_desc, n, d_base, d_crc, d_status, d_nbad=None, stream=None):
         self._check(lib().tfs_packet_verify_device(self.handle, _ptr(d_desc), n, _ptr(d_base), _ptr(d_crc),

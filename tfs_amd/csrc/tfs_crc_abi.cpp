@@ -38,6 +38,8 @@ hipError_t launch_compact_copy(const uint8_t* src, const RawMeta* metas, const i
 hipError_t launch_synth_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, uint64_t first_word, hipStream_t stream);
 hipError_t launch_write_headers(uint8_t* image, const uint64_t* rec_off, const uint32_t* len, const uint32_t* crc,
                                 uint64_t first_id, uint32_t n, hipStream_t stream);
+hipError_t launch_write_packet_headers(uint8_t* base, const uint64_t* rec_off, const uint32_t* len, uint32_t n,
+                                       int32_t pcode, int32_t version, uint64_t first_id, hipStream_t stream);
 hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, uint32_t n, uint64_t nbytes,
                            uint32_t* out, unsigned grid, hipStream_t stream);
 }  // namespace tfscrc
@@ -857,6 +859,17 @@ int tfs_crc32_write_headers_device(tfs_crc_ctx* ctx, void* d_image, const uint64
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   HIP_TRY(ctx, launch_write_headers(static_cast<uint8_t*>(d_image), d_rec_off, d_len, d_crc, first_id, n, st));
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_write_packet_headers_device(tfs_crc_ctx* ctx, void* d_base, const uint64_t* d_frame_off,
+                                          const uint32_t* d_body_len, uint32_t n, int32_t pcode, int32_t version,
+                                          uint64_t first_id, void* stream) {
+  if (!ctx || (n && (!d_base || !d_frame_off || !d_body_len))) return TFS_EXIT_PARAMETER_ERROR;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  HIP_TRY(ctx, launch_write_packet_headers(static_cast<uint8_t*>(d_base), d_frame_off, d_body_len, n, pcode, version,
+                                           first_id, st));
   return TFS_SUCCESS;
 }
 

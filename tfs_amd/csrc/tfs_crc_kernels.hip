@@ -690,6 +690,20 @@ __global__ void write_headers_kernel(uint8_t* __restrict__ image, const uint64_t
   for (int i = 0; i < kFileInfoSize; ++i) d[i] = hb[i];
 }
 
+// Bench/test helper: unsealed V1 frame headers (crc 0) at rec_off[f] for bodies
+// of len[f] bytes (TfsPacketNewHeaderV1::serialize order, little-endian).
+__global__ void write_packet_headers_kernel(uint8_t* __restrict__ base, const uint64_t* __restrict__ rec_off,
+                                            const uint32_t* __restrict__ len, uint32_t n, int32_t pcode,
+                                            int32_t version, uint64_t first_id) {
+  const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= n) return;
+  uint8_t* p = base + rec_off[f];
+  const uint64_t id = first_id + f;
+  const uint32_t w[6] = {kPacketFlagV1, len[f], (uint32_t(pcode) & 0xFFFFu) | (uint32_t(version) << 16),
+                         uint32_t(id), uint32_t(id >> 32), 0u};
+  for (int i = 0; i < 24; ++i) p[i] = uint8_t(w[i >> 2] >> (8 * (i & 3)));
+}
+
 // Calibration kernel (not on the product path): stream the same bytes without
 // the CRC arithmetic.  run == 0: fully coalesced grid-stride, 16 B/lane.
 // run > 0: the CRC kernel's pattern -- one wave per file, each lane reading
@@ -835,6 +849,14 @@ hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, u
     hipLaunchKernelGGL(membench_kernel<true>, g, dim3(kBlock), 0, stream, base, desc, n, nbytes, run, out, align);
   else
     hipLaunchKernelGGL(membench_kernel<false>, g, dim3(kBlock), 0, stream, base, desc, n, nbytes, run, out, align);
+  return hipGetLastError();
+}
+
+hipError_t launch_write_packet_headers(uint8_t* base, const uint64_t* rec_off, const uint32_t* len, uint32_t n,
+                                       int32_t pcode, int32_t version, uint64_t first_id, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(write_packet_headers_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, base, rec_off, len, n,
+                     pcode, version, first_id);
   return hipGetLastError();
 }
 

@@ -51,6 +51,14 @@ def lib():
             "tfs_ds_checker_needs_repair": (ctypes.c_int, [vp, u32]),
             "tfs_ds_verify_block": (ctypes.c_int, [vp, vp, vp, u32, vp]),
             "tfs_ds_compact_block": (ctypes.c_int, [vp, vp, vp, vp, u32]),
+            "tfs_ds_encoder_new": (vp, [vp]),
+            "tfs_ds_encoder_free": (None, [vp]),
+            "tfs_ds_encoder_add": (None, [vp, ctypes.c_int16, ctypes.c_int16, u64, ctypes.c_char_p, i32]),
+            "tfs_ds_encoder_flush": (ctypes.c_int, [vp]),
+            "tfs_ds_encoder_size": (i64, [vp]),
+            "tfs_ds_encoder_data": (vp, [vp]),
+            "tfs_ds_decode": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, u32, ctypes.POINTER(u32),
+                                             ctypes.POINTER(i64)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -167,6 +175,51 @@ class BlockCrcChecker:
         if self.h:
             lib().tfs_ds_checker_free(self.h)
             self.h = None
+
+
+class PacketEncoder:
+    """Send-side packet batch (packet_codec.h): V1 frames sealed on the GPU."""
+
+    def __init__(self, ctx):
+        self.h = lib().tfs_ds_encoder_new(ctx.handle)
+
+    def add(self, pcode, version, pid, body):
+        b = bytes(body)
+        lib().tfs_ds_encoder_add(self.h, pcode, version, pid, b, len(b))
+
+    def flush(self):
+        return lib().tfs_ds_encoder_flush(self.h)
+
+    def output(self):
+        n = lib().tfs_ds_encoder_size(self.h)
+        if n == 0:
+            return b""
+        return ctypes.string_at(lib().tfs_ds_encoder_data(self.h), n)
+
+    def free(self):
+        if self.h:
+            lib().tfs_ds_encoder_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def decode_stream(ctx, data, cap=1 << 16):
+    """Receive side: returns (rc, offsets, status, crc, consumed)."""
+    b = np.frombuffer(bytes(data), np.uint8)
+    off = np.zeros(cap, np.int64)
+    st = np.zeros(cap, np.int32)
+    crc = np.zeros(cap, np.uint32)
+    nfr = ctypes.c_uint32()
+    consumed = ctypes.c_int64()
+    rc = lib().tfs_ds_decode(ctx.handle, b.ctypes.data, b.size, off.ctypes.data, st.ctypes.data, crc.ctypes.data,
+                             cap, ctypes.byref(nfr), ctypes.byref(consumed))
+    k = min(nfr.value, cap)
+    return rc, off[:k], st[:k], crc[:k], consumed.value
 
 
 def verify_block(ctx, block, checker=None):

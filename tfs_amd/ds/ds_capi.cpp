@@ -93,3 +93,34 @@ int tfs_ds_compact_block(tfs_crc_ctx* ctx, void* src, void* dest, uint8_t* crc_o
 }
 
 }  // extern "C"
+
+// ---- packet codec (packet_codec.h) ----------------------------------------
+#include "packet_codec.h"
+
+extern "C" {
+
+void* tfs_ds_encoder_new(tfs_crc_ctx* ctx) { return new tfs::common::PacketEncoder(ctx); }
+void tfs_ds_encoder_free(void* e) { delete static_cast<tfs::common::PacketEncoder*>(e); }
+void tfs_ds_encoder_add(void* e, int16_t pcode, int16_t version, uint64_t id, const char* body, int32_t len) {
+  static_cast<tfs::common::PacketEncoder*>(e)->add(pcode, version, id, body, len);
+}
+int tfs_ds_encoder_flush(void* e) { return static_cast<tfs::common::PacketEncoder*>(e)->flush(); }
+int64_t tfs_ds_encoder_size(void* e) { return int64_t(static_cast<tfs::common::PacketEncoder*>(e)->output().size()); }
+const char* tfs_ds_encoder_data(void* e) { return static_cast<tfs::common::PacketEncoder*>(e)->output().data(); }
+
+// Decode a received buffer: per frame offset/status/crc (cap entries), *nframes, *consumed.
+int tfs_ds_decode(tfs_crc_ctx* ctx, const char* data, int64_t len, int64_t* offsets, int32_t* status, uint32_t* crc,
+                  uint32_t cap, uint32_t* nframes, int64_t* consumed) {
+  tfs::common::PacketDecoder dec(ctx);
+  std::vector<tfs::common::PacketDecoder::Frame> fr;
+  const int rc = dec.decode(data, len, &fr, consumed);
+  *nframes = uint32_t(fr.size());
+  for (size_t i = 0; i < fr.size() && i < cap; ++i) {
+    if (offsets) offsets[i] = fr[i].offset;
+    if (status) status[i] = fr[i].status;
+    if (crc) crc[i] = fr[i].crc;
+  }
+  return rc;
+}
+
+}  // extern "C"
