@@ -1,0 +1,179 @@
+"""On-disk block formats: tfs_amd/ds/block_store.{h,cpp}.
+
+Physical block files with BlockPrefix chains (physical_block.cpp:30-60,172-189),
+main/extension stitching (data_handle.cpp:103-141), the hash index
+(index_handle.cpp:844-878,1015-1060) and real flags (logic_block.cpp:996-1009,
+1250-1273).  Parity note: there is no block file written by the reference in
+/root/reference (the dataserver cannot be built here: tbsys/tbnet are absent),
+so the format is pinned by the reference's struct definitions and write path,
+restated in the writer; the reader is checked against it and against hand-made
+variants (prefix file, hash collisions, broken chains).  Verify-from-disk is
+checked against the oracle on the GPU.
+"""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from tests.conftest import ocrc
+from tfs_amd.synth import synth_bytes
+
+MiB = 1 << 20
+
+
+@pytest.fixture(scope="module")
+def ds():
+    from tfs_amd import dataserver
+    dataserver.lib()
+    return dataserver
+
+
+def make_block(ds, oracle, block_id, sizes, seed=1, flags=None):
+    b = ds.LogicBlock(block_id)
+    for i, ln in enumerate(sizes):
+        payload = synth_bytes(seed * 1000 + i, ln).tobytes()
+        assert b.append(i + 1, payload, ocrc(oracle, 0, payload)) == 0
+    for fid, fl in (flags or {}).items():
+        assert b.set_flag(fid, fl) == 0
+    return b
+
+
+def check_loaded(ds, block, lb, flags=None):
+    assert lb.rc == 0
+    assert np.array_equal(lb.data(), block.raw())
+    m, _ = block.metas()
+    assert np.array_equal(lb.metas, m)
+    exp = np.zeros(len(m), np.int32)
+    for fid, fl in (flags or {}).items():
+        exp[np.nonzero(m["file_id"] == fid)[0][0]] = fl
+    assert np.array_equal(lb.flags, exp)
+
+
+def test_roundtrip_chain_and_index(ds, oracle, tmp_path):
+    rng = np.random.default_rng(5)
+    sizes = [int(x) for x in rng.integers(0, 60000, 80)]
+    flags = {3: 1, 10: 1, 11: 4, 40: 5}
+    blk = make_block(ds, oracle, 77, sizes, flags=flags)
+    mount = str(tmp_path)
+    ext = ds.write_block_files(blk, mount, main_id=5, first_ext_id=100, bucket_size=13, main_size=1 * MiB,
+                               ext_size=256 * 1024)
+    total = int(blk.raw().size)
+    assert len(ext) == -(-(total - (MiB - 512)) // (256 * 1024 - 512))
+    lb = ds.LoadedBlock(None, mount, 5, main_size=1 * MiB, ext_size=256 * 1024)
+    check_loaded(ds, blk, lb, flags)
+    assert lb.chain == [5] + ext and lb.logic_block_id == 77
+    h = lb.header[0]
+    assert h["bucket_size"] == 13 and h["data_file_offset"] == total and h["file_count"] == len(sizes)
+    assert h["index_file_size"] == 48 + 4 * 13 + 20 * len(sizes)
+    assert h["del_file_count"] == sum(1 for f in flags.values() if f & 1)
+    # the files are TFS-shaped: <mount>/<main>, <mount>/extend/<id>, <mount>/index/<main>
+    assert os.path.getsize(os.path.join(mount, "5")) == MiB
+    assert os.path.getsize(os.path.join(mount, "extend", str(ext[0]))) == 256 * 1024
+    raw = open(os.path.join(mount, "5"), "rb").read(24)
+    assert struct.unpack("<IIIIQ", raw) == (77, 0, ext[0], 0, 0)
+
+
+def test_index_entries_carry_unlink_flags(ds, oracle, tmp_path):
+    blk = make_block(ds, oracle, 9, [100] * 6, flags={2: 1, 5: 2})
+    mount = str(tmp_path)
+    ds.write_block_files(blk, mount, 1, 50, bucket_size=4)
+    idx = open(os.path.join(mount, "index", "1"), "rb").read()
+    sizes = {}
+    for pos in range(48 + 16, len(idx), 20):
+        fid, off, sz, nxt = struct.unpack_from("<Qiii", idx, pos)
+        sizes[fid] = sz
+    assert sizes[2] == (136 | 0x08000000 | (1 << 28)) and sizes[5] == (136 | 0x08000000 | (2 << 28))
+    assert sizes[1] == 136  # untouched entries keep the plain size
+    # FileInfo.flag_ on disk stays 0 (unlink_file writes the flag to the index only)
+    data = open(os.path.join(mount, "1"), "rb").read()
+    assert struct.unpack_from("<i", data, 512 + 136 + 28)[0] == 0
+
+
+def test_block_prefix_file_and_collisions(ds, oracle, tmp_path):
+    blk = make_block(ds, oracle, 31, [5000] * 40, seed=2)
+    mount = str(tmp_path)
+    ext = ds.write_block_files(blk, mount, 3, 7, bucket_size=3, main_size=64 * 1024, ext_size=32 * 1024)
+    # move every prefix into <mount>/block_prefix at (id-1)*24 and wipe the in-file copies
+    pf = bytearray(24 * (max([3] + ext) + 1))
+    for pid, path in [(3, os.path.join(mount, "3"))] + [(e, os.path.join(mount, "extend", str(e))) for e in ext]:
+        with open(path, "r+b") as f:
+            pf[(pid - 1) * 24:pid * 24] = f.read(24)
+            f.seek(0)
+            f.write(b"\0" * 24)
+    open(os.path.join(mount, "block_prefix"), "wb").write(bytes(pf))
+    lb = ds.LoadedBlock(None, mount, 3, main_size=64 * 1024, ext_size=32 * 1024)
+    check_loaded(ds, blk, lb)
+    assert lb.chain == [3] + ext
+
+
+def test_broken_chain_and_index_rejected(ds, oracle, tmp_path):
+    blk = make_block(ds, oracle, 8, [3000] * 30, seed=3)
+    mount = str(tmp_path)
+    ext = ds.write_block_files(blk, mount, 2, 20, bucket_size=5, main_size=32 * 1024, ext_size=16 * 1024)
+    with open(os.path.join(mount, "extend", str(ext[1])), "r+b") as f:  # wrong back link
+        f.seek(4)
+        f.write(struct.pack("<I", 999))
+    assert ds.LoadedBlock(None, mount, 2, main_size=32 * 1024, ext_size=16 * 1024).rc != 0
+    blk2 = make_block(ds, oracle, 8, [3000] * 30, seed=3)
+    m2 = str(tmp_path / "b")
+    ds.write_block_files(blk2, m2, 2, 20, bucket_size=5, main_size=32 * 1024, ext_size=16 * 1024)
+    with open(os.path.join(m2, "index", "2"), "r+b") as f:  # bucket pointing past the index
+        f.seek(48)
+        f.write(struct.pack("<i", 1 << 20))
+    assert ds.LoadedBlock(None, m2, 2, main_size=32 * 1024, ext_size=16 * 1024).rc != 0
+
+
+def baseline_block(ds, oracle):
+    """1,024 x 64 KiB files in a 64 MiB main block; the 1,024th spills
+    37,376 B into an extension block."""
+    return make_block(ds, oracle, 4242, [65536] * 1024, seed=9)
+
+
+def test_baseline_layout_spills_into_ext(ds, oracle, tmp_path):
+    blk = baseline_block(ds, oracle)
+    mount = str(tmp_path)
+    ext = ds.write_block_files(blk, mount, 11, 500)
+    assert len(ext) == 1
+    assert blk.raw().size - (64 * MiB - 512) == 37376
+    lb = ds.LoadedBlock(None, mount, 11)
+    check_loaded(ds, blk, lb)
+
+
+@pytest.mark.gpu
+def test_gpu_verify_block_files(ds, oracle, gpu_ctx, tmp_path):
+    blk = baseline_block(ds, oracle)
+    blk.set_flag(100, 1)  # deleted: skipped
+    mount = str(tmp_path)
+    ext = ds.write_block_files(blk, mount, 11, 500)
+    checker = ds.BlockCrcChecker(4)
+    rc, st = ds.verify_block_files(gpu_ctx, mount, 11, checker)
+    assert rc == 0 and len(st) == 1023 and (st == 0).all()
+    # corrupt the payload of the last file where it lies in the extension block,
+    # and one file in the main block
+    with open(os.path.join(mount, "extend", str(ext[0])), "r+b") as f:
+        f.seek(512 + 1000)
+        b = f.read(1)
+        f.seek(512 + 1000)
+        f.write(bytes([b[0] ^ 0x20]))
+    m, _ = blk.metas()
+    off7 = int(m["offset"][7]) + 36 + 5
+    with open(os.path.join(mount, "11"), "r+b") as f:
+        f.seek(512 + off7)
+        b = f.read(1)
+        f.seek(512 + off7)
+        f.write(bytes([b[0] ^ 0x01]))
+    rc, st = ds.verify_block_files(gpu_ctx, mount, 11, checker)
+    assert rc == 2
+    assert st[7] == -1010 and st[-1] == -1010
+    assert (np.delete(st, [7, len(st) - 1]) == 0).all()
+    assert checker.errors(4242) == 2
+    # oracle on the stitched image agrees file by file
+    lb = ds.LoadedBlock(None, mount, 11)
+    img = lb.data().tobytes()
+    live = [i for i in range(len(lb.metas)) if lb.flags[i] == 0]
+    for k, i in enumerate(live):
+        o, sz = int(lb.metas["offset"][i]), int(lb.metas["size"][i])
+        stored = struct.unpack_from("<I", img, o + 32)[0]
+        exp = 0 if ocrc(oracle, 0, img[o + 36:o + sz]) == stored else -1010
+        assert st[k] == exp

@@ -57,6 +57,18 @@ def lib():
             "tfs_ds_encoder_flush": (ctypes.c_int, [vp]),
             "tfs_ds_encoder_size": (i64, [vp]),
             "tfs_ds_encoder_data": (vp, [vp]),
+            "tfs_ds_block_write_files": (ctypes.c_int, [vp, ctypes.c_char_p, i32, i32, u32, u32, i32, vp, u32,
+                                                         ctypes.POINTER(u32)]),
+            "tfs_ds_block_append": (ctypes.c_int, [vp, u64, ctypes.c_char_p, i32, u32]),
+            "tfs_ds_loaded_new": (vp, [vp]),
+            "tfs_ds_loaded_free": (None, [vp]),
+            "tfs_ds_loaded_load": (ctypes.c_int, [vp, ctypes.c_char_p, i32, i32, u32]),
+            "tfs_ds_loaded_size": (i64, [vp]),
+            "tfs_ds_loaded_data": (vp, [vp]),
+            "tfs_ds_loaded_logic_id": (u32, [vp]),
+            "tfs_ds_loaded_metas": (u32, [vp, vp, vp, u32, vp, u32, ctypes.POINTER(u32), vp]),
+            "tfs_ds_verify_block_files": (ctypes.c_int, [vp, ctypes.c_char_p, i32, i32, u32, vp, u32,
+                                                         ctypes.POINTER(u32), vp]),
             "tfs_ds_decode": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, u32, ctypes.POINTER(u32),
                                              ctypes.POINTER(i64)]),
         }
@@ -117,6 +129,11 @@ class LogicBlock:
             return np.zeros(0, np.uint8)
         p = lib().tfs_ds_block_data(self.h)
         return np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(p)).copy()
+
+    def append(self, file_id, payload, crc):
+        """Append FileInfo|payload with a caller-supplied crc (fixtures; no CRC computed)."""
+        b = bytes(payload)
+        return lib().tfs_ds_block_append(self.h, file_id, b, len(b), crc)
 
     def set_flag(self, file_id, flag):
         return lib().tfs_ds_block_set_flag(self.h, file_id, flag)
@@ -220,6 +237,72 @@ def decode_stream(ctx, data, cap=1 << 16):
                              cap, ctypes.byref(nfr), ctypes.byref(consumed))
     k = min(nfr.value, cap)
     return rc, off[:k], st[:k], crc[:k], consumed.value
+
+
+MAIN_BLOCK_SIZE = 64 * 1024 * 1024  # mainblock_size (config_item.h:132)
+EXT_BLOCK_SIZE = 32 * 1024 * 1024   # extblock_size (config_item.h:133)
+INDEX_HEADER_DTYPE = np.dtype([("block_id", "<u4"), ("version", "<i4"), ("file_count", "<i4"), ("size", "<i4"),
+                               ("del_file_count", "<i4"), ("del_size", "<i4"), ("seq_no", "<u4"), ("flag", "<i4"),
+                               ("bucket_size", "<i4"), ("data_file_offset", "<i4"), ("index_file_size", "<i4"),
+                               ("free_head_offset", "<i4")])
+
+
+def write_block_files(block, mount, main_id, first_ext_id, bucket_size=1024, main_size=MAIN_BLOCK_SIZE,
+                      ext_size=EXT_BLOCK_SIZE):
+    """Persist a LogicBlock in TFS's on-disk format (block_store.h); returns the ext ids."""
+    ids = np.zeros(64, np.uint32)
+    n = ctypes.c_uint32()
+    rc = lib().tfs_ds_block_write_files(block.h, mount.encode(), main_size, ext_size, main_id, first_ext_id,
+                                        bucket_size, ids.ctypes.data, 64, ctypes.byref(n))
+    if rc != 0:
+        raise _crc.TfsCrcError(rc, "write_block_files")
+    return ids[:n.value].tolist()
+
+
+class LoadedBlock:
+    """A block read back from disk (chain, index, flags, data in pinned memory)."""
+
+    def __init__(self, ctx, mount, main_id, main_size=MAIN_BLOCK_SIZE, ext_size=EXT_BLOCK_SIZE):
+        self.h = lib().tfs_ds_loaded_new(ctx.handle if ctx is not None else None)
+        self.rc = lib().tfs_ds_loaded_load(self.h, mount.encode(), main_size, ext_size, main_id)
+        if self.rc != 0:
+            return
+        n = lib().tfs_ds_loaded_metas(self.h, None, None, 0, None, 0, None, None)
+        self.metas = np.zeros(n, _crc.META_DTYPE)
+        self.flags = np.zeros(n, np.int32)
+        chain = np.zeros(64, np.uint32)
+        clen = ctypes.c_uint32()
+        self.header = np.zeros(1, INDEX_HEADER_DTYPE)
+        lib().tfs_ds_loaded_metas(self.h, self.metas.ctypes.data, self.flags.ctypes.data, n, chain.ctypes.data, 64,
+                                  ctypes.byref(clen), self.header.ctypes.data)
+        self.chain = chain[:clen.value].tolist()
+        self.logic_block_id = lib().tfs_ds_loaded_logic_id(self.h)
+
+    def data(self):
+        n = lib().tfs_ds_loaded_size(self.h)
+        if n == 0:
+            return np.zeros(0, np.uint8)
+        return np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(lib().tfs_ds_loaded_data(self.h))).copy()
+
+    def free(self):
+        if self.h:
+            lib().tfs_ds_loaded_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def verify_block_files(ctx, mount, main_id, checker=None, main_size=MAIN_BLOCK_SIZE, ext_size=EXT_BLOCK_SIZE):
+    """Verify-on-read from block files on disk: returns (nbad or <0, live statuses)."""
+    st = np.zeros(1 << 16, np.int32)
+    nl = ctypes.c_uint32()
+    rc = lib().tfs_ds_verify_block_files(ctx.handle, mount.encode(), main_size, ext_size, main_id, st.ctypes.data,
+                                         st.size, ctypes.byref(nl), checker.h if checker else None)
+    return rc, st[:nl.value]
 
 
 def verify_block(ctx, block, checker=None):

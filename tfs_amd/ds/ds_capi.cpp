@@ -124,3 +124,65 @@ int tfs_ds_decode(tfs_crc_ctx* ctx, const char* data, int64_t len, int64_t* offs
 }
 
 }  // extern "C"
+
+// ---- on-disk blocks (block_store.h) ----------------------------------------
+#include "block_store.h"
+
+extern "C" {
+
+static tfs::dataserver::BlockStore make_store(const char* mount, int32_t main_size, int32_t ext_size) {
+  tfs::dataserver::BlockStore st;
+  st.mount = mount;
+  st.main_block_size = main_size;
+  st.ext_block_size = ext_size;
+  return st;
+}
+
+int tfs_ds_block_write_files(void* block, const char* mount, int32_t main_size, int32_t ext_size, uint32_t main_id,
+                             uint32_t first_ext_id, int32_t bucket_size, uint32_t* ext_ids, uint32_t cap,
+                             uint32_t* n_ext) {
+  std::vector<uint32_t> ids;
+  const int rc = tfs::dataserver::write_logic_block(make_store(mount, main_size, ext_size), main_id, first_ext_id,
+                                                    *static_cast<LogicBlockImage*>(block), bucket_size, &ids);
+  if (n_ext) *n_ext = uint32_t(ids.size());
+  for (size_t i = 0; ext_ids && i < ids.size() && i < cap; ++i) ext_ids[i] = ids[i];
+  return rc;
+}
+
+int tfs_ds_block_append(void* b, uint64_t file_id, const char* payload, int32_t len, uint32_t crc) {
+  return static_cast<LogicBlockImage*>(b)->append_record(file_id, payload, len, crc);
+}
+
+void* tfs_ds_loaded_new(tfs_crc_ctx* ctx) { return new tfs::dataserver::LoadedBlock(ctx); }
+void tfs_ds_loaded_free(void* b) { delete static_cast<tfs::dataserver::LoadedBlock*>(b); }
+int tfs_ds_loaded_load(void* b, const char* mount, int32_t main_size, int32_t ext_size, uint32_t main_id) {
+  return static_cast<tfs::dataserver::LoadedBlock*>(b)->load(make_store(mount, main_size, ext_size), main_id);
+}
+int64_t tfs_ds_loaded_size(void* b) { return static_cast<tfs::dataserver::LoadedBlock*>(b)->size(); }
+const char* tfs_ds_loaded_data(void* b) { return static_cast<tfs::dataserver::LoadedBlock*>(b)->data(); }
+uint32_t tfs_ds_loaded_logic_id(void* b) { return static_cast<tfs::dataserver::LoadedBlock*>(b)->logic_block_id; }
+// Copy metas/flags (cap entries) and the chain (chain_cap); returns the meta count.
+uint32_t tfs_ds_loaded_metas(void* b, tfs_raw_meta* metas, int32_t* flags, uint32_t cap, uint32_t* chain,
+                             uint32_t chain_cap, uint32_t* chain_len, void* header48) {
+  auto* lb = static_cast<tfs::dataserver::LoadedBlock*>(b);
+  for (size_t i = 0; i < lb->metas.size() && i < cap; ++i) {
+    if (metas) metas[i] = lb->metas[i];
+    if (flags) flags[i] = lb->flags[i];
+  }
+  if (chain_len) *chain_len = uint32_t(lb->chain.size());
+  for (size_t i = 0; chain && i < lb->chain.size() && i < chain_cap; ++i) chain[i] = lb->chain[i];
+  if (header48) memcpy(header48, &lb->header, sizeof lb->header);
+  return uint32_t(lb->metas.size());
+}
+
+int tfs_ds_verify_block_files(tfs_crc_ctx* ctx, const char* mount, int32_t main_size, int32_t ext_size,
+                              uint32_t main_id, int32_t* status, uint32_t cap, uint32_t* n_live, void* checker) {
+  std::vector<int32_t> st;
+  const int rc = tfs::dataserver::verify_block_files(ctx, make_store(mount, main_size, ext_size), main_id, &st,
+                                                     static_cast<BlockCrcChecker*>(checker));
+  if (n_live) *n_live = uint32_t(st.size());
+  for (size_t i = 0; status && i < st.size() && i < cap; ++i) status[i] = st[i];
+  return rc;
+}
+
+}  // extern "C"
