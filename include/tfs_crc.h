@@ -197,6 +197,19 @@ int tfs_block_compact(tfs_crc_ctx* ctx, const void* src_image, uint64_t src_len,
                       const int32_t* flags, uint32_t n, void* dest_image, uint64_t dest_cap, tfs_raw_meta* dest_metas,
                       uint8_t* crc_ok, uint64_t* dest_len, uint32_t* n_live);
 
+/* Device-resident compaction data pass (one kernel, one read of every live
+ * record): for the live files d_live_metas[0..n) (already filtered and in
+ * offset order), re-CRC each payload against its stored crc_ and write
+ * FileInfo{offset_ = d_dest_off[i], size_ = usize_ = meta.size, flag_ =
+ * d_flags[i], rest copied} | payload at d_dest + d_dest_off[i].  Per-file
+ * status as tfs_block_verify; d_n_bad (may be NULL) accumulated into.  The
+ * caller computes d_dest_off (the running sum of live sizes, task.cpp:753-768)
+ * and d_dest must hold sum(size).  Several blocks can share one call when
+ * their images are concatenated in d_src.  Asynchronous on `stream`. */
+int tfs_block_compact_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_len, const tfs_raw_meta* d_live_metas,
+                             const int32_t* d_flags, const int64_t* d_dest_off, uint32_t n, void* d_dest,
+                             uint32_t* d_out_crc, int32_t* d_out_status, uint32_t* d_n_bad, void* stream);
+
 /* Many blocks in one call (the compaction task thread's queue): each job is
  * tfs_block_compact's arguments plus its outputs.  Jobs are pipelined over
  * several streams so the H2D copy of one block, the verify/repack kernels of

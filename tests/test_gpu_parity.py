@@ -221,6 +221,73 @@ def test_block_compact_matches_oracle(gpu_ctx, oracle):
     assert [int(x) for x in dmetas["offset"]] == [int(doff[i]) for i in live]
 
 
+def _oracle_compact(oracle, img, metas, flags):
+    n = len(metas)
+    mo = metas["offset"].astype(np.int64)
+    ms = metas["size"].astype(np.int32)
+    odest = np.zeros(int(ms.sum()) + 64, np.uint8)
+    doff = np.zeros(n, np.int64)
+    dsz = np.zeros(n, np.int32)
+    ook = np.zeros(n, np.uint8)
+    w = oracle.oracle_compact(img.ctypes.data, mo.ctypes.data, ms.ctypes.data, flags.ctypes.data, n,
+                              odest.ctypes.data, doff.ctypes.data, dsz.ctypes.data, ook.ctypes.data)
+    return odest[:w], doff, ook
+
+
+def test_compact_fused_every_shift_class(gpu_ctx, oracle):
+    """The fused compaction kernel stores payload registers at dst = src + delta:
+    delta = 0 mod 16 (nt 16-byte stores), 4/8/12 mod 16 (dword stores) and
+    not 0 mod 4 (byte-copy fallback) -- all byte-identical to the oracle's
+    real_compact restatement, with payloads from 1 byte to several stripes."""
+    rng = np.random.default_rng(91)
+    sizes, flags = [], []
+    for k in range(160):
+        sizes.append(int(rng.choice([1, 3, 17, 31, 32, 33, 100, 1023, 1024, 1025, 2049, 5000, 65536, 70001])))
+        # deleting a record of s bytes shifts every later record by s + 36 (mod 16: k % 16)
+        flags.append(1 if k % 3 == 1 else 0)
+        if flags[-1]:
+            sizes[-1] = 16 + (k % 16 - 36) % 16
+    img, metas = _block_image(oracle, sizes, seed=71)
+    fl = np.array(flags, np.int32)
+    img[int(metas[10]["offset"]) + 36 + 3] ^= 0x80
+    dest, dmetas, ok, rc = gpu_ctx.block_compact(img, metas, fl)
+    odest, doff, ook = _oracle_compact(oracle, img, metas, fl)
+    assert dest.size == odest.size and (dest == odest).all()
+    assert (ok == ook).all()
+    live = [i for i in range(len(sizes)) if not fl[i]]
+    deltas = {(int(doff[i]) - int(metas[i]["offset"])) % 16 for i in live}
+    assert {0, 4, 8, 12} <= deltas and deltas - {0, 4, 8, 12}  # every class exercised
+
+
+def test_block_compact_device_matches_oracle(gpu_ctx, oracle):
+    import tfs_amd.crc as crc
+    rng = np.random.default_rng(92)
+    sizes = [65536] * 50 + [int(x) for x in rng.integers(1, 30000, 50)]
+    img, metas = _block_image(oracle, sizes, seed=72)
+    fl = np.zeros(len(sizes), np.int32)
+    fl[::3] = 1
+    odest, doff, ook = _oracle_compact(oracle, img, metas, fl)
+    live = np.nonzero((fl & 3) == 0)[0]
+    lm = np.ascontiguousarray(metas[live])
+    lf = np.ascontiguousarray(fl[live])
+    ld = np.concatenate([[0], np.cumsum(lm["size"].astype(np.int64))[:-1]]).astype(np.int64)
+    n = len(live)
+    d_src = crc.DeviceBuffer(gpu_ctx, img.size).upload(img)
+    d_m = crc.DeviceBuffer(gpu_ctx, lm.nbytes).upload(lm)
+    d_f = crc.DeviceBuffer(gpu_ctx, lf.nbytes).upload(lf)
+    d_o = crc.DeviceBuffer(gpu_ctx, ld.nbytes).upload(ld)
+    d_dst = crc.DeviceBuffer(gpu_ctx, odest.size + 64)
+    d_crc = crc.DeviceBuffer(gpu_ctx, 4 * n)
+    d_st = crc.DeviceBuffer(gpu_ctx, 4 * n)
+    d_bad = crc.DeviceBuffer(gpu_ctx, 4)
+    d_bad.zero()
+    gpu_ctx.block_compact_device(d_src, img.size, d_m, d_f, d_o, n, d_dst, d_crc, d_st, d_bad)
+    gpu_ctx.sync()
+    assert (d_dst.download(np.uint8, odest.size) == odest).all()
+    assert (d_st.download(np.int32, n) == 0).all() and int(d_bad.download(np.uint32, 1)[0]) == 0
+    assert (ook[live] == 1).all()
+
+
 def _stripe_edge_cases(run, count=24):
     """(offset, len) pairs where the payload starts inside the last dword of
     stripe 0, so the high seed bytes land in stripe 1 (lane 0)."""

@@ -59,7 +59,7 @@ EXPORTED = [
     "tfs_crc32_event_elapsed_ms", "tfs_crc32_event_destroy",
     "tfs_crc32_stream", "tfs_crc32_sync",
     "tfs_packet_verify", "tfs_packet_verify_device", "tfs_packet_seal", "tfs_packet_seal_device",
-    "tfs_crc32_write_packet_headers_device",
+    "tfs_crc32_write_packet_headers_device", "tfs_block_compact_device",
 ]
 
 
@@ -106,6 +106,7 @@ def lib():
             "tfs_block_verify_device": (ctypes.c_int, [vp, vp, u64, vp, u32, vp, vp, vp, vp]),
             "tfs_block_compact": (ctypes.c_int, [vp, vp, u64, vp, vp, u32, vp, u64, vp, vp, vp, vp]),
             "tfs_blocks_compact": (ctypes.c_int, [vp, vp, u32]),
+            "tfs_block_compact_device": (ctypes.c_int, [vp, vp, u64, vp, vp, vp, u32, vp, vp, vp, vp, vp]),
             "tfs_crc32_synth_fill_device": (ctypes.c_int, [vp, vp, u64, u64, u64, vp]),
             "tfs_crc32_write_headers_device": (ctypes.c_int, [vp, vp, vp, vp, vp, u64, u32, vp]),
             "tfs_crc32_membench_device": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, u32, u64, vp, ctypes.c_uint, vp]),
@@ -284,6 +285,12 @@ class Context:
         self._check(lib().tfs_block_verify_device(self.handle, _ptr(d_image), image_len, _ptr(d_metas), n,
                                                   _ptr(d_crc), _ptr(d_status), _ptr(d_nbad), stream),
                     "block_verify_device")
+
+    def block_compact_device(self, d_src, src_len, d_live_metas, d_flags, d_dest_off, n, d_dest, d_crc=None,
+                             d_status=None, d_nbad=None, stream=None):
+        self._check(lib().tfs_block_compact_device(self.handle, _ptr(d_src), src_len, _ptr(d_live_metas),
+                                                   _ptr(d_flags), _ptr(d_dest_off), n, _ptr(d_dest), _ptr(d_crc),
+                                                   _ptr(d_status), _ptr(d_nbad), stream), "block_compact_device")
 
     def blocks_compact(self, jobs):
         """Pipelined compaction of many blocks; `jobs` is a ctypes array of BlockJob."""

@@ -35,6 +35,9 @@ hipError_t launch_block_verify(const uint8_t* image, uint64_t image_len, const R
                                hipStream_t stream);
 hipError_t launch_compact_copy(const uint8_t* src, const RawMeta* metas, const int32_t* flags, const int64_t* dest_off,
                                uint32_t n, uint8_t* dst, hipStream_t stream);
+hipError_t launch_compact_fused(const uint8_t* src, uint64_t src_len, const RawMeta* metas, const int32_t* flags,
+                                const int64_t* dest_off, uint32_t n, uint8_t* dst, const Tables* tg, uint32_t* out_crc,
+                                int32_t* out_status, uint32_t* n_bad, hipStream_t stream);
 hipError_t launch_synth_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, uint64_t first_word, hipStream_t stream);
 hipError_t launch_write_headers(uint8_t* image, const uint64_t* rec_off, const uint32_t* len, const uint32_t* crc,
                                 uint64_t first_id, uint32_t n, hipStream_t stream);
@@ -639,11 +642,11 @@ static int compact_enqueue(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job
   if (nl) {
     HIP_TRY(ctx, hipMemcpyAsync(da, ha, ob + mb + fb, hipMemcpyHostToDevice, cs.stream));
     const uint8_t* d_src = static_cast<const uint8_t*>(cs.d_src.p);
-    // Re-CRC of every live file (the verify the reference's real_compact does not do).
-    HIP_TRY(ctx, launch_block_verify(d_src, job->src_len, d_metas, nl, ctx->d_tables, d_crc, d_status, nullptr,
-                                     cs.stream));
-    HIP_TRY(ctx, launch_compact_copy(d_src, d_metas, d_flags, d_doff, nl, static_cast<uint8_t*>(cs.d_dst.p),
-                                     cs.stream));
+    // One read of every live record: re-CRC (the verify the reference's
+    // real_compact does not do) and repack from the same registers.
+    HIP_TRY(ctx, launch_compact_fused(d_src, job->src_len, d_metas, d_flags, d_doff, nl,
+                                      static_cast<uint8_t*>(cs.d_dst.p), ctx->d_tables, d_crc, d_status, nullptr,
+                                      cs.stream));
     HIP_TRY(ctx, hipMemcpyAsync(cs.h_status.p, d_status, fb, hipMemcpyDeviceToHost, cs.stream));
     if (w) HIP_TRY(ctx, hipMemcpyAsync(job->dest_image, cs.d_dst.p, size_t(w), hipMemcpyDeviceToHost, cs.stream));
   }
@@ -695,6 +698,19 @@ int tfs_blocks_compact(tfs_crc_ctx* ctx, tfs_block_job* jobs, uint32_t njobs) {
   }
   for (auto& cs : ctx->cslots) note(compact_finish(ctx, cs));
   return worst;
+}
+
+int tfs_block_compact_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_len, const tfs_raw_meta* d_live_metas,
+                             const int32_t* d_flags, const int64_t* d_dest_off, uint32_t n, void* d_dest,
+                             uint32_t* d_out_crc, int32_t* d_out_status, uint32_t* d_n_bad, void* stream) {
+  if (!ctx || (n && (!d_src || !d_live_metas || !d_flags || !d_dest_off || !d_dest))) return TFS_EXIT_PARAMETER_ERROR;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  HIP_TRY(ctx, launch_compact_fused(static_cast<const uint8_t*>(d_src), src_len,
+                                    reinterpret_cast<const RawMeta*>(d_live_metas), d_flags, d_dest_off, n,
+                                    static_cast<uint8_t*>(d_dest), ctx->d_tables, d_out_crc, d_out_status, d_n_bad,
+                                    st));
+  return TFS_SUCCESS;
 }
 
 int tfs_block_compact(tfs_crc_ctx* ctx, const void* src_image, uint64_t src_len, const tfs_raw_meta* metas,

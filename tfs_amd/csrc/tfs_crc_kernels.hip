@@ -245,11 +245,27 @@ __device__ __forceinline__ void load_ring(const FileGeo<RUN>& g, int lane, uint4
   }
 }
 
+// Copy-through stores of the fused compaction kernel: the payload bytes a lane
+// holds in registers go to the same position of the destination record
+// (dst = src + delta, delta a multiple of 4).  Written once, never re-read here.
+typedef __attribute__((address_space(1))) uint32_t* gu32wp;
+typedef __attribute__((address_space(1))) u32x4* gu128wp;
+__device__ __forceinline__ void st32(uintptr_t a, uint32_t v) { *reinterpret_cast<gu32wp>(a) = v; }
+__device__ __forceinline__ void st128_nt(uintptr_t a, const uint4& v) {
+  u32x4 w = {v.x, v.y, v.z, v.w};
+  if ((a & 15u) == 0) {
+    __builtin_nontemporal_store(w, reinterpret_cast<gu128wp>(a));
+  } else {  // 4-aligned: four dword stores
+    st32(a, v.x); st32(a + 4, v.y); st32(a + 8, v.z); st32(a + 12, v.w);
+  }
+}
+
 // The lane's chain over stripes 0..nstripes-1 (before the final combine).
-template <int RUN, int PF, bool NT, bool S8>
+// COPY: also store every payload byte of [start, B16) to dst = src + delta.
+template <int RUN, int PF, bool NT, bool S8, bool COPY = false>
 __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase& lb, const FileGeo<RUN>& g,
                                                const Head<RUN>& h, uint4 (&buf)[PF][RUN / 16], int lane,
-                                               uintptr_t junk) {
+                                               uintptr_t junk, intptr_t delta = 0, bool copy_on = false) {
   constexpr uint32_t kStripe = 64u * RUN;
   constexpr int kVec = RUN / 16;
   // Stripe 0: mask the bytes before `start` in the dword at A and inject the
@@ -267,6 +283,13 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
     for (int i = 0; i < RUN / 4; ++i) {
       const uintptr_t q = lo + 4u * i;
       uint32_t w = h.w[i];
+      if (COPY && copy_on) {
+        if (q >= g.start && q < g.B16) {
+          st32(q + delta, w);
+        } else if (q == g.A && g.s) {  // the dword holding `start`: its payload bytes only
+          for (uint32_t k = g.s; k < 4u; ++k) *reinterpret_cast<uint8_t*>(q + k + delta) = uint8_t(w >> (8 * k));
+        }
+      }
       w = q == g.A ? ((w & headmask) ^ seed_lo) : w;
       w = q == g.A + 4 ? (w ^ seed_hi) : w;
       c = step4(T, lb, c, w);
@@ -290,6 +313,11 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
 #pragma unroll
         for (int v = 0; v < kVec; ++v) c = steps16(T, lb, c, buf[f][v]);
         c = (r + f == last && !lane_in_last) ? c_old : c;  // run past B16: not part of the chain
+        if (COPY && copy_on && !(r + f == last && !lane_in_last)) {
+          const uintptr_t q = g.sb0 + uintptr_t(r + f) * kStripe + uintptr_t(lane) * RUN;
+#pragma unroll
+          for (int v = 0; v < kVec; ++v) st128_nt(q + 16u * v + delta, buf[f][v]);
+        }
         const uintptr_t sb = stripe_base<RUN>(g, r + f + PF, junk) + uintptr_t(lane) * RUN;
 #pragma unroll
         for (int v = 0; v < kVec; ++v) buf[f][v] = ld128s<NT>(sb + 16u * v);
@@ -305,6 +333,11 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
 #pragma unroll
         for (int v = 0; v < kVec; ++v) c = steps16(T, lb, c, buf[f][v]);
         c = (r + f == last && !lane_in_last) ? c_old : c;
+        if (COPY && copy_on && !(r + f == last && !lane_in_last)) {
+          const uintptr_t q = g.sb0 + uintptr_t(r + f) * kStripe + uintptr_t(lane) * RUN;
+#pragma unroll
+          for (int v = 0; v < kVec; ++v) st128_nt(q + 16u * v + delta, buf[f][v]);
+        }
       }
     }
   }
@@ -470,6 +503,24 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
   if (MODE == 1 && lane == 0 && bad && n_bad) atomicAdd(n_bad, bad);
 }
 
+// The FileInfo fields the checks need (id_ +0, size_ +12, crc_ +32), read from a
+// header at an arbitrary byte offset (records are packed) -- same in all lanes.
+struct HdrFields {
+  uint64_t id;
+  int32_t size;
+  uint32_t crc;
+};
+__device__ __forceinline__ uint32_t ldu32(const uint8_t* p) {
+  return uint32_t(p[0]) | uint32_t(p[1]) << 8 | uint32_t(p[2]) << 16 | uint32_t(p[3]) << 24;
+}
+__device__ __forceinline__ HdrFields read_hdr(const uint8_t* rec) {
+  HdrFields h;
+  h.id = uint64_t(ldu32(rec)) | uint64_t(ldu32(rec + 4)) << 32;
+  h.size = int32_t(ldu32(rec + 12));
+  h.crc = ldu32(rec + 32);
+  return h;
+}
+
 // Verify files stored in a block image (FileInfo header + payload per RawMeta):
 // the checks of sync_backup.cpp:345-435 / block_console.cpp:543-577.
 __global__ void __launch_bounds__(kBlock) block_verify_kernel(const uint8_t* __restrict__ image, uint64_t image_len,
@@ -492,10 +543,7 @@ __global__ void __launch_bounds__(kBlock) block_verify_kernel(const uint8_t* __r
       status = kExitParameterError;
     } else {
       const uint8_t* rec = image + m.offset;
-      FileInfoHdr h;
-      // 36-byte header at an arbitrary byte offset: byte-wise read, same in all lanes.
-      uint8_t* hb = reinterpret_cast<uint8_t*>(&h);
-      for (int i = 0; i < kFileInfoSize; ++i) hb[i] = rec[i];
+      const HdrFields h = read_hdr(rec);
       c = wave_crc<kRun, kPF, kNT, kS8>(lds_tables, rec + kFileInfoSize, uint32_t(m.size - kFileInfoSize), 0u, lane,
                                         reinterpret_cast<uintptr_t>(tg->slice));
       if (h.id != m.file_id) status = kExitFileInfoError;
@@ -655,6 +703,86 @@ __global__ void __launch_bounds__(kBlock) compact_copy_kernel(const uint8_t* __r
       for (uint32_t i = lane; i < size; i += kWave) dp[i] = sp[i];
     }
   }
+}
+
+// Fused compaction: one read of each live record computes its
+// payload CRC (the re-CRC verify) and, from the same registers, writes the
+// record to its new offset with offset_/size_/usize_/flag_ rewritten
+// (task.cpp:753-798).  Checks and statuses as block_verify_kernel.  Records
+// whose new offset is not congruent mod 4 with the old one take a byte copy
+// after the CRC (a second read of that record only).
+__global__ void __launch_bounds__(kBlock) compact_fused_kernel(const uint8_t* __restrict__ src, uint64_t src_len,
+                                                               const RawMeta* __restrict__ metas,
+                                                               const int32_t* __restrict__ flags,
+                                                               const int64_t* __restrict__ dest_off, uint32_t n,
+                                                               uint8_t* __restrict__ dst, const Tables* __restrict__ tg,
+                                                               uint32_t* out_crc, int32_t* out_status,
+                                                               uint32_t* n_bad) {
+  __shared__ uint32_t lds_tables[LdsLayout<kS8>::bytes / 4];
+  load_tables<kRun, kPAR, kS8>(lds_tables, tg);
+  const int lane = threadIdx.x & (kWave - 1);
+  const LaneBase lb = lane_base_of(lane);
+  const uint32_t wpb = kBlock / kWave;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uintptr_t junk = reinterpret_cast<uintptr_t>(tg->slice);
+  uint32_t bad = 0;
+  for (uint32_t f = blockIdx.x * wpb + wave; f < n; f += gridDim.x * wpb) {
+    const RawMeta m = metas[f];
+    const int64_t doff = dest_off[f];
+    int32_t status = kSuccess;
+    uint32_t c = 0;
+    if (m.size <= kFileInfoSize) {
+      status = kExitReadFileSizeError;
+    } else if (m.offset < 0 || uint64_t(m.offset) + uint64_t(m.size) > src_len || doff < 0) {
+      status = kExitParameterError;
+    } else {
+      const uint8_t* rec = src + m.offset;
+      uint8_t* drec = dst + doff;
+      const HdrFields hd = read_hdr(rec);
+      // header: FileInfo with offset_(8) size_(12) usize_(16) flag_(28) rewritten
+      if (lane < kFileInfoSize) {
+        uint8_t b = rec[lane];
+        const int fld = lane >> 2, sh = 8 * (lane & 3);
+        if (fld == 2) b = uint8_t(uint32_t(int32_t(doff)) >> sh);
+        else if (fld == 3 || fld == 4) b = uint8_t(uint32_t(m.size) >> sh);
+        else if (fld == 7) b = uint8_t(uint32_t(flags[f]) >> sh);
+        drec[lane] = b;
+      }
+      const uint8_t* p = rec + kFileInfoSize;
+      const uint32_t len = uint32_t(m.size - kFileInfoSize);
+      const intptr_t delta = intptr_t(drec) - intptr_t(rec);
+      const FileGeo<kRun> g = make_geo<kRun>(p, len, 0u);
+      const Head<kRun> h = load_head<kRun>(g, lane);
+      uint4 buf[kPF][kRun / 16];
+      load_ring<kRun, kPF, kNT>(g, lane, buf, junk);
+      const bool fused = (delta & 3) == 0;
+      c = g.nstripes ? lane_chain<kRun, kPF, kNT, kS8, true>(lds_tables, lb, g, h, buf, lane, junk, delta, fused)
+                     : 0u;
+      if (fused && g.nstripes) {
+        // tail [B16, end): dwords then bytes, from lane 0's registers
+        if (lane == 0) {
+          const uint32_t ntw = uint32_t((g.end & ~uintptr_t(3)) - g.B16) / 4u;
+          for (uint32_t i = 0; i < 3u; ++i)
+            if (i < ntw) st32(g.B16 + 4u * i + delta, h.tw[i]);
+          const uintptr_t B = g.end & ~uintptr_t(3);
+          for (uint32_t i = 0; i < 3u; ++i)
+            if (B + i < g.end) *reinterpret_cast<uint8_t*>(B + i + delta) = uint8_t(h.tb[i]);
+        }
+      } else {  // tiny file, or a destination not congruent mod 4: byte copy
+        for (uint32_t i = lane; i < len; i += kWave) drec[kFileInfoSize + i] = p[i];
+      }
+      c = finish_file<kRun, kS8>(lds_tables, lb, g, h, c, lane);
+      if (hd.id != m.file_id) status = kExitFileInfoError;
+      else if (hd.size != m.size) status = kExitSyncFileError;
+      else if (c != hd.crc) status = kExitCheckCrcError;
+    }
+    if (lane == 0) {
+      if (out_crc) out_crc[f] = c;
+      if (out_status) out_status[f] = status;
+      bad += status != kSuccess ? 1u : 0u;
+    }
+  }
+  if (lane == 0 && bad && n_bad) atomicAdd(n_bad, bad);
 }
 
 // Synthetic payload bytes: word i = splitmix64(seed + (first_word + i + 1) * GOLDEN)
@@ -817,6 +945,15 @@ hipError_t launch_block_verify(const uint8_t* image, uint64_t image_len, const R
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(block_verify_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, image, image_len, metas, n, tg,
                      out_crc, out_status, n_bad);
+  return hipGetLastError();
+}
+
+hipError_t launch_compact_fused(const uint8_t* src, uint64_t src_len, const RawMeta* metas, const int32_t* flags,
+                                const int64_t* dest_off, uint32_t n, uint8_t* dst, const Tables* tg, uint32_t* out_crc,
+                                int32_t* out_status, uint32_t* n_bad, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(compact_fused_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len, metas, flags,
+                     dest_off, n, dst, tg, out_crc, out_status, n_bad);
   return hipGetLastError();
 }
 
