@@ -142,6 +142,7 @@ struct CompactSlot {
 };
 constexpr int kCompactSlots = 3;
 constexpr uint32_t kSchedSlots = 256;
+constexpr int kVariantUnfusedCompact = 7;  // TFS_CRC_VARIANT=7: two-pass device compaction (A/B baseline)
 
 }  // namespace
 
@@ -706,6 +707,14 @@ int tfs_block_compact_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_l
   if (!ctx || (n && (!d_src || !d_live_metas || !d_flags || !d_dest_off || !d_dest))) return TFS_EXIT_PARAMETER_ERROR;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  if (ctx->variant == kVariantUnfusedCompact) {  // measurement knob: verify, then a separate copy pass
+    HIP_TRY(ctx, launch_block_verify(static_cast<const uint8_t*>(d_src), src_len,
+                                     reinterpret_cast<const RawMeta*>(d_live_metas), n, ctx->d_tables, d_out_crc,
+                                     d_out_status, d_n_bad, st));
+    HIP_TRY(ctx, launch_compact_copy(static_cast<const uint8_t*>(d_src), reinterpret_cast<const RawMeta*>(d_live_metas),
+                                     d_flags, d_dest_off, n, static_cast<uint8_t*>(d_dest), st));
+    return TFS_SUCCESS;
+  }
   HIP_TRY(ctx, launch_compact_fused(static_cast<const uint8_t*>(d_src), src_len,
                                     reinterpret_cast<const RawMeta*>(d_live_metas), d_flags, d_dest_off, n,
                                     static_cast<uint8_t*>(d_dest), ctx->d_tables, d_out_crc, d_out_status, d_n_bad,
