@@ -672,6 +672,10 @@ def bench_compact(args):
         dist.destroy_process_group()
 
 
+def live_bytes_total(windows, rec):
+    return float(sum(w["n"] for w in windows)) * rec
+
+
 def bench_compact_device(args):
     """the compaction data pass on device-resident blocks -- one
     fused kernel re-CRCs every live record and writes it to its new offset
@@ -712,8 +716,9 @@ def bench_compact_device(args):
         m["offset"] = idx * rec
         m["size"] = rec
         fl = np.zeros(idx.size, np.int32)
-        do = np.arange(idx.size, dtype=np.int64) * rec
-        dst = crc.DeviceBuffer(ctx, idx.size * rec + 64)
+        dstride = rec if not os.environ.get("TFS_BENCH_PAD16") else (rec + 15) // 16 * 16  # A/B: 16-aligned dests
+        do = np.arange(idx.size, dtype=np.int64) * dstride
+        dst = crc.DeviceBuffer(ctx, idx.size * dstride + 64)
         windows.append(dict(base=img.ptr + w0 * blk, length=nb * blk, n=int(idx.size),
                             m=crc.DeviceBuffer(ctx, m.nbytes).upload(m), f=crc.DeviceBuffer(ctx, fl.nbytes).upload(fl),
                             o=crc.DeviceBuffer(ctx, do.nbytes).upload(do), dst=dst,
@@ -722,6 +727,24 @@ def bench_compact_device(args):
     os.environ["TFS_CRC_VARIANT"] = "7"
     ctx2 = crc.Context(local)
     os.environ["TFS_CRC_VARIANT"] = "0"
+    # The product form: every live record of every block in ONE launch
+    # (tfs_compact_jobs_device); block b's live records are packed into its own
+    # destination block at b * blk.
+    nlive1 = live1.size
+    jobs = np.zeros(nblocks * nlive1, crc.COMPACT_JOB_DTYPE)
+    bidx = np.repeat(np.arange(nblocks, dtype=np.uint64), nlive1)
+    loc = np.tile(np.arange(nlive1, dtype=np.uint64) * rec, nblocks)
+    jobs["src_offset"] = bidx * blk + np.tile(live1.astype(np.uint64) * rec, nblocks)
+    jobs["dest_offset"] = bidx * (nlive1 * rec) + loc
+    jobs["file_id"] = 1 + bidx * nfiles + np.tile(live1.astype(np.uint64), nblocks)
+    jobs["size"] = rec
+    jobs["new_offset"] = loc.astype(np.int32)
+    d_jobs = crc.DeviceBuffer(ctx, jobs.nbytes).upload(jobs)
+    d_jdst = crc.DeviceBuffer(ctx, nblocks * nlive1 * rec + 64)
+    d_jst = crc.DeviceBuffer(ctx, 4 * jobs.size)
+
+    def step_jobs(c):
+        c.compact_jobs_device(img, total, d_jobs, int(jobs.size), d_jdst, None, d_jst, d_bad)
 
     def step(c):
         for w in windows:
@@ -730,11 +753,12 @@ def bench_compact_device(args):
 
     d_bad.zero()
     for _ in range(max(1, args.warmup)):
+        step_jobs(ctx)
         step(ctx)
     ctx.sync()
     if int(d_bad.download(np.uint32, 1)[0]) != 0:
         raise SystemExit("compact_device: CRC mismatches on clean blocks")
-    # parity: block 0 of window 0 against the oracle's real_compact restatement
+    # parity: block 0 against the oracle's real_compact restatement
     ora = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle_crc.so"))
     ora.oracle_compact.restype = ctypes.c_int64
     ora.oracle_compact.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint32] + [ctypes.c_void_p] * 4
@@ -747,12 +771,12 @@ def bench_compact_device(args):
     ook = np.zeros(nfiles, np.uint8)
     wlen = ora.oracle_compact(host.ctypes.data, mo.ctypes.data, ms.ctypes.data, flags1.ctypes.data, nfiles,
                               odest.ctypes.data, doff.ctypes.data, dsz.ctypes.data, ook.ctypes.data)
-    got = windows[0]["dst"].download(np.uint8, int(wlen))
     # the bench writes flag_ = 0 for every live file (flags1 is 0 on live files) -> identical bytes
-    if not (got == odest[:wlen]).all():
-        raise SystemExit("compact_device: GPU repack disagrees with oracle")
+    for got in (windows[0]["dst"].download(np.uint8, int(wlen)), d_jdst.download(np.uint8, int(wlen))):
+        if not os.environ.get("TFS_BENCH_PAD16") and not (got == odest[:wlen]).all():
+            raise SystemExit("compact_device: GPU repack disagrees with oracle")
 
-    def timed(c):
+    def timed(c, fn=step):
         ev0, ev1 = crc.Event(c), crc.Event(c)
         if dist:
             dist.barrier()
@@ -760,7 +784,7 @@ def bench_compact_device(args):
         t0 = time.perf_counter()
         ev0.record()
         for _ in range(args.steps):
-            step(c)
+            fn(c)
         ev1.record()
         c.sync()
         if dist:
@@ -769,8 +793,23 @@ def bench_compact_device(args):
 
     step(ctx2)
     ctx2.sync()
-    el, kms = timed(ctx)
+    extra = {}
+    if args.membench:  # streaming-copy ceiling for the same number of live bytes
+        nb = int(live_bytes_total(windows, rec)) // 16 * 16
+        cdst = crc.DeviceBuffer(ctx, nb + 64)
+        for pat in (50000, 51000):
+            e0, e1 = crc.Event(ctx), crc.Event(ctx)
+            ctx.membench_device(pat, img, None, 0, nb, cdst)
+            e0.record()
+            for _ in range(3):
+                ctx.membench_device(pat, img, None, 0, nb, cdst)
+            e1.record()
+            ctx.sync()
+            extra["copy_p%d_GBs_rw" % pat] = 2 * nb / (e0.elapsed_ms(e1) / 3 / 1e3) / 1e9
+        cdst.free()
+    el_w, kms_w = timed(ctx)
     el2, kms2 = timed(ctx2)
+    el, kms = timed(ctx, step_jobs)
     nlive = sum(w["n"] for w in windows)
     live_bytes = float(nlive) * rec
     algo = 2 * live_bytes + nlive * (16 + 4 + 8 + 4)  # read + write live records, metas/flags/offsets/status
@@ -784,16 +823,17 @@ def bench_compact_device(args):
             nblocks, nlive, live_bytes / 2**30)},
         "roofline": {"bound": "hbm", "achieved": algo / (kms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": algo / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "compact_fused_kernel", "kernel_ms_avg": kms},
-        "unfused_ab": {"variant": 7, "ms_per_step": kms2, "value": world * args.steps * float(total) / el2 / 2**30,
-                       "speedup_fused": kms2 / kms},
+                     "kernel": "compact_fused_kernel<WIDE> (one launch)", "kernel_ms_avg": kms},
+        "membench": extra,
+        "ab": {"fused_one_launch_ms": kms, "fused_windows_ms": kms_w, "unfused_windows_ms": kms2,
+               "windows": len(windows), "speedup_vs_unfused": kms2 / kms},
     }
     if rank == 0:
         print(json.dumps(res), flush=True)
     for w in windows:
         for k in ("m", "f", "o", "dst", "st"):
             w[k].free()
-    for b in (img, d_crc, d_bad):
+    for b in (img, d_crc, d_bad, d_jobs, d_jdst, d_jst):
         b.free()
     ctx2.close()
     ctx.close()

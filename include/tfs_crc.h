@@ -210,6 +210,23 @@ int tfs_block_compact_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_l
                              const int32_t* d_flags, const int64_t* d_dest_off, uint32_t n, void* d_dest,
                              uint32_t* d_out_crc, int32_t* d_out_status, uint32_t* d_n_bad, void* stream);
 
+/* The same data pass over many device-resident blocks in one launch (64-bit
+ * offsets; one entry per live record, any order).  Writes FileInfo{offset_ =
+ * new_offset, size_ = usize_ = size, flag_ = flag} | payload at d_dest +
+ * dest_offset after checking id/size/crc as above. */
+typedef struct tfs_compact_job {
+  uint64_t src_offset;
+  uint64_t dest_offset;
+  uint64_t file_id;
+  int32_t size;
+  int32_t flag;
+  int32_t new_offset;
+  int32_t reserved;
+} tfs_compact_job;
+int tfs_compact_jobs_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_len, const tfs_compact_job* d_jobs,
+                            uint32_t n, void* d_dest, uint32_t* d_out_crc, int32_t* d_out_status, uint32_t* d_n_bad,
+                            void* stream);
+
 /* Many blocks in one call (the compaction task thread's queue): each job is
  * tfs_block_compact's arguments plus its outputs.  Jobs are pipelined over
  * several streams so the H2D copy of one block, the verify/repack kernels of

@@ -288,6 +288,45 @@ def test_block_compact_device_matches_oracle(gpu_ctx, oracle):
     assert (ook[live] == 1).all()
 
 
+def test_compact_jobs_device_many_blocks(gpu_ctx, oracle):
+    """tfs_compact_jobs_device: several blocks' live records in one launch,
+    each block packed into its own destination region; equals the oracle's
+    real_compact of every block."""
+    import tfs_amd.crc as crc
+    rng = np.random.default_rng(93)
+    blocks, jobs, expect = [], [], []
+    src_base = dst_base = 0
+    for b in range(5):
+        sizes = [65536] * 12 + [int(x) for x in rng.integers(1, 12000, 20)]
+        img, metas = _block_image(oracle, sizes, seed=80 + b)
+        fl = np.zeros(len(sizes), np.int32)
+        fl[b % 3::3] = 1
+        odest, doff, ook = _oracle_compact(oracle, img, metas, fl)
+        for i in np.nonzero((fl & 3) == 0)[0]:
+            jobs.append((src_base + int(metas[i]["offset"]), dst_base + int(doff[i]), int(metas[i]["file_id"]),
+                         int(metas[i]["size"]), int(fl[i]), int(doff[i]), 0))
+        blocks.append(img[:int(metas["size"].astype(np.int64).sum())])
+        expect.append((dst_base, odest))
+        src_base += blocks[-1].size
+        dst_base += odest.size + (b * 7) % 16   # destination blocks at assorted alignments
+    src = np.concatenate(blocks)
+    j = np.array(jobs, dtype=crc.COMPACT_JOB_DTYPE)
+    rng.shuffle(j)   # any order
+    d_src = crc.DeviceBuffer(gpu_ctx, src.size + 64).upload(src)
+    d_j = crc.DeviceBuffer(gpu_ctx, j.nbytes).upload(j)
+    d_dst = crc.DeviceBuffer(gpu_ctx, dst_base + 64)
+    d_dst.zero()
+    d_st = crc.DeviceBuffer(gpu_ctx, 4 * len(j))
+    d_bad = crc.DeviceBuffer(gpu_ctx, 4)
+    d_bad.zero()
+    gpu_ctx.compact_jobs_device(d_src, src.size, d_j, len(j), d_dst, None, d_st, d_bad)
+    gpu_ctx.sync()
+    out = d_dst.download(np.uint8, dst_base)
+    for base, od in expect:
+        assert (out[base:base + od.size] == od).all()
+    assert int(d_bad.download(np.uint32, 1)[0]) == 0
+
+
 def _stripe_edge_cases(run, count=24):
     """(offset, len) pairs where the payload starts inside the last dword of
     stripe 0, so the high seed bytes land in stripe 1 (lane 0)."""

@@ -41,6 +41,8 @@ FILEINFO_SIZE = 36
 
 DESC_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("aux", "<u4")])  # tfs_crc_desc / tfs_crc_vdesc
 PACKET_DESC_DTYPE = np.dtype([("offset", "<u8"), ("len", "<u4"), ("reserved", "<u4")])  # tfs_packet_desc
+COMPACT_JOB_DTYPE = np.dtype([("src_offset", "<u8"), ("dest_offset", "<u8"), ("file_id", "<u8"), ("size", "<i4"),
+                              ("flag", "<i4"), ("new_offset", "<i4"), ("reserved", "<i4")])  # tfs_compact_job
 META_DTYPE = np.dtype([("file_id", "<u8"), ("offset", "<i4"), ("size", "<i4")])  # tfs_raw_meta
 FILEINFO_DTYPE = np.dtype([("id_", "<u8"), ("offset_", "<i4"), ("size_", "<i4"), ("usize_", "<i4"),
                            ("modify_time_", "<i4"), ("create_time_", "<i4"), ("flag_", "<i4"),
@@ -59,7 +61,7 @@ EXPORTED = [
     "tfs_crc32_event_elapsed_ms", "tfs_crc32_event_destroy",
     "tfs_crc32_stream", "tfs_crc32_sync",
     "tfs_packet_verify", "tfs_packet_verify_device", "tfs_packet_seal", "tfs_packet_seal_device",
-    "tfs_crc32_write_packet_headers_device", "tfs_block_compact_device",
+    "tfs_crc32_write_packet_headers_device", "tfs_block_compact_device", "tfs_compact_jobs_device",
 ]
 
 
@@ -107,6 +109,7 @@ def lib():
             "tfs_block_compact": (ctypes.c_int, [vp, vp, u64, vp, vp, u32, vp, u64, vp, vp, vp, vp]),
             "tfs_blocks_compact": (ctypes.c_int, [vp, vp, u32]),
             "tfs_block_compact_device": (ctypes.c_int, [vp, vp, u64, vp, vp, vp, u32, vp, vp, vp, vp, vp]),
+            "tfs_compact_jobs_device": (ctypes.c_int, [vp, vp, u64, vp, u32, vp, vp, vp, vp, vp]),
             "tfs_crc32_synth_fill_device": (ctypes.c_int, [vp, vp, u64, u64, u64, vp]),
             "tfs_crc32_write_headers_device": (ctypes.c_int, [vp, vp, vp, vp, vp, u64, u32, vp]),
             "tfs_crc32_membench_device": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, u32, u64, vp, ctypes.c_uint, vp]),
@@ -291,6 +294,12 @@ class Context:
         self._check(lib().tfs_block_compact_device(self.handle, _ptr(d_src), src_len, _ptr(d_live_metas),
                                                    _ptr(d_flags), _ptr(d_dest_off), n, _ptr(d_dest), _ptr(d_crc),
                                                    _ptr(d_status), _ptr(d_nbad), stream), "block_compact_device")
+
+    def compact_jobs_device(self, d_src, src_len, d_jobs, n, d_dest, d_crc=None, d_status=None, d_nbad=None,
+                            stream=None):
+        self._check(lib().tfs_compact_jobs_device(self.handle, _ptr(d_src), src_len, _ptr(d_jobs), n, _ptr(d_dest),
+                                                  _ptr(d_crc), _ptr(d_status), _ptr(d_nbad), stream),
+                    "compact_jobs_device")
 
     def blocks_compact(self, jobs):
         """Pipelined compaction of many blocks; `jobs` is a ctypes array of BlockJob."""

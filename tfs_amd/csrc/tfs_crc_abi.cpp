@@ -38,6 +38,9 @@ hipError_t launch_compact_copy(const uint8_t* src, const RawMeta* metas, const i
 hipError_t launch_compact_fused(const uint8_t* src, uint64_t src_len, const RawMeta* metas, const int32_t* flags,
                                 const int64_t* dest_off, uint32_t n, uint8_t* dst, const Tables* tg, uint32_t* out_crc,
                                 int32_t* out_status, uint32_t* n_bad, hipStream_t stream);
+hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const CompactJob* jobs, uint32_t n, uint8_t* dst,
+                               const Tables* tg, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
+                               hipStream_t stream);
 hipError_t launch_synth_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, uint64_t first_word, hipStream_t stream);
 hipError_t launch_write_headers(uint8_t* image, const uint64_t* rec_off, const uint32_t* len, const uint32_t* crc,
                                 uint64_t first_id, uint32_t n, hipStream_t stream);
@@ -51,6 +54,7 @@ static_assert(sizeof(tfs_crc_desc) == 16 && sizeof(tfs_crc_vdesc) == 16, "descri
 static_assert(sizeof(tfs_raw_meta) == sizeof(tfscrc::RawMeta), "RawMeta ABI");
 static_assert(sizeof(tfs_file_info) == 36, "FileInfo ABI");
 static_assert(sizeof(tfs_packet_desc) == sizeof(tfscrc::PacketDesc), "packet descriptor ABI");
+static_assert(sizeof(tfs_compact_job) == sizeof(tfscrc::CompactJob) && sizeof(tfs_compact_job) == 40, "compact job ABI");
 
 namespace {
 
@@ -719,6 +723,18 @@ int tfs_block_compact_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_l
                                     reinterpret_cast<const RawMeta*>(d_live_metas), d_flags, d_dest_off, n,
                                     static_cast<uint8_t*>(d_dest), ctx->d_tables, d_out_crc, d_out_status, d_n_bad,
                                     st));
+  return TFS_SUCCESS;
+}
+
+int tfs_compact_jobs_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_len, const tfs_compact_job* d_jobs,
+                            uint32_t n, void* d_dest, uint32_t* d_out_crc, int32_t* d_out_status, uint32_t* d_n_bad,
+                            void* stream) {
+  if (!ctx || (n && (!d_src || !d_jobs || !d_dest))) return TFS_EXIT_PARAMETER_ERROR;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  HIP_TRY(ctx, launch_compact_jobs(static_cast<const uint8_t*>(d_src), src_len,
+                                   reinterpret_cast<const CompactJob*>(d_jobs), n, static_cast<uint8_t*>(d_dest),
+                                   ctx->d_tables, d_out_crc, d_out_status, d_n_bad, st));
   return TFS_SUCCESS;
 }
 

@@ -61,6 +61,18 @@ struct RawMeta {
   int32_t size;
 };
 
+// One live record of a multi-block device compaction (same bytes as
+// tfs_compact_job in include/tfs_crc.h).
+struct CompactJob {
+  uint64_t src_offset;   // FileInfo of the record in the source images
+  uint64_t dest_offset;  // where the repacked record goes
+  uint64_t file_id;      // expected FileInfo.id_
+  int32_t size;          // record size incl. the 36-byte FileInfo
+  int32_t flag;          // FileInfo.flag_ to write
+  int32_t new_offset;    // FileInfo.offset_ to write (offset inside the new block)
+  int32_t reserved;
+};
+
 // Packet frames (BasePacket / BasePacketStreamer, src/common/base_packet*.{h,cpp}).
 // Same bytes as tfs_packet_desc in include/tfs_crc.h.
 struct PacketDesc {

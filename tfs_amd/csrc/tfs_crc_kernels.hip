@@ -711,10 +711,14 @@ __global__ void __launch_bounds__(kBlock) compact_copy_kernel(const uint8_t* __r
 // (task.cpp:753-798).  Checks and statuses as block_verify_kernel.  Records
 // whose new offset is not congruent mod 4 with the old one take a byte copy
 // after the CRC (a second read of that record only).
+// WIDE: per-record CompactJob (64-bit offsets, many blocks per launch); else the
+// single-block form (RawMeta + flags + int64 dest offsets).
+template <bool WIDE>
 __global__ void __launch_bounds__(kBlock) compact_fused_kernel(const uint8_t* __restrict__ src, uint64_t src_len,
                                                                const RawMeta* __restrict__ metas,
                                                                const int32_t* __restrict__ flags,
-                                                               const int64_t* __restrict__ dest_off, uint32_t n,
+                                                               const int64_t* __restrict__ dest_off,
+                                                               const CompactJob* __restrict__ jobs, uint32_t n,
                                                                uint8_t* __restrict__ dst, const Tables* __restrict__ tg,
                                                                uint32_t* out_crc, int32_t* out_status,
                                                                uint32_t* n_bad) {
@@ -727,29 +731,42 @@ __global__ void __launch_bounds__(kBlock) compact_fused_kernel(const uint8_t* __
   const uintptr_t junk = reinterpret_cast<uintptr_t>(tg->slice);
   uint32_t bad = 0;
   for (uint32_t f = blockIdx.x * wpb + wave; f < n; f += gridDim.x * wpb) {
-    const RawMeta m = metas[f];
-    const int64_t doff = dest_off[f];
+    uint64_t soff, doff, fid;
+    int32_t size, flag, new_off;
+    bool range_ok;
+    if (WIDE) {
+      const CompactJob j = jobs[f];
+      soff = j.src_offset, doff = j.dest_offset, fid = j.file_id;
+      size = j.size, flag = j.flag, new_off = j.new_offset;
+      range_ok = soff + uint64_t(size) <= src_len;
+    } else {
+      const RawMeta m = metas[f];
+      const int64_t d = dest_off[f];
+      soff = uint64_t(int64_t(m.offset)), doff = uint64_t(d), fid = m.file_id;
+      size = m.size, flag = flags[f], new_off = int32_t(d);
+      range_ok = m.offset >= 0 && d >= 0 && uint64_t(m.offset) + uint64_t(m.size) <= src_len;
+    }
     int32_t status = kSuccess;
     uint32_t c = 0;
-    if (m.size <= kFileInfoSize) {
+    if (size <= kFileInfoSize) {
       status = kExitReadFileSizeError;
-    } else if (m.offset < 0 || uint64_t(m.offset) + uint64_t(m.size) > src_len || doff < 0) {
+    } else if (!range_ok) {
       status = kExitParameterError;
     } else {
-      const uint8_t* rec = src + m.offset;
+      const uint8_t* rec = src + soff;
       uint8_t* drec = dst + doff;
       const HdrFields hd = read_hdr(rec);
       // header: FileInfo with offset_(8) size_(12) usize_(16) flag_(28) rewritten
       if (lane < kFileInfoSize) {
         uint8_t b = rec[lane];
         const int fld = lane >> 2, sh = 8 * (lane & 3);
-        if (fld == 2) b = uint8_t(uint32_t(int32_t(doff)) >> sh);
-        else if (fld == 3 || fld == 4) b = uint8_t(uint32_t(m.size) >> sh);
-        else if (fld == 7) b = uint8_t(uint32_t(flags[f]) >> sh);
+        if (fld == 2) b = uint8_t(uint32_t(new_off) >> sh);
+        else if (fld == 3 || fld == 4) b = uint8_t(uint32_t(size) >> sh);
+        else if (fld == 7) b = uint8_t(uint32_t(flag) >> sh);
         drec[lane] = b;
       }
       const uint8_t* p = rec + kFileInfoSize;
-      const uint32_t len = uint32_t(m.size - kFileInfoSize);
+      const uint32_t len = uint32_t(size - kFileInfoSize);
       const intptr_t delta = intptr_t(drec) - intptr_t(rec);
       const FileGeo<kRun> g = make_geo<kRun>(p, len, 0u);
       const Head<kRun> h = load_head<kRun>(g, lane);
@@ -772,8 +789,8 @@ __global__ void __launch_bounds__(kBlock) compact_fused_kernel(const uint8_t* __
         for (uint32_t i = lane; i < len; i += kWave) drec[kFileInfoSize + i] = p[i];
       }
       c = finish_file<kRun, kS8>(lds_tables, lb, g, h, c, lane);
-      if (hd.id != m.file_id) status = kExitFileInfoError;
-      else if (hd.size != m.size) status = kExitSyncFileError;
+      if (hd.id != fid) status = kExitFileInfoError;
+      else if (hd.size != size) status = kExitSyncFileError;
       else if (c != hd.crc) status = kExitCheckCrcError;
     }
     if (lane == 0) {
@@ -876,6 +893,25 @@ __global__ void __launch_bounds__(kBlock) membench_kernel(const uint8_t* __restr
   if (acc == 0x9E3779B9u) out[0] = acc;  // keep the loads alive
 }
 
+// Calibration: streaming copy of nbytes (multiple of 16), 16 B per lane,
+// grid-stride; NT = non-temporal loads and stores.
+template <bool NT>
+__global__ void __launch_bounds__(kBlock) membench_copy_kernel(const uint8_t* __restrict__ src,
+                                                               uint8_t* __restrict__ dst, uint64_t nbytes) {
+  const uint64_t nv = nbytes / 16;
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  const uintptr_t s = reinterpret_cast<uintptr_t>(src), d = reinterpret_cast<uintptr_t>(dst);
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nv; i += stride) {
+    const uint4 v = ld128s<NT>(s + 16 * i);
+    if (NT) {
+      st128_nt(d + 16 * i, v);
+    } else {
+      const u32x4 w = {v.x, v.y, v.z, v.w};
+      *reinterpret_cast<gu128wp>(d + 16 * i) = w;
+    }
+  }
+}
+
 }  // namespace tfscrc
 
 // ---------------------------------------------------------------------------
@@ -952,8 +988,17 @@ hipError_t launch_compact_fused(const uint8_t* src, uint64_t src_len, const RawM
                                 const int64_t* dest_off, uint32_t n, uint8_t* dst, const Tables* tg, uint32_t* out_crc,
                                 int32_t* out_status, uint32_t* n_bad, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(compact_fused_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len, metas, flags,
-                     dest_off, n, dst, tg, out_crc, out_status, n_bad);
+  hipLaunchKernelGGL(compact_fused_kernel<false>, dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len, metas,
+                     flags, dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad);
+  return hipGetLastError();
+}
+
+hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const CompactJob* jobs, uint32_t n, uint8_t* dst,
+                               const Tables* tg, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
+                               hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(compact_fused_kernel<true>, dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len, nullptr,
+                     nullptr, nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad);
   return hipGetLastError();
 }
 
@@ -976,7 +1021,18 @@ hipError_t launch_synth_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, uint
 hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, uint32_t n, uint64_t nbytes,
                            uint32_t* out, unsigned grid, hipStream_t stream) {
   // pattern: 0 = coalesced, 16 = stripe pattern (run 16); +1000 = non-temporal loads;
-  // +10000 = stripes anchored at 128-byte boundaries (else 16)
+  // +10000 = stripes anchored at 128-byte boundaries (else 16);
+  // 50000 / 51000 = streaming copy of nbytes into `out` (default / non-temporal)
+  if (pattern == 50000 || pattern == 51000) {
+    const dim3 g(grid ? grid : 2048u);
+    if (pattern == 51000)
+      hipLaunchKernelGGL(membench_copy_kernel<true>, g, dim3(kBlock), 0, stream, base,
+                         reinterpret_cast<uint8_t*>(out), nbytes);
+    else
+      hipLaunchKernelGGL(membench_copy_kernel<false>, g, dim3(kBlock), 0, stream, base,
+                         reinterpret_cast<uint8_t*>(out), nbytes);
+    return hipGetLastError();
+  }
   const uint32_t align = pattern >= 10000 ? 128u : 16u;
   pattern %= 10000;
   const bool nt = pattern >= 1000;
