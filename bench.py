@@ -53,8 +53,10 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--e2e", action="store_true", help="also measure the pinned H2D-inclusive rate (stderr)")
+    p.add_argument("--ec-mib", type=int, default=1536,
+                   help="member size in MiB for --workload ec (< 2048: ErasureCode sizes are int)")
     p.add_argument("--membench", action="store_true", help="also time raw streaming reads (stderr)")
-    p.add_argument("--workload", default="verify", choices=["verify", "zipf", "compact", "e2e", "packet", "compact_device"],
+    p.add_argument("--workload", default="verify", choices=["verify", "zipf", "compact", "e2e", "packet", "compact_device", "ec"],
                    help="verify = BASELINE configs[1] (the headline line); zipf = configs[2]; "
                         "compact = configs[3]; e2e = pinned-host verify incl. H2D (configs[4] end-to-end)")
     p.add_argument("--ab", default="", help="comma list of TFS_CRC_VARIANT ids: interleaved A/B timing (stderr)")
@@ -131,7 +133,7 @@ def main():
     args = parse()
     if args.workload != "verify":
         return {"zipf": bench_zipf, "compact": bench_compact, "e2e": bench_e2e,
-                "packet": bench_packet, "compact_device": bench_compact_device}[args.workload](args)
+                "packet": bench_packet, "compact_device": bench_compact_device, "ec": bench_ec}[args.workload](args)
     world, rank, local, dist = _dist_init()
     import tfs_amd.crc as crc
     from tfs_amd.synth import synth_bytes
@@ -836,6 +838,80 @@ def bench_compact_device(args):
     for b in (img, d_crc, d_bad, d_jobs, d_jdst, d_jst):
         b.free()
     ctx2.close()
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+def bench_ec(args):
+    """ErasureCode encode (MarshallingTask, task.cpp:1179-1290) and
+    decode of 3 erased members (ReinstateTask) with k=5, m=3 (the reference
+    test's configuration), device-resident members of --ec-mib MiB each."""
+    import tfs_amd.crc as crc
+    from tfs_amd.ec import ErasureCode
+    world, rank, local, dist = _dist_init()
+    ctx = crc.Context(local)
+    k, m = 5, 3
+    size = args.ec_mib << 20
+    if size >= 1 << 31:
+        raise SystemExit("ec: member size must stay below 2 GiB (int, erasure_code.h)")
+    d = [crc.DeviceBuffer(ctx, size + 64) for _ in range(k + m)]
+    for i in range(k):
+        ctx.synth_fill_device(d[i], size, 0xEC0 + 31 * rank + i, 0)
+    enc = ErasureCode(ctx, k, m)
+    if enc.encode_device(d, size) != 0:
+        raise SystemExit("ec: encode failed")
+    ctx.sync()
+    # parity spot check against the oracle on the first 64 KiB (test infrastructure)
+    ora = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle_ec.so"))
+    ora.oracle_ec_encode.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    chunk = 64 << 10
+    host = [d[i].download(np.uint8, chunk) for i in range(k)] + [np.zeros(chunk, np.uint8) for _ in range(m)]
+    pp = (ctypes.c_void_p * (k + m))(*[h.ctypes.data for h in host])
+    ora.oracle_ec_encode(k, m, pp, None, chunk)
+    for i in range(k, k + m):
+        if not (d[i].download(np.uint8, chunk) == host[i]).all():
+            raise SystemExit("ec: GPU parity disagrees with oracle")
+    erased = [1, 0, 1, 0, 0, 0, 1, 0]   # two data members and one parity member lost
+    dec = ErasureCode(ctx, k, m, erased)
+    out = {}
+    for name, fn, rd, wr in (("encode", lambda: enc.encode_device(d, size), k, m),
+                             ("decode", lambda: dec.decode_device(d, size), k, 3)):
+        for _ in range(max(1, args.warmup)):
+            fn()
+        e0, e1 = crc.Event(ctx), crc.Event(ctx)
+        if dist:
+            dist.barrier()
+        ctx.sync()
+        t0 = time.perf_counter()
+        e0.record()
+        for _ in range(args.steps):
+            fn()
+        e1.record()
+        ctx.sync()
+        if dist:
+            dist.barrier()
+        el = _max_over_ranks(dist, time.perf_counter() - t0)
+        kms = e0.elapsed_ms(e1) / args.steps
+        out[name] = {"ms": kms, "GiBs_data": world * args.steps * k * size / el / 2**30,
+                     "hbm_GBs": (rd + wr) * size / (kms / 1e3) / 1e9}
+    res = {
+        "metric": "GiB/s of data encoded (ErasureCode k=5 m=3, Cauchy bitmatrix w=8 ps=128), device-resident",
+        "value": out["encode"]["GiBs_data"], "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": out["encode"]["ms"], "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic (splitmix64) members",
+        "config": {"workload": "SURVEY §8 f4: k=5 + m=3 members of %d MiB" % args.ec_mib},
+        "roofline": {"bound": "hbm", "achieved": out["encode"]["hbm_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": out["encode"]["hbm_GBs"] / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "ec_apply_kernel<3>", "kernel_ms_avg": out["encode"]["ms"]},
+        "decode": out["decode"],
+    }
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    enc.free()
+    dec.free()
+    for b in d:
+        b.free()
     ctx.close()
     if dist:
         dist.destroy_process_group()

@@ -41,3 +41,13 @@ fi
   echo 'extern "C" uint32_t ref_func_crc(uint32_t c, const char* d, int32_t n) { return tfs::common::Func::crc(c, d, n); }'
 } | g++ -x c++ -O2 -finline-functions -fno-strict-aliasing -fPIC -shared -o "$OUT/libref_crc.so" -
 echo "build_ref: wrote $OUT/libref_crc.so"
+
+# Erasure code: the reference's vendored jerasure + galois
+# compile on their own (only libc headers); they are compiled in place from
+# /root/reference with oracle/ec_ref_driver.cpp (ErasureCode's glue, restated).
+DS="$REF/src/dataserver"
+if [ -f "$DS/jerasure.cpp" ] && [ -f "$DS/galois.cpp" ]; then
+  g++ -O2 -finline-functions -fno-strict-aliasing -fPIC -shared -w -I"$DS" \
+    "$DS/jerasure.cpp" "$DS/galois.cpp" "$HERE/ec_ref_driver.cpp" -o "$OUT/libref_ec.so"
+  echo "build_ref: wrote $OUT/libref_ec.so"
+fi

@@ -1,0 +1,104 @@
+// tfs_ec_kernels.hip -- gfx950 region kernel of TFS's erasure code.
+//
+// The reference (ErasureCode::encode/decode, src/dataserver/erasure_code.cpp:
+// 141-235 over jerasure_bitmatrix_dotprod, jerasure.cpp:304-348) works on
+// units of w * packetsize = 8 * 128 bytes per device: output packet r of an
+// output device is the XOR of every source packet (s, c) whose bit is set in
+// row r of that device's 8 x (k*8) bitmatrix block.  XOR is associative and
+// exact, so any order gives the reference's bytes.
+//
+// Mapping: a wave takes 4 units (4 KiB of every device) per step; lane l owns
+// 8 bytes at offset 8*(l & 15) of packet c of unit (l >> 4), for all 8 packets
+// c -- every load instruction reads four whole 128-byte lines.  The bitmatrix
+// is expanded to 0 / ~0 words in device memory; its addresses are wave-uniform
+// (scalar loads), so each bit costs one v_bitop3 (acc ^ (in & mask)) per dword.
+// OG (<= 4) outputs are accumulated in registers per launch.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tfs_ec_device.h"
+
+namespace tfsec {
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef const __attribute__((address_space(1))) u32x2* gu64p;
+typedef __attribute__((address_space(1))) u32x2* gu64wp;
+
+__device__ __forceinline__ u32x2 ld64nt(const uint8_t* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<gu64p>(reinterpret_cast<uintptr_t>(p)));
+}
+__device__ __forceinline__ void st64nt(uint8_t* p, u32x2 v) {
+  __builtin_nontemporal_store(v, reinterpret_cast<gu64wp>(reinterpret_cast<uintptr_t>(p)));
+}
+__device__ __forceinline__ uint32_t xand(uint32_t acc, uint32_t in, uint32_t m) {
+  // truth table indexed (src0 << 2) | (src1 << 1) | src2: acc ^ (in & m) = 0x78
+  return __builtin_amdgcn_bitop3_b32(acc, in, m, 0x78);
+}
+
+template <int OG>
+__global__ void __launch_bounds__(256) ec_apply_kernel(EcArgs a, const uint32_t* __restrict__ masks) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t u = uint32_t(lane) >> 4;
+  const uint32_t off = 8u * uint32_t(lane & 15);
+  const uint64_t ntiles = (a.units + 3) / 4;
+  // wave-uniform loop counters (so the mask addresses are scalar loads)
+  const uint64_t wave = uint64_t(blockIdx.x) * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t nwaves = uint64_t(gridDim.x) * (blockDim.x / 64);
+  for (uint64_t t = wave; t < ntiles; t += nwaves) {
+    const uint64_t unit = t * 4 + u;
+    const bool ok = unit < a.units;
+    const uint64_t base = unit * 1024u + off;
+    u32x2 acc[OG][8];
+#pragma unroll
+    for (int o = 0; o < OG; ++o)
+#pragma unroll
+      for (int r = 0; r < 8; ++r) acc[o][r] = u32x2{0u, 0u};
+    u32x2 in[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) in[c] = ok ? ld64nt(a.src[0] + base + 128u * c) : u32x2{0u, 0u};
+    for (uint32_t s = 0; s < a.S; ++s) {
+      u32x2 nx[8];
+      const bool more = s + 1 < a.S;
+      const uint8_t* np = a.src[more ? s + 1 : s];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) nx[c] = (ok && more) ? ld64nt(np + base + 128u * c) : u32x2{0u, 0u};
+#pragma unroll
+      for (int o = 0; o < OG; ++o)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const uint32_t* m = masks + ((uint32_t(o) * 8u + uint32_t(r)) * a.S + s) * 8u;
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            const uint32_t mk = m[c];
+            acc[o][r].x = xand(acc[o][r].x, in[c].x, mk);
+            acc[o][r].y = xand(acc[o][r].y, in[c].y, mk);
+          }
+        }
+#pragma unroll
+      for (int c = 0; c < 8; ++c) in[c] = nx[c];
+    }
+    if (ok) {
+#pragma unroll
+      for (int o = 0; o < OG; ++o)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) st64nt(a.dst[o] + base + 128u * r, acc[o][r]);
+    }
+  }
+}
+
+hipError_t launch_ec_apply(const EcArgs& a, int og, hipStream_t stream) {
+  if (a.units == 0) return hipSuccess;
+  const uint64_t ntiles = (a.units + 3) / 4;
+  uint64_t blocks = (ntiles + 3) / 4;
+  if (blocks > 2048) blocks = 2048;
+  const dim3 g(static_cast<unsigned>(blocks)), b(256);
+  switch (og) {
+    case 1: hipLaunchKernelGGL(ec_apply_kernel<1>, g, b, 0, stream, a, a.masks); break;
+    case 2: hipLaunchKernelGGL(ec_apply_kernel<2>, g, b, 0, stream, a, a.masks); break;
+    case 3: hipLaunchKernelGGL(ec_apply_kernel<3>, g, b, 0, stream, a, a.masks); break;
+    default: hipLaunchKernelGGL(ec_apply_kernel<4>, g, b, 0, stream, a, a.masks); break;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace tfsec
