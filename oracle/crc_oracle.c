@@ -285,7 +285,7 @@ static uint32_t le32(const unsigned char* p) {
 }
 
 /* Classify one frame of `avail` bytes the way getPacketInfo + decode would.
- * Returns ORACLE_PACKET_CHECKED with *body/*body_len/*stored set when decode
+ * Returns ORACLE_PACKET_CHECKED with *body, *body_len and *stored set when decode
  * checks a CRC, else the final status. */
 static int32_t packet_classify(const unsigned char* p, uint32_t avail, uint32_t* body_off, int32_t* body_len,
                                uint32_t* stored) {

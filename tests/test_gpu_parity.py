@@ -457,3 +457,67 @@ def test_blocks_compact_pipelined_matches_oracle(gpu_ctx, oracle):
     for k in keep:
         if isinstance(k[0], crc.PinnedBuffer):
             k[0].free()
+
+
+def test_blocks_compact_zero_copy_matches_oracle(gpu_ctx, oracle, monkeypatch):
+    """Page-locked source and destination images: the fused kernel reads the live
+    records over PCIe and writes the new block in place (no whole-block DMA).
+    Records congruent mod 4 take that path; a block with arbitrary record sizes
+    falls back to the DMA form.  Every block equals the oracle's real_compact
+    restatement, and the DMA form (TFS_CRC_VARIANT=8) gives the same bytes."""
+    import tfs_amd.crc as crc
+    rng = np.random.default_rng(45)
+    shapes = [
+        [65536] * 48,                                                     # BASELINE records (65,572 B)
+        [int(x) * 4 for x in rng.integers(1, 3000, 60)],                  # any size, multiple of 4
+        [int(x) for x in rng.integers(1, 12000, 50)],                     # arbitrary: DMA fallback
+        [65536] * 10 + [9 * 1024 * 1024 + 4] + [4096] * 10,              # a > 8 MiB "big file"
+    ]
+    monkeypatch.setenv("TFS_CRC_VARIANT", "8")
+    dma_ctx = crc.Context(0)
+    monkeypatch.setenv("TFS_CRC_VARIANT", "0")
+    bufs = []
+    try:
+        results = {}
+        for name, ctx in (("zc", gpu_ctx), ("dma", dma_ctx)):
+            jobs = (crc.BlockJob * len(shapes))()
+            keep = []
+            for b, sizes in enumerate(shapes):
+                img, metas = _block_image(oracle, sizes, seed=90 + b)
+                flags = np.zeros(len(sizes), np.int32)
+                flags[(b + 1) % 2::2] |= 1
+                if b == 3:
+                    flags[10] = 0                                           # keep the big file
+                if b == 1:
+                    img[int(metas[5]["offset"]) + 40] ^= 8                  # a corrupted live file
+                src = crc.PinnedBuffer(ctx, img.size)
+                src.array[:] = img
+                cap = int(metas["size"].astype(np.int64).sum()) + 64
+                dst = crc.PinnedBuffer(ctx, cap)
+                dst.array[:] = 0
+                bufs += [src, dst]
+                ok = np.zeros(len(sizes), np.uint8)
+                dm = np.zeros(len(sizes), crc.META_DTYPE)
+                keep.append((img, metas, flags, dst, ok, dm))
+                j = jobs[b]
+                j.src_image, j.src_len, j.metas, j.flags, j.n = src.ptr, img.size, metas.ctypes.data, \
+                    flags.ctypes.data, len(sizes)
+                j.dest_image, j.dest_cap, j.dest_metas, j.crc_ok = dst.ptr, cap, dm.ctypes.data, ok.ctypes.data
+            rc = ctx.blocks_compact(jobs)
+            assert rc == -1010
+            out = []
+            for b, (img, metas, flags, dst, ok, dm) in enumerate(keep):
+                odest, doff, ook = _oracle_compact(oracle, img, metas, flags)
+                w = int(jobs[b].dest_len)
+                assert w == odest.size, (name, b)
+                assert (dst.array[:w] == odest).all(), (name, b)
+                assert (ok == ook).all(), (name, b)
+                assert jobs[b].status == (-1010 if b == 1 else 0), (name, b)
+                out.append(dst.array[:w].copy())
+            results[name] = out
+        for a, b in zip(results["zc"], results["dma"]):
+            assert (a == b).all()
+    finally:
+        for p in bufs:
+            p.free()
+        dma_ctx.close()

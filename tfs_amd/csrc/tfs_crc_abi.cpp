@@ -147,6 +147,7 @@ struct CompactSlot {
 constexpr int kCompactSlots = 3;
 constexpr uint32_t kSchedSlots = 256;
 constexpr int kVariantUnfusedCompact = 7;  // TFS_CRC_VARIANT=7: two-pass device compaction (A/B baseline)
+constexpr int kVariantDmaCompact = 8;      // TFS_CRC_VARIANT=8: host compaction through whole-block DMA copies
 
 }  // namespace
 
@@ -586,6 +587,10 @@ int tfs_block_verify(tfs_crc_ctx* ctx, const void* image, uint64_t image_len, co
 // slots the H2D of block i+1, the kernels of block i and the D2H of block i-1
 // overlap (PCIe is full duplex; the copy engines run beside the kernels).
 
+static int compact_dma(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job, uint32_t nl, int64_t w, uint8_t* da,
+                       const uint8_t* ha, size_t aux_h2d, const RawMeta* d_metas, const int32_t* d_flags,
+                       const int64_t* d_doff, uint32_t* d_crc, int32_t* d_status);
+
 static int compact_enqueue(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job) {
   const uint32_t n = job->n;
   cs.job = job;
@@ -617,6 +622,17 @@ static int compact_enqueue(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job
   int64_t* h_doff = reinterpret_cast<int64_t*>(ha);
   RawMeta* h_metas = reinterpret_cast<RawMeta*>(ha + ob);
   int32_t* h_flags = reinterpret_cast<int32_t*>(ha + ob + mb);
+  // Zero-copy form: when both images are page-locked, the fused kernel reads the
+  // live records straight out of the source image over PCIe and writes the new
+  // block straight into the destination image, so only live bytes cross the
+  // link (the deleted records of a fragmented block never leave host memory).
+  // It needs every live record's source and destination congruent mod 4;
+  // otherwise the kernel's byte-copy fallback would re-read the record over
+  // PCIe, and the whole-block DMA form below is used instead.
+  bool zc = nl && ctx->variant != kVariantDmaCompact && is_pinned_host(job->src_image) &&
+            is_pinned_host(job->dest_image);
+  const uintptr_t src_a = reinterpret_cast<uintptr_t>(job->src_image);
+  const uintptr_t dst_a = reinterpret_cast<uintptr_t>(job->dest_image);
   int64_t off = 0;
   for (uint32_t k = 0; k < nl; ++k) {
     const uint32_t i = cs.live_idx[k];
@@ -624,7 +640,15 @@ static int compact_enqueue(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job
     h_metas[k] = RawMeta{job->metas[i].file_id, job->metas[i].offset, job->metas[i].size};
     h_flags[k] = job->flags[i];
     if (job->dest_metas) job->dest_metas[k] = tfs_raw_meta{job->metas[i].file_id, int32_t(off), job->metas[i].size};
+    if (((src_a + uint64_t(job->metas[i].offset)) ^ (dst_a + uint64_t(off))) & 3u) zc = false;
     off += job->metas[i].size;
+  }
+  void* zc_src = nullptr;
+  void* zc_dst = nullptr;
+  if (zc && (hipHostGetDevicePointer(&zc_src, const_cast<void*>(job->src_image), 0) != hipSuccess ||
+             hipHostGetDevicePointer(&zc_dst, job->dest_image, 0) != hipSuccess)) {
+    (void)hipGetLastError();
+    zc = false;
   }
   uint8_t* da = static_cast<uint8_t*>(cs.d_aux.p);
   int64_t* d_doff = reinterpret_cast<int64_t*>(da);
@@ -632,6 +656,31 @@ static int compact_enqueue(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job
   int32_t* d_flags = reinterpret_cast<int32_t*>(da + ob + mb);
   uint32_t* d_crc = reinterpret_cast<uint32_t*>(da + ((aux_bytes + 15) & ~size_t(15)));
   int32_t* d_status = reinterpret_cast<int32_t*>(d_crc + nl);
+  HIP_TRY(ctx, cs.h_status.reserve(fb + 4));
+  if (zc) {
+    HIP_TRY(ctx, hipMemcpyAsync(da, ha, ob + mb + fb, hipMemcpyHostToDevice, cs.stream));
+    HIP_TRY(ctx, launch_compact_fused(static_cast<const uint8_t*>(zc_src), job->src_len, d_metas, d_flags, d_doff, nl,
+                                      static_cast<uint8_t*>(zc_dst), ctx->d_tables, d_crc, d_status, nullptr,
+                                      cs.stream));
+    HIP_TRY(ctx, hipMemcpyAsync(cs.h_status.p, d_status, fb, hipMemcpyDeviceToHost, cs.stream));
+  } else {
+    const int rc = compact_dma(ctx, cs, job, nl, w, da, ha, ob + mb + fb, d_metas, d_flags, d_doff, d_crc, d_status);
+    if (rc != TFS_SUCCESS) return rc;
+  }
+  if (!cs.done) HIP_TRY(ctx, hipEventCreateWithFlags(&cs.done, hipEventDisableTiming));
+  HIP_TRY(ctx, hipEventRecord(cs.done, cs.stream));
+  job->dest_len = uint64_t(w);
+  job->n_live = nl;
+  cs.busy = true;
+  return TFS_SUCCESS;
+}
+
+// Whole-block form: H2D of the source image, fused kernel device to device,
+// D2H of the new block.
+static int compact_dma(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job, uint32_t nl, int64_t w, uint8_t* da,
+                       const uint8_t* ha, size_t aux_h2d, const RawMeta* d_metas, const int32_t* d_flags,
+                       const int64_t* d_doff, uint32_t* d_crc, int32_t* d_status) {
+  const size_t fb = size_t(nl) * 4;
   HIP_TRY(ctx, cs.d_src.reserve(job->src_len + 16));
   HIP_TRY(ctx, cs.d_dst.reserve(uint64_t(w) + 16));
   HIP_TRY(ctx, cs.h_status.reserve(fb + 4));
@@ -645,7 +694,7 @@ static int compact_enqueue(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job
     }
   }
   if (nl) {
-    HIP_TRY(ctx, hipMemcpyAsync(da, ha, ob + mb + fb, hipMemcpyHostToDevice, cs.stream));
+    HIP_TRY(ctx, hipMemcpyAsync(da, ha, aux_h2d, hipMemcpyHostToDevice, cs.stream));
     const uint8_t* d_src = static_cast<const uint8_t*>(cs.d_src.p);
     // One read of every live record: re-CRC (the verify the reference's
     // real_compact does not do) and repack from the same registers.
@@ -655,11 +704,6 @@ static int compact_enqueue(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job
     HIP_TRY(ctx, hipMemcpyAsync(cs.h_status.p, d_status, fb, hipMemcpyDeviceToHost, cs.stream));
     if (w) HIP_TRY(ctx, hipMemcpyAsync(job->dest_image, cs.d_dst.p, size_t(w), hipMemcpyDeviceToHost, cs.stream));
   }
-  if (!cs.done) HIP_TRY(ctx, hipEventCreateWithFlags(&cs.done, hipEventDisableTiming));
-  HIP_TRY(ctx, hipEventRecord(cs.done, cs.stream));
-  job->dest_len = uint64_t(w);
-  job->n_live = nl;
-  cs.busy = true;
   return TFS_SUCCESS;
 }
 

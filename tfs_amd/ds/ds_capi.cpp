@@ -2,6 +2,7 @@
 // can drive the write / close / verify / compact call sites the way the
 // reference's gtest programs drive LogicBlock/DataFile directly
 // (tests/dataserver/test_logic_block_and_compact.cpp).  Host C++ only.
+#include <atomic>
 #include <cstring>
 #include <string>
 
@@ -90,6 +91,47 @@ int tfs_ds_compact_block(tfs_crc_ctx* ctx, void* src, void* dest, uint8_t* crc_o
   const int r = compact_block(ctx, *static_cast<LogicBlockImage*>(src), *static_cast<LogicBlockImage*>(dest), &ok);
   for (size_t i = 0; i < ok.size() && i < cap; ++i) crc_ok[i] = ok[i];
   return r;
+}
+
+// BASELINE.json configs[0] through the dataserver-shaped code: n payloads of
+// `len` bytes written into `block` by `nthreads` worker threads (DataService's
+// PacketQueueThreads, base_service.cpp:187-192).  Per file: DataFile::set_data
+// (the staging memcpy, data_file.cpp:104), then close through the CloseBatcher
+// (one GPU verify of every pending lease's client CRC, data_management.cpp:
+// 196-198, then FileInfo|payload appended, logic_block.cpp:171-178).  Then
+// verify-on-read of the whole block (sync_backup.cpp:383-429).  Returns the
+// number of files that failed either check, or a negative status.
+int tfs_ds_loopback_block(tfs_crc_ctx* ctx, const char* payloads, uint32_t n, int32_t len, const uint32_t* client_crc,
+                          int nthreads, void* block) {
+  if (!ctx || !block || len < 0 || (n && (!payloads || !client_crc))) return TFS_EXIT_PARAMETER_ERROR;
+  LogicBlockImage& blk = *static_cast<LogicBlockImage*>(block);
+  if (nthreads < 1) nthreads = 1;
+  std::atomic<int> bad{0}, err{0};
+  {
+    CloseBatcher batcher(ctx, size_t(nthreads), 100);
+    std::vector<std::thread> workers;
+    for (int t = 0; t < nthreads; ++t)
+      workers.emplace_back([&, t] {
+        for (uint32_t i = uint32_t(t); i < n; i += uint32_t(nthreads)) {
+          DataFile df(i + 1, "/tmp", ctx);
+          if (df.set_data(payloads + size_t(i) * size_t(len), len, 0) < 0) {
+            err = TFS_EXIT_PARAMETER_ERROR;
+            continue;
+          }
+          CloseFileInfo info;
+          info.block_id_ = blk.block_id();
+          info.file_id_ = i + 1;
+          info.crc_ = client_crc[i];
+          const int rc = batcher.close(info, df, blk);
+          if (rc == TFS_EXIT_DATA_FILE_ERROR) ++bad;
+          else if (rc != TFS_SUCCESS) err = rc;
+        }
+      });
+    for (auto& w : workers) w.join();
+  }
+  if (err.load() != 0) return err.load();
+  const int nb = verify_block(ctx, blk, nullptr, nullptr);
+  return nb < 0 ? nb : bad.load() + nb;
 }
 
 }  // extern "C"
