@@ -56,11 +56,12 @@ def parse():
     p.add_argument("--ec-mib", type=int, default=1536,
                    help="member size in MiB for --workload ec (< 2048: ErasureCode sizes are int)")
     p.add_argument("--membench", action="store_true", help="also time raw streaming reads (stderr)")
-    p.add_argument("--workload", default="verify", choices=["verify", "zipf", "compact", "e2e", "packet", "compact_device", "ec"],
+    p.add_argument("--workload", default="verify", choices=["verify", "zipf", "compact", "e2e", "packet", "compact_device", "ec", "loopback"],
                    help="verify = BASELINE configs[1] (the headline line); zipf = configs[2]; "
                         "compact = configs[3]; e2e = pinned-host verify incl. H2D (configs[4] end-to-end)")
     p.add_argument("--ab", default="", help="comma list of TFS_CRC_VARIANT ids: interleaved A/B timing (stderr)")
     p.add_argument("--ab-rounds", type=int, default=6)
+    p.add_argument("--slots", default="", help="--workload compact: also time these blocks-in-flight counts (stderr A/B)")
     return p.parse_args()
 
 
@@ -114,7 +115,8 @@ def cpu_baseline(sample_u8, offs, lens, expected, seconds):
                 break
         ad = time.perf_counter() - t1
         assert (out == expected).all()
-        allcore = {"value": reps * float(np.sum(lens)) / ad / 2**30, "cores": threads}
+        allcore = {"value": reps * float(np.sum(lens)) / ad / 2**30, "cores": threads, "nproc": os.cpu_count(),
+                   "cpu_model": _cpu_model()}
     except Exception as e:  # reported, never fatal
         allcore = {"error": str(e)}
     return {
@@ -133,7 +135,8 @@ def main():
     args = parse()
     if args.workload != "verify":
         return {"zipf": bench_zipf, "compact": bench_compact, "e2e": bench_e2e,
-                "packet": bench_packet, "compact_device": bench_compact_device, "ec": bench_ec}[args.workload](args)
+                "packet": bench_packet, "compact_device": bench_compact_device, "ec": bench_ec,
+                "loopback": bench_loopback}[args.workload](args)
     world, rank, local, dist = _dist_init()
     import tfs_amd.crc as crc
     from tfs_amd.synth import synth_bytes
@@ -662,6 +665,15 @@ def bench_compact(args):
         c.blocks_compact(ab_jobs)
         ab[name + "_ms_per_block"] = _max_over_ranks(dist, time.perf_counter() - t0) / nab * 1e3
     ctx_dma.close()
+    for s in [int(x) for x in args.slots.split(",") if x]:  # blocks in flight (measurement knob)
+        os.environ["TFS_CRC_COMPACT_SLOTS"] = str(s)
+        cs = crc.Context(local)
+        del os.environ["TFS_CRC_COMPACT_SLOTS"]
+        cs.blocks_compact(warm)
+        t0 = time.perf_counter()
+        cs.blocks_compact(ab_jobs)
+        ab["zero_copy_slots%d_ms_per_block" % s] = (time.perf_counter() - t0) / nab * 1e3
+        cs.close()
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
@@ -936,6 +948,121 @@ def bench_ec(args):
     dec.free()
     for b in d:
         b.free()
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def bench_loopback(args):
+    """BASELINE configs[0]: src/dataserver write + verify over one 64 MiB block of
+    1024 x 64 KiB synthetic payloads, single-process loopback (no nameserver).
+    Per file: stage (DataFile::set_data), CRC (DataFile::get_crc), compare with the
+    client CRC, append FileInfo|payload; then verify every record against its
+    stored crc_.  GPU leg (the value): the dataserver-shaped C++ harness through
+    the C ABI, 8 worker threads (thread_count default, base_service.cpp:163-166)
+    closing through the CloseBatcher.  CPU legs (cpu_baseline, test
+    infrastructure): the oracle's restatement of the same loop, one thread and
+    all cores (one block per thread)."""
+    import concurrent.futures as cf
+    import tfs_amd.crc as crc
+    import tfs_amd.dataserver as ds
+    from tfs_amd.synth import synth_bytes
+    world, rank, local, dist = _dist_init()
+    ctx = crc.Context(local)
+    n, L = FILES_PER_BLOCK, FILE_SIZE
+    pay = synth_bytes(0x9E3779B97F4A7C15 + rank, n * L)
+    offs = np.arange(n, dtype=np.uint64) * L
+    client = ctx.batch(pay, offs, np.full(n, L, np.uint32))  # the client's Func::crc (tfs_file.cpp:961-963)
+    ora = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle_crc.so"))
+    ora.oracle_loopback_block.restype = ctypes.c_int32
+    ora.oracle_loopback_block.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+
+    def cpu_once(stage, image, stored):
+        return ora.oracle_loopback_block(pay.ctypes.data, n, L, client.ctypes.data, stage.ctypes.data,
+                                         image.ctypes.data, stored.ctypes.data)
+
+    bufs = (np.zeros(L, np.uint8), np.zeros(n * (L + FILEINFO), np.uint8), np.zeros(n, np.uint32))
+    if cpu_once(*bufs) != 0:
+        raise SystemExit("loopback: CPU restatement rejects the GPU client CRCs")
+    cpu_image = bufs[1].copy()
+
+    def gpu_once():
+        blk = ds.LogicBlock(1)
+        bad = ds.loopback_block(ctx, pay, n, L, client, 8, blk)
+        return bad, blk
+
+    bad, blk = gpu_once()
+    if bad != 0:
+        raise SystemExit("loopback: harness reported %d bad files" % bad)
+    # parity: every record the harness persisted equals the CPU loop's record for that file id
+    m, _ = blk.metas()
+    raw = blk.raw()
+    for i in np.linspace(0, n - 1, 64).astype(np.int64):
+        k = int(np.nonzero(m["file_id"] == i + 1)[0][0])
+        o = int(m["offset"][k])
+        got = raw[o:o + FILEINFO + L]
+        exp = cpu_image[i * (L + FILEINFO):(i + 1) * (L + FILEINFO)]
+        if not ((got[FILEINFO:] == exp[FILEINFO:]).all() and (got[32:36] == exp[32:36]).all()):
+            raise SystemExit("loopback: harness record %d differs from the CPU loop" % i)
+    blk.free()
+    reps = max(args.steps, 4)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        bad, blk = gpu_once()
+        blk.free()
+        if bad:
+            raise SystemExit("loopback: bad files")
+    el = _max_over_ranks(dist, time.perf_counter() - t0)
+    res = {
+        "metric": "GiB/s payload written + verified, single-process loopback of one 64 MiB block (BASELINE configs[0])",
+        "value": world * reps * n * L / el / 2**30, "unit": "GiB/s", "n_gpus": world, "steps": reps, "warmup": 1,
+        "ms_per_step": el / reps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u8", "data": "synthetic (splitmix64) 1024 x 64 KiB payloads",
+        "config": {"workload": "configs[0]: DataFile set_data -> close (CloseBatcher, 8 worker threads) -> "
+                               "FileInfo|payload append; then verify_block of the whole block",
+                   "files": n, "file_size": L},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        secs = min(args.cpu_seconds, 10.0)
+        t0, k = time.perf_counter(), 0
+        while True:
+            cpu_once(*bufs)
+            k += 1
+            if time.perf_counter() - t0 >= secs:
+                break
+        one = k * n * L / (time.perf_counter() - t0) / 2**30
+        threads = min(16, os.cpu_count() or 1)
+        tb = [(np.zeros(L, np.uint8), np.zeros(n * (L + FILEINFO), np.uint8), np.zeros(n, np.uint32))
+              for _ in range(threads)]
+        with cf.ThreadPoolExecutor(threads) as ex:
+            t0 = time.perf_counter()
+            rounds = 0
+            while time.perf_counter() - t0 < min(secs, 5.0):
+                list(ex.map(lambda b: cpu_once(*b), tb))
+                rounds += 1
+            allc = rounds * threads * n * L / (time.perf_counter() - t0) / 2**30
+        res["cpu_baseline"] = {
+            "value": one, "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": "%d loopbacks of the 1024 x 64 KiB block (stage, crc, compare, append, then re-CRC verify), "
+                      "oracle restatement of Func::crc, single thread, %.1f s" % (k, secs),
+            "allcore": {"value": allc, "cores": threads, "nproc": os.cpu_count(), "cpu_model": _cpu_model()},
+        }
+    if rank == 0:
+        print(json.dumps(res), flush=True)
     ctx.close()
     if dist:
         dist.destroy_process_group()

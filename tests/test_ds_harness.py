@@ -202,3 +202,29 @@ def test_verify_block_crc_errors_drive_repair(gpu_ctx, ds, oracle, tmp_path):
     nbad, st = ds.verify_block(gpu_ctx, blk, checker)
     assert nbad == 4 and checker.needs_repair(600)
     checker.free()
+
+
+def test_loopback_block_like_config1(gpu_ctx, ds, oracle):
+    """BASELINE configs[0] through the harness (tfs_ds_loopback_block): worker
+    threads stage and close every file through the CloseBatcher, then the block
+    is verified.  Files whose client CRC is wrong are rejected (-8013) and not
+    persisted; every persisted record equals FileInfo{crc_ = Func::crc(0, payload)}
+    followed by the payload, as the oracle's loopback writes it."""
+    n, L = 96, 4096 + 13
+    pay = synth_bytes(0xC0F1, n * L)
+    client = np.array([ocrc(oracle, 0, pay[i * L:(i + 1) * L].tobytes()) for i in range(n)], np.uint32)
+    wrong = [3, 40, 95]
+    client[wrong] ^= 0x10
+    blk = ds.LogicBlock(7)
+    bad = ds.loopback_block(gpu_ctx, pay, n, L, client, 8, blk)
+    assert bad == len(wrong)
+    metas, flags = blk.metas()
+    assert sorted(int(x) for x in metas["file_id"]) == [i + 1 for i in range(n) if i not in wrong]
+    raw = blk.raw()
+    for m in metas:
+        i = int(m["file_id"]) - 1
+        fi = _file_info(raw, int(m["offset"]))
+        assert fi["id_"] == i + 1 and fi["size_"] == L + FILEINFO and fi["offset_"] == int(m["offset"])
+        assert fi["crc_"] == client[i]
+        assert raw[int(m["offset"]) + FILEINFO:int(m["offset"]) + FILEINFO + L].tobytes() == pay[i * L:(i + 1) * L].tobytes()
+    blk.free()

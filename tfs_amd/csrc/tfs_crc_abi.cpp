@@ -144,7 +144,7 @@ struct CompactSlot {
     stream = nullptr;
   }
 };
-constexpr int kCompactSlots = 3;
+constexpr int kCompactSlots = 8;          // slots allocated; ctx->compact_slots of them are used
 constexpr uint32_t kSchedSlots = 256;
 constexpr int kVariantUnfusedCompact = 7;  // TFS_CRC_VARIANT=7: two-pass device compaction (A/B baseline)
 constexpr int kVariantDmaCompact = 8;      // TFS_CRC_VARIANT=8: host compaction through whole-block DMA copies
@@ -164,6 +164,7 @@ struct tfs_crc_ctx {
   // line per counter), one slot per launch, zeroed on the launch stream first.
   uint32_t* d_sched = nullptr;
   std::atomic<uint32_t> sched_seq{0};
+  int compact_slots = 8;  // blocks in flight in tfs_blocks_compact (TFS_CRC_COMPACT_SLOTS, 1..8)
   int variant = 0;  // kernel variant (TFS_CRC_VARIANT, measurement knob; 0 = product default)
   DevBuf packet_scratch;  // device-resident packet calls (parse descriptors, verdicts)
   hipStream_t packet_scratch_stream = nullptr;
@@ -350,6 +351,7 @@ int tfs_crc32_ctx_create(int device, tfs_crc_ctx** out) {
   auto* ctx = new tfs_crc_ctx();
   ctx->device = device;
   if (const char* v = getenv("TFS_CRC_VARIANT")) ctx->variant = atoi(v);
+  if (const char* v = getenv("TFS_CRC_COMPACT_SLOTS")) ctx->compact_slots = std::min(std::max(atoi(v), 1), kCompactSlots);
   int rc = TFS_SUCCESS;
   do {
     hipError_t e = hipSetDevice(device);
@@ -736,7 +738,7 @@ int tfs_blocks_compact(tfs_crc_ctx* ctx, tfs_block_job* jobs, uint32_t njobs) {
     if (rc != TFS_SUCCESS && (worst == TFS_SUCCESS || worst == TFS_EXIT_CHECK_CRC_ERROR)) worst = rc;
   };
   for (uint32_t j = 0; j < njobs; ++j) {
-    CompactSlot& cs = ctx->cslots[j % kCompactSlots];
+    CompactSlot& cs = ctx->cslots[j % uint32_t(ctx->compact_slots)];
     note(compact_finish(ctx, cs));
     const int rc = compact_enqueue(ctx, cs, &jobs[j]);
     if (rc != TFS_SUCCESS) {

@@ -51,6 +51,7 @@ def lib():
             "tfs_ds_checker_needs_repair": (ctypes.c_int, [vp, u32]),
             "tfs_ds_verify_block": (ctypes.c_int, [vp, vp, vp, u32, vp]),
             "tfs_ds_compact_block": (ctypes.c_int, [vp, vp, vp, vp, u32]),
+            "tfs_ds_loopback_block": (ctypes.c_int, [vp, vp, u32, i32, vp, ctypes.c_int, vp]),
             "tfs_ds_encoder_new": (vp, [vp]),
             "tfs_ds_encoder_free": (None, [vp]),
             "tfs_ds_encoder_add": (None, [vp, ctypes.c_int16, ctypes.c_int16, u64, ctypes.c_char_p, i32]),
@@ -318,3 +319,14 @@ def compact_block(ctx, src, dest):
     ok = np.zeros(max(len(m), 1), np.uint8)
     rc = lib().tfs_ds_compact_block(ctx.handle, src.h, dest.h, ok.ctypes.data, ok.size)
     return rc, ok[:len(m)]
+
+
+def loopback_block(ctx, payloads, n, length, client_crc, nthreads, block):
+    """BASELINE configs[0] through the harness: n payloads written by `nthreads`
+    worker threads (DataFile -> CloseBatcher close), then the whole block verified.
+    Returns the number of files that failed either check (or a negative status)."""
+    p = np.ascontiguousarray(payloads, dtype=np.uint8)
+    c = np.ascontiguousarray(client_crc, dtype=np.uint32)
+    if p.size < n * length or c.size < n:
+        raise ValueError("payloads/client_crc too small")
+    return lib().tfs_ds_loopback_block(ctx.handle, p.ctypes.data, n, length, c.ctypes.data, nthreads, block.h)
