@@ -521,39 +521,3 @@ def test_blocks_compact_zero_copy_matches_oracle(gpu_ctx, oracle, monkeypatch):
         for p in bufs:
             p.free()
         dma_ctx.close()
-
-
-def test_size_ordered_launch_device(gpu_ctx, oracle):
-    """>= 8192 files of mixed sizes take the largest-first ticket order (the
-    counting-sort pre-pass); every CRC and verdict still lands at its own index."""
-    import tfs_amd.crc as crc
-    rng = np.random.default_rng(2024)
-    n = 9000
-    lens = np.where(rng.random(n) < 0.1, rng.integers(100000, 300000, n), rng.integers(0, 5000, n)).astype(np.uint32)
-    offs = (np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64) + 3)]) + 5).astype(np.uint64)
-    total = int(offs[-1] + lens[-1] + 64)
-    buf = synth_bytes(99, total)
-    d = np.zeros(n, crc.DESC_DTYPE)
-    d["offset"], d["len"] = offs, lens
-    exp = np.zeros(n, np.uint32)
-    oracle.oracle_crc_batch(d.ctypes.data, n, buf.ctypes.data, exp.ctypes.data)
-    img = crc.DeviceBuffer(gpu_ctx, total).upload(buf)
-    dd = crc.DeviceBuffer(gpu_ctx, d.nbytes).upload(d)
-    out = crc.DeviceBuffer(gpu_ctx, 4 * n)
-    gpu_ctx.batch_device(dd, n, img, out)
-    gpu_ctx.sync()
-    assert (out.download(np.uint32, n) == exp).all()
-    v = d.copy()
-    v["aux"] = exp
-    bad = [7, 4000, 8999]
-    v["aux"][bad] ^= 1
-    vd = crc.DeviceBuffer(gpu_ctx, v.nbytes).upload(v)
-    ok = crc.DeviceBuffer(gpu_ctx, n)
-    nb = crc.DeviceBuffer(gpu_ctx, 4)
-    nb.zero()
-    gpu_ctx.verify_device(vd, n, img, None, ok, nb)
-    gpu_ctx.sync()
-    assert int(nb.download(np.uint32, 1)[0]) == 3
-    assert sorted(np.nonzero(ok.download(np.uint8, n) == 0)[0].tolist()) == bad
-    for b in (img, dd, out, vd, ok, nb):
-        b.free()

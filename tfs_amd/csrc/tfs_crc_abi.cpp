@@ -24,7 +24,7 @@
 namespace tfscrc {
 hipError_t launch_crc_files(int mode, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
                             uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
-                            int variant, uint32_t vseed, uint32_t* order_scratch);
+                            int variant, uint32_t vseed);
 hipError_t launch_packet_parse(const uint8_t* base, const PacketDesc* pd, uint32_t n, int mode, Desc* desc,
                                int32_t* pre, hipStream_t stream);
 hipError_t launch_packet_finish(uint8_t* base, const PacketDesc* pd, const Desc* desc, uint32_t n, int mode,
@@ -148,7 +148,6 @@ constexpr int kCompactSlots = 8;          // slots allocated; ctx->compact_slots
 constexpr uint32_t kSchedSlots = 256;
 constexpr int kVariantUnfusedCompact = 7;  // TFS_CRC_VARIANT=7: two-pass device compaction (A/B baseline)
 constexpr int kVariantDmaCompact = 8;      // TFS_CRC_VARIANT=8: host compaction through whole-block DMA copies
-constexpr int kVariantNoOrder = 9;         // TFS_CRC_VARIANT=9: identity ticket order (no size-ordered launches)
 
 }  // namespace
 
@@ -169,12 +168,6 @@ struct tfs_crc_ctx {
   int variant = 0;  // kernel variant (TFS_CRC_VARIANT, measurement knob; 0 = product default)
   DevBuf packet_scratch;  // device-resident packet calls (parse descriptors, verdicts)
   hipStream_t packet_scratch_stream = nullptr;
-  // Size-ordered launches (class counters + ticket order), shared by this ctx's
-  // CRC launches under order_mu; a launch on another stream first waits for
-  // the last user's stream.
-  std::mutex order_mu;
-  DevBuf order_scratch;
-  hipStream_t order_stream = nullptr;
 };
 
 namespace {
@@ -263,24 +256,6 @@ hipError_t sched_slot(tfs_crc_ctx* ctx, hipStream_t st, uint32_t** out) {
   return hipMemsetAsync(*out, 0, kSchedSlotBytes, st);
 }
 
-// Order scratch for one launch of n files on st, or NULL for the identity order
-// (small batches, or TFS_CRC_VARIANT=9).  The caller holds ctx->order_mu until
-// the launch is enqueued.
-hipError_t order_scratch_for(tfs_crc_ctx* ctx, uint32_t n, hipStream_t st, uint32_t** out) {
-  *out = nullptr;
-  if (n < kOrderMinFiles || ctx->variant == kVariantNoOrder) return hipSuccess;
-  const size_t bytes = kOrderCtrBytes + size_t(n) * 4u;
-  if (ctx->order_stream && (ctx->order_stream != st || bytes > ctx->order_scratch.cap)) {
-    const hipError_t e = hipStreamSynchronize(ctx->order_stream);
-    if (e != hipSuccess) return e;
-  }
-  const hipError_t e = ctx->order_scratch.reserve(bytes);
-  if (e != hipSuccess) return e;
-  ctx->order_stream = st;
-  *out = static_cast<uint32_t*>(ctx->order_scratch.p);
-  return hipSuccess;
-}
-
 Slot* free_slot(tfs_crc_ctx* ctx) {
   for (auto& s : ctx->slots)
     if (!s.busy) return &s;
@@ -312,14 +287,9 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
   HIP_TRY(ctx, hipMemsetAsync(s.d_bad.p, 0, 4, ctx->stream));
   uint32_t* sched = nullptr;
   HIP_TRY(ctx, sched_slot(ctx, ctx->stream, &sched));
-  {
-    std::lock_guard<std::mutex> og(ctx->order_mu);
-    uint32_t* order = nullptr;
-    HIP_TRY(ctx, order_scratch_for(ctx, n, ctx->stream, &order));
-    HIP_TRY(ctx, launch_crc_files(mode, d_base, static_cast<const Desc*>(s.d_desc.p), n, ctx->d_tables,
-                                  static_cast<uint32_t*>(s.d_crc.p), static_cast<uint8_t*>(s.d_ok.p),
-                                  static_cast<uint32_t*>(s.d_bad.p), sched, ctx->stream, ctx->variant, 0u, order));
-  }
+  HIP_TRY(ctx, launch_crc_files(mode, d_base, static_cast<const Desc*>(s.d_desc.p), n, ctx->d_tables,
+                                static_cast<uint32_t*>(s.d_crc.p), static_cast<uint8_t*>(s.d_ok.p),
+                                static_cast<uint32_t*>(s.d_bad.p), sched, ctx->stream, ctx->variant, 0u));
   HIP_TRY(ctx, hipMemcpyAsync(s.h_crc.p, s.d_crc.p, size_t(n) * 4, hipMemcpyDeviceToHost, ctx->stream));
   if (mode == 1) {
     HIP_TRY(ctx, hipMemcpyAsync(s.h_ok.p, s.d_ok.p, n, hipMemcpyDeviceToHost, ctx->stream));
@@ -418,7 +388,6 @@ int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx) {
     cs.release();
   }
   ctx->packet_scratch.release();
-  ctx->order_scratch.release();
   if (ctx->d_tables) (void)hipFree(ctx->d_tables);
   if (ctx->d_sched) (void)hipFree(ctx->d_sched);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -509,11 +478,8 @@ int tfs_crc32_batch_device(tfs_crc_ctx* ctx, const tfs_crc_desc* d_desc, uint32_
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   uint32_t* sched = nullptr;
   HIP_TRY(ctx, sched_slot(ctx, st, &sched));
-  std::lock_guard<std::mutex> og(ctx->order_mu);
-  uint32_t* order = nullptr;
-  HIP_TRY(ctx, order_scratch_for(ctx, n, st, &order));
   HIP_TRY(ctx, launch_crc_files(0, static_cast<const uint8_t*>(d_base), reinterpret_cast<const Desc*>(d_desc), n,
-                                ctx->d_tables, d_out_crc, nullptr, nullptr, sched, st, ctx->variant, 0u, order));
+                                ctx->d_tables, d_out_crc, nullptr, nullptr, sched, st, ctx->variant, 0u));
   return TFS_SUCCESS;
 }
 
@@ -524,11 +490,8 @@ int tfs_crc32_verify_device(tfs_crc_ctx* ctx, const tfs_crc_vdesc* d_desc, uint3
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   uint32_t* sched = nullptr;
   HIP_TRY(ctx, sched_slot(ctx, st, &sched));
-  std::lock_guard<std::mutex> og(ctx->order_mu);
-  uint32_t* order = nullptr;
-  HIP_TRY(ctx, order_scratch_for(ctx, n, st, &order));
   HIP_TRY(ctx, launch_crc_files(1, static_cast<const uint8_t*>(d_base), reinterpret_cast<const Desc*>(d_desc), n,
-                                ctx->d_tables, d_out_crc, d_out_ok, d_n_bad, sched, st, ctx->variant, 0u, order));
+                                ctx->d_tables, d_out_crc, d_out_ok, d_n_bad, sched, st, ctx->variant, 0u));
   return TFS_SUCCESS;
 }
 
@@ -861,7 +824,7 @@ static int packet_enqueue(tfs_crc_ctx* ctx, int mode, const PacketDesc* d_pd, ui
   uint32_t* sched = nullptr;
   HIP_TRY(ctx, sched_slot(ctx, st, &sched));
   HIP_TRY(ctx, launch_crc_files(mode, d_base, d_desc, n, ctx->d_tables, crc, mode == 1 ? d_ok : nullptr, nullptr,
-                                sched, st, ctx->variant, kPacketFlagV1, nullptr));
+                                sched, st, ctx->variant, kPacketFlagV1));
   HIP_TRY(ctx, launch_packet_finish(d_base, d_pd, d_desc, n, mode, d_pre, d_ok, crc, d_status, d_n_bad, st));
   return TFS_SUCCESS;
 }

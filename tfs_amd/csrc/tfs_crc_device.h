@@ -38,13 +38,6 @@ constexpr int kFileInfoSize = 36;  // sizeof(FileInfo), internal.h:432-446
 constexpr uint32_t kSchedStride = 64;                    // u32 between counters
 constexpr uint32_t kSchedSlotBytes = 8u * kSchedStride * 4u;  // 2 KiB per launch
 
-// Size-ordered launches (largest files first): a counting sort of the
-// descriptors by size class floor(log2(len)), counters on their own 256-B lines.
-constexpr uint32_t kSizeClasses = 32;
-constexpr uint32_t kOrderStride = 64;  // u32 between counters
-constexpr uint32_t kOrderCtrBytes = (kSizeClasses + 1u) * kOrderStride * 4u;  // + "mixed sizes" flag
-constexpr uint32_t kOrderMinFiles = 8192;  // fewer files: the pre-pass only adds latency
-
 // TFS status codes (src/common/error_msg.h)
 constexpr int32_t kSuccess = 0;
 constexpr int32_t kExitCheckCrcError = -1010;

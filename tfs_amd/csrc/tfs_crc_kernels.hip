@@ -29,7 +29,6 @@
 #include <stdint.h>
 
 #include "tfs_crc_device.h"
-#include "tfs_order_kernels.h"
 
 namespace tfscrc {
 
@@ -409,15 +408,8 @@ constexpr bool kS8 = true;
 struct Tickets {
   uint32_t* ctr;  // 8 zeroed counters for this launch, kSchedStride u32 apart (one per 256-byte line)
   uint32_t n, group;
-  // Interleaved positions (size-ordered launches): group g owns positions g,
-  // g+8, g+16, ... of the largest-first order, so every group sees every size
-  // class; otherwise group g owns the contiguous eighth [gbegin(g), gbegin(g+1)).
-  bool ilv;
   __device__ __forceinline__ uint32_t gbegin(uint32_t g) const { return uint32_t((uint64_t(n) * g) >> 3); }
-  __device__ __forceinline__ uint32_t gcount(uint32_t g) const {
-    return ilv ? (n > g ? (n - g + 7u) >> 3 : 0u) : gbegin(g + 1) - gbegin(g);
-  }
-  __device__ __forceinline__ uint32_t pos(uint32_t g, uint32_t j) const { return ilv ? j * 8u + g : gbegin(g) + j; }
+  __device__ __forceinline__ uint32_t gcount(uint32_t g) const { return gbegin(g + 1) - gbegin(g); }
   // Issue the atomic of the home group in lane 0; the result stays in lane 0's register.
   __device__ __forceinline__ uint32_t issue(int lane) const {
     uint32_t j = 0;
@@ -428,7 +420,7 @@ struct Tickets {
   __device__ __forceinline__ uint32_t resolve(uint32_t jv, int lane) {
     uint32_t j = __builtin_amdgcn_readlane(jv, 0);
     for (uint32_t tries = 0;; ++tries) {
-      if (j < gcount(group)) return pos(group, j);
+      if (j < gcount(group)) return gbegin(group) + j;
       if (tries == 7) return n;
       group = (group + 1) & 7u;  // steal
       uint32_t k = 0;
@@ -448,8 +440,7 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
                                                            const Desc* __restrict__ desc, uint32_t n,
                                                            const Tables* __restrict__ tg, uint32_t* out_crc,
                                                            uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched,
-                                                           uint32_t vseed, const uint32_t* __restrict__ order,
-                                                           const uint32_t* __restrict__ order_flag) {
+                                                           uint32_t vseed) {
   __shared__ uint32_t lds_tables[LdsLayout<S8>::bytes / 4];
   load_tables<RUN, false, S8>(lds_tables, tg);
   const int lane = threadIdx.x & (kWave - 1);
@@ -457,16 +448,12 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
   const uint32_t wpb = kBlock / kWave;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t stride = gridDim.x * wpb;
-  // Size-ordered launch (order_size_* pre-pass): ticket positions walk the
-  // files largest class first; uniform-size batches keep the identity order.
-  const bool use_order = DYN && order != nullptr && *order_flag != 0u;
-  Tickets tk{sched, n, blockIdx.x & 7u, use_order};
-  auto file_of = [&](uint32_t p) -> uint32_t { return (use_order && p < n) ? order[p] : p; };
+  Tickets tk{sched, n, blockIdx.x & 7u};
   uint32_t f, fn;
   if (DYN) {
-    f = file_of(tk.resolve(tk.issue(lane), lane));
+    f = tk.resolve(tk.issue(lane), lane);
     if (f >= n) return;
-    fn = file_of(tk.resolve(tk.issue(lane), lane));
+    fn = tk.resolve(tk.issue(lane), lane);
   } else {
     f = blockIdx.x * wpb + wave;
     if (f >= n) return;
@@ -493,7 +480,7 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
       ng = make_geo<RUN>(base + ncur.offset, ncur.len, MODE == 0 ? ncur.aux : vseed);
       nh = load_head<RUN>(ng, lane);
       load_ring<RUN, PF, NT>(ng, lane, buf, junk);
-      fnn = DYN ? file_of(tk.resolve(jv, lane)) : fn + stride;
+      fnn = DYN ? tk.resolve(jv, lane) : fn + stride;
       if (fnn < n) nxt = desc[fnn];
       if (DYN && fnn < n) jv = tk.issue(lane);
     }
@@ -946,11 +933,11 @@ static unsigned grid_for(uint32_t nwork) {
 template <int MODE>
 static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
                                  uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched,
-                                 hipStream_t stream, uint32_t vseed, const uint32_t* order, const uint32_t* order_flag) {
+                                 hipStream_t stream, uint32_t vseed) {
   const dim3 grid(grid_for(n)), block(kBlock);
 #define TFS_LAUNCH(R, P, N, D, S)                                                                          \
   hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N, D, S>), grid, block, 0, stream, base, desc, n, tg, out_crc, \
-                     out_ok, n_bad, sched, vseed, order, order_flag)
+                     out_ok, n_bad, sched, vseed)
   switch (variant) {
     case 1: TFS_LAUNCH(16, 5, true, false, true); break;
     case 2: TFS_LAUNCH(16, 4, true, true, true); break;
@@ -966,27 +953,10 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
 
 hipError_t launch_crc_files(int mode, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
                             uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
-                            int variant, uint32_t vseed, uint32_t* order_scratch) {
-  // order_scratch (may be NULL): kOrderCtrBytes of class counters, then n u32 of
-  // ticket order; owned by the caller until the launch completes.
+                            int variant, uint32_t vseed) {
   if (n == 0) return hipSuccess;
-  const uint32_t* order = nullptr;
-  const uint32_t* flag = nullptr;
-  if (order_scratch) {
-    uint32_t* ctr = order_scratch;
-    uint32_t* ord = order_scratch + kOrderCtrBytes / 4;
-    const hipError_t e = hipMemsetAsync(ctr, 0, kOrderCtrBytes, stream);
-    if (e != hipSuccess) return e;
-    const unsigned nb = (n + 1023u) / 1024u;
-    hipLaunchKernelGGL(order_count_kernel, dim3(nb < 256u ? nb : 256u), dim3(1024), 0, stream, desc, n, ctr);
-    hipLaunchKernelGGL(order_scan_kernel, dim3(1), dim3(64), 0, stream, ctr);
-    hipLaunchKernelGGL(order_scatter_kernel, dim3(nb), dim3(1024), 0, stream, desc, n, ctr, ord);
-    order = ord;
-    flag = ctr + kSizeClasses * kOrderStride;
-  }
-  if (mode == 0)
-    return launch_variant<0>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, sched, stream, vseed, order, flag);
-  return launch_variant<1>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, sched, stream, vseed, order, flag);
+  if (mode == 0) return launch_variant<0>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, sched, stream, vseed);
+  return launch_variant<1>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, sched, stream, vseed);
 }
 
 hipError_t launch_packet_parse(const uint8_t* base, const PacketDesc* pd, uint32_t n, int mode, Desc* desc,
