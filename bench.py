@@ -592,7 +592,8 @@ def bench_compact(args):
     from tfs_amd.synth import synth_bytes  # noqa: F401
     world, rank, local, dist = _dist_init()
     ctx = crc.Context(local)
-    nfiles, rec = FILES_PER_BLOCK, FILEINFO + FILE_SIZE
+    psize = int(os.environ.get("TFS_BENCH_PAYLOAD", FILE_SIZE))  # A/B knob: 65548 -> 16-byte multiple records
+    nfiles, rec = FILES_PER_BLOCK, FILEINFO + psize
     blk_bytes = nfiles * rec
     ndistinct = 8
     nblocks = args.compact_blocks
@@ -606,10 +607,10 @@ def bench_compact(args):
     d_desc = crc.DeviceBuffer(ctx, 16 * nfiles)
     d_crc = crc.DeviceBuffer(ctx, 4 * nfiles)
     d_off = crc.DeviceBuffer(ctx, 8 * nfiles).upload(np.arange(nfiles, dtype=np.uint64) * rec)
-    d_len = crc.DeviceBuffer(ctx, 4 * nfiles).upload(np.full(nfiles, FILE_SIZE, np.uint32))
+    d_len = crc.DeviceBuffer(ctx, 4 * nfiles).upload(np.full(nfiles, psize, np.uint32))
     desc = np.zeros(nfiles, crc.DESC_DTYPE)
     desc["offset"] = np.arange(nfiles) * rec + FILEINFO
-    desc["len"] = FILE_SIZE
+    desc["len"] = psize
     d_desc.upload(desc)
     for b in range(ndistinct):
         # build one real block image (checksum-on-write + FileInfo headers) on the GPU, then to pinned host

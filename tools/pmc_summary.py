@@ -1,61 +1,75 @@
 #!/usr/bin/env python3
-"""tools/pmc_summary.py TAG -- summarise gpurun_out/prof_TAG into profiles/TAG/
-(kernel stats csv, per-counter medians for the verify kernel, corrected HBM
-traffic per launch) and point profiles/pmc_latest.json at it."""
-import collections
+"""Fold rocprofv3 passes of one kernel into a PMC summary JSON (and, with
+--latest, profiles/pmc_latest.json, which bench.py reads for roofline.traffic).
+
+HBM bytes per launch follow MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE (KiB)
+reports half the bytes of a wide coalesced stream, so read bytes = FETCH_SIZE x
+1024 x 2, cross-checked by TCC_EA0_RDREQ x 128 B; WRITE_SIZE (KiB) as is.
+Counter values are medians over the kernel's dispatches."""
+import argparse
 import csv
-import glob
 import json
 import os
-import shutil
 import statistics
-import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-tag = sys.argv[1]
-src = os.path.join(ROOT, "gpurun_out", "prof_" + tag)
-dst = os.path.join(ROOT, "profiles", tag)
-os.makedirs(dst, exist_ok=True)
-shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
-bench_line = open(os.path.join(src, "bench_trace.json")).read().strip().splitlines()[-1]
-open(os.path.join(dst, "bench_under_rocprof.json"), "w").write(bench_line + "\n")
-vals = collections.defaultdict(list)
-kname = None
-for f in glob.glob(os.path.join(src, "pmc_*", "run_counter_collection.csv")):
-    grp = os.path.basename(os.path.dirname(f))
-    shutil.copy(f, os.path.join(dst, grp + ".csv"))
-    for r in csv.DictReader(open(f)):
-        if "crc_files_kernel<1" in r["Kernel_Name"]:
-            vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-            kname = r["Kernel_Name"].split("(")[0]
-med = {k: statistics.median(v) for k, v in vals.items()}
-stats = {}
-for r in csv.DictReader(open(os.path.join(dst, "kernel_stats.csv"))):
-    if "crc_files_kernel<1" in r["Name"]:
-        stats = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
-                 "max_ns": float(r["MaxNs"])}
-nfiles = 1048576
-algo = nfiles * (65536 + 21)
-rd = med.get("FETCH_SIZE", 0.0) * 1024 * 2
-wr = med.get("WRITE_SIZE", 0.0) * 1024
-summ = {
-    "kernel": kname, "tag": tag,
-    "launch_work": "1,048,576 files x 64 KiB payload (block images, FileInfo|payload)",
-    "rocprof_kernel_stats": stats,
-    "counters_median": med,
-    "read_bytes_corrected": rd,
-    "read_bytes_from_rdreq_x128": med.get("TCC_EA0_RDREQ_sum", 0.0) * 128,
-    "write_bytes": wr,
-    "traffic_bytes_per_launch": rd + wr,
-    "algorithmic_bytes_per_launch": algo,
-    "traffic_over_algorithmic": (rd + wr) / algo if rd else None,
-    "achieved_GBs_algorithmic_at_rocprof_avg": algo / (stats["avg_ns"] * 1e-9) / 1e9 if stats else None,
-    "correction": "gfx950 FETCH_SIZE reports half the bytes of a wide coalesced stream (MI355X_MICROARCH.md §HBM): x2; "
-                  "cross-checked by TCC_EA0_RDREQ x 128 B",
-    "effective_clock_GHz": med["GRBM_GUI_ACTIVE"] / 8 / (stats["avg_ns"] * 1e-9) / 1e9
-    if stats and "GRBM_GUI_ACTIVE" in med else None,
-}
-json.dump(summ, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
-json.dump(dict(summ, source="profiles/%s/pmc_summary.json" % tag),
-          open(os.path.join(ROOT, "profiles", "pmc_latest.json"), "w"), indent=1)
-print(json.dumps(summ, indent=1))
+
+def counters(paths, kernel):
+    vals = {}
+    for p in paths:
+        with open(p) as fh:
+            for row in csv.DictReader(fh):
+                if kernel in row["Kernel_Name"]:
+                    vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+    return {k: statistics.median(v) for k, v in vals.items()}
+
+
+def kernel_stats(path, kernel):
+    with open(path) as fh:
+        for row in csv.DictReader(fh):
+            if kernel in row["Name"]:
+                return {"calls": int(row["Calls"]), "avg_ns": float(row["AverageNs"]),
+                        "min_ns": float(row["MinNs"]), "max_ns": float(row["MaxNs"])}
+    raise SystemExit("kernel %r not in %s" % (kernel, path))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kernel", default="crc_files_kernel<1, 16, 5, true, true, true>")
+    ap.add_argument("--tag", required=True)
+    ap.add_argument("--algo-bytes", type=float, default=1048576.0 * 65557)
+    ap.add_argument("--stats", required=True, help="kernel_stats.csv of rocprofv3 --stats on the same command")
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--latest", action="store_true")
+    ap.add_argument("csvs", nargs="+", help="counter_collection.csv of each --pmc pass")
+    a = ap.parse_args()
+    c = counters(a.csvs, a.kernel)
+    ks = kernel_stats(a.stats, a.kernel)
+    read = c["FETCH_SIZE"] * 1024.0 * 2.0
+    write = c.get("WRITE_SIZE", 0.0) * 1024.0
+    res = {
+        "kernel": a.kernel, "tag": a.tag,
+        "launch_work": "1,048,576 files x 64 KiB payload (block images, FileInfo|payload)",
+        "rocprof_kernel_stats": ks, "counters_median": c,
+        "read_bytes_corrected": read,
+        "read_bytes_from_rdreq_x128": c["TCC_EA0_RDREQ_sum"] * 128.0 if "TCC_EA0_RDREQ_sum" in c else None,
+        "write_bytes": write, "traffic_bytes_per_launch": read + write,
+        "algorithmic_bytes_per_launch": a.algo_bytes,
+        "traffic_over_algorithmic": (read + write) / a.algo_bytes,
+        "achieved_GBs_algorithmic_at_rocprof_avg": a.algo_bytes / (ks["avg_ns"] * 1e-9) / 1e9,
+        "correction": "gfx950 FETCH_SIZE reports half the bytes of a wide coalesced stream "
+                      "(MI355X_MICROARCH.md §HBM): x2; cross-checked by TCC_EA0_RDREQ x 128 B",
+        "source": os.path.relpath(a.out, os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+    }
+    os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
+    with open(a.out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    if a.latest:
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        with open(os.path.join(root, "profiles", "pmc_latest.json"), "w") as fh:
+            json.dump(res, fh, indent=1)
+    print(json.dumps({k: res[k] for k in ("traffic_bytes_per_launch", "traffic_over_algorithmic",
+                                            "achieved_GBs_algorithmic_at_rocprof_avg")}))
+
+
+if __name__ == "__main__":
+    main()
