@@ -230,8 +230,12 @@ int tfs_compact_jobs_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_le
 /* Many blocks in one call (the compaction task thread's queue): each job is
  * tfs_block_compact's arguments plus its outputs.  Jobs are pipelined over
  * several streams so the H2D copy of one block, the verify/repack kernels of
- * the next and the D2H copy of another overlap.  Page-locked source/dest
- * images (tfs_crc32_host_malloc_pinned) are copied directly; pageable ones are
+ * the next and the D2H copy of another overlap.  When both source and dest
+ * images are page-locked (tfs_crc32_host_malloc_pinned / hipHostRegister) and
+ * every live record keeps its alignment mod 4, the kernel reads the live
+ * records from, and writes the new block to, host memory directly (zero-copy:
+ * only live bytes cross PCIe, no whole-block copies).  Otherwise page-locked
+ * images are copied directly (whole block H2D, new block D2H); pageable ones are
  * staged.  Returns the worst job status (TFS_EXIT_CHECK_CRC_ERROR if only CRC
  * mismatches were found). */
 typedef struct tfs_block_job {
