@@ -260,6 +260,56 @@ __device__ __forceinline__ void st128_nt(uintptr_t a, const uint4& v) {
   }
 }
 
+// Copy-through of one stripe (RUN = 16) to dst = src + delta, delta = 16m + 4k
+// with k in 1..3: the aligned 16-byte destination chunk under lane l holds the
+// last k dwords of lane l-1 and the first 4-k of lane l, so every lane stores
+// one whole dwordx4 instead of four dword stores (over PCIe -- zero-copy host
+// compaction -- four partial writes per 16 bytes cost 6 %).  Lane 0 takes the
+// previous stripe's lane-63 dwords (`cy/cz/cw`); right after stripe 0 (stored
+// dword by dword) it stores only its own dwords.  `flush`: this lane ends the
+// record's last stripe, so its own last k dwords go out as dword stores.
+struct ShiftCarry {
+  uint32_t y, z, w;
+  bool valid;
+};
+__device__ __forceinline__ void store_shifted(uintptr_t chunk, const uint4& v, uint32_t k, int lane, ShiftCarry& cr,
+                                              bool store, bool flush) {
+  uint32_t p1 = __shfl_up(v.w, 1, kWave), p2 = __shfl_up(v.z, 1, kWave), p3 = __shfl_up(v.y, 1, kWave);
+  if (lane == 0) {
+    p1 = cr.w;
+    p2 = cr.z;
+    p3 = cr.y;
+  }
+  if (store) {
+    if (lane == 0 && !cr.valid) {
+      if (k == 1) {
+        st32(chunk + 4, v.x); st32(chunk + 8, v.y); st32(chunk + 12, v.z);
+      } else if (k == 2) {
+        st32(chunk + 8, v.x); st32(chunk + 12, v.y);
+      } else {
+        st32(chunk + 12, v.x);
+      }
+    } else {
+      const uint4 o = k == 1 ? make_uint4(p1, v.x, v.y, v.z)
+                             : (k == 2 ? make_uint4(p2, p1, v.x, v.y) : make_uint4(p3, p2, p1, v.x));
+      st128_nt(chunk, o);
+    }
+    if (flush) {
+      if (k == 1) {
+        st32(chunk + 16, v.w);
+      } else if (k == 2) {
+        st32(chunk + 16, v.z); st32(chunk + 20, v.w);
+      } else {
+        st32(chunk + 16, v.y); st32(chunk + 20, v.z); st32(chunk + 24, v.w);
+      }
+    }
+  }
+  cr.y = __builtin_amdgcn_readlane(v.y, kWave - 1);
+  cr.z = __builtin_amdgcn_readlane(v.z, kWave - 1);
+  cr.w = __builtin_amdgcn_readlane(v.w, kWave - 1);
+  cr.valid = true;
+}
+
 // The lane's chain over stripes 0..nstripes-1 (before the final combine).
 // COPY: also store every payload byte of [start, B16) to dst = src + delta.
 template <int RUN, int PF, bool NT, bool S8, bool COPY = false>
@@ -300,6 +350,21 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
     // refilled (past the last stripe: the L2-resident `junk` region).
     const uint32_t last = g.nstripes - 1;
     const bool lane_in_last = uint32_t(lane) < g.nvalid;
+    // Copy-through of stripe st (COPY only): whole dwordx4 stores at any
+    // destination shift congruent mod 4 (store_shifted).
+    const uint32_t kshift = uint32_t(delta >> 2) & 3u;
+    ShiftCarry carry{0u, 0u, 0u, false};
+    static_assert(!COPY || RUN == 16, "copy-through assumes one 16-byte run per lane");
+    auto copy_stripe = [&](uint32_t st, const uint4& v) {
+      const bool valid = !(st == last && !lane_in_last);
+      const uintptr_t q = g.sb0 + uintptr_t(st) * kStripe + uintptr_t(lane) * RUN;
+      if (kshift == 0u) {
+        if (valid) st128_nt(q + delta, v);
+      } else {
+        store_shifted(q + uintptr_t(delta) - 4u * kshift, v, kshift, lane, carry, valid,
+                      st == last && uint32_t(lane) + 1u == g.nvalid);
+      }
+    };
     uint32_t r = 1;
     for (; r + PF <= g.nstripes; r += PF) {
 #pragma unroll
@@ -313,11 +378,7 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
 #pragma unroll
         for (int v = 0; v < kVec; ++v) c = steps16(T, lb, c, buf[f][v]);
         c = (r + f == last && !lane_in_last) ? c_old : c;  // run past B16: not part of the chain
-        if (COPY && copy_on && !(r + f == last && !lane_in_last)) {
-          const uintptr_t q = g.sb0 + uintptr_t(r + f) * kStripe + uintptr_t(lane) * RUN;
-#pragma unroll
-          for (int v = 0; v < kVec; ++v) st128_nt(q + 16u * v + delta, buf[f][v]);
-        }
+        if (COPY && copy_on) copy_stripe(r + f, buf[f][0]);
         const uintptr_t sb = stripe_base<RUN>(g, r + f + PF, junk) + uintptr_t(lane) * RUN;
 #pragma unroll
         for (int v = 0; v < kVec; ++v) buf[f][v] = ld128s<NT>(sb + 16u * v);
@@ -333,11 +394,7 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
 #pragma unroll
         for (int v = 0; v < kVec; ++v) c = steps16(T, lb, c, buf[f][v]);
         c = (r + f == last && !lane_in_last) ? c_old : c;
-        if (COPY && copy_on && !(r + f == last && !lane_in_last)) {
-          const uintptr_t q = g.sb0 + uintptr_t(r + f) * kStripe + uintptr_t(lane) * RUN;
-#pragma unroll
-          for (int v = 0; v < kVec; ++v) st128_nt(q + 16u * v + delta, buf[f][v]);
-        }
+        if (COPY && copy_on) copy_stripe(r + f, buf[f][0]);
       }
     }
   }

@@ -21,7 +21,7 @@ void put_file_info(char* dst, const tfs_file_info& fi) { memcpy(dst, &fi, kFileI
 // ---------------- DataFile (data_file.cpp) ----------------
 
 DataFile::DataFile(uint64_t fn, const std::string& tmp_dir, tfs_crc_ctx* ctx)
-    : data_(WRITE_DATA_TMPBUF_SIZE), ctx_(ctx) {
+    : data_(new char[WRITE_DATA_TMPBUF_SIZE]), ctx_(ctx) {
   char name[512];
   snprintf(name, sizeof name, "%s/%llu.dat", tmp_dir.c_str(), static_cast<unsigned long long>(fn));
   tmp_file_name_ = name;
@@ -45,12 +45,12 @@ int DataFile::set_data(const char* data, int32_t len, int32_t offset) {
     if (fd_ == -1) {
       fd_ = open(tmp_file_name_.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0600);
       if (fd_ == -1) return -1;
-      if (write(fd_, data_.data(), length_) != length_) return -1;
+      if (write(fd_, data_.get(), length_) != length_) return -1;
     }
     if (lseek(fd_, offset, SEEK_SET) == -1) return -1;
     if (write(fd_, data, len) != len) return -1;
   } else {
-    memcpy(data_.data() + offset, data, len);
+    memcpy(data_.get() + offset, data, len);
   }
   if (length > length_) length_ = length;
   return len;
@@ -67,7 +67,7 @@ char* DataFile::get_data(char* data, int32_t* len, int32_t offset) {
       return nullptr;
     }
     if (data == nullptr) {
-      data = data_.data();
+      data = data_.get();
       *len = WRITE_DATA_TMPBUF_SIZE;
     }
     const ssize_t r = read(fd_, data, *len);
@@ -79,11 +79,11 @@ char* DataFile::get_data(char* data, int32_t* len, int32_t offset) {
     return data;
   }
   if (data == nullptr) {
-    data = data_.data() + offset;
+    data = data_.get() + offset;
     *len = length_ - offset;
   } else {
     if (*len > length_ - offset) *len = length_ - offset;
-    memcpy(data, data_.data() + offset, *len);
+    memcpy(data, data_.get() + offset, *len);
   }
   return data;
 }
@@ -94,15 +94,15 @@ uint32_t DataFile::get_crc() {
     if (length_ > WRITE_DATA_TMPBUF_SIZE) {  // data_file.cpp:172-187: re-read in 2 MiB chunks, running seed
       if (fd_ == -1 || lseek(fd_, 0, SEEK_SET) == -1) return crc_;
       ssize_t rlen;
-      while ((rlen = read(fd_, data_.data(), WRITE_DATA_TMPBUF_SIZE)) > 0) {
+      while ((rlen = read(fd_, data_.get(), WRITE_DATA_TMPBUF_SIZE)) > 0) {
         tfs_crc_desc d{0, uint32_t(rlen), crc_};
         uint32_t out = 0;
-        status_ = tfs_crc32_batch(ctx_, &d, 1, data_.data(), uint64_t(rlen), &out);
+        status_ = tfs_crc32_batch(ctx_, &d, 1, data_.get(), uint64_t(rlen), &out);
         if (status_ != TFS_SUCCESS) return 0;
         crc_ = out;
       }
     } else {
-      status_ = tfs_datafile_get_crc(ctx_, data_.data(), length_, &crc_);
+      status_ = tfs_datafile_get_crc(ctx_, data_.get(), length_, &crc_);
       if (status_ != TFS_SUCCESS) crc_ = 0;
     }
   }
@@ -210,6 +210,7 @@ CloseBatcher::~CloseBatcher() {
   }
   cv_.notify_all();
   worker_.join();
+  if (gather_) tfs_crc32_host_free_pinned(ctx_, gather_);
 }
 
 int CloseBatcher::close(const CloseFileInfo& info, DataFile& df, LogicBlockImage& block) {
@@ -249,7 +250,23 @@ void CloseBatcher::flush(std::vector<Req*>& reqs) {
   std::vector<tfs_crc_vdesc> d(reqs.size());
   uint64_t total = 0;
   for (size_t i = 0; i < reqs.size(); ++i) total += uint64_t(reqs[i]->df->get_length());
-  std::vector<char> gathered(size_t(total) + 16);
+  if (total + 16 > gather_cap_) {
+    if (gather_) tfs_crc32_host_free_pinned(ctx_, gather_);
+    gather_ = nullptr;
+    gather_cap_ = 0;
+    void* p = nullptr;
+    const size_t want = size_t(total) + 16 + size_t(total) / 2;
+    if (tfs_crc32_host_malloc_pinned(ctx_, want, &p) == TFS_SUCCESS) {
+      gather_ = static_cast<char*>(p);
+      gather_cap_ = want;
+    }
+  }
+  std::vector<char> pageable;  // only if the pinned allocation failed
+  char* gathered = gather_;
+  if (!gathered) {
+    pageable.resize(size_t(total) + 16);
+    gathered = pageable.data();
+  }
   uint64_t off = 0;
   for (size_t i = 0; i < reqs.size(); ++i) {
     DataFile& df = *reqs[i]->df;
@@ -257,7 +274,7 @@ void CloseBatcher::flush(std::vector<Req*>& reqs) {
     int32_t got = 0;
     while (got < n) {
       int32_t rl = n - got;
-      if (!df.get_data(gathered.data() + off + got, &rl, got) || rl <= 0) break;
+      if (!df.get_data(gathered + off + got, &rl, got) || rl <= 0) break;
       got += rl;
     }
     d[i] = tfs_crc_vdesc{off, uint32_t(n), reqs[i]->info->crc_};
@@ -266,7 +283,7 @@ void CloseBatcher::flush(std::vector<Req*>& reqs) {
   std::vector<uint32_t> crc(reqs.size());
   std::vector<uint8_t> ok(reqs.size());
   uint32_t nbad = 0;
-  const int rc = tfs_crc32_verify(ctx_, d.data(), uint32_t(reqs.size()), gathered.data(), total, crc.data(), ok.data(),
+  const int rc = tfs_crc32_verify(ctx_, d.data(), uint32_t(reqs.size()), gathered, total, crc.data(), ok.data(),
                                   &nbad);
   for (size_t i = 0; i < reqs.size(); ++i) {
     Req& r = *reqs[i];
@@ -275,7 +292,7 @@ void CloseBatcher::flush(std::vector<Req*>& reqs) {
     } else if (!ok[i]) {
       r.status = TFS_EXIT_DATA_FILE_ERROR;  // data_management.cpp:198
     } else {
-      r.status = r.block->append_record(r.info->file_id_, gathered.data() + d[i].offset, int32_t(d[i].len), crc[i]);
+      r.status = r.block->append_record(r.info->file_id_, gathered + d[i].offset, int32_t(d[i].len), crc[i]);
     }
   }
 }

@@ -16,6 +16,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -48,11 +49,11 @@ class DataFile {
   uint32_t get_crc();
   int last_status() const { return status_; }
   void set_over();
-  const char* buffer() const { return data_.data(); }
+  const char* buffer() const { return data_.get(); }
 
  private:
   int32_t length_ = 0;
-  std::vector<char> data_;
+  std::unique_ptr<char[]> data_;  // data_file.h:83: a plain char array, not zero-filled
   uint32_t crc_ = 0;
   int fd_ = -1;
   std::string tmp_file_name_;
@@ -129,6 +130,8 @@ class CloseBatcher {
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
   std::vector<Req*> queue_;
+  char* gather_ = nullptr;  // page-locked gather buffer (the verify DMA reads it directly)
+  size_t gather_cap_ = 0;
   bool stop_ = false;
   uint64_t batches_ = 0;
   std::thread worker_;
