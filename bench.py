@@ -56,7 +56,7 @@ def parse():
     p.add_argument("--ec-mib", type=int, default=1536,
                    help="member size in MiB for --workload ec (< 2048: ErasureCode sizes are int)")
     p.add_argument("--membench", action="store_true", help="also time raw streaming reads (stderr)")
-    p.add_argument("--workload", default="verify", choices=["verify", "zipf", "compact", "e2e", "packet", "compact_device", "ec", "loopback"],
+    p.add_argument("--workload", default="verify", choices=["verify", "zipf", "compact", "e2e", "packet", "compact_device", "ec", "loopback", "block_verify"],
                    help="verify = BASELINE configs[1] (the headline line); zipf = configs[2]; "
                         "compact = configs[3]; e2e = pinned-host verify incl. H2D (configs[4] end-to-end)")
     p.add_argument("--ab", default="", help="comma list of TFS_CRC_VARIANT ids: interleaved A/B timing (stderr)")
@@ -136,7 +136,7 @@ def main():
     if args.workload != "verify":
         return {"zipf": bench_zipf, "compact": bench_compact, "e2e": bench_e2e,
                 "packet": bench_packet, "compact_device": bench_compact_device, "ec": bench_ec,
-                "loopback": bench_loopback}[args.workload](args)
+                "loopback": bench_loopback, "block_verify": bench_block_verify}[args.workload](args)
     world, rank, local, dist = _dist_init()
     import tfs_amd.crc as crc
     from tfs_amd.synth import synth_bytes
@@ -703,6 +703,85 @@ def bench_compact(args):
     if rank == 0:
         print(json.dumps(res), flush=True)
     for b in srcs + dests:
+        b.free()
+    for b in (d_img, d_desc, d_crc, d_off, d_len):
+        b.free()
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+def bench_block_verify(args):
+    """Verify-on-read of fragmented blocks held in page-locked host memory (the
+    block files of tfs_amd/ds/block_store.h load into such buffers): per block one
+    tfs_block_verify over its live records (sync_backup.cpp:345-435 checks).
+    The kernel reads only the named records over PCIe (zero-copy); the
+    whole-block DMA form (TFS_CRC_VARIANT=8) is timed beside it."""
+    import tfs_amd.crc as crc
+    world, rank, local, dist = _dist_init()
+    ctx = crc.Context(local)
+    nfiles, rec = FILES_PER_BLOCK, FILEINFO + FILE_SIZE
+    blk_bytes = nfiles * rec
+    ndistinct, nblocks = 8, args.compact_blocks
+    d_img = crc.DeviceBuffer(ctx, blk_bytes + 64)
+    d_desc = crc.DeviceBuffer(ctx, 16 * nfiles)
+    d_crc = crc.DeviceBuffer(ctx, 4 * nfiles)
+    d_off = crc.DeviceBuffer(ctx, 8 * nfiles).upload(np.arange(nfiles, dtype=np.uint64) * rec)
+    d_len = crc.DeviceBuffer(ctx, 4 * nfiles).upload(np.full(nfiles, FILE_SIZE, np.uint32))
+    desc = np.zeros(nfiles, crc.DESC_DTYPE)
+    desc["offset"], desc["len"] = np.arange(nfiles) * rec + FILEINFO, FILE_SIZE
+    d_desc.upload(desc)
+    srcs = []
+    for b in range(ndistinct):
+        ctx.synth_fill_device(d_img, blk_bytes + 64 - (blk_bytes + 64) % 8, 0xB1F + 13 * b + rank, 0)
+        ctx.batch_device(d_desc, nfiles, d_img, d_crc)
+        ctx.write_headers_device(d_img, d_off, d_len, d_crc, 1, nfiles)
+        ctx.sync()
+        p = crc.PinnedBuffer(ctx, blk_bytes)
+        p.array[:] = d_img.download(np.uint8, blk_bytes)
+        srcs.append(p)
+    live = np.nonzero(_fragmented_flags(nfiles) == 0)[0]
+    metas = np.zeros(live.size, crc.META_DTYPE)
+    metas["file_id"], metas["offset"], metas["size"] = 1 + live, live * rec, rec
+    os.environ["TFS_CRC_VARIANT"] = "8"
+    ctx_dma = crc.Context(local)
+    os.environ["TFS_CRC_VARIANT"] = "0"
+    ora = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle_crc.so"))
+    ora.oracle_verify_file.restype = ctypes.c_int32
+    ora.oracle_verify_file.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
+                                       ctypes.POINTER(ctypes.c_uint32)]
+    c0, st0, nb0, _ = ctx.block_verify(srcs[0].array, metas)
+    for i in np.linspace(0, live.size - 1, 16).astype(np.int64):  # parity spot check (test infrastructure)
+        oc = ctypes.c_uint32()
+        code = ora.oracle_verify_file(srcs[0].ptr, blk_bytes, int(metas["offset"][i]), rec, ctypes.byref(oc))
+        if code != st0[i] or oc.value != int(c0[i]):
+            raise SystemExit("block_verify: GPU disagrees with oracle at record %d" % i)
+    out = {}
+    for name, c, nb in (("dma", ctx_dma, min(nblocks, 512)), ("zero_copy", ctx, nblocks)):
+        c.block_verify(srcs[0].array, metas)
+        if dist:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for j in range(nb):
+            _, st, nbad, _ = c.block_verify(srcs[j % ndistinct].array, metas)
+            if nbad:
+                raise SystemExit("block_verify: mismatches on clean blocks")
+        out[name] = (_max_over_ranks(dist, time.perf_counter() - t0), nb)
+    ctx_dma.close()
+    el, nb = out["zero_copy"]
+    res = {
+        "metric": "GiB/s verify-on-read of fragmented blocks in page-locked host memory (source block bytes)",
+        "value": float(world) * nb * blk_bytes / el / 2**30, "unit": "GiB/s", "n_gpus": world, "steps": nb,
+        "warmup": 1, "ms_per_step": el / nb * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic 64 KiB files, 1024 per block, evens + every 3rd of the rest deleted (%d live)" % live.size,
+        "config": {"workload": "one tfs_block_verify per block over its live records, %d blocks" % nb,
+                   "live_payload_GiBs": float(world) * nb * live.size * FILE_SIZE / el / 2**30},
+        "ab": {"zero_copy_ms_per_block": el / nb * 1e3, "dma_ms_per_block": out["dma"][0] / out["dma"][1] * 1e3},
+    }
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    for b in srcs:
         b.free()
     for b in (d_img, d_desc, d_crc, d_off, d_len):
         b.free()

@@ -521,3 +521,31 @@ def test_blocks_compact_zero_copy_matches_oracle(gpu_ctx, oracle, monkeypatch):
         for p in bufs:
             p.free()
         dma_ctx.close()
+
+
+def test_block_verify_zero_copy_pinned_image(gpu_ctx, oracle):
+    """A page-locked block image is verified in place (zero-copy, only the named
+    records cross PCIe): same CRCs and statuses as the staged pageable path,
+    including out-of-range metas, which must not be read."""
+    import tfs_amd.crc as crc
+    rng = np.random.default_rng(46)
+    sizes = [65536] * 30 + [int(x) for x in rng.integers(1, 20000, 30)]
+    img, metas = _block_image(oracle, sizes, seed=47)
+    img[int(metas[4]["offset"]) + 36 + 9] ^= 0x02
+    live = np.ascontiguousarray(metas[1::3])                      # a fragmented block: every 3rd record
+    bad_meta = np.zeros(1, crc.META_DTYPE)
+    bad_meta[0] = (5, img.size - 10, 4096)                        # runs past the image
+    m = np.concatenate([live, bad_meta])
+    pin = crc.PinnedBuffer(gpu_ctx, img.size)
+    try:
+        pin.array[:] = img
+        c1, s1, n1, r1 = gpu_ctx.block_verify(pin.array, m)
+        c2, s2, n2, r2 = gpu_ctx.block_verify(img.copy(), m)
+        assert (s1 == s2).all() and n1 == n2 and r1 == r2
+        assert (c1[:-1] == c2[:-1]).all()
+        assert s1[-1] == -1016 and s1[1] == -1010 and (s1[2:-1] == 0).all() and s1[0] == 0
+        for i in range(len(live)):
+            o, sz = int(live[i]["offset"]), int(live[i]["size"])
+            assert int(c1[i]) == ocrc(oracle, 0, img[o + 36:o + sz].tobytes())
+    finally:
+        pin.free()

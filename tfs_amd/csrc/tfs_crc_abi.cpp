@@ -147,7 +147,7 @@ struct CompactSlot {
 constexpr int kCompactSlots = 8;          // slots allocated; ctx->compact_slots of them are used
 constexpr uint32_t kSchedSlots = 256;
 constexpr int kVariantUnfusedCompact = 7;  // TFS_CRC_VARIANT=7: two-pass device compaction (A/B baseline)
-constexpr int kVariantDmaCompact = 8;      // TFS_CRC_VARIANT=8: host compaction through whole-block DMA copies
+constexpr int kVariantDmaCompact = 8;      // TFS_CRC_VARIANT=8: whole-block DMA copies for host compaction / block verify
 
 }  // namespace
 
@@ -557,9 +557,19 @@ int tfs_block_verify(tfs_crc_ctx* ctx, const void* image, uint64_t image_len, co
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   Slot* s = free_slot(ctx);
   if (!s) return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "all %d slots busy", kSlots);
+  // A page-locked image is read in place (zero-copy): only the records the
+  // metas name cross PCIe -- a third of a fragmented block -- instead of a
+  // whole-block copy.  Pageable images are staged.
   const uint8_t* d_base = nullptr;
-  int rc = stage_span(ctx, *s, image, 0, image_len, &d_base);
-  if (rc) return rc;
+  void* zc = nullptr;
+  if (ctx->variant != kVariantDmaCompact && is_pinned_host(image) &&
+      hipHostGetDevicePointer(&zc, const_cast<void*>(image), 0) == hipSuccess) {
+    d_base = static_cast<const uint8_t*>(zc);
+  } else {
+    (void)hipGetLastError();
+    const int rc = stage_span(ctx, *s, image, 0, image_len, &d_base);
+    if (rc) return rc;
+  }
   HIP_TRY(ctx, s->d_desc.reserve(size_t(n) * sizeof(RawMeta)));
   HIP_TRY(ctx, s->d_crc.reserve(size_t(n) * 4));
   HIP_TRY(ctx, s->d_ok.reserve(size_t(n) * 4));
