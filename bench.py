@@ -426,15 +426,27 @@ def bench_zipf(args):
     ctx = crc.Context(local)
     nblocks = args.blocks
     blocks = zipf_sizes(42 + rank, nblocks)
+    # A/B knob (measurement only): TFS_BENCH_ZIPF_ALIGN=a places every payload
+    # at an a-byte boundary and trims its length to a multiple of a.
+    align = int(os.environ.get("TFS_BENCH_ZIPF_ALIGN", "0"))
     offs, lens = [], []
     for b, L in enumerate(blocks):
-        rec = np.concatenate([[0], np.cumsum(36 + L)[:-1]])
-        offs.append(b * (64 << 20) + rec + 36)
+        if align:
+            L = np.maximum(L // align * align, align)
+            o, po = b * (64 << 20), []
+            for x in L:
+                o = (o + 36 + align - 1) // align * align
+                po.append(o)
+                o += int(x)
+            offs.append(np.array(po, np.int64))
+        else:
+            rec = np.concatenate([[0], np.cumsum(36 + L)[:-1]])
+            offs.append(b * (64 << 20) + rec + 36)
         lens.append(L)
     offs = np.concatenate(offs).astype(np.uint64)
     lens = np.concatenate(lens).astype(np.uint32)
     n = len(lens)
-    total = nblocks * (64 << 20)
+    total = max(nblocks * (64 << 20), (int(offs[-1]) + int(lens[-1]) + 8191) // 4096 * 4096)
     img = crc.DeviceBuffer(ctx, total)
     ctx.synth_fill_device(img, total, 0xC0FFEE + rank, 0)
     desc = np.zeros(n, crc.DESC_DTYPE)
