@@ -1,0 +1,70 @@
+"""The read call site: LogicBlock::read_file (logic_block.cpp:374-440)
+as the harness restates it -- truncation, offset and meta errors, the FileInfo
+checks on the first fragment with the real flag -- and the verify-on-read hook
+the build adds behind DataManagement::read_data (data_management.cpp:238-268;
+the reference hands FileInfo.crc_ to the client unchecked, dataservice.cpp:1557)."""
+import numpy as np
+import pytest
+
+from conftest import ocrc
+from tfs_amd.synth import synth_bytes
+
+FI = 36
+
+
+@pytest.fixture(scope="module")
+def ds():
+    from tfs_amd import dataserver
+    dataserver.lib()
+    return dataserver
+
+
+def _block(ds, oracle, sizes):
+    b = ds.LogicBlock(9)
+    pays = []
+    for i, ln in enumerate(sizes):
+        p = synth_bytes(500 + i, ln).tobytes()
+        assert b.append(i + 1, p, ocrc(oracle, 0, p)) == 0
+        pays.append(p)
+    return b, pays
+
+
+def test_read_file_semantics(ds, oracle):
+    b, pays = _block(ds, oracle, [1000, 70001, 5])
+    raw = b.raw()
+    m, _ = b.metas()
+    rc, data = b.read_file(2, 70001 + FI)
+    o = int(m["offset"][1])
+    assert rc == 0 and data == raw[o:o + FI + 70001].tobytes()
+    rc, data = b.read_file(3, 1 << 20)                       # truncated to the record (:388-391)
+    assert rc == 0 and len(data) == FI + 5 and data[FI:] == pays[2]
+    rc, data = b.read_file(2, 4096, 100)                     # a later fragment: no FileInfo check
+    assert rc == 0 and data == raw[o + 100:o + 4196].tobytes()
+    assert b.read_file(2, 10, 70001 + FI + 1)[0] == -8002    # EXIT_READ_OFFSET_ERROR
+    assert b.read_file(77, 100)[0] == -8025                  # EXIT_META_NOT_FOUND_ERROR
+    assert b.set_flag(1, 1) == 0                             # FI_DELETED
+    assert b.read_file(1, 2000)[0] == -8016                  # EXIT_FILE_INFO_ERROR (normal read)
+    assert b.read_file(1, 2000, force=True)[0] == 0          # READ_DATA_OPTION_FLAG_FORCE
+    assert b.set_flag(1, 4) == 0                             # FI_CONCEAL
+    assert b.read_file(1, 2000)[0] == -8016
+    assert b.set_flag(1, 2) == 0                             # FI_INVALID rejects even a forced read
+    assert b.read_file(1, 2000, force=True)[0] == -8016
+    b.free()
+
+
+@pytest.mark.gpu
+def test_read_file_verified_on_gpu(gpu_ctx, ds, oracle):
+    b, pays = _block(ds, oracle, [65536, 3000, 0])
+    chk = ds.BlockCrcChecker(4)
+    rc, data = b.read_file_verified(gpu_ctx, 1, chk)
+    assert rc == 0 and data[FI:] == pays[0]
+    assert b.read_file_verified(gpu_ctx, 3, chk)[0] == 0     # empty payload: crc 0
+    m, _ = b.metas()
+    assert b.corrupt(int(m["offset"][1]) + FI + 17, 0x04) == 0
+    rc, data = b.read_file_verified(gpu_ctx, 2, chk)
+    assert rc == -1010 and chk.errors(9) == 1               # EXIT_CHECK_CRC_ERROR, reported to BlockChecker
+    assert data[FI:] != pays[1] and len(data) == FI + 3000
+    assert b.set_flag(1, 1) == 0
+    assert b.read_file_verified(gpu_ctx, 1, chk)[0] == -8016
+    chk.free()
+    b.free()

@@ -52,6 +52,8 @@ def lib():
             "tfs_ds_verify_block": (ctypes.c_int, [vp, vp, vp, u32, vp]),
             "tfs_ds_compact_block": (ctypes.c_int, [vp, vp, vp, vp, u32]),
             "tfs_ds_loopback_block": (ctypes.c_int, [vp, vp, u32, i32, vp, ctypes.c_int, vp]),
+            "tfs_ds_block_read_file": (ctypes.c_int, [vp, u64, vp, ctypes.POINTER(i32), i32, ctypes.c_int]),
+            "tfs_ds_read_file_verified": (ctypes.c_int, [vp, vp, u64, vp, i32, ctypes.POINTER(i32), vp]),
             "tfs_ds_encoder_new": (vp, [vp]),
             "tfs_ds_encoder_free": (None, [vp]),
             "tfs_ds_encoder_add": (None, [vp, ctypes.c_int16, ctypes.c_int16, u64, ctypes.c_char_p, i32]),
@@ -135,6 +137,21 @@ class LogicBlock:
         """Append FileInfo|payload with a caller-supplied crc (fixtures; no CRC computed)."""
         b = bytes(payload)
         return lib().tfs_ds_block_append(self.h, file_id, b, len(b), crc)
+
+    def read_file(self, file_id, nbytes, offset=0, force=False):
+        """LogicBlock::read_file (logic_block.cpp:374-440): returns (rc, bytes)."""
+        buf = np.zeros(max(nbytes, 1), np.uint8)
+        n = ctypes.c_int32(nbytes)
+        rc = lib().tfs_ds_block_read_file(self.h, file_id, buf.ctypes.data, ctypes.byref(n), offset, int(force))
+        return rc, buf[:max(n.value, 0)].tobytes()
+
+    def read_file_verified(self, ctx, file_id, checker=None, cap=1 << 24):
+        """read_data + GPU verify-on-read against FileInfo.crc_: returns (rc, FileInfo|payload)."""
+        buf = np.zeros(cap, np.uint8)
+        n = ctypes.c_int32(0)
+        rc = lib().tfs_ds_read_file_verified(ctx.handle, self.h, file_id, buf.ctypes.data, cap, ctypes.byref(n),
+                                             checker.h if checker else None)
+        return rc, buf[:min(max(n.value, 0), cap)].tobytes()
 
     def set_flag(self, file_id, flag):
         return lib().tfs_ds_block_set_flag(self.h, file_id, flag)

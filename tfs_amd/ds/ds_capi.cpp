@@ -2,6 +2,7 @@
 // can drive the write / close / verify / compact call sites the way the
 // reference's gtest programs drive LogicBlock/DataFile directly
 // (tests/dataserver/test_logic_block_and_compact.cpp).  Host C++ only.
+#include <algorithm>
 #include <atomic>
 #include <cstring>
 #include <string>
@@ -84,6 +85,22 @@ int tfs_ds_verify_block(tfs_crc_ctx* ctx, void* block, int32_t* status, uint32_t
   const int r = verify_block(ctx, *static_cast<LogicBlockImage*>(block), &st, static_cast<BlockCrcChecker*>(checker));
   for (size_t i = 0; i < st.size() && i < cap; ++i) status[i] = st[i];
   return r;
+}
+
+// LogicBlock::read_file (logic_block.cpp:374-440) into buf; *nbytes in/out.
+int tfs_ds_block_read_file(void* b, uint64_t file_id, char* buf, int32_t* nbytes, int32_t offset, int force) {
+  return static_cast<LogicBlockImage*>(b)->read_file(file_id, buf, nbytes, offset, force != 0);
+}
+
+// read_data of a whole file + the GPU verify-on-read hook; FileInfo|payload into buf (cap bytes).
+int tfs_ds_read_file_verified(tfs_crc_ctx* ctx, void* block, uint64_t file_id, char* buf, int32_t cap, int32_t* len,
+                              void* checker) {
+  std::vector<char> out;
+  const int rc = read_file_verified(ctx, *static_cast<LogicBlockImage*>(block), file_id, &out,
+                                    static_cast<BlockCrcChecker*>(checker));
+  *len = int32_t(out.size());
+  if (buf && !out.empty()) memcpy(buf, out.data(), std::min(out.size(), size_t(cap > 0 ? cap : 0)));
+  return rc;
 }
 
 int tfs_ds_compact_block(tfs_crc_ctx* ctx, void* src, void* dest, uint8_t* crc_ok, uint32_t cap) {

@@ -14,6 +14,8 @@ namespace dataserver {
 
 namespace {
 constexpr int32_t kFileInfoSize = TFS_FILEINFO_SIZE;
+constexpr int32_t kExitReadOffset = -8002;    // EXIT_READ_OFFSET_ERROR, error_msg.h:138
+constexpr int32_t kExitMetaNotFound = -8025;  // EXIT_META_NOT_FOUND_ERROR, error_msg.h:161
 
 void put_file_info(char* dst, const tfs_file_info& fi) { memcpy(dst, &fi, kFileInfoSize); }
 }  // namespace
@@ -151,6 +153,25 @@ int LogicBlockImage::read_file(uint64_t file_id, std::vector<char>& out) const {
   auto it = index_.find(file_id);
   if (it == index_.end()) return TFS_EXIT_FILE_INFO_ERROR;
   out.assign(data_.begin() + it->second.offset, data_.begin() + it->second.offset + it->second.size);
+  return TFS_SUCCESS;
+}
+
+int LogicBlockImage::read_file(uint64_t file_id, char* buf, int32_t* nbytes, int32_t offset, bool force) const {
+  auto it = index_.find(file_id);
+  if (it == index_.end()) return kExitMetaNotFound;
+  const tfs_raw_meta& m = it->second;
+  if (offset + *nbytes > m.size) *nbytes = m.size - offset;  // truncate to the record (:388-391)
+  if (*nbytes < 0) return kExitReadOffset;
+  if (int64_t(m.offset) + offset + *nbytes > int64_t(data_.size())) return TFS_EXIT_PARAMETER_ERROR;
+  memcpy(buf, data_.data() + m.offset + offset, size_t(*nbytes));
+  if (offset == 0) {  // :414-435
+    if (*nbytes < kFileInfoSize) return TFS_EXIT_READ_FILE_SIZE_ERROR;
+    tfs_file_info fi;
+    memcpy(&fi, buf, sizeof fi);
+    const int32_t real = flag_of(file_id);  // get_real_flag: the index keeps the unlink flag
+    const int32_t reject = force ? TFS_FI_INVALID : (TFS_FI_DELETED | TFS_FI_INVALID | TFS_FI_CONCEAL);
+    if (fi.id_ != file_id || (real & reject)) return TFS_EXIT_FILE_INFO_ERROR;
+  }
   return TFS_SUCCESS;
 }
 
@@ -307,6 +328,25 @@ void BlockCrcChecker::add_crc_error(uint32_t block_id, uint64_t file_id) {
 int BlockCrcChecker::crc_errors(uint32_t block_id) const {
   auto it = errors_.find(block_id);
   return it == errors_.end() ? 0 : it->second;
+}
+
+int read_file_verified(tfs_crc_ctx* ctx, const LogicBlockImage& block, uint64_t file_id, std::vector<char>* out,
+                       BlockCrcChecker* checker) {
+  std::vector<tfs_raw_meta> metas = block.sorted_metas();
+  int32_t size = -1;
+  for (auto& m : metas)
+    if (m.file_id == file_id) size = m.size;
+  if (size < 0) return kExitMetaNotFound;
+  out->assign(size_t(size), 0);
+  int32_t nbytes = size;
+  int rc = block.read_file(file_id, out->data(), &nbytes, 0, false);
+  if (rc != TFS_SUCCESS) return rc;
+  tfs_file_info fi;
+  memcpy(&fi, out->data(), sizeof fi);
+  const tfs_crc_vdesc d{uint64_t(kFileInfoSize), uint32_t(nbytes - kFileInfoSize), fi.crc_};
+  rc = tfs_crc32_verify(ctx, &d, 1, out->data(), uint64_t(nbytes), nullptr, nullptr, nullptr);
+  if (rc == TFS_EXIT_CHECK_CRC_ERROR && checker) checker->add_crc_error(block.block_id(), file_id);
+  return rc;
 }
 
 int verify_block(tfs_crc_ctx* ctx, const LogicBlockImage& block, std::vector<int32_t>* status,

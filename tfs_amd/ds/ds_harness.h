@@ -81,6 +81,11 @@ class LogicBlockImage {
   int append_record(uint64_t file_id, const char* payload, int32_t len, uint32_t crc);
   // LogicBlock::read_file at offset 0 (logic_block.cpp:374-440): FileInfo|payload.
   int read_file(uint64_t file_id, std::vector<char>& out) const;
+  // The full read of logic_block.cpp:374-440: *nbytes truncated to the record,
+  // EXIT_META_NOT_FOUND_ERROR / EXIT_READ_OFFSET_ERROR, and on the first
+  // fragment the FileInfo checks (id, real flag: FI_DELETED|FI_INVALID|
+  // FI_CONCEAL rejected, only FI_INVALID with `force`) -> EXIT_FILE_INFO_ERROR.
+  int read_file(uint64_t file_id, char* buf, int32_t* nbytes, int32_t offset, bool force) const;
   int set_flag(uint64_t file_id, int32_t flag);
   int32_t flag_of(uint64_t file_id) const;
   // index in offset order (traverse_sorted_segment_meta, index_handle.cpp:870-878)
@@ -153,6 +158,15 @@ class BlockCrcChecker {
   std::map<uint32_t, int> errors_;
   std::vector<std::pair<uint32_t, uint64_t>> repair_;
 };
+
+// DataManagement::read_data (data_management.cpp:238-268) of a whole file plus
+// the verify-on-read hook the build adds at this call site (the reference
+// returns FileInfo.crc_ to the client unchecked, dataservice.cpp:1557): the
+// payload is re-CRC'd on the GPU against FileInfo.crc_; a mismatch returns
+// EXIT_CHECK_CRC_ERROR and is reported to `checker` (may be NULL).  `out`
+// receives FileInfo|payload either way.
+int read_file_verified(tfs_crc_ctx* ctx, const LogicBlockImage& block, uint64_t file_id, std::vector<char>* out,
+                       BlockCrcChecker* checker);
 
 // Verify-on-read of every live file of a block (one GPU batch); per-file status
 // as sync_backup.cpp:419-435 / block_console.cpp:543-577.  Mismatches are
