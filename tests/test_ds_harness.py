@@ -228,3 +228,44 @@ def test_loopback_block_like_config1(gpu_ctx, ds, oracle):
         assert fi["crc_"] == client[i]
         assert raw[int(m["offset"]) + FILEINFO:int(m["offset"]) + FILEINFO + L].tobytes() == pay[i * L:(i + 1) * L].tobytes()
     blk.free()
+
+
+def test_recombine_block_skips_bad_crc(gpu_ctx, ds, oracle):
+    """TranBlock::recombine_data (tools/transfer/block_console.cpp:502-613): deleted and
+    invalid files are skipped, a FileInfo that disagrees with the index is skipped (:543),
+    a payload whose CRC != crc_ is skipped (:569-577), concealed files are kept with their
+    flag, and the survivors are repacked with offsets rewritten."""
+    src = ds.LogicBlock(900)
+    rng = np.random.default_rng(902)
+    pays = {}
+    for fid in range(1, 21):
+        p = rng.integers(0, 256, int(rng.integers(0, 70000)), dtype=np.uint8).tobytes()
+        pays[fid] = p
+        assert src.append(fid, p, ocrc(oracle, 0, p)) == 0
+    m, _ = src.metas()
+    off = {int(x["file_id"]): int(x["offset"]) for x in m}
+    assert src.set_flag(3, 1) == 0          # FI_DELETED
+    assert src.set_flag(4, 2) == 0          # FI_INVALID
+    assert src.set_flag(5, 4) == 0          # FI_CONCEAL: kept
+    big = [f for f in (7, 11, 16) if len(pays[f]) > 0]
+    for f in big:                           # payload corruption -> skipped for its CRC
+        src.corrupt(off[f] + FILEINFO + len(pays[f]) // 2, 0x20)
+    src.corrupt(off[9], 0x01)               # FileInfo id_ disagrees with the index
+    dest = ds.LogicBlock(901)
+    rc, nskip = ds.recombine_block(gpu_ctx, src, dest)
+    assert rc == 0 and nskip == len(big)
+    keep = [f for f in range(1, 21) if f not in (3, 4, 9) and f not in big]
+    dm, df = dest.metas()
+    assert [int(x) for x in dm["file_id"]] == keep
+    assert [int(x) for x in df] == [4 if f == 5 else 0 for f in keep]
+    raw = dest.raw()
+    o = 0
+    for f in keep:
+        fi = _file_info(raw, o)
+        assert fi["id_"] == f and fi["offset_"] == o and fi["size_"] == FILEINFO + len(pays[f])
+        assert raw[o + FILEINFO:o + fi["size_"]].tobytes() == pays[f]
+        assert fi["crc_"] == ocrc(oracle, 0, pays[f])
+        o += int(fi["size_"])
+    assert o == raw.size
+    nbad, _ = ds.verify_block(gpu_ctx, dest)
+    assert nbad == 0

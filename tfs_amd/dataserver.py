@@ -53,6 +53,7 @@ def lib():
             "tfs_ds_compact_block": (ctypes.c_int, [vp, vp, vp, vp, u32]),
             "tfs_ds_loopback_block": (ctypes.c_int, [vp, vp, u32, i32, vp, ctypes.c_int, vp]),
             "tfs_ds_block_read_file": (ctypes.c_int, [vp, u64, vp, ctypes.POINTER(i32), i32, ctypes.c_int]),
+            "tfs_ds_recombine_block": (ctypes.c_int, [vp, vp, vp, ctypes.POINTER(ctypes.c_int)]),
             "tfs_ds_read_file_verified": (ctypes.c_int, [vp, vp, u64, vp, i32, ctypes.POINTER(i32), vp]),
             "tfs_ds_encoder_new": (vp, [vp]),
             "tfs_ds_encoder_free": (None, [vp]),
@@ -347,3 +348,10 @@ def loopback_block(ctx, payloads, n, length, client_crc, nthreads, block):
     if p.size < n * length or c.size < n:
         raise ValueError("payloads/client_crc too small")
     return lib().tfs_ds_loopback_block(ctx.handle, p.ctypes.data, n, length, c.ctypes.data, nthreads, block.h)
+
+
+def recombine_block(ctx, src, dest):
+    """TranBlock::recombine_data over the GPU: returns (rc, files skipped for their CRC)."""
+    k = ctypes.c_int(0)
+    rc = lib().tfs_ds_recombine_block(ctx.handle, src.h, dest.h, ctypes.byref(k))
+    return rc, k.value

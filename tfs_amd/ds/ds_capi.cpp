@@ -87,6 +87,10 @@ int tfs_ds_verify_block(tfs_crc_ctx* ctx, void* block, int32_t* status, uint32_t
   return r;
 }
 
+int tfs_ds_recombine_block(tfs_crc_ctx* ctx, void* src, void* dest, int* skipped_crc) {
+  return recombine_block(ctx, *static_cast<LogicBlockImage*>(src), *static_cast<LogicBlockImage*>(dest), skipped_crc);
+}
+
 // LogicBlock::read_file (logic_block.cpp:374-440) into buf; *nbytes in/out.
 int tfs_ds_block_read_file(void* b, uint64_t file_id, char* buf, int32_t* nbytes, int32_t offset, int force) {
   return static_cast<LogicBlockImage*>(b)->read_file(file_id, buf, nbytes, offset, force != 0);

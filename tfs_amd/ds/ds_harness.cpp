@@ -367,6 +367,59 @@ int verify_block(tfs_crc_ctx* ctx, const LogicBlockImage& block, std::vector<int
   return int(nbad);
 }
 
+int recombine_block(tfs_crc_ctx* ctx, const LogicBlockImage& src, LogicBlockImage& dest, int* skipped_crc) {
+  const std::vector<tfs_raw_meta> metas = src.sorted_metas();
+  std::vector<int32_t> flags = src.sorted_flags();
+  std::vector<tfs_raw_meta> check;
+  std::vector<size_t> where;
+  for (size_t i = 0; i < metas.size(); ++i) {
+    if ((flags[i] & (TFS_FI_DELETED | TFS_FI_INVALID)) || metas[i].file_id == 0) {
+      flags[i] |= TFS_FI_INVALID;
+      continue;
+    }
+    uint32_t id_lo = 0;  // memcmp(&finfo, data_finfo, sizeof(FILEINFO_SIZE)): 4 bytes
+    if (metas[i].offset < 0 || int64_t(metas[i].offset) + kFileInfoSize > src.data_size()) {
+      flags[i] |= TFS_FI_INVALID;
+      continue;
+    }
+    memcpy(&id_lo, src.data().data() + metas[i].offset, 4);
+    if (id_lo != uint32_t(metas[i].file_id)) {
+      flags[i] |= TFS_FI_INVALID;
+      continue;
+    }
+    check.push_back(metas[i]);
+    where.push_back(i);
+  }
+  std::vector<int32_t> st(check.size());
+  uint32_t nbad = 0;
+  int rc = tfs_block_verify(ctx, src.data().data(), uint64_t(src.data_size()), check.data(), uint32_t(check.size()),
+                            nullptr, st.data(), &nbad);
+  if (rc != TFS_SUCCESS && rc != TFS_EXIT_CHECK_CRC_ERROR) return rc;
+  int dropped = 0;
+  for (size_t k = 0; k < check.size(); ++k) {
+    if (st[k] == TFS_SUCCESS) continue;
+    dropped += st[k] == TFS_EXIT_CHECK_CRC_ERROR ? 1 : 0;
+    flags[where[k]] |= TFS_FI_INVALID;  // not copied
+  }
+  if (skipped_crc) *skipped_crc = dropped;
+  uint64_t cap = 16;
+  for (auto& m : metas) cap += uint64_t(m.size);
+  std::vector<char> out(static_cast<size_t>(cap));
+  std::vector<tfs_raw_meta> dmetas(metas.size());
+  uint64_t dlen = 0;
+  uint32_t nlive = 0;
+  rc = tfs_block_compact(ctx, src.data().data(), uint64_t(src.data_size()), metas.data(), flags.data(),
+                         uint32_t(metas.size()), out.data(), cap, dmetas.data(), nullptr, &dlen, &nlive);
+  if (rc != TFS_SUCCESS) return rc;  // every survivor was verified: a mismatch here is an error
+  out.resize(size_t(dlen));
+  dmetas.resize(nlive);
+  std::vector<int32_t> dflags;
+  for (size_t i = 0; i < metas.size(); ++i)
+    if (!(flags[i] & (TFS_FI_DELETED | TFS_FI_INVALID))) dflags.push_back(flags[i]);
+  dest.replace(std::move(out), dmetas, dflags);
+  return TFS_SUCCESS;
+}
+
 int compact_block(tfs_crc_ctx* ctx, const LogicBlockImage& src, LogicBlockImage& dest, std::vector<uint8_t>* crc_ok) {
   const std::vector<tfs_raw_meta> metas = src.sorted_metas();
   const std::vector<int32_t> flags = src.sorted_flags();

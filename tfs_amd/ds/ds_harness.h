@@ -174,6 +174,16 @@ int read_file_verified(tfs_crc_ctx* ctx, const LogicBlockImage& block, uint64_t 
 int verify_block(tfs_crc_ctx* ctx, const LogicBlockImage& block, std::vector<int32_t>* status,
                  BlockCrcChecker* checker);
 
+// TranBlock::recombine_data (tools/transfer/block_console.cpp:502-613): every file
+// of `src` in offset order, skipping FI_DELETED|FI_INVALID, id 0 (:534-539), a
+// stored FileInfo that disagrees with the index entry (:543; the tool compares
+// sizeof(FILEINFO_SIZE) = 4 bytes, the low half of id_) and a payload whose CRC
+// is not crc_ (:569-577); the rest is repacked with offset_/size_/usize_
+// rewritten and flag_ kept (FI_CONCEAL survives, :526-531,587).  One GPU verify,
+// then the fused compaction pass over the survivors.  *skipped_crc: files
+// dropped for their CRC.  Returns TFS_SUCCESS or a negative code.
+int recombine_block(tfs_crc_ctx* ctx, const LogicBlockImage& src, LogicBlockImage& dest, int* skipped_crc);
+
 // CompactTask::real_compact with re-CRC (task.cpp:713-836): dest receives the
 // live files repacked; crc_ok per source file (1 ok / 0 mismatch / 2 skipped).
 int compact_block(tfs_crc_ctx* ctx, const LogicBlockImage& src, LogicBlockImage& dest, std::vector<uint8_t>* crc_ok);
