@@ -263,6 +263,7 @@ def test_recombine_block_skips_bad_crc(gpu_ctx, ds, oracle):
     for f in keep:
         fi = _file_info(raw, o)
         assert fi["id_"] == f and fi["offset_"] == o and fi["size_"] == FILEINFO + len(pays[f])
+        assert fi["flag_"] == (4 if f == 5 else 0)      # new_info.flag_ = finfo.flag_ (:587)
         assert raw[o + FILEINFO:o + fi["size_"]].tobytes() == pays[f]
         assert fi["crc_"] == ocrc(oracle, 0, pays[f])
         o += int(fi["size_"])
