@@ -1127,6 +1127,20 @@ def bench_loopback(args):
         if bad:
             raise SystemExit("loopback: bad files (64 threads)")
     el64 = time.perf_counter() - t1
+    # phase breakdown: the whole-block verify alone, and the appends alone (no CRC)
+    bad, blk = gpu_once()
+    t2 = time.perf_counter()
+    for _ in range(reps):
+        ds.verify_block(ctx, blk)
+    verify_ms = (time.perf_counter() - t2) / reps * 1e3
+    blk.free()
+    t3 = time.perf_counter()
+    for _ in range(reps):
+        b2 = ds.LogicBlock(2)
+        for i in range(n):
+            b2.append(i + 1, memoryview(pay)[i * L:(i + 1) * L], int(client[i]))
+        b2.free()
+    append_ms = (time.perf_counter() - t3) / reps * 1e3
     res = {
         "metric": "GiB/s payload written + verified, single-process loopback of one 64 MiB block (BASELINE configs[0])",
         "value": world * reps * n * L / el / 2**30, "unit": "GiB/s", "n_gpus": world, "steps": reps, "warmup": 1,
@@ -1136,6 +1150,7 @@ def bench_loopback(args):
                                "FileInfo|payload append; then verify_block of the whole block",
                    "files": n, "file_size": L},
         "threads64_GiBs": reps * n * L / el64 / 2**30,
+        "phases_ms": {"verify_block": verify_ms, "append_only_python": append_ms},
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         secs = min(args.cpu_seconds, 10.0)

@@ -549,3 +549,46 @@ def test_block_verify_zero_copy_pinned_image(gpu_ctx, oracle):
             assert int(c1[i]) == ocrc(oracle, 0, img[o + 36:o + sz].tobytes())
     finally:
         pin.free()
+
+
+def test_small_pinned_batches_read_in_place(gpu_ctx, oracle):
+    """tfs_crc32_verify / tfs_crc32_batch / submit+wait on a page-locked buffer whose
+    span is <= 8 MiB run as one zero-copy launch (payloads, descriptors and verdicts in
+    host memory, n_bad counted from the verdicts): same results as the staged pageable
+    path and the oracle, ragged and empty files, several slots in flight."""
+    import tfs_amd.crc as crc
+    rng = np.random.default_rng(77)
+    n = 300
+    lens = rng.integers(0, 40000, n).astype(np.uint32)
+    lens[:5] = [0, 1, 3, 4, 65536]
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + rng.integers(0, 7, n - 1).astype(np.uint64))
+    size = int(offs[-1] + lens[-1]) + 16
+    assert size <= 8 << 20
+    data = rng.integers(0, 256, size, dtype=np.uint8)
+    exp = np.array([ocrc(oracle, 0, data[int(o):int(o) + int(l)].tobytes()) for o, l in zip(offs, lens)], np.uint32)
+    bad = np.array([7, 100, 299])
+    expected = exp.copy()
+    expected[bad] ^= 1
+    seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    pin = crc.PinnedBuffer(gpu_ctx, size)
+    try:
+        pin.array[:] = data
+        c1, ok1, nb1, rc1 = gpu_ctx.verify(pin.array, offs, lens, expected)
+        c2, ok2, nb2, rc2 = gpu_ctx.verify(data.copy(), offs, lens, expected)
+        assert (c1 == exp).all() and (c2 == exp).all()
+        assert (ok1 == ok2).all() and nb1 == nb2 == len(bad) and rc1 == rc2 == -1010
+        assert (ok1[bad] == 0).all() and ok1.sum() == n - len(bad)
+        c3, ok3, nb3, rc3 = gpu_ctx.verify(pin.array, offs, lens, exp)
+        assert nb3 == 0 and rc3 == 0 and ok3.all()
+        s1 = gpu_ctx.batch(pin.array, offs, lens, seeds)
+        s2 = gpu_ctx.batch(data.copy(), offs, lens, seeds)
+        assert (s1 == s2).all()
+        for i in (0, 1, 4, 150):
+            assert int(s1[i]) == ocrc(oracle, int(seeds[i]), data[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes())
+        hs = [gpu_ctx.submit_verify(pin.array, offs[k::3], lens[k::3], expected[k::3]) for k in range(3)]
+        for k, h in enumerate(hs):
+            c, ok, nb, rc = gpu_ctx.wait(h)
+            assert (c == exp[k::3]).all() and nb == int((ok == 0).sum()) == int(np.isin(np.arange(n)[k::3], bad).sum())
+    finally:
+        pin.free()

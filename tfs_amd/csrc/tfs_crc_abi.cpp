@@ -107,11 +107,12 @@ struct PinBuf {
 // One in-flight host-memory submission (async API) or the scratch of a sync call.
 struct Slot {
   DevBuf d_data, d_desc, d_crc, d_ok, d_bad, d_aux;
-  PinBuf h_data, h_crc, h_ok, h_bad;
+  PinBuf h_data, h_crc, h_ok, h_bad, h_desc;
   hipEvent_t done = nullptr;
   bool busy = false;
   uint64_t ticket = 0;
   int status = TFS_SUCCESS;
+  bool count_bad = false;  // zero-copy launch: n_bad is counted from h_ok
   // user outputs for the async path
   uint32_t n = 0;
   uint32_t* out_crc = nullptr;
@@ -119,7 +120,7 @@ struct Slot {
   uint32_t* n_bad = nullptr;
   void release() {
     d_data.release(); d_desc.release(); d_crc.release(); d_ok.release(); d_bad.release(); d_aux.release();
-    h_data.release(); h_crc.release(); h_ok.release(); h_bad.release();
+    h_data.release(); h_crc.release(); h_ok.release(); h_bad.release(); h_desc.release();
     if (done) (void)hipEventDestroy(done);
     done = nullptr;
   }
@@ -147,7 +148,8 @@ struct CompactSlot {
 constexpr int kCompactSlots = 8;          // slots allocated; ctx->compact_slots of them are used
 constexpr uint32_t kSchedSlots = 256;
 constexpr int kVariantUnfusedCompact = 7;  // TFS_CRC_VARIANT=7: two-pass device compaction (A/B baseline)
-constexpr int kVariantDmaCompact = 8;      // TFS_CRC_VARIANT=8: whole-block DMA copies for host compaction / block verify
+constexpr int kVariantDmaCompact = 8;      // TFS_CRC_VARIANT=8: DMA staging for host compaction / block verify / small batches
+constexpr uint64_t kZeroCopySpan = 8ull << 20;  // page-locked batches up to this span are read in place
 
 }  // namespace
 
@@ -271,6 +273,34 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
   if (!span_of(dd, n, base_len, &lo, &hi))
     return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "descriptor range exceeds base_len %llu",
                    (unsigned long long)base_len);
+  HIP_TRY(ctx, s.h_crc.reserve(size_t(n) * 4));
+  HIP_TRY(ctx, s.h_ok.reserve(n));
+  HIP_TRY(ctx, s.h_bad.reserve(4));
+  if (!s.done) HIP_TRY(ctx, hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+  // A small batch in page-locked memory (a CloseBatcher batch, one file read): the
+  // kernel reads payloads and descriptors and writes its verdicts in host memory,
+  // one launch instead of H2D + launch + three D2H.  Such calls are latency-bound.
+  if (ctx->variant != kVariantDmaCompact && hi - lo <= kZeroCopySpan && is_pinned_host(base)) {
+    HIP_TRY(ctx, s.h_desc.reserve(size_t(n) * sizeof(Desc)));
+    memcpy(s.h_desc.p, d, size_t(n) * sizeof(Desc));
+    void *zb = nullptr, *zd = nullptr, *zcrc = nullptr, *zok = nullptr;
+    if (hipHostGetDevicePointer(&zb, const_cast<void*>(base), 0) == hipSuccess &&
+        hipHostGetDevicePointer(&zd, s.h_desc.p, 0) == hipSuccess &&
+        hipHostGetDevicePointer(&zcrc, s.h_crc.p, 0) == hipSuccess &&
+        hipHostGetDevicePointer(&zok, s.h_ok.p, 0) == hipSuccess) {
+      uint32_t* sched = nullptr;
+      HIP_TRY(ctx, sched_slot(ctx, ctx->stream, &sched));
+      // n_bad is counted from the verdicts on the host (no atomics on host memory)
+      HIP_TRY(ctx, launch_crc_files(mode, static_cast<const uint8_t*>(zb), static_cast<const Desc*>(zd), n,
+                                    ctx->d_tables, static_cast<uint32_t*>(zcrc), static_cast<uint8_t*>(zok),
+                                    nullptr, sched, ctx->stream, ctx->variant, 0u));
+      HIP_TRY(ctx, hipEventRecord(s.done, ctx->stream));
+      s.count_bad = true;
+      return TFS_SUCCESS;
+    }
+    (void)hipGetLastError();  // not mappable: stage it
+  }
+  s.count_bad = false;
   const uint8_t* d_base = nullptr;
   int rc = stage_span(ctx, s, base, lo, hi, &d_base);
   if (rc) return rc;
@@ -304,6 +334,12 @@ int finish_slot(tfs_crc_ctx* ctx, Slot& s, int mode, uint32_t n, uint32_t* out_c
                 uint32_t* n_bad) {
   HIP_TRY(ctx, hipEventSynchronize(s.done));
   if (out_crc && n) memcpy(out_crc, s.h_crc.p, size_t(n) * 4);
+  if (mode == 1 && s.count_bad) {
+    const uint8_t* ok = static_cast<const uint8_t*>(s.h_ok.p);
+    uint32_t bad = 0;
+    for (uint32_t i = 0; i < n; ++i) bad += ok[i] ? 0u : 1u;
+    *static_cast<uint32_t*>(s.h_bad.p) = bad;
+  }
   if (mode == 1) {
     if (out_ok && n) memcpy(out_ok, s.h_ok.p, n);
     const uint32_t bad = n ? *static_cast<uint32_t*>(s.h_bad.p) : 0u;

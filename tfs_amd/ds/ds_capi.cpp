@@ -4,6 +4,10 @@
 // (tests/dataserver/test_logic_block_and_compact.cpp).  Host C++ only.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <memory>
 #include <cstring>
 #include <string>
 
@@ -127,23 +131,41 @@ int tfs_ds_loopback_block(tfs_crc_ctx* ctx, const char* payloads, uint32_t n, in
   if (!ctx || !block || len < 0 || (n && (!payloads || !client_crc))) return TFS_EXIT_PARAMETER_ERROR;
   LogicBlockImage& blk = *static_cast<LogicBlockImage*>(block);
   if (nthreads < 1) nthreads = 1;
+  blk.reserve(blk.data_size() + int64_t(n) * (int64_t(len) + TFS_FILEINFO_SIZE));
   std::atomic<int> bad{0}, err{0};
+  // TFS_DS_TRACE=1: per-phase thread-time totals on stderr (diagnostics only)
+  const bool trace = getenv("TFS_DS_TRACE") != nullptr;
+  std::atomic<int64_t> t_new{0}, t_set{0}, t_close{0}, t_free{0};
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto us = [](auto a, auto b) { return int64_t(std::chrono::duration_cast<std::chrono::microseconds>(b - a).count()); };
+  const auto t_begin = now();
   {
     CloseBatcher batcher(ctx, size_t(nthreads), 100);
     std::vector<std::thread> workers;
     for (int t = 0; t < nthreads; ++t)
       workers.emplace_back([&, t] {
         for (uint32_t i = uint32_t(t); i < n; i += uint32_t(nthreads)) {
-          DataFile df(i + 1, "/tmp", ctx);
-          if (df.set_data(payloads + size_t(i) * size_t(len), len, 0) < 0) {
+          const auto t0 = now();
+          std::unique_ptr<DataFile> df(new DataFile(i + 1, "/tmp", ctx));
+          const auto t1 = now();
+          if (df->set_data(payloads + size_t(i) * size_t(len), len, 0) < 0) {
             err = TFS_EXIT_PARAMETER_ERROR;
             continue;
           }
+          const auto t2 = now();
           CloseFileInfo info;
           info.block_id_ = blk.block_id();
           info.file_id_ = i + 1;
           info.crc_ = client_crc[i];
-          const int rc = batcher.close(info, df, blk);
+          const int rc = batcher.close(info, *df, blk);
+          const auto t3 = now();
+          df.reset();
+          if (trace) {
+            t_new += us(t0, t1);
+            t_set += us(t1, t2);
+            t_close += us(t2, t3);
+            t_free += us(t3, now());
+          }
           if (rc == TFS_EXIT_DATA_FILE_ERROR) ++bad;
           else if (rc != TFS_SUCCESS) err = rc;
         }
@@ -151,7 +173,12 @@ int tfs_ds_loopback_block(tfs_crc_ctx* ctx, const char* payloads, uint32_t n, in
     for (auto& w : workers) w.join();
   }
   if (err.load() != 0) return err.load();
+  const auto t_writes = now();
   const int nb = verify_block(ctx, blk, nullptr, nullptr);
+  if (trace)
+    fprintf(stderr, "loopback trace: writes %lld us wall, verify %lld us; thread-us new %lld set %lld close %lld free %lld\n",
+            (long long)us(t_begin, t_writes), (long long)us(t_writes, now()), (long long)t_new.load(),
+            (long long)t_set.load(), (long long)t_close.load(), (long long)t_free.load());
   return nb < 0 ? nb : bad.load() + nb;
 }
 

@@ -2,10 +2,12 @@
 #include "ds_harness.h"
 
 #include <fcntl.h>
+#include <sys/mman.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <ctime>
 
@@ -117,28 +119,42 @@ LogicBlockImage::LogicBlockImage(uint32_t block_id, int64_t capacity) : block_id
 
 int LogicBlockImage::append_record(uint64_t file_id, const char* payload, int32_t len, uint32_t crc) {
   if (len < 0) return TFS_EXIT_PARAMETER_ERROR;
-  const int64_t off = int64_t(data_.size());
   tfs_file_info fi;
   memset(&fi, 0, sizeof fi);
   fi.id_ = file_id;
-  fi.offset_ = int32_t(off);
   fi.size_ = len + kFileInfoSize;   // logic_block.cpp:173
   fi.usize_ = fi.size_;             // :235
   fi.modify_time_ = int32_t(time(nullptr));
   fi.create_time_ = fi.modify_time_;
   fi.flag_ = 0;
   fi.crc_ = crc;                    // :177
-  data_.resize(size_t(off + fi.size_));
+  int64_t off;
+  {
+    std::unique_lock<std::shared_mutex> g(mu_);
+    off = int64_t(data_.size());
+    fi.offset_ = int32_t(off);
+    data_.resize(size_t(off + fi.size_));  // moves the image only when past the reservation
+    index_[file_id] = tfs_raw_meta{file_id, int32_t(off), fi.size_};
+    flags_[file_id] = 0;
+  }
+  std::shared_lock<std::shared_mutex> g(mu_);
   put_file_info(data_.data() + off, fi);
   if (len) memcpy(data_.data() + off + kFileInfoSize, payload, size_t(len));
-  index_[file_id] = tfs_raw_meta{file_id, int32_t(off), fi.size_};
-  flags_[file_id] = 0;
   return TFS_SUCCESS;
+}
+
+void LogicBlockImage::reserve(int64_t bytes) {
+  std::unique_lock<std::shared_mutex> g(mu_);
+  if (bytes <= int64_t(data_.capacity())) return;
+  data_.reserve(size_t(bytes));
+  const uintptr_t a = (reinterpret_cast<uintptr_t>(data_.data()) + (2u << 20) - 1) & ~uintptr_t((2u << 20) - 1);
+  const uintptr_t e = (reinterpret_cast<uintptr_t>(data_.data()) + data_.capacity()) & ~uintptr_t((2u << 20) - 1);
+  if (e > a) madvise(reinterpret_cast<void*>(a), e - a, MADV_HUGEPAGE);  // advisory; failure is harmless
 }
 
 int LogicBlockImage::close_write_file(uint64_t file_id, DataFile& df, uint32_t crc) {
   const int32_t file_size = df.get_length();
-  if (int64_t(data_.size()) + file_size + kFileInfoSize > capacity_) return TFS_EXIT_PARAMETER_ERROR;
+  if (data_size() + file_size + kFileInfoSize > capacity_) return TFS_EXIT_PARAMETER_ERROR;
   std::vector<char> payload(static_cast<size_t>(file_size));
   int32_t off = 0;
   while (off < file_size) {  // logic_block.cpp:258-306: drain the DataFile
@@ -201,7 +217,7 @@ std::vector<int32_t> LogicBlockImage::sorted_flags() const {
   return f;
 }
 
-void LogicBlockImage::replace(std::vector<char>&& data, const std::vector<tfs_raw_meta>& metas,
+void LogicBlockImage::replace(ByteImage&& data, const std::vector<tfs_raw_meta>& metas,
                               const std::vector<int32_t>& flags) {
   data_ = std::move(data);
   index_.clear();
@@ -232,6 +248,9 @@ CloseBatcher::~CloseBatcher() {
   cv_.notify_all();
   worker_.join();
   if (gather_) tfs_crc32_host_free_pinned(ctx_, gather_);
+  if (getenv("TFS_DS_TRACE"))
+    fprintf(stderr, "close batcher: %llu batches, gather %lld us, verify %lld us\n", (unsigned long long)batches_,
+            (long long)gather_us_, (long long)verify_us_);
 }
 
 int CloseBatcher::close(const CloseFileInfo& info, DataFile& df, LogicBlockImage& block) {
@@ -239,11 +258,17 @@ int CloseBatcher::close(const CloseFileInfo& info, DataFile& df, LogicBlockImage
   r.info = &info;
   r.df = &df;
   r.block = &block;
-  std::unique_lock<std::mutex> lk(mu_);
-  queue_.push_back(&r);
-  if (queue_.size() >= max_batch_) cv_.notify_all();
-  done_cv_.wait(lk, [&] { return r.done; });
-  return r.status;
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    queue_.push_back(&r);
+    if (queue_.size() >= max_batch_) cv_.notify_all();
+    done_cv_.wait(lk, [&] { return r.done; });
+  }
+  if (r.status != kAppend) return r.status;
+  // Checked: persist from this thread (LogicBlock::close_write_file runs on the
+  // worker, logic_block.cpp:156-372), so the appends of a batch run side by side.
+  if (const char* p = df.in_memory_payload()) return block.append_record(info.file_id_, p, df.get_length(), r.crc);
+  return block.close_write_file(info.file_id_, df, r.crc);
 }
 
 void CloseBatcher::run() {
@@ -268,6 +293,7 @@ void CloseBatcher::run() {
 void CloseBatcher::flush(std::vector<Req*>& reqs) {
   // Gather every payload into one buffer, one GPU verify for the whole batch
   // (expected = the client's CloseFileInfo.crc_).
+  const auto t0 = std::chrono::steady_clock::now();
   std::vector<tfs_crc_vdesc> d(reqs.size());
   uint64_t total = 0;
   for (size_t i = 0; i < reqs.size(); ++i) total += uint64_t(reqs[i]->df->get_length());
@@ -304,8 +330,12 @@ void CloseBatcher::flush(std::vector<Req*>& reqs) {
   std::vector<uint32_t> crc(reqs.size());
   std::vector<uint8_t> ok(reqs.size());
   uint32_t nbad = 0;
+  const auto t1 = std::chrono::steady_clock::now();
   const int rc = tfs_crc32_verify(ctx_, d.data(), uint32_t(reqs.size()), gathered, total, crc.data(), ok.data(),
                                   &nbad);
+  const auto t2 = std::chrono::steady_clock::now();
+  gather_us_ += std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count();
+  verify_us_ += std::chrono::duration_cast<std::chrono::microseconds>(t2 - t1).count();
   for (size_t i = 0; i < reqs.size(); ++i) {
     Req& r = *reqs[i];
     if (rc != TFS_SUCCESS && rc != TFS_EXIT_CHECK_CRC_ERROR) {
@@ -313,7 +343,8 @@ void CloseBatcher::flush(std::vector<Req*>& reqs) {
     } else if (!ok[i]) {
       r.status = TFS_EXIT_DATA_FILE_ERROR;  // data_management.cpp:198
     } else {
-      r.status = r.block->append_record(r.info->file_id_, gathered + d[i].offset, int32_t(d[i].len), crc[i]);
+      r.status = kAppend;
+      r.crc = crc[i];
     }
   }
 }
@@ -404,7 +435,7 @@ int recombine_block(tfs_crc_ctx* ctx, const LogicBlockImage& src, LogicBlockImag
   if (skipped_crc) *skipped_crc = dropped;
   uint64_t cap = 16;
   for (auto& m : metas) cap += uint64_t(m.size);
-  std::vector<char> out(static_cast<size_t>(cap));
+  ByteImage out(static_cast<size_t>(cap));
   std::vector<tfs_raw_meta> dmetas(metas.size());
   uint64_t dlen = 0;
   uint32_t nlive = 0;
@@ -425,7 +456,7 @@ int compact_block(tfs_crc_ctx* ctx, const LogicBlockImage& src, LogicBlockImage&
   const std::vector<int32_t> flags = src.sorted_flags();
   uint64_t cap = 16;
   for (auto& m : metas) cap += uint64_t(m.size);
-  std::vector<char> out(static_cast<size_t>(cap));
+  ByteImage out(static_cast<size_t>(cap));
   std::vector<tfs_raw_meta> dmetas(metas.size());
   std::vector<uint8_t> ok(metas.size());
   uint64_t dlen = 0;

@@ -18,8 +18,10 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "../../include/tfs_crc.h"
@@ -50,6 +52,8 @@ class DataFile {
   int last_status() const { return status_; }
   void set_over();
   const char* buffer() const { return data_.get(); }
+  // The staged payload when it never spilled to the tmp file (length <= 2 MiB).
+  const char* in_memory_payload() const { return fd_ == -1 ? data_.get() : nullptr; }
 
  private:
   int32_t length_ = 0;
@@ -71,6 +75,28 @@ struct CloseFileInfo {  // internal.h:716-726
 
 // The logical data area of one block (main + extension blocks stitched, as
 // DataHandle presents them: data_handle.cpp:103-141) plus its index.
+// Block bytes: a vector whose growth does not zero-fill (every byte below size()
+// belongs to a record that its writer fills), so appends touch each page once.
+template <typename T>
+struct DefaultInitAlloc : std::allocator<T> {
+  template <typename U>
+  struct rebind {
+    using other = DefaultInitAlloc<U>;
+  };
+  DefaultInitAlloc() = default;
+  template <typename U>
+  DefaultInitAlloc(const DefaultInitAlloc<U>&) noexcept {}
+  template <typename U>
+  void construct(U* p) noexcept {
+    ::new (static_cast<void*>(p)) U;
+  }
+  template <typename U, typename... A>
+  void construct(U* p, A&&... a) {
+    ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+  }
+};
+using ByteImage = std::vector<char, DefaultInitAlloc<char>>;
+
 class LogicBlockImage {
  public:
   explicit LogicBlockImage(uint32_t block_id, int64_t capacity = 64LL * 1024 * 1024);
@@ -78,7 +104,12 @@ class LogicBlockImage {
   // LogicBlock::close_write_file (logic_block.cpp:156-372), insert path:
   // FileInfo{id, offset=data_offset, size=len+36, usize, mtime, ctime, flag=0, crc}|payload.
   int close_write_file(uint64_t file_id, DataFile& df, uint32_t crc);
+  // Thread-safe: the record's range and index entry are taken under the lock, the
+  // FileInfo|payload bytes are filled beside other writers (records are disjoint).
   int append_record(uint64_t file_id, const char* payload, int32_t len, uint32_t crc);
+  // Size the image for `bytes` of records up front (a block file is preallocated on
+  // disk), so appends never move it; huge pages where the kernel offers them.
+  void reserve(int64_t bytes);
   // LogicBlock::read_file at offset 0 (logic_block.cpp:374-440): FileInfo|payload.
   int read_file(uint64_t file_id, std::vector<char>& out) const;
   // The full read of logic_block.cpp:374-440: *nbytes truncated to the record,
@@ -91,17 +122,21 @@ class LogicBlockImage {
   // index in offset order (traverse_sorted_segment_meta, index_handle.cpp:870-878)
   std::vector<tfs_raw_meta> sorted_metas() const;
   std::vector<int32_t> sorted_flags() const;
-  const std::vector<char>& data() const { return data_; }
-  std::vector<char>& data() { return data_; }
-  int64_t data_size() const { return int64_t(data_.size()); }
-  void replace(std::vector<char>&& data, const std::vector<tfs_raw_meta>& metas, const std::vector<int32_t>& flags);
+  const ByteImage& data() const { return data_; }
+  ByteImage& data() { return data_; }
+  int64_t data_size() const {
+    std::shared_lock<std::shared_mutex> g(mu_);
+    return int64_t(data_.size());
+  }
+  void replace(ByteImage&& data, const std::vector<tfs_raw_meta>& metas, const std::vector<int32_t>& flags);
 
  private:
   uint32_t block_id_;
   int64_t capacity_;
-  std::vector<char> data_;
+  ByteImage data_;
   std::map<uint64_t, tfs_raw_meta> index_;
   std::map<uint64_t, int32_t> flags_;
+  mutable std::shared_mutex mu_;  // exclusive: layout/index changes; shared: filling a record
 };
 
 // DataManagement::close_write_file (data_management.cpp:173-236): CRC compare
@@ -125,8 +160,10 @@ class CloseBatcher {
     DataFile* df;
     LogicBlockImage* block;
     int status = 1;
+    uint32_t crc = 0;
     bool done = false;
   };
+  static constexpr int kAppend = 1;  // checked, the closing thread persists it
   void run();
   void flush(std::vector<Req*>& reqs);
   tfs_crc_ctx* ctx_;
@@ -139,6 +176,7 @@ class CloseBatcher {
   size_t gather_cap_ = 0;
   bool stop_ = false;
   uint64_t batches_ = 0;
+  int64_t gather_us_ = 0, verify_us_ = 0;  // TFS_DS_TRACE diagnostics
   std::thread worker_;
 };
 
