@@ -592,3 +592,51 @@ def test_small_pinned_batches_read_in_place(gpu_ctx, oracle):
             assert (c == exp[k::3]).all() and nb == int((ok == 0).sum()) == int(np.isin(np.arange(n)[k::3], bad).sum())
     finally:
         pin.free()
+
+
+def test_device_resident_max_len_and_64bit_offsets(gpu_ctx, oracle):
+    """Maximum sizes: one file of INT32_MAX bytes (Func::crc's `len` is int32, func.h:90)
+    with a non-zero seed, a file straddling the 4 GiB offset boundary and one past 5 GiB
+    (descriptor offsets are u64), computed and verified on the device; each checked
+    against the oracle over the device's own bytes."""
+    import ctypes
+    import tfs_amd.crc as crc
+    G = 1 << 30
+    files = [(36, (1 << 31) - 1, 0x4E534654), (4 * G - 5, 100 * 1024 + 3, 0), (5 * G + 3, (1 << 20) + 7, 7)]
+    nbytes = (5 * G + 3 + (1 << 20) + 7 + 4095) // 4096 * 4096
+    img = crc.DeviceBuffer(gpu_ctx, nbytes)
+    try:
+        gpu_ctx.synth_fill_device(img, nbytes, 99, 0)
+        d = np.zeros(len(files), crc.DESC_DTYPE)
+        d["offset"] = [f[0] for f in files]
+        d["len"] = [f[1] for f in files]
+        d["aux"] = [f[2] for f in files]
+        dd = crc.DeviceBuffer(gpu_ctx, d.nbytes).upload(d)
+        out = crc.DeviceBuffer(gpu_ctx, 4 * len(files))
+        gpu_ctx.batch_device(dd, len(files), img, out)
+        gpu_ctx.sync()
+        got = out.download(np.uint32)
+        for i, (o, ln, seed) in enumerate(files):
+            host = img.download(np.uint8, ln, o)
+            want = oracle.oracle_crc(seed, ctypes.cast(host.ctypes.data, ctypes.c_char_p), ln)
+            del host
+            assert int(got[i]) == want, (i, hex(int(got[i])), hex(want))
+        # verify-on-read starts from seed 0 (sync_backup.cpp:383): expected = crc(0, payload)
+        z = d.copy()
+        z["aux"] = 0
+        zd = crc.DeviceBuffer(gpu_ctx, z.nbytes).upload(z)
+        gpu_ctx.batch_device(zd, len(files), img, out)
+        gpu_ctx.sync()
+        v = d.copy()
+        v["aux"] = out.download(np.uint32)
+        assert int(v["aux"][1]) == int(got[1])                  # seed 0 there already
+        v["aux"][0] ^= 0x80000000
+        vd = crc.DeviceBuffer(gpu_ctx, v.nbytes).upload(v)
+        okd = crc.DeviceBuffer(gpu_ctx, len(files))
+        nb = crc.DeviceBuffer(gpu_ctx, 4)
+        nb.zero()
+        gpu_ctx.verify_device(vd, len(files), img, None, okd, nb)
+        gpu_ctx.sync()
+        assert int(nb.download(np.uint32)[0]) == 1 and okd.download().tolist() == [0, 1, 1]
+    finally:
+        img.free()
