@@ -496,6 +496,22 @@ def bench_zipf(args):
                      "frac": algo / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
                      "kernel": "crc_files_kernel<0> (compute)", "kernel_ms_avg": kms},
     }
+    if args.membench:
+        # The kernel's access pattern over this geometry without the CRC arithmetic
+        # (whole 1 KiB stripes of every file, 128-byte anchored, nt), and a plain
+        # grid-stride stream of the same image: the ceilings the Zipf kernel is held to.
+        mb = crc.DeviceBuffer(ctx, 16)
+        stripes = np.maximum(lens.astype(np.int64) - 127, 0) // 1024
+        for pat, nb in ((11016, float(stripes.sum()) * 1024.0), (1000, float(total))):
+            ctx.membench_device(pat, img, d_desc, n, total, mb)
+            e0, e1 = crc.Event(ctx), crc.Event(ctx)
+            e0.record()
+            for _ in range(5):
+                ctx.membench_device(pat, img, d_desc, n, total, mb)
+            e1.record()
+            ctx.sync()
+            res.setdefault("membench_GBs", {})["p%d" % pat] = nb / (e0.elapsed_ms(e1) / 5 / 1e3) / 1e9
+        mb.free()
     if rank == 0:
         print(json.dumps(res), flush=True)
     del ev
