@@ -52,6 +52,8 @@ def parse():
     p.add_argument("--compact-blocks", type=int, default=4096, help="blocks per GPU for --workload compact/e2e")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--e2e-blocks", type=int, default=128,
+                   help="blocks per GPU for the end-to-end (H2D-inclusive) leg of the default line; 0 = off")
     p.add_argument("--e2e", action="store_true", help="also measure the pinned H2D-inclusive rate (stderr)")
     p.add_argument("--ec-mib", type=int, default=1536,
                    help="member size in MiB for --workload ec (< 2048: ErasureCode sizes are int)")
@@ -266,8 +268,9 @@ def main():
         "data": "synthetic (splitmix64 payloads, FileInfo-headed block images, generated on device)",
         "config": {
             "workload": "device-resident CRC32 verify: %d blocks x %d files x 64 KiB per GPU (%d files, %.1f GiB "
-                        "payload); 16 steps = 1 TiB per GPU (BASELINE configs[1])" % (
-                            nblocks, FILES_PER_BLOCK, nfiles, nfiles * FILE_SIZE / 2**30),
+                        "payload); %d steps = %.3g TiB per GPU (BASELINE configs[1]: 16 steps of 1024 blocks = 1 TiB)" % (
+                            nblocks, FILES_PER_BLOCK, nfiles, nfiles * FILE_SIZE / 2**30,
+                            args.steps, args.steps * nfiles * FILE_SIZE / 2**40),
             "files_per_gpu": nfiles,
             "file_size": FILE_SIZE,
             "layout": "block image, FileInfo(36 B)|payload, payload 4-byte aligned",
@@ -298,6 +301,14 @@ def main():
                                               expected[idx], args.cpu_seconds)
     if args.e2e:
         print(json.dumps({"e2e": e2e_rate(ctx)}), file=sys.stderr)
+    if args.e2e_blocks > 0:
+        # configs[4] asks for device-resident AND end-to-end at every N: the same
+        # job's PCIe-inclusive rate, reported beside `value` (never as `value`).
+        gibs, pcie, el = e2e_blocks(ctx, dist, world, rank, args.e2e_blocks)
+        result["end_to_end"] = {
+            "value": gibs, "unit": "GiB/s", "pcie_GBs": pcie, "ms_per_block": el / args.e2e_blocks * 1e3,
+            "workload": "%d pinned host 64 MiB block images per GPU -> H2D -> verify -> verdicts back, "
+                        "3 in flight, max over ranks" % args.e2e_blocks}
     if rank == 0:
         print(json.dumps(result), flush=True)
     del ev
@@ -1200,12 +1211,12 @@ def bench_loopback(args):
         dist.destroy_process_group()
 
 
-def bench_e2e(args):
-    """Verify-on-read starting in host memory: pinned block images -> H2D ->
-    verify -> verdicts back, several blocks in flight (submit/wait)."""
+def e2e_blocks(ctx, dist, world, rank, nsub, inflight=3):
+    """configs[4] end-to-end leg: pinned host block images -> H2D -> verify ->
+    verdicts back, `inflight` blocks in flight (submit/wait), timed between
+    barriers, max over ranks.  Returns (payload GiB/s over all ranks, PCIe GB/s,
+    elapsed s)."""
     import tfs_amd.crc as crc
-    world, rank, local, dist = _dist_init()
-    ctx = crc.Context(local)
     nfiles, rec = FILES_PER_BLOCK, FILEINFO + FILE_SIZE
     blk_bytes = nfiles * rec
     ndistinct = 8
@@ -1227,8 +1238,6 @@ def bench_e2e(args):
         exps.append(d_crc.download(np.uint32))
     offs = desc["offset"]
     lens = desc["len"]
-    nsub = args.compact_blocks
-    inflight = 3
     hs = []
     for i in range(2):  # warmup
         ctx.wait(ctx.submit_verify(srcs[i].array, offs, lens, exps[i]))
@@ -1245,21 +1254,32 @@ def bench_e2e(args):
     el = _max_over_ranks(dist, time.perf_counter() - t0)
     if bad:
         raise SystemExit("e2e: mismatches on clean data")
-    payload = float(world) * nsub * nfiles * FILE_SIZE
-    res = {
-        "metric": "GiB/s CRC32 verify end-to-end from pinned host block images (H2D included)",
-        "value": payload / el / 2**30, "unit": "GiB/s", "n_gpus": world, "steps": nsub, "warmup": 2,
-        "ms_per_step": el / nsub * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "u8", "data": "synthetic 64 KiB files, 1024 per 64 MiB block",
-        "config": {"workload": "pinned host blocks -> GPU verify, %d in flight, %d blocks" % (inflight, nsub)},
-        "pcie_GBs": float(world) * nsub * blk_bytes / el / 1e9,
-    }
-    if rank == 0:
-        print(json.dumps(res), flush=True)
     for b in srcs:
         b.free()
     for b in (d_img, d_desc, d_crc):
         b.free()
+    payload = float(world) * nsub * nfiles * FILE_SIZE
+    return payload / el / 2**30, float(world) * nsub * blk_bytes / el / 1e9, el
+
+
+def bench_e2e(args):
+    """Verify-on-read starting in host memory: pinned block images -> H2D ->
+    verify -> verdicts back, several blocks in flight (submit/wait)."""
+    import tfs_amd.crc as crc
+    world, rank, local, dist = _dist_init()
+    ctx = crc.Context(local)
+    nsub, inflight = args.compact_blocks, 3
+    gibs, pcie, el = e2e_blocks(ctx, dist, world, rank, nsub, inflight)
+    res = {
+        "metric": "GiB/s CRC32 verify end-to-end from pinned host block images (H2D included)",
+        "value": gibs, "unit": "GiB/s", "n_gpus": world, "steps": nsub, "warmup": 2,
+        "ms_per_step": el / nsub * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u8", "data": "synthetic 64 KiB files, 1024 per 64 MiB block",
+        "config": {"workload": "pinned host blocks -> GPU verify, %d in flight, %d blocks" % (inflight, nsub)},
+        "pcie_GBs": pcie,
+    }
+    if rank == 0:
+        print(json.dumps(res), flush=True)
     ctx.close()
     if dist:
         dist.destroy_process_group()
