@@ -67,7 +67,7 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(sample_u8, offs, lens, expected, seconds):
+def cpu_baseline(sample_u8, offs, lens, expected, seconds, what="64 KiB payloads"):
     """Single-thread reference CRC over a bounded sample (test infrastructure)."""
     ref_so = os.path.join(ROOT, "oracle", "_ref", "libref_crc.so")
     ora_so = os.path.join(ROOT, "oracle", "liboracle_crc.so")
@@ -126,9 +126,9 @@ def cpu_baseline(sample_u8, offs, lens, expected, seconds):
         "unit": "GiB/s",
         "cores": 1,
         "kind": kind,
-        "sample": "%d passes over %d x 64 KiB payloads (%.0f MiB) copied from the GPU-resident batch; "
+        "sample": "%d passes over %d x %s (%.0f MiB) copied from the GPU-resident batch; "
                   "Func::crc(0, payload) vs stored crc, single thread, %.1f s" % (
-                      passes, len(offs), float(np.sum(lens)) / 2**20, dt),
+                      passes, len(offs), what, float(np.sum(lens)) / 2**20, dt),
         "allcore": allcore,
     }
 
@@ -507,6 +507,16 @@ def bench_zipf(args):
                      "frac": algo / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
                      "kernel": "crc_files_kernel<0> (compute)", "kernel_ms_avg": kms},
     }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        # the reference CRC on the host over a bounded sample of the same Zipf files
+        idx = np.linspace(0, n - 1, min(n, 1024)).astype(np.int64)
+        sl = lens[idx].astype(np.int64)
+        so = np.concatenate([[0], np.cumsum(sl)[:-1]])
+        sample = np.zeros(int(sl.sum()), np.uint8)
+        for j, i in enumerate(idx):
+            sample[so[j]:so[j] + sl[j]] = img.download(np.uint8, int(lens[i]), int(offs[i]))
+        res["cpu_baseline"] = cpu_baseline(sample, so, sl, got[idx], args.cpu_seconds,
+                                           "Zipf-sized payloads (evenly spaced files of the batch)")
     if args.membench:
         # The kernel's access pattern over this geometry without the CRC arithmetic
         # (whole 1 KiB stripes of every file, 128-byte anchored, nt), and a plain
@@ -739,6 +749,25 @@ def bench_compact(args):
         "pcie_GBs": float(world) * nblocks * pcie_block / el / 1e9,
         "ab": dict(ab, speedup=ab["dma_ms_per_block"] / ab["zero_copy_ms_per_block"], blocks=nab),
     }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        # CPU restatement of CompactTask::real_compact with the added re-CRC
+        # (oracle_compact, task.cpp:713-836) over the same pinned source images,
+        # single thread; the dataserver itself is not buildable here (tbsys/tbnet).
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            wc = ora.oracle_compact(srcs[reps % ndistinct].ptr, mo.ctypes.data, ms.ctypes.data, flags.ctypes.data,
+                                    nfiles, odest.ctypes.data, doff.ctypes.data, dsz.ctypes.data, ook.ctypes.data)
+            if wc != w or not ook[flags == 0].all():
+                raise SystemExit("compact: oracle baseline disagrees")
+            reps += 1
+            if time.perf_counter() - t0 >= args.cpu_seconds:
+                break
+        dt = time.perf_counter() - t0
+        res["cpu_baseline"] = {
+            "value": reps * blk_bytes / dt / 2**30, "unit": "GiB/s of source block bytes", "cores": 1,
+            "kind": "port",
+            "sample": "%d compactions of the %d pinned source block images (re-CRC of %d live files + repack), "
+                      "oracle_compact single thread, %.1f s" % (reps, ndistinct, live, dt)}
     if rank == 0:
         print(json.dumps(res), flush=True)
     for b in srcs + dests:
