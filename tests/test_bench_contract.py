@@ -1,0 +1,48 @@
+"""bench.py's output contract on a real GPU, at a reduced size: one JSON line
+with the metric/value/roofline keys the driver reads, the cpu_baseline leg on
+rank 0, and the configs[4] end-to-end leg (pinned H2D + verify) beside the
+device-resident value.  Runs bench.py as a child process (one GPU process at a
+time); the full-size line is the driver's own round-end run."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+
+def _run(args, timeout=240):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, capture_output=True,
+                       text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+def test_default_line_contract_small():
+    res = _run(["--blocks", "16", "--steps", "3", "--warmup", "1", "--cpu-seconds", "0.5", "--e2e-blocks", "6"])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "end_to_end"):
+        assert k in res, k
+    assert res["n_gpus"] == 1 and res["steps"] == 3 and res["scaling"] == "weak" and res["dtype"] == "u8"
+    assert res["value"] > 0 and res["higher_is_better"] is True
+    rf = res["roofline"]
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9
+    assert rf["traffic"] is None  # PMC traffic is only quoted for the full-size launch it was measured on
+    cb = res["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] == 1 and cb["kind"] in ("reference", "port")
+    e2e = res["end_to_end"]
+    assert 0 < e2e["value"] < res["value"] and e2e["pcie_GBs"] > 0
+
+
+@pytest.mark.gpu
+def test_zipf_and_compact_lines_carry_cpu_baseline():
+    z = _run(["--workload", "zipf", "--blocks", "8", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0.3"])
+    assert z["roofline"]["bound"] == "hbm" and z["cpu_baseline"]["value"] > 0
+    c = _run(["--workload", "compact", "--compact-blocks", "16", "--cpu-seconds", "0.3"])
+    assert c["value"] > 0 and c["cpu_baseline"]["kind"] == "port" and c["ab"]["speedup"] > 0
