@@ -48,6 +48,18 @@ for rnd in range(2):  # two interleaved rounds: box noise shows as round-to-roun
         d_desc = crc.DeviceBuffer(ctx, desc.nbytes).upload(desc)
         res.setdefault("wave_per_%dKiB_GBs" % (seg >> 10), []).append(timed(1016, d_desc, n, TOTAL))
         d_desc.free()
+# Occupancy: the same patterns at 1, 2 and 4 workgroups of 16 waves per CU
+# (the CRC kernel is held to 1 by its 128 KiB of LDS tables).
+seg = 65536
+n = TOTAL // seg
+desc = np.zeros(n, crc.DESC_DTYPE)
+desc["offset"] = np.arange(n, dtype=np.uint64) * seg
+desc["len"] = seg + 16
+d_desc = crc.DeviceBuffer(ctx, desc.nbytes).upload(desc)
+for grid in (256, 512, 1024):
+    res["wave_per_64KiB_grid%d_GBs" % grid] = timed(1016, d_desc, n, TOTAL, grid=grid)
+    res["grid_stride_grid%d_GBs" % grid] = timed(1000, None, 0, TOTAL, grid=grid)
+d_desc.free()
 print(json.dumps({"locality_probe": res}), flush=True)
 img.free()
 out.free()
