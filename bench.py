@@ -1090,6 +1090,8 @@ def bench_ec(args):
                      "kernel": "ec_apply_kernel<3>", "kernel_ms_avg": out["encode"]["ms"]},
         "decode": out["decode"],
     }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        res["cpu_baseline"] = ec_cpu_baseline(d, k, m, args.cpu_seconds, min(4 << 20, size // 1024 * 1024))
     if rank == 0:
         print(json.dumps(res), flush=True)
     enc.free()
@@ -1099,6 +1101,36 @@ def bench_ec(args):
     ctx.close()
     if dist:
         dist.destroy_process_group()
+
+
+def ec_cpu_baseline(d, k, m, seconds, chunk=4 << 20):
+    """The reference's jerasure bitmatrix encode (oracle/_ref/libref_ec.so, built
+    from the reference sources) or the oracle's restatement, single thread, over
+    the first `chunk` bytes of the same members; its parity must equal the GPU's."""
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "libref_ec.so")
+    if os.path.exists(ref_so):
+        L, kind = ctypes.CDLL(ref_so), "reference"
+        L.ref_ec_encode.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+        run = lambda pp: L.ref_ec_encode(k, m, pp, chunk)  # noqa: E731
+    else:
+        L, kind = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle_ec.so")), "port"
+        L.oracle_ec_encode.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        run = lambda pp: L.oracle_ec_encode(k, m, pp, None, chunk)  # noqa: E731
+    host = [d[i].download(np.uint8, chunk) for i in range(k)] + [np.zeros(chunk, np.uint8) for _ in range(m)]
+    pp = (ctypes.c_void_p * (k + m))(*[h.ctypes.data for h in host])
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        run(pp)
+        reps += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    for i in range(k, k + m):
+        if not (d[i].download(np.uint8, chunk) == host[i]).all():
+            raise SystemExit("ec: CPU baseline parity disagrees with the GPU")
+    return {"value": reps * k * chunk / dt / 2**30, "unit": "GiB/s", "cores": 1, "kind": kind,
+            "sample": "%d encodes of k=%d x %d MiB (first bytes of the same members), jerasure_bitmatrix_encode "
+                      "w=8 ps=128, single thread, %.1f s" % (reps, k, chunk >> 20, dt)}
 
 
 def _cpu_model():

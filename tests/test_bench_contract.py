@@ -46,3 +46,10 @@ def test_zipf_and_compact_lines_carry_cpu_baseline():
     assert z["roofline"]["bound"] == "hbm" and z["cpu_baseline"]["value"] > 0
     c = _run(["--workload", "compact", "--compact-blocks", "16", "--cpu-seconds", "0.3"])
     assert c["value"] > 0 and c["cpu_baseline"]["kind"] == "port" and c["ab"]["speedup"] > 0
+
+
+@pytest.mark.gpu
+def test_ec_line_carries_cpu_baseline():
+    e = _run(["--workload", "ec", "--ec-mib", "16", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0.3"])
+    assert e["roofline"]["bound"] == "hbm" and e["value"] > 0
+    assert e["cpu_baseline"]["value"] > 0 and e["cpu_baseline"]["kind"] in ("reference", "port")
