@@ -67,7 +67,7 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(sample_u8, offs, lens, expected, seconds, what="64 KiB payloads"):
+def cpu_baseline(sample_u8, offs, lens, expected, seconds, what="64 KiB payloads", seed=0):
     """Single-thread reference CRC over a bounded sample (test infrastructure)."""
     ref_so = os.path.join(ROOT, "oracle", "_ref", "libref_crc.so")
     ora_so = os.path.join(ROOT, "oracle", "liboracle_crc.so")
@@ -87,7 +87,7 @@ def cpu_baseline(sample_u8, offs, lens, expected, seconds, what="64 KiB payloads
     t0 = time.perf_counter()
     while True:
         for i in range(len(offs)):
-            c = f(0, base + int(offs[i]), int(lens[i]))
+            c = f(seed, base + int(offs[i]), int(lens[i]))
             if c != int(expected[i]):
                 raise SystemExit("cpu baseline disagrees with GPU expected crc at file %d" % i)
             nbytes += int(lens[i])
@@ -98,6 +98,8 @@ def cpu_baseline(sample_u8, offs, lens, expected, seconds, what="64 KiB payloads
     # all-core variant through the oracle's pthread batch (one file per task)
     allcore = None
     try:
+        if seed != 0:  # the oracle's pthread batch computes seed-0 CRCs only
+            raise StopIteration
         O = ctypes.CDLL(ora_so)
         O.oracle_crc_batch_mt.restype = ctypes.c_int
         O.oracle_crc_batch_mt.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
@@ -119,6 +121,8 @@ def cpu_baseline(sample_u8, offs, lens, expected, seconds, what="64 KiB payloads
         assert (out == expected).all()
         allcore = {"value": reps * float(np.sum(lens)) / ad / 2**30, "cores": threads, "nproc": os.cpu_count(),
                    "cpu_model": _cpu_model()}
+    except StopIteration:
+        allcore = None
     except Exception as e:  # reported, never fatal
         allcore = {"error": str(e)}
     return {
@@ -127,9 +131,9 @@ def cpu_baseline(sample_u8, offs, lens, expected, seconds, what="64 KiB payloads
         "cores": 1,
         "kind": kind,
         "sample": "%d passes over %d x %s (%.0f MiB) copied from the GPU-resident batch; "
-                  "Func::crc(0, payload) vs stored crc, single thread, %.1f s" % (
-                      passes, len(offs), what, float(np.sum(lens)) / 2**20, dt),
-        "allcore": allcore,
+                  "Func::crc(%s, payload) vs stored crc, single thread, %.1f s" % (
+                      passes, len(offs), what, float(np.sum(lens)) / 2**20, "0" if seed == 0 else hex(seed), dt),
+        **({"allcore": allcore} if allcore is not None else {}),
     }
 
 
@@ -615,6 +619,16 @@ def bench_packet(args):
                      "frac": algo / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
                      "kernel": "packet_parse + crc_files_kernel<1> + packet_finish", "kernel_ms_avg": kms},
     }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        # BasePacket::decode's CRC on the host: Func::crc(TFS_PACKET_FLAG_V1, body) over sampled bodies
+        idx = np.linspace(0, n - 1, min(n, 1024)).astype(np.int64)
+        sample = np.zeros(len(idx) * body, np.uint8)
+        for j, i in enumerate(idx):
+            sample[j * body:(j + 1) * body] = img.download(np.uint8, body, int(off[i]) + 24)
+        cb = cpu_baseline(sample, np.arange(len(idx)) * body, np.full(len(idx), body), got[idx],
+                          args.cpu_seconds, "%d-B WriteDataMessage bodies" % body, seed=0x4E534654)
+        cb["unit"] = "GiB/s of body bytes"
+        res["cpu_baseline"] = cb
     if rank == 0:
         print(json.dumps(res), flush=True)
     del ev
@@ -1014,6 +1028,32 @@ def bench_compact_device(args):
         "ab": {"fused_one_launch_ms": kms, "fused_windows_ms": kms_w, "unfused_windows_ms": kms2,
                "windows": len(windows), "speedup_vs_unfused": kms2 / kms},
     }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        # CPU restatement of real_compact + re-CRC (oracle_compact) over block 0 of the same image, one thread
+        ora = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle_crc.so"))
+        ora.oracle_compact.restype = ctypes.c_int64
+        ora.oracle_compact.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint32] + [ctypes.c_void_p] * 4
+        src = img.download(np.uint8, blk)
+        mo = np.arange(nfiles, dtype=np.int64) * rec
+        ms = np.full(nfiles, rec, np.int32)
+        odest = np.zeros(blk, np.uint8)
+        doff = np.zeros(nfiles, np.int64)
+        dsz = np.zeros(nfiles, np.int32)
+        ook = np.zeros(nfiles, np.uint8)
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            ora.oracle_compact(src.ctypes.data, mo.ctypes.data, ms.ctypes.data, flags1.ctypes.data, nfiles,
+                               odest.ctypes.data, doff.ctypes.data, dsz.ctypes.data, ook.ctypes.data)
+            reps += 1
+            if time.perf_counter() - t0 >= args.cpu_seconds:
+                break
+        dt = time.perf_counter() - t0
+        if not (ook[flags1 == 0] == 1).all():
+            raise SystemExit("compact_device: oracle re-CRC disagrees with the GPU-written headers")
+        res["cpu_baseline"] = {
+            "value": reps * blk / dt / 2**30, "unit": "GiB/s of source block bytes", "cores": 1, "kind": "port",
+            "sample": "%d compactions of resident block 0 copied to host (re-CRC of %d live files + repack), "
+                      "oracle_compact single thread, %.1f s" % (reps, len(live1), dt)}
     if rank == 0:
         print(json.dumps(res), flush=True)
     for w in windows:

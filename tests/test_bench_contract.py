@@ -53,3 +53,12 @@ def test_ec_line_carries_cpu_baseline():
     e = _run(["--workload", "ec", "--ec-mib", "16", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0.3"])
     assert e["roofline"]["bound"] == "hbm" and e["value"] > 0
     assert e["cpu_baseline"]["value"] > 0 and e["cpu_baseline"]["kind"] in ("reference", "port")
+
+
+@pytest.mark.gpu
+def test_packet_and_compact_device_lines_carry_cpu_baseline():
+    p = _run(["--workload", "packet", "--blocks", "8", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0.3"])
+    assert p["cpu_baseline"]["value"] > 0 and "0x4e534654" in p["cpu_baseline"]["sample"]
+    c = _run(["--workload", "compact_device", "--blocks", "8", "--steps", "2", "--warmup", "1",
+              "--cpu-seconds", "0.3"])
+    assert c["cpu_baseline"]["value"] > 0 and c["cpu_baseline"]["kind"] == "port"
