@@ -861,6 +861,14 @@ def bench_block_verify(args):
                    "live_payload_GiBs": float(world) * nb * live.size * FILE_SIZE / el / 2**30},
         "ab": {"zero_copy_ms_per_block": el / nb * 1e3, "dma_ms_per_block": out["dma"][0] / out["dma"][1] * 1e3},
     }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        # the reference CRC over the live payloads of the same page-locked image, checked against the
+        # FileInfo crc_ values the GPU verified (sync_backup.cpp:412-435's loop without the pread)
+        cb = cpu_baseline(srcs[0].array, live * rec + FILEINFO, np.full(live.size, FILE_SIZE), c0,
+                          args.cpu_seconds, "live 64 KiB payloads of a page-locked block image")
+        cb["source_block_GiBs"] = cb["value"] * blk_bytes / (live.size * FILE_SIZE)
+        cb["unit"] = "GiB/s of live payload"
+        res["cpu_baseline"] = cb
     if rank == 0:
         print(json.dumps(res), flush=True)
     for b in srcs:

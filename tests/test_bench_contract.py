@@ -62,3 +62,9 @@ def test_packet_and_compact_device_lines_carry_cpu_baseline():
     c = _run(["--workload", "compact_device", "--blocks", "8", "--steps", "2", "--warmup", "1",
               "--cpu-seconds", "0.3"])
     assert c["cpu_baseline"]["value"] > 0 and c["cpu_baseline"]["kind"] == "port"
+
+
+@pytest.mark.gpu
+def test_block_verify_line_carries_cpu_baseline():
+    b = _run(["--workload", "block_verify", "--compact-blocks", "16", "--cpu-seconds", "0.3"])
+    assert b["value"] > 0 and b["cpu_baseline"]["source_block_GiBs"] > b["cpu_baseline"]["value"] > 0
