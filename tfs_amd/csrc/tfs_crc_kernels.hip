@@ -312,7 +312,9 @@ __device__ __forceinline__ void store_shifted(uintptr_t chunk, const uint4& v, u
 
 // The lane's chain over stripes 0..nstripes-1 (before the final combine).
 // COPY: also store every payload byte of [start, B16) to dst = src + delta.
-template <int RUN, int PF, bool NT, bool S8, bool COPY = false>
+// G (measurement knob): refill the ring G slots at a time, so each wave issues G
+// consecutive stripes (G KiB contiguous) back to back instead of one per stripe.
+template <int RUN, int PF, bool NT, bool S8, bool COPY = false, int G = 1>
 __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase& lb, const FileGeo<RUN>& g,
                                                const Head<RUN>& h, uint4 (&buf)[PF][RUN / 16], int lane,
                                                uintptr_t junk, intptr_t delta = 0, bool copy_on = false) {
@@ -379,9 +381,14 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
         for (int v = 0; v < kVec; ++v) c = steps16(T, lb, c, buf[f][v]);
         c = (r + f == last && !lane_in_last) ? c_old : c;  // run past B16: not part of the chain
         if (COPY && copy_on) copy_stripe(r + f, buf[f][0]);
-        const uintptr_t sb = stripe_base<RUN>(g, r + f + PF, junk) + uintptr_t(lane) * RUN;
+        if ((f + 1) % G == 0) {
 #pragma unroll
-        for (int v = 0; v < kVec; ++v) buf[f][v] = ld128s<NT>(sb + 16u * v);
+          for (int q = f + 1 - G; q <= f; ++q) {
+            const uintptr_t sb = stripe_base<RUN>(g, r + q + PF, junk) + uintptr_t(lane) * RUN;
+#pragma unroll
+            for (int v = 0; v < kVec; ++v) buf[q][v] = ld128s<NT>(sb + 16u * v);
+          }
+        }
       }
     }
     // Remaining 0..PF-1 stripes are already in buf[0..].
@@ -492,7 +499,7 @@ struct Tickets {
 // Files are software-pipelined per wave: the next file's stripe-0/tail words
 // and its first PF stripes are in flight while this file's lane chains are
 // combined, so HBM never waits on a file boundary.
-template <int MODE, int RUN, int PF, bool NT, bool DYN, bool S8>
+template <int MODE, int RUN, int PF, bool NT, bool DYN, bool S8, int G = 1>
 __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __restrict__ base,
                                                            const Desc* __restrict__ desc, uint32_t n,
                                                            const Tables* __restrict__ tg, uint32_t* out_crc,
@@ -526,7 +533,7 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
   uint32_t jv = DYN && fn < n ? tk.issue(lane) : 0u;  // ticket of the file after next, in flight
   uint32_t bad = 0;
   for (;;) {
-    const uint32_t c = g.nstripes ? lane_chain<RUN, PF, NT, S8>(lds_tables, lb, g, h, buf, lane, junk) : 0u;
+    const uint32_t c = g.nstripes ? lane_chain<RUN, PF, NT, S8, false, G>(lds_tables, lb, g, h, buf, lane, junk) : 0u;
     // Start the next file's loads before combining this one.
     const bool more = fn < n;
     FileGeo<RUN> ng = g;
@@ -1002,6 +1009,18 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
     case 4: TFS_LAUNCH(16, 5, true, true, false); break;
     case 5: TFS_LAUNCH(16, 8, true, true, true); break;
     case 6: TFS_LAUNCH(16, 3, true, true, true); break;
+#undef TFS_LAUNCH
+#define TFS_LAUNCH_G(R, P, N, D, S, G)                                                                        \
+  hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N, D, S, G>), grid, block, 0, stream, base, desc, n, tg, out_crc, \
+                     out_ok, n_bad, sched, vseed)
+    case 9: TFS_LAUNCH_G(16, 6, true, true, true, 2); break;
+    case 10: TFS_LAUNCH_G(16, 6, true, true, true, 3); break;
+    case 11: TFS_LAUNCH_G(16, 8, true, true, true, 4); break;
+    case 12: TFS_LAUNCH_G(16, 4, true, true, true, 2); break;
+#undef TFS_LAUNCH_G
+#define TFS_LAUNCH(R, P, N, D, S)                                                                          \
+  hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N, D, S>), grid, block, 0, stream, base, desc, n, tg, out_crc, \
+                     out_ok, n_bad, sched, vseed)
     default: TFS_LAUNCH(kRun, kPF, kNT, kDYN, kS8); break;
   }
 #undef TFS_LAUNCH
