@@ -205,9 +205,35 @@ struct Head {
   uint32_t tb[3];
 };
 
-template <int RUN>
+// HV (measurement knob): one dwordx4 per lane for stripe 0 and one for the tail
+// instead of RUN/4 dword loads and 3 dword + 3 byte loads.  A 16-byte chunk that
+// holds at least one payload byte lies in the same page as that byte, so the
+// bytes read outside the payload cannot fault; they are masked as before.
+template <int RUN, bool HV = false>
 __device__ __forceinline__ Head<RUN> load_head(const FileGeo<RUN>& g, int lane) {
   Head<RUN> h;
+  if constexpr (HV && RUN == 16) {
+    const uintptr_t lo = g.sb0 + uintptr_t(lane) * 16u;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (g.nstripes && lo + 16u > g.A && lo < g.B16) v = ld128(lo);
+    const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uintptr_t q = lo + 4u * i;
+      h.w[i] = (q >= g.A && q < g.B16) ? vw[i] : 0u;
+    }
+    uint4 t = make_uint4(0u, 0u, 0u, 0u);
+    if (g.nstripes && g.end > g.B16) t = ld128(g.B16);
+    const uint32_t tw[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) h.tw[i] = (g.nstripes && g.B16 + 4u * i + 4u <= g.end) ? tw[i] : 0u;
+    const uint32_t bo = uint32_t((g.end & ~uintptr_t(3)) - g.B16);  // byte offset of the last partial dword
+    const uint32_t bw = bo >= 12u ? t.w : (bo >= 8u ? t.z : (bo >= 4u ? t.y : t.x));
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      h.tb[i] = (g.nstripes && (g.end & ~uintptr_t(3)) + i < g.end) ? ((bw >> (8 * i)) & 0xFFu) : 0u;
+    return h;
+  }
   const uintptr_t lo = g.sb0 + uintptr_t(lane) * RUN;
 #pragma unroll
   for (int i = 0; i < RUN / 4; ++i) {
@@ -499,7 +525,7 @@ struct Tickets {
 // Files are software-pipelined per wave: the next file's stripe-0/tail words
 // and its first PF stripes are in flight while this file's lane chains are
 // combined, so HBM never waits on a file boundary.
-template <int MODE, int RUN, int PF, bool NT, bool DYN, bool S8, int G = 1>
+template <int MODE, int RUN, int PF, bool NT, bool DYN, bool S8, int G = 1, bool HV = false>
 __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __restrict__ base,
                                                            const Desc* __restrict__ desc, uint32_t n,
                                                            const Tables* __restrict__ tg, uint32_t* out_crc,
@@ -525,7 +551,7 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
   }
   Desc cur = desc[f];
   FileGeo<RUN> g = make_geo<RUN>(base + cur.offset, cur.len, MODE == 0 ? cur.aux : vseed);
-  Head<RUN> h = load_head<RUN>(g, lane);
+  Head<RUN> h = load_head<RUN, HV>(g, lane);
   const uintptr_t junk = reinterpret_cast<uintptr_t>(tg->slice);
   uint4 buf[PF][RUN / 16];
   load_ring<RUN, PF, NT>(g, lane, buf, junk);
@@ -542,7 +568,7 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
     uint32_t fnn = n;
     if (more) {
       ng = make_geo<RUN>(base + ncur.offset, ncur.len, MODE == 0 ? ncur.aux : vseed);
-      nh = load_head<RUN>(ng, lane);
+      nh = load_head<RUN, HV>(ng, lane);
       load_ring<RUN, PF, NT>(ng, lane, buf, junk);
       fnn = DYN ? tk.resolve(jv, lane) : fn + stride;
       if (fnn < n) nxt = desc[fnn];
@@ -1018,6 +1044,10 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
     case 11: TFS_LAUNCH_G(16, 8, true, true, true, 4); break;
     case 12: TFS_LAUNCH_G(16, 4, true, true, true, 2); break;
 #undef TFS_LAUNCH_G
+    case 13:
+      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, true>), grid, block, 0, stream, base,
+                         desc, n, tg, out_crc, out_ok, n_bad, sched, vseed);
+      break;
 #define TFS_LAUNCH(R, P, N, D, S)                                                                          \
   hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N, D, S>), grid, block, 0, stream, base, desc, n, tg, out_crc, \
                      out_ok, n_bad, sched, vseed)
