@@ -443,6 +443,9 @@ __device__ __forceinline__ uint32_t finish_file(const uint32_t* T, const LaneBas
     for (uint32_t i = 0; i < g.len; ++i) t = step1(T, lb, t, ld8(g.start + i));
     return t;
   }
+#ifdef TFS_DIAG_SKIP_COMBINE
+  return c;  // diagnostic build only (tools/combine_probe.sh): wrong CRCs, times the kernel without the combine
+#endif
   // Move each lane's chain to its place: the distance from the end of its last
   // run to B16, in runs: (63-lane) - (E-B16)/RUN, plus a whole stripe for lanes
   // whose run in the last stripe lies past B16 (their chain ended a stripe earlier).
