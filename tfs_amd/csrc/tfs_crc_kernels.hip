@@ -489,20 +489,29 @@ constexpr bool kNT = true;
 constexpr bool kPAR = false;
 constexpr bool kDYN = true;
 constexpr bool kS8 = true;
+constexpr bool kIL = true;  // interleaved ticket groups (Tickets<IL>): +2 % verify, +4 % Zipf
 
 // Work distribution.  Static: wave w takes files w, w+W, w+2W, ... (W = all
 // waves) -- ideal when every file has the same size.  Dynamic: eight ticket
 // counters (one per group of workgroups, blockIdx % 8, i.e. one per XCD under
-// round-robin placement) each own 1/8 of the files in order; a wave takes the
+// round-robin placement) each own 1/8 of the files; a wave takes the
 // next ticket of its group and steals from the other groups once its own is
 // exhausted, so waves finish together for any size distribution (the kernel
 // ends with its slowest wave).  The ticket for the next-but-one file is taken
 // one file ahead, so the atomic's latency hides under a file's work.
+// IL (product default, kIL): group g owns files g, g+8, g+16, ..., so the eight
+// XCDs read one moving address window together; IL = false gives group g the
+// contiguous eighth [n*g/8, n*(g+1)/8) (eight windows 1/8 of the batch apart,
+// 2-4 % slower in interleaved A/B; TFS_CRC_VARIANT=14).
+template <bool IL = false>
 struct Tickets {
   uint32_t* ctr;  // 8 zeroed counters for this launch, kSchedStride u32 apart (one per 256-byte line)
   uint32_t n, group;
   __device__ __forceinline__ uint32_t gbegin(uint32_t g) const { return uint32_t((uint64_t(n) * g) >> 3); }
-  __device__ __forceinline__ uint32_t gcount(uint32_t g) const { return gbegin(g + 1) - gbegin(g); }
+  __device__ __forceinline__ uint32_t gcount(uint32_t g) const {
+    return IL ? (n > g ? (n - g + 7u) >> 3 : 0u) : gbegin(g + 1) - gbegin(g);
+  }
+  __device__ __forceinline__ uint32_t file_of(uint32_t g, uint32_t j) const { return IL ? j * 8u + g : gbegin(g) + j; }
   // Issue the atomic of the home group in lane 0; the result stays in lane 0's register.
   __device__ __forceinline__ uint32_t issue(int lane) const {
     uint32_t j = 0;
@@ -513,7 +522,7 @@ struct Tickets {
   __device__ __forceinline__ uint32_t resolve(uint32_t jv, int lane) {
     uint32_t j = __builtin_amdgcn_readlane(jv, 0);
     for (uint32_t tries = 0;; ++tries) {
-      if (j < gcount(group)) return gbegin(group) + j;
+      if (j < gcount(group)) return file_of(group, j);
       if (tries == 7) return n;
       group = (group + 1) & 7u;  // steal
       uint32_t k = 0;
@@ -528,7 +537,7 @@ struct Tickets {
 // Files are software-pipelined per wave: the next file's stripe-0/tail words
 // and its first PF stripes are in flight while this file's lane chains are
 // combined, so HBM never waits on a file boundary.
-template <int MODE, int RUN, int PF, bool NT, bool DYN, bool S8, int G = 1, bool HV = false>
+template <int MODE, int RUN, int PF, bool NT, bool DYN, bool S8, int G = 1, bool HV = false, bool IL = false>
 __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __restrict__ base,
                                                            const Desc* __restrict__ desc, uint32_t n,
                                                            const Tables* __restrict__ tg, uint32_t* out_crc,
@@ -541,7 +550,7 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
   const uint32_t wpb = kBlock / kWave;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t stride = gridDim.x * wpb;
-  Tickets tk{sched, n, blockIdx.x & 7u};
+  Tickets<IL> tk{sched, n, blockIdx.x & 7u};
   uint32_t f, fn;
   if (DYN) {
     f = tk.resolve(tk.issue(lane), lane);
@@ -1051,10 +1060,17 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, true>), grid, block, 0, stream, base,
                          desc, n, tg, out_crc, out_ok, n_bad, sched, vseed);
       break;
+    case 14:  // contiguous ticket groups (the product before interleaving)
+      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, false>), grid, block, 0, stream,
+                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed);
+      break;
 #define TFS_LAUNCH(R, P, N, D, S)                                                                          \
   hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N, D, S>), grid, block, 0, stream, base, desc, n, tg, out_crc, \
                      out_ok, n_bad, sched, vseed)
-    default: TFS_LAUNCH(kRun, kPF, kNT, kDYN, kS8); break;
+    default:
+      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL>), grid, block, 0, stream,
+                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed);
+      break;
   }
 #undef TFS_LAUNCH
   return hipGetLastError();
