@@ -489,7 +489,7 @@ constexpr bool kNT = true;
 constexpr bool kPAR = false;
 constexpr bool kDYN = true;
 constexpr bool kS8 = true;
-constexpr bool kIL = true;  // interleaved ticket groups (Tickets<IL>): +2 % verify, +4 % Zipf
+constexpr bool kIL = true;  // interleaved ticket groups (Tickets<IL>): +3 % Zipf, box-dependent +-3 % verify
 
 // Work distribution.  Static: wave w takes files w, w+W, w+2W, ... (W = all
 // waves) -- ideal when every file has the same size.  Dynamic: eight ticket
@@ -501,17 +501,26 @@ constexpr bool kIL = true;  // interleaved ticket groups (Tickets<IL>): +2 % ver
 // one file ahead, so the atomic's latency hides under a file's work.
 // IL (product default, kIL): group g owns files g, g+8, g+16, ..., so the eight
 // XCDs read one moving address window together; IL = false gives group g the
-// contiguous eighth [n*g/8, n*(g+1)/8) (eight windows 1/8 of the batch apart,
-// 2-4 % slower in interleaved A/B; TFS_CRC_VARIANT=14).
-template <bool IL = false>
+// contiguous eighth [n*g/8, n*(g+1)/8) (eight windows 1/8 of the batch apart;
+// 2.5-3.7 % slower on Zipf, +-3 % box-dependent on uniform files; TFS_CRC_VARIANT=14).
+// W (measurement knob, IL only): W consecutive files per slot -- group g owns
+// files [8Wk + gW, 8Wk + gW + W) -- so fewer file-boundary lines are shared by two XCDs.
+template <bool IL = false, int W = 1>
 struct Tickets {
   uint32_t* ctr;  // 8 zeroed counters for this launch, kSchedStride u32 apart (one per 256-byte line)
   uint32_t n, group;
   __device__ __forceinline__ uint32_t gbegin(uint32_t g) const { return uint32_t((uint64_t(n) * g) >> 3); }
   __device__ __forceinline__ uint32_t gcount(uint32_t g) const {
+    if constexpr (IL && W > 1) {
+      const uint32_t rem = n % (8u * W), lo = g * W;
+      return (n / (8u * W)) * W + (rem > lo ? (rem - lo < uint32_t(W) ? rem - lo : uint32_t(W)) : 0u);
+    }
     return IL ? (n > g ? (n - g + 7u) >> 3 : 0u) : gbegin(g + 1) - gbegin(g);
   }
-  __device__ __forceinline__ uint32_t file_of(uint32_t g, uint32_t j) const { return IL ? j * 8u + g : gbegin(g) + j; }
+  __device__ __forceinline__ uint32_t file_of(uint32_t g, uint32_t j) const {
+    if constexpr (IL && W > 1) return (j / W) * (8u * W) + g * W + j % W;
+    return IL ? j * 8u + g : gbegin(g) + j;
+  }
   // Issue the atomic of the home group in lane 0; the result stays in lane 0's register.
   __device__ __forceinline__ uint32_t issue(int lane) const {
     uint32_t j = 0;
@@ -537,7 +546,8 @@ struct Tickets {
 // Files are software-pipelined per wave: the next file's stripe-0/tail words
 // and its first PF stripes are in flight while this file's lane chains are
 // combined, so HBM never waits on a file boundary.
-template <int MODE, int RUN, int PF, bool NT, bool DYN, bool S8, int G = 1, bool HV = false, bool IL = false>
+template <int MODE, int RUN, int PF, bool NT, bool DYN, bool S8, int G = 1, bool HV = false, bool IL = false,
+          int W = 1>
 __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __restrict__ base,
                                                            const Desc* __restrict__ desc, uint32_t n,
                                                            const Tables* __restrict__ tg, uint32_t* out_crc,
@@ -550,7 +560,7 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
   const uint32_t wpb = kBlock / kWave;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t stride = gridDim.x * wpb;
-  Tickets<IL> tk{sched, n, blockIdx.x & 7u};
+  Tickets<IL, W> tk{sched, n, blockIdx.x & 7u};
   uint32_t f, fn;
   if (DYN) {
     f = tk.resolve(tk.issue(lane), lane);
@@ -1059,6 +1069,14 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
     case 13:
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, true>), grid, block, 0, stream, base,
                          desc, n, tg, out_crc, out_ok, n_bad, sched, vseed);
+      break;
+    case 15:
+      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, true, 2>), grid, block, 0, stream,
+                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed);
+      break;
+    case 16:
+      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, true, 4>), grid, block, 0, stream,
+                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed);
       break;
     case 14:  // contiguous ticket groups (the product before interleaving)
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, false>), grid, block, 0, stream,
