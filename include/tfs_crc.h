@@ -343,6 +343,12 @@ int tfs_crc32_event_destroy(tfs_crc_ctx* ctx, void* ev);
 /* The ctx's HIP stream (as void*) and a synchronize on it. */
 void* tfs_crc32_stream(tfs_crc_ctx* ctx);
 int tfs_crc32_sync(tfs_crc_ctx* ctx);
+/* Extra non-blocking streams on ctx's device for the *_device calls (each stream
+ * gets its own scheduler slot; at most 255 besides the ctx stream), a
+ * synchronize on one, and its release. */
+int tfs_crc32_stream_create(tfs_crc_ctx* ctx, void** stream);
+int tfs_crc32_stream_sync(tfs_crc_ctx* ctx, void* stream);
+int tfs_crc32_stream_destroy(tfs_crc_ctx* ctx, void* stream);
 
 #ifdef __cplusplus
 }

@@ -59,7 +59,8 @@ EXPORTED = [
     "tfs_crc32_dev_malloc", "tfs_crc32_dev_free", "tfs_crc32_host_malloc_pinned", "tfs_crc32_host_free_pinned",
     "tfs_crc32_memcpy", "tfs_crc32_memset_device", "tfs_crc32_event_create", "tfs_crc32_event_record",
     "tfs_crc32_event_elapsed_ms", "tfs_crc32_event_destroy",
-    "tfs_crc32_stream", "tfs_crc32_sync",
+    "tfs_crc32_stream", "tfs_crc32_sync", "tfs_crc32_stream_create", "tfs_crc32_stream_sync",
+    "tfs_crc32_stream_destroy",
     "tfs_packet_verify", "tfs_packet_verify_device", "tfs_packet_seal", "tfs_packet_seal_device",
     "tfs_crc32_write_packet_headers_device", "tfs_block_compact_device", "tfs_compact_jobs_device",
 ]
@@ -125,6 +126,9 @@ def lib():
             "tfs_crc32_event_destroy": (ctypes.c_int, [vp, vp]),
             "tfs_crc32_stream": (vp, [vp]),
             "tfs_crc32_sync": (ctypes.c_int, [vp]),
+            "tfs_crc32_stream_create": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
+            "tfs_crc32_stream_sync": (ctypes.c_int, [vp, vp]),
+            "tfs_crc32_stream_destroy": (ctypes.c_int, [vp, vp]),
             "tfs_packet_verify": (ctypes.c_int, [vp, vp, u32, vp, u64, vp, vp, vp]),
             "tfs_packet_verify_device": (ctypes.c_int, [vp, vp, u32, vp, vp, vp, vp, vp]),
             "tfs_packet_seal": (ctypes.c_int, [vp, vp, u32, vp, u64, vp, vp]),
@@ -205,6 +209,17 @@ class Context:
 
     def sync(self):
         self._check(lib().tfs_crc32_sync(self.handle), "sync")
+
+    def stream_create(self):
+        p = ctypes.c_void_p()
+        self._check(lib().tfs_crc32_stream_create(self.handle, ctypes.byref(p)), "stream_create")
+        return p.value
+
+    def stream_sync(self, stream):
+        self._check(lib().tfs_crc32_stream_sync(self.handle, stream), "stream_sync")
+
+    def stream_destroy(self, stream):
+        self._check(lib().tfs_crc32_stream_destroy(self.handle, stream), "stream_destroy")
 
     # ---- host-memory batches -------------------------------------------------
     def batch(self, base, offsets, lens, seeds=0):

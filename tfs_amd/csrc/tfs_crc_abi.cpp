@@ -24,7 +24,7 @@
 namespace tfscrc {
 hipError_t launch_crc_files(int mode, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
                             uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
-                            int variant, uint32_t vseed);
+                            int variant, uint32_t vseed, uint32_t* done_flag, uint32_t seq);
 hipError_t launch_packet_parse(const uint8_t* base, const PacketDesc* pd, uint32_t n, int mode, Desc* desc,
                                int32_t* pre, hipStream_t stream);
 hipError_t launch_packet_finish(uint8_t* base, const PacketDesc* pd, const Desc* desc, uint32_t n, int mode,
@@ -82,10 +82,12 @@ struct DevBuf {
   }
 };
 
-// Growable pinned host allocation.
+// Growable pinned host allocation.  `coherent`: fine-grained memory for words
+// the GPU writes while the host polls them (verdicts, completion flags).
 struct PinBuf {
   void* p = nullptr;
   size_t cap = 0;
+  bool coherent = false;
   hipError_t reserve(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
     if (p) (void)hipHostFree(p);
@@ -93,7 +95,7 @@ struct PinBuf {
     cap = 0;
     size_t want = std::max<size_t>(bytes, 4096);
     want = (want + 0xFFFF) & ~size_t(0xFFFF);
-    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(&p, want, coherent ? hipHostMallocCoherent : hipHostMallocDefault);
     if (e == hipSuccess) cap = want;
     return e;
   }
@@ -107,12 +109,15 @@ struct PinBuf {
 // One in-flight host-memory submission (async API) or the scratch of a sync call.
 struct Slot {
   DevBuf d_data, d_desc, d_crc, d_ok, d_bad, d_aux;
-  PinBuf h_data, h_crc, h_ok, h_bad, h_desc;
+  PinBuf h_data, h_crc, h_ok, h_bad, h_desc, h_flag;
   hipEvent_t done = nullptr;
   bool busy = false;
   uint64_t ticket = 0;
   int status = TFS_SUCCESS;
   bool count_bad = false;  // zero-copy launch: n_bad is counted from h_ok
+  bool spin = false;       // zero-copy launch: completion = h_flag reaching `seq`
+  uint32_t seq = 0;
+  Slot() { h_crc.coherent = h_ok.coherent = h_bad.coherent = h_flag.coherent = true; }
   // user outputs for the async path
   uint32_t n = 0;
   uint32_t* out_crc = nullptr;
@@ -120,7 +125,7 @@ struct Slot {
   uint32_t* n_bad = nullptr;
   void release() {
     d_data.release(); d_desc.release(); d_crc.release(); d_ok.release(); d_bad.release(); d_aux.release();
-    h_data.release(); h_crc.release(); h_ok.release(); h_bad.release(); h_desc.release();
+    h_data.release(); h_crc.release(); h_ok.release(); h_bad.release(); h_desc.release(); h_flag.release();
     if (done) (void)hipEventDestroy(done);
     done = nullptr;
   }
@@ -162,10 +167,14 @@ struct tfs_crc_ctx {
   Slot slots[kSlots];
   CompactSlot cslots[kCompactSlots];
   uint64_t next_ticket = 1;
-  // Work-distribution counters: kSchedSlots slots of 8 counters (one 256-byte
-  // line per counter), one slot per launch, zeroed on the launch stream first.
+  // Work-distribution counters: kSchedSlots slots of 8 ticket counters and a
+  // finished-waves counter (one 256-byte line each).  A slot belongs to one
+  // stream (slot 0 = ctx->stream), so the launches sharing it are ordered; each
+  // launch leaves it zeroed (launch_exit in the kernels).
   uint32_t* d_sched = nullptr;
-  std::atomic<uint32_t> sched_seq{0};
+  std::mutex sched_mu;
+  std::vector<hipStream_t> sched_streams;
+  std::atomic<uint32_t> flag_seq{0};  // completion-flag values of zero-copy launches
   int compact_slots = 8;  // blocks in flight in tfs_blocks_compact (TFS_CRC_COMPACT_SLOTS, 1..8)
   int variant = 0;  // kernel variant (TFS_CRC_VARIANT, measurement knob; 0 = product default)
   DevBuf packet_scratch;  // device-resident packet calls (parse descriptors, verdicts)
@@ -203,6 +212,8 @@ void build_tables(Tables* t) {
     make_shift_table(t->stripe64_8[ri], 64 * run);
     for (int j = 0; j < kLevels; ++j) make_shift_table(t->level8[ri][j], run << j);
   }
+  make_shift_table5(t->wg_jump, 16ull * (64ull * kWgWaves - 1ull));
+  for (int j = 0; j < kWgLevels; ++j) make_shift_table5(t->wg_level[j], 16ull << j);
 }
 
 bool is_pinned_host(const void* p) {
@@ -251,11 +262,44 @@ int stage_span(tfs_crc_ctx* ctx, Slot& s, const void* base, uint64_t lo, uint64_
   return TFS_SUCCESS;
 }
 
-// A zeroed scheduler slot for one launch on `st` (see tfs_crc_ctx::d_sched).
+// The scheduler slot of stream `st` (see tfs_crc_ctx::d_sched).  Launches on
+// one stream are ordered and each leaves its slot zeroed, so no memset launch is
+// needed; two streams never share a slot.
 hipError_t sched_slot(tfs_crc_ctx* ctx, hipStream_t st, uint32_t** out) {
-  const uint32_t k = ctx->sched_seq.fetch_add(1) % kSchedSlots;
+  std::lock_guard<std::mutex> g(ctx->sched_mu);
+  size_t k = 0;
+  while (k < ctx->sched_streams.size() && ctx->sched_streams[k] != st) ++k;
+  if (k == ctx->sched_streams.size()) {
+    k = 0;  // a slot released by tfs_crc32_stream_destroy, else a new one
+    while (k < ctx->sched_streams.size() && ctx->sched_streams[k] != nullptr) ++k;
+    if (k == kSchedSlots) return hipErrorOutOfMemory;  // more than 256 live streams on one context
+    if (k == ctx->sched_streams.size()) ctx->sched_streams.push_back(st);
+    else ctx->sched_streams[k] = st;
+  }
   *out = ctx->d_sched + (kSchedSlotBytes / 4u) * k;
-  return hipMemsetAsync(*out, 0, kSchedSlotBytes, st);
+  return hipSuccess;
+}
+
+// Host side of a zero-copy launch's completion: spin on the page-locked flag
+// the kernel's last workgroup stores (launch_exit); the event recorded behind
+// the kernel is polled now and then so a failed launch is reported, never
+// waited on forever.
+int wait_flag(tfs_crc_ctx* ctx, Slot& s) {
+  volatile uint32_t* fl = static_cast<volatile uint32_t*>(s.h_flag.p);
+  for (uint32_t spins = 1; *fl != s.seq; ++spins) {
+    __builtin_ia32_pause();
+    if ((spins & 255u) == 0) {
+      const hipError_t e = hipEventQuery(s.done);
+      if (e == hipSuccess) {
+        if (*fl == s.seq) break;
+        return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "kernel completed without its completion flag (seq %u)",
+                       s.seq);
+      }
+      if (e != hipErrorNotReady)
+        return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "zero-copy launch failed: %s", hipGetErrorString(e));
+    }
+  }
+  return TFS_SUCCESS;
 }
 
 Slot* free_slot(tfs_crc_ctx* ctx) {
@@ -276,26 +320,44 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
   HIP_TRY(ctx, s.h_crc.reserve(size_t(n) * 4));
   HIP_TRY(ctx, s.h_ok.reserve(n));
   HIP_TRY(ctx, s.h_bad.reserve(4));
+  HIP_TRY(ctx, s.h_flag.reserve(64));
   if (!s.done) HIP_TRY(ctx, hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
-  // A small batch in page-locked memory (a CloseBatcher batch, one file read): the
-  // kernel reads payloads and descriptors and writes its verdicts in host memory,
-  // one launch instead of H2D + launch + three D2H.  Such calls are latency-bound.
-  if (ctx->variant != kVariantDmaCompact && hi - lo <= kZeroCopySpan && is_pinned_host(base)) {
+  s.spin = false;
+  // A small batch (a CloseBatcher batch, one scalar Func::crc, one file read):
+  // the kernel reads payloads and descriptors from page-locked memory and writes
+  // its verdicts and a completion flag there -- one launch, no copies, and the
+  // host spins on the flag instead of an event.  Pageable payloads are first
+  // copied into the slot's page-locked staging buffer.  Such calls are bound by
+  // latency, not bandwidth.
+  if (ctx->variant != kVariantDmaCompact && hi - lo <= kZeroCopySpan) {
+    void* host_span = nullptr;  // page-locked host address of base + lo
+    if (is_pinned_host(base)) {
+      host_span = const_cast<uint8_t*>(static_cast<const uint8_t*>(base) + lo);
+    } else {
+      (void)hipGetLastError();
+      HIP_TRY(ctx, s.h_data.reserve(hi - lo + 16));
+      if (hi > lo) memcpy(s.h_data.p, static_cast<const uint8_t*>(base) + lo, hi - lo);
+      host_span = s.h_data.p;
+    }
     HIP_TRY(ctx, s.h_desc.reserve(size_t(n) * sizeof(Desc)));
     memcpy(s.h_desc.p, d, size_t(n) * sizeof(Desc));
-    void *zb = nullptr, *zd = nullptr, *zcrc = nullptr, *zok = nullptr;
-    if (hipHostGetDevicePointer(&zb, const_cast<void*>(base), 0) == hipSuccess &&
+    void *zb = nullptr, *zd = nullptr, *zcrc = nullptr, *zok = nullptr, *zflag = nullptr;
+    if (hipHostGetDevicePointer(&zb, host_span, 0) == hipSuccess &&
         hipHostGetDevicePointer(&zd, s.h_desc.p, 0) == hipSuccess &&
         hipHostGetDevicePointer(&zcrc, s.h_crc.p, 0) == hipSuccess &&
-        hipHostGetDevicePointer(&zok, s.h_ok.p, 0) == hipSuccess) {
+        hipHostGetDevicePointer(&zok, s.h_ok.p, 0) == hipSuccess &&
+        hipHostGetDevicePointer(&zflag, s.h_flag.p, 0) == hipSuccess) {
       uint32_t* sched = nullptr;
       HIP_TRY(ctx, sched_slot(ctx, ctx->stream, &sched));
+      s.seq = ctx->flag_seq.fetch_add(1) + 1u;
+      if (s.seq == 0) s.seq = ctx->flag_seq.fetch_add(1) + 1u;  // 0 is the flag's initial value
       // n_bad is counted from the verdicts on the host (no atomics on host memory)
-      HIP_TRY(ctx, launch_crc_files(mode, static_cast<const uint8_t*>(zb), static_cast<const Desc*>(zd), n,
-                                    ctx->d_tables, static_cast<uint32_t*>(zcrc), static_cast<uint8_t*>(zok),
-                                    nullptr, sched, ctx->stream, ctx->variant, 0u));
+      HIP_TRY(ctx, launch_crc_files(mode, static_cast<const uint8_t*>(zb) - lo, static_cast<const Desc*>(zd), n,
+                                    ctx->d_tables, static_cast<uint32_t*>(zcrc), static_cast<uint8_t*>(zok), nullptr,
+                                    sched, ctx->stream, ctx->variant, 0u, static_cast<uint32_t*>(zflag), s.seq));
       HIP_TRY(ctx, hipEventRecord(s.done, ctx->stream));
       s.count_bad = true;
+      s.spin = true;
       return TFS_SUCCESS;
     }
     (void)hipGetLastError();  // not mappable: stage it
@@ -308,31 +370,30 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
   HIP_TRY(ctx, s.d_crc.reserve(size_t(n) * 4));
   HIP_TRY(ctx, s.d_ok.reserve(n));
   HIP_TRY(ctx, s.d_bad.reserve(4));
-  HIP_TRY(ctx, s.h_crc.reserve(size_t(n) * 4));
-  HIP_TRY(ctx, s.h_ok.reserve(n));
-  HIP_TRY(ctx, s.h_bad.reserve(4));
-  // descriptors go through pinned memory too (h_ok doubles as nothing here; use d_aux staging)
-  HIP_TRY(ctx, s.d_aux.reserve(16));
   HIP_TRY(ctx, hipMemcpyAsync(s.d_desc.p, d, size_t(n) * sizeof(Desc), hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(ctx, hipMemsetAsync(s.d_bad.p, 0, 4, ctx->stream));
   uint32_t* sched = nullptr;
   HIP_TRY(ctx, sched_slot(ctx, ctx->stream, &sched));
   HIP_TRY(ctx, launch_crc_files(mode, d_base, static_cast<const Desc*>(s.d_desc.p), n, ctx->d_tables,
                                 static_cast<uint32_t*>(s.d_crc.p), static_cast<uint8_t*>(s.d_ok.p),
-                                static_cast<uint32_t*>(s.d_bad.p), sched, ctx->stream, ctx->variant, 0u));
+                                static_cast<uint32_t*>(s.d_bad.p), sched, ctx->stream, ctx->variant, 0u, nullptr, 0u));
   HIP_TRY(ctx, hipMemcpyAsync(s.h_crc.p, s.d_crc.p, size_t(n) * 4, hipMemcpyDeviceToHost, ctx->stream));
   if (mode == 1) {
     HIP_TRY(ctx, hipMemcpyAsync(s.h_ok.p, s.d_ok.p, n, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(s.h_bad.p, s.d_bad.p, 4, hipMemcpyDeviceToHost, ctx->stream));
   }
-  if (!s.done) HIP_TRY(ctx, hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
   HIP_TRY(ctx, hipEventRecord(s.done, ctx->stream));
   return TFS_SUCCESS;
 }
 
 int finish_slot(tfs_crc_ctx* ctx, Slot& s, int mode, uint32_t n, uint32_t* out_crc, uint8_t* out_ok,
                 uint32_t* n_bad) {
-  HIP_TRY(ctx, hipEventSynchronize(s.done));
+  if (s.spin) {
+    const int rc = wait_flag(ctx, s);
+    if (rc) return rc;
+  } else {
+    HIP_TRY(ctx, hipEventSynchronize(s.done));
+  }
   if (out_crc && n) memcpy(out_crc, s.h_crc.p, size_t(n) * 4);
   if (mode == 1 && s.count_bad) {
     const uint8_t* ok = static_cast<const uint8_t*>(s.h_ok.p);
@@ -409,6 +470,9 @@ int tfs_crc32_ctx_create(int device, tfs_crc_ctx** out) {
     if (e != hipSuccess) { rc = set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "hipMemcpy(tables): %s", hipGetErrorString(e)); break; }
     e = hipMalloc(reinterpret_cast<void**>(&ctx->d_sched), size_t(kSchedSlots) * kSchedSlotBytes);
     if (e != hipSuccess) { rc = set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "hipMalloc(sched): %s", hipGetErrorString(e)); break; }
+    e = hipMemset(ctx->d_sched, 0, size_t(kSchedSlots) * kSchedSlotBytes);  // then kept zero by the kernels
+    if (e != hipSuccess) { rc = set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "hipMemset(sched): %s", hipGetErrorString(e)); break; }
+    ctx->sched_streams.push_back(ctx->stream);
   } while (0);
   *out = ctx;  // returned even on failure so the caller can read last_error; destroy it
   return rc;
@@ -515,7 +579,7 @@ int tfs_crc32_batch_device(tfs_crc_ctx* ctx, const tfs_crc_desc* d_desc, uint32_
   uint32_t* sched = nullptr;
   HIP_TRY(ctx, sched_slot(ctx, st, &sched));
   HIP_TRY(ctx, launch_crc_files(0, static_cast<const uint8_t*>(d_base), reinterpret_cast<const Desc*>(d_desc), n,
-                                ctx->d_tables, d_out_crc, nullptr, nullptr, sched, st, ctx->variant, 0u));
+                                ctx->d_tables, d_out_crc, nullptr, nullptr, sched, st, ctx->variant, 0u, nullptr, 0u));
   return TFS_SUCCESS;
 }
 
@@ -527,7 +591,7 @@ int tfs_crc32_verify_device(tfs_crc_ctx* ctx, const tfs_crc_vdesc* d_desc, uint3
   uint32_t* sched = nullptr;
   HIP_TRY(ctx, sched_slot(ctx, st, &sched));
   HIP_TRY(ctx, launch_crc_files(1, static_cast<const uint8_t*>(d_base), reinterpret_cast<const Desc*>(d_desc), n,
-                                ctx->d_tables, d_out_crc, d_out_ok, d_n_bad, sched, st, ctx->variant, 0u));
+                                ctx->d_tables, d_out_crc, d_out_ok, d_n_bad, sched, st, ctx->variant, 0u, nullptr, 0u));
   return TFS_SUCCESS;
 }
 
@@ -870,7 +934,7 @@ static int packet_enqueue(tfs_crc_ctx* ctx, int mode, const PacketDesc* d_pd, ui
   uint32_t* sched = nullptr;
   HIP_TRY(ctx, sched_slot(ctx, st, &sched));
   HIP_TRY(ctx, launch_crc_files(mode, d_base, d_desc, n, ctx->d_tables, crc, mode == 1 ? d_ok : nullptr, nullptr,
-                                sched, st, ctx->variant, kPacketFlagV1));
+                                sched, st, ctx->variant, kPacketFlagV1, nullptr, 0u));
   HIP_TRY(ctx, launch_packet_finish(d_base, d_pd, d_desc, n, mode, d_pre, d_ok, crc, d_status, d_n_bad, st));
   return TFS_SUCCESS;
 }
@@ -1099,6 +1163,37 @@ int tfs_crc32_sync(tfs_crc_ctx* ctx) {
   if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_stream_create(tfs_crc_ctx* ctx, void** stream) {
+  if (!ctx || !stream) return TFS_EXIT_PARAMETER_ERROR;
+  *stream = nullptr;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  hipStream_t st = nullptr;
+  HIP_TRY(ctx, hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  *stream = st;
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_stream_sync(tfs_crc_ctx* ctx, void* stream) {
+  if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  HIP_TRY(ctx, hipStreamSynchronize(stream ? static_cast<hipStream_t>(stream) : ctx->stream));
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_stream_destroy(tfs_crc_ctx* ctx, void* stream) {
+  if (!ctx || !stream || stream == ctx->stream) return TFS_EXIT_PARAMETER_ERROR;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  HIP_TRY(ctx, hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+  {
+    // Its scheduler slot is zero (every launch leaves it so) and may be rebound.
+    std::lock_guard<std::mutex> g(ctx->sched_mu);
+    for (auto& s : ctx->sched_streams)
+      if (s == static_cast<hipStream_t>(stream)) s = nullptr;
+  }
+  HIP_TRY(ctx, hipStreamDestroy(static_cast<hipStream_t>(stream)));
   return TFS_SUCCESS;
 }
 

@@ -34,9 +34,27 @@ template <bool S8> struct LdsLayout {
 constexpr int kFileInfoSize = 36;  // sizeof(FileInfo), internal.h:432-446
 
 // Dynamic work distribution: 8 ticket counters per launch, each on its own
-// 256-byte line (atomics to one line serialise: ~88 per us for the whole line).
+// 256-byte line (atomics to one line serialise: ~88 per us for the whole line),
+// and a ninth line counting finished waves (or workgroups).  A slot is bound to
+// one stream, so its launches are ordered; the last wave (workgroup) to finish
+// zeroes the slot, so the next launch on that stream finds it clean without a
+// memset launch in between.
 constexpr uint32_t kSchedStride = 64;                    // u32 between counters
-constexpr uint32_t kSchedSlotBytes = 8u * kSchedStride * 4u;  // 2 KiB per launch
+constexpr uint32_t kSchedDone = 8u * kSchedStride;       // index of the finished-waves counter
+constexpr uint32_t kSchedSlotBytes = 9u * kSchedStride * 4u;  // 2.25 KiB per stream
+
+// Latency form (small batches): one workgroup of kWgWaves waves per file; wave w
+// takes stripes w, w+16, ... of the file, so a 64 KiB file is 4-5 stripes per
+// wave instead of 65 in one wave.  Lane chains jump over the 1023 foreign runs
+// between two of their stripes (shift(c, 16*1023)), are moved into place with
+// shift(c, 16*d) for d < 2^kWgLevels runs, XOR-reduced in the wave, then across
+// waves through LDS.  Shift tables in 5-bit form (conflict-free, 1 KiB each).
+constexpr int kWgWaves = kBlock / kWave;  // 16
+constexpr int kWgLevels = 11;             // 16 B * 2^0 .. 2^10
+constexpr uint32_t kWgMaxFiles = 256;     // batches up to this many files take the latency form
+constexpr uint32_t kWgJumpOff = 4u * 256u * 32u * 4u;             // after the replicated slice tables (128 KiB)
+constexpr uint32_t kWgLevelOff = kWgJumpOff + 1024u;
+constexpr uint32_t kWgLdsBytes = kWgLevelOff + uint32_t(kWgLevels) * 1024u;  // 140 KiB
 
 // TFS status codes (src/common/error_msg.h)
 constexpr int32_t kSuccess = 0;
@@ -112,6 +130,8 @@ struct Tables {
   uint32_t stripe8[kNumRuns][4][256];                   // byte-table forms of the same shifts
   uint32_t stripe64_8[kNumRuns][4][256];
   uint32_t level8[kNumRuns][kLevels][4][256];
+  uint32_t wg_jump[kShiftChunks][32];              // latency form: shift(c, 16 * (64 * kWgWaves - 1))
+  uint32_t wg_level[kWgLevels][kShiftChunks][32];  // latency form: shift(c, 16 * 2^j)
 };
 
 constexpr int run_index(int run) { return run == 16 ? 0 : run == 32 ? 1 : run == 64 ? 2 : 3; }

@@ -135,16 +135,24 @@ __device__ __forceinline__ uint32_t steps16(const uint32_t* T, const LaneBase& l
   return step4x(T, lb, x, 0u);
 }
 
+// The 32 copies of the four slice tables (conflict-free lookups).  Dword index
+// i = region<<14 | b<<6 | half<<5 | j (see the address layout above): copies
+// j..j+3 of one entry are adjacent, so each thread writes four copies with one
+// 16-byte LDS store (8 per thread for 128 KiB).
+__device__ __forceinline__ void load_slice_tables(uint32_t* T, const Tables* __restrict__ tg) {
+  for (uint32_t q = threadIdx.x; q < 4u * 256u * 8u; q += blockDim.x) {
+    const uint32_t region = q >> 12, b = (q >> 4) & 255u, half = (q >> 3) & 1u;
+    const uint32_t t = 3u - (region * 2u + half);  // T3, T2, T1, T0
+    const uint32_t v = tg->slice[t][b];
+    *reinterpret_cast<uint4*>(T + 4u * q) = make_uint4(v, v, v, v);
+  }
+}
+
 // Stage the tables: 32 copies of each slice table (conflict-free lookups) and
 // the stripe-shift tables for RUN.  Every thread of the workgroup takes part.
 template <int RUN, bool PAR, bool S8>
 __device__ __forceinline__ void load_tables(uint32_t* T, const Tables* __restrict__ tg) {
-  // dword index i = region<<14 | b<<6 | half<<5 | j  (see the address layout above)
-  for (uint32_t i = threadIdx.x; i < 4u * 256u * 32u; i += blockDim.x) {
-    const uint32_t region = i >> 14, b = (i >> 6) & 255u, half = (i >> 5) & 1u;
-    const uint32_t t = 3u - (region * 2u + half);  // T3, T2, T1, T0
-    T[i] = tg->slice[t][b];
-  }
+  load_slice_tables(T, tg);
   using LL = LdsLayout<S8>;
   const uint32_t ri = run_index(RUN);
   const uint32_t nent = S8 ? 1024u : kShiftChunks * 32u;
@@ -541,6 +549,27 @@ struct Tickets {
   }
 };
 
+// End of a launch (every wave, or every workgroup, calls this once, after its
+// last ticket atomic has returned): count it on the slot's finished line; the
+// last one zeroes the slot for the next launch on the same stream and, for a
+// zero-copy host batch, stores `seq` into the page-locked completion word the
+// host spins on.  The system-scope fences make each unit's verdicts in host
+// memory visible before it is counted, and all of them before the flag.
+__device__ __forceinline__ void launch_exit(uint32_t* sched, uint32_t units, uint32_t* done_flag, uint32_t seq) {
+  if (done_flag) __threadfence_system();
+  if (!sched) return;
+  const uint32_t old = atomicAdd(&sched[kSchedDone], 1u);
+  if (old + 1u == units) {
+#pragma unroll
+    for (uint32_t gi = 0; gi < 8u; ++gi) atomicExch(&sched[gi * kSchedStride], 0u);
+    atomicExch(&sched[kSchedDone], 0u);
+    if (done_flag) {
+      __threadfence_system();
+      __hip_atomic_store(done_flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 // MODE 0: compute (aux = seed) -> out_crc.  MODE 1: verify (aux = expected, seed
 // `vseed`: 0 for files, TFS_PACKET_FLAG_V1 for packet bodies).
 // Files are software-pipelined per wave: the next file's stripe-0/tail words
@@ -552,7 +581,7 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
                                                            const Desc* __restrict__ desc, uint32_t n,
                                                            const Tables* __restrict__ tg, uint32_t* out_crc,
                                                            uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched,
-                                                           uint32_t vseed) {
+                                                           uint32_t vseed, uint32_t* done_flag, uint32_t seq) {
   __shared__ uint32_t lds_tables[LdsLayout<S8>::bytes / 4];
   load_tables<RUN, false, S8>(lds_tables, tg);
   const int lane = threadIdx.x & (kWave - 1);
@@ -561,14 +590,16 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t stride = gridDim.x * wpb;
   Tickets<IL, W> tk{sched, n, blockIdx.x & 7u};
+  uint32_t bad = 0;
+  do {  // `break` = this wave has no (more) files; every wave reaches launch_exit
   uint32_t f, fn;
   if (DYN) {
     f = tk.resolve(tk.issue(lane), lane);
-    if (f >= n) return;
+    if (f >= n) break;
     fn = tk.resolve(tk.issue(lane), lane);
   } else {
     f = blockIdx.x * wpb + wave;
-    if (f >= n) return;
+    if (f >= n) break;
     fn = f + stride;
   }
   Desc cur = desc[f];
@@ -579,7 +610,6 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
   load_ring<RUN, PF, NT>(g, lane, buf, junk);
   Desc nxt = fn < n ? desc[fn] : Desc{0, 0, 0};
   uint32_t jv = DYN && fn < n ? tk.issue(lane) : 0u;  // ticket of the file after next, in flight
-  uint32_t bad = 0;
   for (;;) {
     const uint32_t c = g.nstripes ? lane_chain<RUN, PF, NT, S8, false, G>(lds_tables, lb, g, h, buf, lane, junk) : 0u;
     // Start the next file's loads before combining this one.
@@ -612,7 +642,167 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
     g = ng;
     h = nh;
   }
+  } while (false);
   if (MODE == 1 && lane == 0 && bad && n_bad) atomicAdd(n_bad, bad);
+  if (lane == 0) launch_exit(sched, gridDim.x * wpb, done_flag, seq);
+}
+
+// ---------------------------------------------------------------------------
+// Latency form: one workgroup of 16 waves per file, for batches
+// of at most kWgMaxFiles files -- a CloseBatcher batch, one scalar Func::crc
+// call, one file read back.  Such calls are bound by latency, not bandwidth:
+// with one wave per file a 64 KiB file is a chain of 65 dependent stripes; here
+// wave w takes stripes w, w+16, ... (4-5 for 64 KiB), all loads in flight at
+// once.  Same stripe geometry and slice tables as crc_files_kernel; lane chains
+// jump over the 1023 foreign runs between two of their stripes, are moved to
+// the end of the body with shift(c, 16*d), XOR-reduced in the wave and then
+// across the 16 waves through LDS.  Wave 0 folds in the tail and writes the
+// verdict.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void load_wg_tables(uint32_t* T, const Tables* __restrict__ tg) {
+  load_slice_tables(T, tg);
+  constexpr uint32_t kEnt = uint32_t(kShiftChunks) * 32u;
+  const uint32_t* jt = tg->wg_jump[0];
+  for (uint32_t i = threadIdx.x; i < kEnt; i += blockDim.x) T[kWgJumpOff / 4u + i] = jt[i];
+  const uint32_t* lv = tg->wg_level[0][0];
+  for (uint32_t i = threadIdx.x; i < uint32_t(kWgLevels) * kEnt; i += blockDim.x)
+    T[(kWgLevelOff + 1024u * (i / kEnt)) / 4u + i % kEnt] = lv[i];
+}
+
+// shift(c, 16 * d) for d < 2^kWgLevels.
+__device__ __forceinline__ uint32_t wg_shift_runs(const uint32_t* T, uint32_t c, uint32_t d) {
+#pragma unroll
+  for (int j = 0; j < kWgLevels; ++j) {
+    const uint32_t sh = shift5(T, kWgLevelOff + 1024u * uint32_t(j), c);
+    c = ((d >> j) & 1u) ? sh : c;
+  }
+  return c;
+}
+
+constexpr int kWgPF = 4;  // stripes in flight per wave
+
+// Address of this lane's run of stripe s (junk past the file / for the head stripe).
+__device__ __forceinline__ uintptr_t wg_run_addr(const FileGeo<16>& g, uint32_t s, int lane, uintptr_t junk) {
+  return (s >= 1u && s < g.nstripes ? g.sb0 + uintptr_t(s) * 1024u : junk) + uintptr_t(lane) * 16u;
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(kBlock) crc_wg_kernel(const uint8_t* __restrict__ base,
+                                                        const Desc* __restrict__ desc, uint32_t n,
+                                                        const Tables* __restrict__ tg, uint32_t* out_crc,
+                                                        uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched,
+                                                        uint32_t vseed, uint32_t* done_flag, uint32_t seq) {
+  __shared__ uint32_t lds_tables[kWgLdsBytes / 4];
+  __shared__ uint32_t part[kWgWaves];
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const LaneBase lb = lane_base_of(lane);
+  const uintptr_t junk = reinterpret_cast<uintptr_t>(tg->slice);
+  uint32_t f = blockIdx.x;
+  Desc cur{0, 0, 0};
+  FileGeo<16> g{};
+  Head<16> h{};
+  uint4 buf[kWgPF];
+  // Issue a file's loads: descriptor, then (wave 0) the head stripe and tail
+  // words, and this wave's first kWgPF stripes.
+  auto issue = [&](uint32_t ff) {
+    cur = desc[ff];
+    g = make_geo<16>(base + cur.offset, cur.len, MODE == 0 ? cur.aux : vseed);
+    if (wave == 0) h = load_head<16>(g, lane);
+#pragma unroll
+    for (int k = 0; k < kWgPF; ++k) buf[k] = ld128s<true>(wg_run_addr(g, wave + 16u * uint32_t(k), lane, junk));
+  };
+  // The first file's loads are in flight while the tables are staged.
+  if (f < n) issue(f);
+  load_wg_tables(lds_tables, tg);
+  __syncthreads();
+  uint32_t bad = 0;
+  while (f < n) {
+    // ---- this wave's lane chains over stripes wave, wave+16, ...
+    const uint32_t K = g.nstripes > wave ? (g.nstripes - 1u - wave) / 16u + 1u : 0u;
+    const uint32_t last = g.nstripes - 1u;
+    const bool lane_in_last = uint32_t(lane) < g.nvalid;
+    const uint32_t headmask = 0xffffffffu << (8 * g.s);
+    const uint32_t seed_lo = g.seed << (8 * g.s);
+    const uint32_t seed_hi = g.s ? (g.seed >> (32 - 8 * g.s)) : 0u;
+    // seed bytes owed to lane 0's first dword of stripe 1 (A is the last dword of stripe 0)
+    const uint32_t inj = (wave == 1 && lane == 0 && g.A + 4 == g.sb0 + 1024u) ? seed_hi : 0u;
+    uint32_t c = 0;
+    for (uint32_t k0 = 0; k0 < K; k0 += kWgPF) {
+#pragma unroll
+      for (int fi = 0; fi < kWgPF; ++fi) {
+        const uint32_t k = k0 + uint32_t(fi);
+        if (k < K) {
+          const uint32_t st = wave + 16u * k;
+          const uint32_t c_old = c;
+          if (k) c = shift5(lds_tables, kWgJumpOff, c);
+          if (st == 0) {  // head stripe: bytes before `start` masked, seed injected at A
+            const uintptr_t lo = g.sb0 + uintptr_t(lane) * 16u;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const uintptr_t q = lo + 4u * i;
+              uint32_t w = h.w[i];
+              w = q == g.A ? ((w & headmask) ^ seed_lo) : w;
+              w = q == g.A + 4 ? (w ^ seed_hi) : w;
+              c = step4(lds_tables, lb, c, w);
+            }
+          } else {
+            c = steps16(lds_tables, lb, c ^ (st == 1u ? inj : 0u), buf[fi]);
+          }
+          c = (st == last && !lane_in_last) ? c_old : c;  // run past B16: not part of the chain
+          buf[fi] = ld128s<true>(wg_run_addr(g, st + 16u * kWgPF, lane, junk));
+        }
+      }
+    }
+    // ---- move the chain to the end of the body: its last valid run is
+    // r = slast*64 + lane of R = (nstripes-1)*64 + nvalid runs
+    uint32_t slast = wave + 16u * (K - 1u);
+    bool has = K > 0u;
+    if (has && slast == last && !lane_in_last) {
+      has = K >= 2u;
+      slast -= 16u;
+    }
+    const uint32_t R = last * 64u + g.nvalid;
+    c = has ? wg_shift_runs(lds_tables, c, R - 1u - (slast * 64u + uint32_t(lane))) : 0u;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) c ^= __shfl_xor(c, m, kWave);
+    if (lane == 0) part[wave] = c;
+    __syncthreads();
+    if (wave == 0) {
+      uint32_t crc;
+      if (g.nstripes == 0) {  // tiny (< kMinParallelLen): the byte loop of func.cpp:429-433
+        crc = g.seed;
+        for (uint32_t i = 0; i < g.len; ++i) crc = step1(lds_tables, lb, crc, ld8(g.start + i));
+      } else {
+        crc = 0;
+#pragma unroll
+        for (int w = 0; w < kWgWaves; ++w) crc ^= part[w];
+        const uint32_t ntw = uint32_t((g.end & ~uintptr_t(3)) - g.B16) / 4u;
+        const uint32_t ntb = uint32_t(g.end & 3u);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+          if (uint32_t(i) < ntw) crc = step4(lds_tables, lb, crc, h.tw[i]);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+          if (uint32_t(i) < ntb) crc = step1(lds_tables, lb, crc, h.tb[i]);
+      }
+      if (lane == 0) {
+        if (out_crc) out_crc[f] = crc;
+        if (MODE == 1) {
+          const bool ok = crc == cur.aux;
+          if (out_ok) out_ok[f] = ok ? 1 : 0;
+          bad += ok ? 0u : 1u;
+        }
+      }
+    }
+    f += gridDim.x;
+    if (f < n) issue(f);
+    __syncthreads();  // part[] is rewritten for the next file
+  }
+  if (threadIdx.x == 0) {
+    if (MODE == 1 && bad && n_bad) atomicAdd(n_bad, bad);
+    launch_exit(sched, gridDim.x, done_flag, seq);
+  }
 }
 
 // The FileInfo fields the checks need (id_ +0, size_ +12, crc_ +32), read from a
@@ -1045,11 +1235,19 @@ static unsigned grid_for(uint32_t nwork) {
 template <int MODE>
 static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
                                  uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched,
-                                 hipStream_t stream, uint32_t vseed) {
+                                 hipStream_t stream, uint32_t vseed, uint32_t* done_flag, uint32_t seq) {
+  // Latency form for small batches of the product configuration (TFS_CRC_VARIANT
+  // 20 forces it for any n; 21 and the measurement variants 1-16 never use it).
+  if (variant == 20 || (variant == 0 && n <= kWgMaxFiles)) {
+    const unsigned wg = n < kMaxGrid ? n : kMaxGrid;
+    hipLaunchKernelGGL((crc_wg_kernel<MODE>), dim3(wg), dim3(kBlock), 0, stream, base, desc, n, tg, out_crc, out_ok,
+                       n_bad, sched, vseed, done_flag, seq);
+    return hipGetLastError();
+  }
   const dim3 grid(grid_for(n)), block(kBlock);
 #define TFS_LAUNCH(R, P, N, D, S)                                                                          \
   hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N, D, S>), grid, block, 0, stream, base, desc, n, tg, out_crc, \
-                     out_ok, n_bad, sched, vseed)
+                     out_ok, n_bad, sched, vseed, done_flag, seq)
   switch (variant) {
     case 1: TFS_LAUNCH(16, 5, true, false, true); break;
     case 2: TFS_LAUNCH(16, 4, true, true, true); break;
@@ -1060,7 +1258,7 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
 #undef TFS_LAUNCH
 #define TFS_LAUNCH_G(R, P, N, D, S, G)                                                                        \
   hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N, D, S, G>), grid, block, 0, stream, base, desc, n, tg, out_crc, \
-                     out_ok, n_bad, sched, vseed)
+                     out_ok, n_bad, sched, vseed, done_flag, seq)
     case 9: TFS_LAUNCH_G(16, 6, true, true, true, 2); break;
     case 10: TFS_LAUNCH_G(16, 6, true, true, true, 3); break;
     case 11: TFS_LAUNCH_G(16, 8, true, true, true, 4); break;
@@ -1068,26 +1266,26 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
 #undef TFS_LAUNCH_G
     case 13:
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, true>), grid, block, 0, stream, base,
-                         desc, n, tg, out_crc, out_ok, n_bad, sched, vseed);
+                         desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
       break;
     case 15:
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, true, 2>), grid, block, 0, stream,
-                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed);
+                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
       break;
     case 16:
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, true, 4>), grid, block, 0, stream,
-                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed);
+                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
       break;
     case 14:  // contiguous ticket groups (the product before interleaving)
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, false>), grid, block, 0, stream,
-                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed);
+                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
       break;
 #define TFS_LAUNCH(R, P, N, D, S)                                                                          \
   hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N, D, S>), grid, block, 0, stream, base, desc, n, tg, out_crc, \
-                     out_ok, n_bad, sched, vseed)
+                     out_ok, n_bad, sched, vseed, done_flag, seq)
     default:
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL>), grid, block, 0, stream,
-                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed);
+                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
       break;
   }
 #undef TFS_LAUNCH
@@ -1096,10 +1294,11 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
 
 hipError_t launch_crc_files(int mode, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
                             uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
-                            int variant, uint32_t vseed) {
+                            int variant, uint32_t vseed, uint32_t* done_flag, uint32_t seq) {
   if (n == 0) return hipSuccess;
-  if (mode == 0) return launch_variant<0>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, sched, stream, vseed);
-  return launch_variant<1>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, sched, stream, vseed);
+  if (mode == 0)
+    return launch_variant<0>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, sched, stream, vseed, done_flag, seq);
+  return launch_variant<1>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, sched, stream, vseed, done_flag, seq);
 }
 
 hipError_t launch_packet_parse(const uint8_t* base, const PacketDesc* pd, uint32_t n, int mode, Desc* desc,

@@ -18,6 +18,8 @@ namespace {
 constexpr int32_t kFileInfoSize = TFS_FILEINFO_SIZE;
 constexpr int32_t kExitReadOffset = -8002;    // EXIT_READ_OFFSET_ERROR, error_msg.h:138
 constexpr int32_t kExitMetaNotFound = -8025;  // EXIT_META_NOT_FOUND_ERROR, error_msg.h:161
+constexpr int32_t kExitBlockExhaust = -8004;  // EXIT_BLOCK_EXHAUST_ERROR, error_msg.h:140
+constexpr int32_t kTfsError = -1;             // TFS_ERROR: DataFile::get_data failed (logic_block.cpp:264-270)
 
 void put_file_info(char* dst, const tfs_file_info& fi) { memcpy(dst, &fi, kFileInfoSize); }
 }  // namespace
@@ -94,21 +96,28 @@ char* DataFile::get_data(char* data, int32_t* len, int32_t offset) {
 
 uint32_t DataFile::get_crc() {
   status_ = TFS_SUCCESS;
-  if (crc_ == 0) {
-    if (length_ > WRITE_DATA_TMPBUF_SIZE) {  // data_file.cpp:172-187: re-read in 2 MiB chunks, running seed
-      if (fd_ == -1 || lseek(fd_, 0, SEEK_SET) == -1) return crc_;
-      ssize_t rlen;
-      while ((rlen = read(fd_, data_.get(), WRITE_DATA_TMPBUF_SIZE)) > 0) {
-        tfs_crc_desc d{0, uint32_t(rlen), crc_};
-        uint32_t out = 0;
-        status_ = tfs_crc32_batch(ctx_, &d, 1, data_.get(), uint64_t(rlen), &out);
-        if (status_ != TFS_SUCCESS) return 0;
-        crc_ = out;
-      }
-    } else {
-      status_ = tfs_datafile_get_crc(ctx_, data_.get(), length_, &crc_);
-      if (status_ != TFS_SUCCESS) crc_ = 0;
+  if (crc_ != 0) return crc_;
+  // The running CRC stays local until every chunk has been computed: a device
+  // failure part-way leaves crc_ at 0 ("not computed", recomputed on the next
+  // call, :170) instead of caching a partial value, and last_status() tells the
+  // close path it was the device, not the client's data.
+  if (length_ > WRITE_DATA_TMPBUF_SIZE) {  // data_file.cpp:172-187: re-read in 2 MiB chunks, running seed
+    if (fd_ == -1 || lseek(fd_, 0, SEEK_SET) == -1) return crc_;
+    uint32_t run = 0;
+    ssize_t rlen;
+    while ((rlen = read(fd_, data_.get(), WRITE_DATA_TMPBUF_SIZE)) > 0) {
+      tfs_crc_desc d{0, uint32_t(rlen), run};
+      uint32_t out = 0;
+      status_ = tfs_crc32_batch(ctx_, &d, 1, data_.get(), uint64_t(rlen), &out);
+      if (status_ != TFS_SUCCESS) return 0;
+      run = out;
     }
+    crc_ = run;
+  } else {
+    uint32_t out = 0;
+    status_ = tfs_datafile_get_crc(ctx_, data_.get(), length_, &out);
+    if (status_ != TFS_SUCCESS) return 0;
+    crc_ = out;
   }
   return crc_;
 }
@@ -132,6 +141,11 @@ int LogicBlockImage::append_record(uint64_t file_id, const char* payload, int32_
   {
     std::unique_lock<std::shared_mutex> g(mu_);
     off = int64_t(data_.size());
+    // Capacity and the int32 FileInfo/RawMeta offset are checked under the lock
+    // that reserves the range, so batched and unbatched closes accept the same
+    // writes and concurrent appends cannot overrun the block together.
+    if (off + int64_t(fi.size_) > capacity_ || off + int64_t(fi.size_) > int64_t(INT32_MAX))
+      return kExitBlockExhaust;
     fi.offset_ = int32_t(off);
     data_.resize(size_t(off + fi.size_));  // moves the image only when past the reservation
     index_[file_id] = tfs_raw_meta{file_id, int32_t(off), fi.size_};
@@ -154,12 +168,12 @@ void LogicBlockImage::reserve(int64_t bytes) {
 
 int LogicBlockImage::close_write_file(uint64_t file_id, DataFile& df, uint32_t crc) {
   const int32_t file_size = df.get_length();
-  if (data_size() + file_size + kFileInfoSize > capacity_) return TFS_EXIT_PARAMETER_ERROR;
+  if (const char* p = df.in_memory_payload()) return append_record(file_id, p, file_size, crc);
   std::vector<char> payload(static_cast<size_t>(file_size));
   int32_t off = 0;
   while (off < file_size) {  // logic_block.cpp:258-306: drain the DataFile
     int32_t rl = file_size - off;
-    if (!df.get_data(payload.data() + off, &rl, off) || rl <= 0) return -1;
+    if (!df.get_data(payload.data() + off, &rl, off) || rl <= 0) return kTfsError;
     off += rl;
   }
   return append_record(file_id, payload.data(), file_size, crc);
@@ -267,7 +281,6 @@ int CloseBatcher::close(const CloseFileInfo& info, DataFile& df, LogicBlockImage
   if (r.status != kAppend) return r.status;
   // Checked: persist from this thread (LogicBlock::close_write_file runs on the
   // worker, logic_block.cpp:156-372), so the appends of a batch run side by side.
-  if (const char* p = df.in_memory_payload()) return block.append_record(info.file_id_, p, df.get_length(), r.crc);
   return block.close_write_file(info.file_id_, df, r.crc);
 }
 
@@ -314,6 +327,11 @@ void CloseBatcher::flush(std::vector<Req*>& reqs) {
     pageable.resize(size_t(total) + 16);
     gathered = pageable.data();
   }
+  // A lease whose payload cannot be read back (spill-file I/O error) is not
+  // verified: it fails with TFS_ERROR as LogicBlock::close_write_file would
+  // (logic_block.cpp:264-270), instead of checking stale gather-buffer bytes.
+  std::vector<size_t> which;  // request index of each descriptor
+  which.reserve(reqs.size());
   uint64_t off = 0;
   for (size_t i = 0; i < reqs.size(); ++i) {
     DataFile& df = *reqs[i]->df;
@@ -324,27 +342,32 @@ void CloseBatcher::flush(std::vector<Req*>& reqs) {
       if (!df.get_data(gathered + off + got, &rl, got) || rl <= 0) break;
       got += rl;
     }
-    d[i] = tfs_crc_vdesc{off, uint32_t(n), reqs[i]->info->crc_};
+    if (got < n) {
+      reqs[i]->status = kTfsError;
+      continue;
+    }
+    d[which.size()] = tfs_crc_vdesc{off, uint32_t(n), reqs[i]->info->crc_};
+    which.push_back(i);
     off += uint64_t(n);
   }
-  std::vector<uint32_t> crc(reqs.size());
-  std::vector<uint8_t> ok(reqs.size());
+  const uint32_t nv = uint32_t(which.size());
+  std::vector<uint32_t> crc(nv);
+  std::vector<uint8_t> ok(nv);
   uint32_t nbad = 0;
   const auto t1 = std::chrono::steady_clock::now();
-  const int rc = tfs_crc32_verify(ctx_, d.data(), uint32_t(reqs.size()), gathered, total, crc.data(), ok.data(),
-                                  &nbad);
+  const int rc = nv ? tfs_crc32_verify(ctx_, d.data(), nv, gathered, off, crc.data(), ok.data(), &nbad) : TFS_SUCCESS;
   const auto t2 = std::chrono::steady_clock::now();
   gather_us_ += std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count();
   verify_us_ += std::chrono::duration_cast<std::chrono::microseconds>(t2 - t1).count();
-  for (size_t i = 0; i < reqs.size(); ++i) {
-    Req& r = *reqs[i];
+  for (size_t k = 0; k < nv; ++k) {
+    Req& r = *reqs[which[k]];
     if (rc != TFS_SUCCESS && rc != TFS_EXIT_CHECK_CRC_ERROR) {
-      r.status = rc;
-    } else if (!ok[i]) {
+      r.status = rc;  // device failure: reported as such, never as client corruption
+    } else if (!ok[k]) {
       r.status = TFS_EXIT_DATA_FILE_ERROR;  // data_management.cpp:198
     } else {
       r.status = kAppend;
-      r.crc = crc[i];
+      r.crc = crc[k];
     }
   }
 }

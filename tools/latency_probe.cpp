@@ -1,0 +1,99 @@
+// latency_probe.cpp -- per-call latency of the small-batch paths of the C ABI
+// (the dataserver's close path: one lease or a CloseBatcher batch per call).
+// Build (CPU side, no HIP headers needed):
+//   g++ -O2 -std=c++17 tools/latency_probe.cpp -Ltfs_amd -ltfs_crc -Wl,-rpath,$PWD/tfs_amd -o tools/latency_probe
+// Prints one JSON object: p50/p99 microseconds per case.
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../include/tfs_crc.h"
+
+static double pct(std::vector<double> v, double p) {
+  std::sort(v.begin(), v.end());
+  return v[std::min(v.size() - 1, size_t(p * double(v.size())))];
+}
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? atoi(argv[1]) : 300;
+  tfs_crc_ctx* ctx = nullptr;
+  if (tfs_crc32_ctx_create(0, &ctx) != TFS_SUCCESS) {
+    fprintf(stderr, "ctx: %s\n", ctx ? tfs_crc32_last_error(ctx) : "?");
+    return 1;
+  }
+  const uint32_t kFile = 65536, kMax = 64;
+  void* pinned = nullptr;
+  tfs_crc32_host_malloc_pinned(ctx, size_t(kMax) * kFile + 64, &pinned);
+  std::vector<char> pageable(size_t(kMax) * kFile + 64);
+  for (size_t i = 0; i < pageable.size(); ++i) pageable[i] = char(i * 2654435761u >> 13);
+  memcpy(pinned, pageable.data(), pageable.size());
+  void* dbuf = nullptr;
+  tfs_crc32_dev_malloc(ctx, pageable.size(), &dbuf);
+  tfs_crc32_memcpy(ctx, dbuf, pageable.data(), pageable.size(), nullptr);
+  void *d_desc = nullptr, *d_ok = nullptr, *d_bad = nullptr;
+  tfs_crc32_dev_malloc(ctx, 16 * kMax, &d_desc);
+  tfs_crc32_dev_malloc(ctx, kMax, &d_ok);
+  tfs_crc32_dev_malloc(ctx, 4, &d_bad);
+
+  std::vector<tfs_crc_vdesc> vd(kMax);
+  std::vector<uint32_t> crc(kMax);
+  std::vector<uint8_t> ok(kMax);
+  for (uint32_t i = 0; i < kMax; ++i) {
+    tfs_crc_desc d{uint64_t(i) * kFile, kFile, 0};
+    tfs_crc32_batch(ctx, &d, 1, pageable.data(), pageable.size(), &crc[i]);
+    vd[i] = tfs_crc_vdesc{uint64_t(i) * kFile, kFile, crc[i]};
+  }
+  tfs_crc32_memcpy(ctx, d_desc, vd.data(), 16 * kMax, nullptr);
+
+  std::string out = "{";
+  auto run = [&](const char* name, std::function<int()> fn) {
+    for (int i = 0; i < 20; ++i) fn();
+    std::vector<double> us;
+    us.reserve(iters);
+    int bad = 0;
+    for (int i = 0; i < iters; ++i) {
+      const auto t0 = std::chrono::steady_clock::now();
+      bad |= fn();
+      const auto t1 = std::chrono::steady_clock::now();
+      us.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
+    }
+    char b[256];
+    snprintf(b, sizeof b, "%s\"%s\": {\"p50_us\": %.1f, \"p99_us\": %.1f, \"status\": %d}", out.size() > 1 ? ", " : "",
+             name, pct(us, 0.5), pct(us, 0.99), bad);
+    out += b;
+  };
+  uint32_t nbad = 0;
+  run("scalar_64k_pageable", [&] { return int(tfs_crc32(0, pageable.data(), kFile) != crc[0]); });
+  run("memset_sync", [&] { return tfs_crc32_memset_device(ctx, d_bad, 0, 4, nullptr) | tfs_crc32_sync(ctx); });
+  for (uint32_t n : {1u, 8u, 64u}) {
+    std::string s = "verify_pinned_n" + std::to_string(n);
+    run(s.c_str(), [&, n] {
+      return tfs_crc32_verify(ctx, vd.data(), n, pinned, size_t(kMax) * kFile, crc.data(), ok.data(), &nbad);
+    });
+    s = "verify_pageable_n" + std::to_string(n);
+    run(s.c_str(), [&, n] {
+      return tfs_crc32_verify(ctx, vd.data(), n, pageable.data(), size_t(kMax) * kFile, crc.data(), ok.data(), &nbad);
+    });
+    s = "verify_device_n" + std::to_string(n);
+    run(s.c_str(), [&, n] {
+      return tfs_crc32_verify_device(ctx, static_cast<tfs_crc_vdesc*>(d_desc), n, dbuf, nullptr,
+                                     static_cast<uint8_t*>(d_ok), nullptr, nullptr) |
+             tfs_crc32_sync(ctx);
+    });
+  }
+  tfs_crc_vdesc tiny{0, 4, 0};
+  {
+    tfs_crc_desc d{0, 4, 0};
+    tfs_crc32_batch(ctx, &d, 1, pageable.data(), 4, &tiny.expected);
+  }
+  run("verify_pinned_4B", [&] { return tfs_crc32_verify(ctx, &tiny, 1, pinned, 4, nullptr, ok.data(), &nbad); });
+  out += "}";
+  printf("%s\n", out.c_str());
+  tfs_crc32_host_free_pinned(ctx, pinned);
+  tfs_crc32_ctx_destroy(ctx);
+  return 0;
+}
