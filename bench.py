@@ -51,6 +51,9 @@ def parse():
     p.add_argument("--blocks", type=int, default=1024, help="resident blocks per GPU (1024 = 1 M files)")
     p.add_argument("--compact-blocks", type=int, default=4096, help="blocks per GPU for --workload compact/e2e")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--parity-every", type=int, default=64,
+                   help="headline: every K-th resident block is checked in full against the oracle "
+                        "(outside the timed region)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--e2e-blocks", type=int, default=128,
                    help="blocks per GPU for the end-to-end (H2D-inclusive) leg of the default line; 0 = off")
@@ -180,11 +183,16 @@ def main():
     d_ok = crc.DeviceBuffer(ctx, nfiles)
     d_bad = crc.DeviceBuffer(ctx, 4)
 
-    # parity spot check of the resident bytes against the oracle (test infrastructure)
+    # Parity outside the timed region (test infrastructure): 48 files' bytes against
+    # the host generator, and every K-th resident block in full -- all 1,024 CRCs
+    # of the block recomputed by the oracle (multi-threaded) over the device's bytes.
     sample_idx = np.linspace(0, nfiles - 1, 48).astype(np.int64)
     ora = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle_crc.so"))
     ora.oracle_crc.restype = ctypes.c_uint32
     ora.oracle_crc.argtypes = [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_int32]
+    ora.oracle_crc_batch_mt.restype = ctypes.c_int
+    ora.oracle_crc_batch_mt.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_int]
     for i in sample_idx:
         o = int(desc["offset"][i])
         host = img.download(np.uint8, FILE_SIZE, o).tobytes()
@@ -192,6 +200,19 @@ def main():
         assert host == synth_bytes(data_seed, FILE_SIZE, g * block_bytes + o % block_bytes).tobytes()
         if ora.oracle_crc(0, host, FILE_SIZE) != int(expected[i]):
             raise SystemExit("GPU CRC disagrees with oracle at file %d" % i)
+    checked = mism = 0
+    bd = np.zeros(FILES_PER_BLOCK, crc.DESC_DTYPE)
+    bd["offset"] = np.arange(FILES_PER_BLOCK, dtype=np.uint64) * rec + FILEINFO
+    bd["len"] = FILE_SIZE
+    bout = np.zeros(FILES_PER_BLOCK, np.uint32)
+    for b in range(0, nblocks, max(1, args.parity_every)):
+        host = img.download(np.uint8, block_bytes, b * block_bytes)
+        ora.oracle_crc_batch_mt(bd.ctypes.data, FILES_PER_BLOCK, host.ctypes.data, bout.ctypes.data,
+                                _cpu_budget())
+        mism += int((bout != expected[b * FILES_PER_BLOCK:(b + 1) * FILES_PER_BLOCK]).sum())
+        checked += FILES_PER_BLOCK
+    if mism:
+        raise SystemExit("GPU CRCs disagree with the oracle on %d of %d fully checked files" % (mism, checked))
 
     def step():
         ctx.verify_device(d_vdesc, nfiles, img, None, d_ok, d_bad)
@@ -218,11 +239,28 @@ def main():
     nbad = int(d_bad.download(np.uint32)[0])
     if nbad:
         raise SystemExit("verify reported %d mismatches on clean data" % nbad)
+    # every file of the last pass has verdict 1 (a skipped file would keep its 0)
+    d_ok.zero()
+    ctx.sync()
+    step()
+    ctx.sync()
+    all_ok = bool((d_ok.download(np.uint8, nfiles) == 1).all())
+    if not all_ok:
+        raise SystemExit("verify left files without a verdict")
     if dist:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        t = torch.tensor([checked, mism, 0 if all_ok else 1], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        checked, mism, all_ok = int(t[0]), int(t[1]), int(t[2]) == 0
+    # the partition by block id: rank r owns global blocks r, r+N, ...
+    parts = [rank_blocks(nblocks * world, world, r) for r in range(world)]
+    allb = np.concatenate(parts)
+    partition = {"rule": "global block g -> rank g % N", "blocks_per_rank": [int(p.size) for p in parts],
+                 "disjoint": bool(np.unique(allb).size == allb.size),
+                 "covers": bool(np.array_equal(np.sort(allb), np.arange(nblocks * world)))}
     payload_bytes = float(world) * args.steps * nfiles * FILE_SIZE
     value = payload_bytes / elapsed / 2**30
     avg_kern_s = float(np.mean(kern_ms)) / 1e3
@@ -279,7 +317,12 @@ def main():
             "file_size": FILE_SIZE,
             "layout": "block image, FileInfo(36 B)|payload, payload 4-byte aligned",
             "partition": "by block id across ranks, no collective",
+            "partition_check": partition,
         },
+        "parity": {"files_checked": checked, "mismatches": mism, "verdicts_all_ok": all_ok,
+                   "method": "every %d-th resident block of every rank: all 1,024 CRCs recomputed by the oracle "
+                             "(pthreads) over the device's bytes; 48 files' bytes vs the host generator; every "
+                             "verdict of a full pass is 1" % max(1, args.parity_every)},
         "roofline": {
             "bound": "hbm",
             "achieved": achieved,
@@ -1179,6 +1222,20 @@ def ec_cpu_baseline(d, k, m, seconds, chunk=4 << 20):
     return {"value": reps * k * chunk / dt / 2**30, "unit": "GiB/s", "cores": 1, "kind": kind,
             "sample": "%d encodes of k=%d x %d MiB (first bytes of the same members), jerasure_bitmatrix_encode "
                       "w=8 ps=128, single thread, %.1f s" % (reps, k, chunk >> 20, dt)}
+
+
+def _cpu_budget():
+    """Host CPUs this process may use: the scheduler affinity capped by the cgroup
+    quota (cpu.max) -- on the GPU box 16 of the machine's 256 hardware threads."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            quota, period = fh.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
 def _cpu_model():

@@ -306,6 +306,52 @@ int tfs_packet_seal(tfs_crc_ctx* ctx, const tfs_packet_desc* d, uint32_t n, void
 int tfs_packet_seal_device(tfs_crc_ctx* ctx, const tfs_packet_desc* d_desc, uint32_t n, void* d_base,
                            uint32_t* d_out_crc, int32_t* d_out_status, void* stream);
 
+/* ---- device group: one context per local GPU --------------- */
+
+/* The dataserver is one process (DataService::initialize, dataservice.cpp:151-377;
+ * PacketQueueThread workers, base_service.cpp:187-192).  A group holds one
+ * context per GPU, each with a host worker thread bound to the GPU's NUMA node
+ * and page-locked memory from that node.  Blocks are routed by block id
+ * (member = block_id % size): a block's files never straddle GPUs and nothing
+ * is exchanged between members -- no collective.  `devices` lists the member
+ * devices (repeats allowed: several contexts on one GPU); NULL = every visible
+ * device.  On failure *out is still set (read tfs_crc_group_last_error, then
+ * destroy it). */
+typedef struct tfs_crc_group tfs_crc_group;
+int tfs_crc_group_create(const int* devices, uint32_t n, tfs_crc_group** out);
+int tfs_crc_group_destroy(tfs_crc_group* g);
+const char* tfs_crc_group_last_error(const tfs_crc_group* g);
+uint32_t tfs_crc_group_size(const tfs_crc_group* g);
+/* Member i's context (for the per-file calls above), and the routing rule. */
+tfs_crc_ctx* tfs_crc_group_ctx(tfs_crc_group* g, uint32_t i);
+uint32_t tfs_crc_group_member_of(const tfs_crc_group* g, uint32_t block_id);
+tfs_crc_ctx* tfs_crc_group_ctx_for_block(tfs_crc_group* g, uint32_t block_id);
+/* NUMA node of member i's GPU (-1 unknown); 1 when its worker thread runs on it. */
+int tfs_crc_group_numa_node(const tfs_crc_group* g, uint32_t i);
+int tfs_crc_group_member_bound(const tfs_crc_group* g, uint32_t i);
+/* Page-locked host memory allocated on member i's NUMA node (block images,
+ * receive buffers of that GPU's blocks). */
+int tfs_crc_group_host_malloc(tfs_crc_group* g, uint32_t i, uint64_t bytes, void** p);
+int tfs_crc_group_host_free(tfs_crc_group* g, uint32_t i, void* p);
+
+/* Verify-on-read of many block images (tfs_block_verify's arguments per job),
+ * each on its block's GPU; members run concurrently.  Returns the worst job
+ * status (TFS_EXIT_CHECK_CRC_ERROR if only CRC mismatches were found). */
+typedef struct tfs_block_verify_job {
+  uint32_t block_id;
+  const void* image;
+  uint64_t image_len;
+  const tfs_raw_meta* metas;
+  uint32_t n;
+  uint32_t* out_crc;    /* n entries or NULL */
+  int32_t* out_status;  /* n entries or NULL */
+  uint32_t n_bad;       /* out */
+  int status;           /* out */
+} tfs_block_verify_job;
+int tfs_crc_group_blocks_verify(tfs_crc_group* g, tfs_block_verify_job* jobs, uint32_t njobs);
+/* Compaction of many blocks (tfs_blocks_compact per member), block_ids[j] routes jobs[j]. */
+int tfs_crc_group_blocks_compact(tfs_crc_group* g, const uint32_t* block_ids, tfs_block_job* jobs, uint32_t njobs);
+
 /* ---- test / bench helpers (not part of the dataserver boundary) -------- */
 
 /* Fill nbytes (multiple of 8) of device memory with the splitmix64 synthetic
@@ -343,6 +389,12 @@ int tfs_crc32_event_destroy(tfs_crc_ctx* ctx, void* ev);
 /* The ctx's HIP stream (as void*) and a synchronize on it. */
 void* tfs_crc32_stream(tfs_crc_ctx* ctx);
 int tfs_crc32_sync(tfs_crc_ctx* ctx);
+/* Fault injection (tests of the callers' error paths, like the reference's
+ * `ds_client send_crc_error`, src/tools/dataserver/ds_client.cpp:522-566): after
+ * `skip` more host-memory submissions (batch / verify / submit / scalar /
+ * block verify / block compaction / packet calls) the next `count` ones fail with
+ * TFS_CRC_EXIT_DEVICE_ERROR before any GPU work.  count = 0 disarms. */
+int tfs_crc32_inject_device_error(tfs_crc_ctx* ctx, uint32_t skip, uint32_t count);
 /* Extra non-blocking streams on ctx's device for the *_device calls (each stream
  * gets its own scheduler slot; at most 255 besides the ctx stream), a
  * synchronize on one, and its release. */

@@ -1,0 +1,179 @@
+"""Multi-GPU drop-in (BASELINE configs[4]): the device group routes
+blocks by block id to one context per GPU, members run concurrently, no
+collective.  On the one-GPU test box the group holds two contexts on device 0
+(what a two-GPU node looks like to the routing), so every path that matters --
+routing, per-member worker threads, per-member batchers, NUMA-placed pinned
+images -- runs for real; results are byte-exact against the oracle.  The last
+test launches bench.py as two ranks (torch.distributed.run, gloo) sharing the
+GPU, as the driver launches it on an 8-GPU node."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, ocrc
+from test_gpu_parity import _block_image, _oracle_compact
+from tfs_amd.synth import synth_bytes
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def group():
+    import tfs_amd.crc as crc
+    g = crc.Group([0, 0])
+    yield g
+    g.close()
+
+
+def test_group_routing_and_members(group):
+    import tfs_amd.crc as crc
+    assert group.size() == 2
+    assert [group.member_of(b) for b in range(6)] == [0, 1, 0, 1, 0, 1]
+    h0, h1 = group.ctx(0).handle.value, group.ctx(1).handle.value
+    assert h0 and h1 and h0 != h1
+    assert group.ctx_for_block(7).handle.value == h1
+    assert group.numa_node(0) >= -1
+    # the member contexts compute like any context
+    assert crc.func_crc(0, b"123456789") == 0x2DFD2D88
+    for i in range(2):
+        assert int(group.ctx(i).batch(np.frombuffer(b"123456789", np.uint8), [0], [9])[0]) == 0x2DFD2D88
+
+
+def test_group_blocks_verify_numa_pinned_images(group, oracle):
+    """Eight fragmented block images in page-locked memory from their member's NUMA
+    node, verified in one group call: per-file CRCs and statuses equal the oracle's,
+    corrupted files are found in the right block."""
+    import tfs_amd.crc as crc
+    rng = np.random.default_rng(50)
+    nblk = 8
+    keep, jobs = [], (crc.BlockVerifyJob * nblk)()
+    for b in range(nblk):
+        sizes = [65536] * 24 + [int(x) for x in rng.integers(1, 30000, 16)]
+        img, metas = _block_image(oracle, sizes, seed=500 + b)
+        if b in (3, 6):
+            img[int(metas[b]["offset"]) + 36 + 11] ^= 0x20
+        pin = group.host_malloc(group.member_of(100 + b), img.size)
+        pin.array[:] = img
+        live = np.ascontiguousarray(metas[b % 2::2])
+        out_crc = np.zeros(len(live), np.uint32)
+        out_st = np.zeros(len(live), np.int32)
+        keep.append((pin, img, live, out_crc, out_st))
+        j = jobs[b]
+        j.block_id, j.image, j.image_len = 100 + b, pin.ptr, img.size
+        j.metas, j.n, j.out_crc, j.out_status = live.ctypes.data, len(live), out_crc.ctypes.data, out_st.ctypes.data
+    try:
+        rc = group.blocks_verify(jobs)
+        assert rc == -1010
+        for b, (pin, img, live, out_crc, out_st) in enumerate(keep):
+            for i in range(len(live)):
+                o, sz = int(live[i]["offset"]), int(live[i]["size"])
+                assert int(out_crc[i]) == ocrc(oracle, 0, img[o + 36:o + sz].tobytes()), (b, i)
+                code = oracle.oracle_verify_file(img.ctypes.data, img.size, o, sz, None)
+                assert int(out_st[i]) == code, (b, i)
+            assert jobs[b].n_bad == int((out_st != 0).sum())
+            assert jobs[b].status == (-1010 if jobs[b].n_bad else 0)
+        assert sum(jobs[b].n_bad for b in range(nblk)) == 2     # file b of blocks 3 and 6 (odd index -> in b%2::2)
+    finally:
+        for k in keep:
+            k[0].free()
+
+
+def test_group_blocks_compact_routed(group, oracle):
+    import tfs_amd.crc as crc
+    rng = np.random.default_rng(51)
+    nblk = 6
+    jobs = (crc.BlockJob * nblk)()
+    keep = []
+    for b in range(nblk):
+        sizes = [65536] * 20 + [int(x) for x in rng.integers(1, 20000, 20)]
+        img, metas = _block_image(oracle, sizes, seed=600 + b)
+        flags = np.zeros(len(sizes), np.int32)
+        flags[b % 3::3] = 1
+        cap = int(metas["size"].astype(np.int64).sum()) + 64
+        dest = np.zeros(cap, np.uint8)
+        ok = np.zeros(len(sizes), np.uint8)
+        keep.append((img, metas, flags, dest, ok))
+        j = jobs[b]
+        j.src_image, j.src_len, j.metas, j.flags, j.n = img.ctypes.data, img.size, metas.ctypes.data, \
+            flags.ctypes.data, len(sizes)
+        j.dest_image, j.dest_cap, j.crc_ok = dest.ctypes.data, cap, ok.ctypes.data
+    assert group.blocks_compact(np.arange(200, 200 + nblk), jobs) == 0
+    for b, (img, metas, flags, dest, ok) in enumerate(keep):
+        odest, doff, ook = _oracle_compact(oracle, img, metas, flags)
+        assert jobs[b].dest_len == odest.size and (dest[:odest.size] == odest).all(), b
+        assert (ok == ook).all(), b
+
+
+def test_service_loopback_routes_by_block(group, oracle):
+    """configs[0]'s write+verify over four blocks on a "two-GPU" node: 8 worker
+    threads, each file's DataFile and close on its block's GPU, per-member
+    CloseBatchers; wrong client CRCs are rejected (-8013), every persisted record
+    is byte-exact and carries the oracle's CRC."""
+    import tfs_amd.crc as crc
+    import tfs_amd.dataserver as ds
+    nblk, per, ln = 4, 64, 65536
+    n = nblk * per
+    pay = synth_bytes(0x5E4, n * ln)
+    client = np.array([ocrc(oracle, 0, pay[i * ln:(i + 1) * ln].tobytes()) for i in range(n)], np.uint32)
+    wrong = [5, 77, 130]
+    client[wrong] ^= 0x8000
+    svc = ds.CrcService(group, max_batch=8, max_wait_us=100)
+    blocks = [ds.LogicBlock(300 + b) for b in range(nblk)]
+    try:
+        assert svc.loopback(pay, per, ln, client, 8, blocks) == len(wrong)
+        for b, blk in enumerate(blocks):
+            m, _ = blk.metas()
+            raw = blk.raw()
+            ids = sorted(int(x) for x in m["file_id"])
+            assert ids == [i + 1 for i in range(n) if i % nblk == b and i not in wrong], b
+            for k in range(len(m)):
+                fid, o = int(m["file_id"][k]), int(m["offset"][k])
+                rec = raw[o:o + 36 + ln]
+                fi = np.frombuffer(rec[:36].tobytes(), crc.FILEINFO_DTYPE)[0]
+                assert int(fi["id_"]) == fid and int(fi["size_"]) == ln + 36
+                assert int(fi["crc_"]) == int(client[fid - 1])
+                assert (rec[36:] == pay[(fid - 1) * ln:fid * ln]).all()
+        rc, nb = svc.verify_blocks(blocks)
+        assert rc == 0 and nb.tolist() == [0] * nblk
+        blocks[2].corrupt(36 + 100)
+        rc, nb = svc.verify_blocks(blocks)
+        assert rc == -1010 and nb.tolist() == [0, 0, 1, 0]
+    finally:
+        svc.free()
+        for blk in blocks:
+            blk.free()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_bench_two_ranks_partitioned_by_block(tmp_path):
+    """bench.py as the driver runs it at N = 2 (torch.distributed.run, one process per
+    rank, gloo for the barrier and max-of-times), both ranks on the one GPU: the
+    line reports n_gpus 2, the ranks' blocks are disjoint and cover the set, and
+    every verify pass is clean on every rank (bench.py exits non-zero otherwise)."""
+    env = dict(os.environ, TFS_BENCH_SHARE_DEVICE="1", MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--blocks", "32", "--steps", "2", "--warmup", "1", "--no-cpu", "--e2e-blocks", "4",
+           "--parity-every", "8"]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["value"] > 0 and res["end_to_end"]["value"] > 0
+    part = res["config"]["partition_check"]
+    assert part["disjoint"] and part["covers"] and part["blocks_per_rank"] == [32, 32]
+    assert res["parity"]["files_checked"] >= 4 * 1024 and res["parity"]["mismatches"] == 0
+    assert res["parity"]["verdicts_all_ok"]

@@ -60,7 +60,11 @@ EXPORTED = [
     "tfs_crc32_memcpy", "tfs_crc32_memset_device", "tfs_crc32_event_create", "tfs_crc32_event_record",
     "tfs_crc32_event_elapsed_ms", "tfs_crc32_event_destroy",
     "tfs_crc32_stream", "tfs_crc32_sync", "tfs_crc32_stream_create", "tfs_crc32_stream_sync",
-    "tfs_crc32_stream_destroy",
+    "tfs_crc32_stream_destroy", "tfs_crc32_inject_device_error",
+    "tfs_crc_group_create", "tfs_crc_group_destroy", "tfs_crc_group_last_error", "tfs_crc_group_size",
+    "tfs_crc_group_ctx", "tfs_crc_group_member_of", "tfs_crc_group_ctx_for_block", "tfs_crc_group_numa_node",
+    "tfs_crc_group_member_bound", "tfs_crc_group_host_malloc", "tfs_crc_group_host_free",
+    "tfs_crc_group_blocks_verify", "tfs_crc_group_blocks_compact",
     "tfs_packet_verify", "tfs_packet_verify_device", "tfs_packet_seal", "tfs_packet_seal_device",
     "tfs_crc32_write_packet_headers_device", "tfs_block_compact_device", "tfs_compact_jobs_device",
 ]
@@ -129,6 +133,20 @@ def lib():
             "tfs_crc32_stream_create": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
             "tfs_crc32_stream_sync": (ctypes.c_int, [vp, vp]),
             "tfs_crc32_stream_destroy": (ctypes.c_int, [vp, vp]),
+            "tfs_crc32_inject_device_error": (ctypes.c_int, [vp, u32, u32]),
+            "tfs_crc_group_create": (ctypes.c_int, [vp, u32, ctypes.POINTER(vp)]),
+            "tfs_crc_group_destroy": (ctypes.c_int, [vp]),
+            "tfs_crc_group_last_error": (ctypes.c_char_p, [vp]),
+            "tfs_crc_group_size": (u32, [vp]),
+            "tfs_crc_group_ctx": (vp, [vp, u32]),
+            "tfs_crc_group_member_of": (u32, [vp, u32]),
+            "tfs_crc_group_ctx_for_block": (vp, [vp, u32]),
+            "tfs_crc_group_numa_node": (ctypes.c_int, [vp, u32]),
+            "tfs_crc_group_member_bound": (ctypes.c_int, [vp, u32]),
+            "tfs_crc_group_host_malloc": (ctypes.c_int, [vp, u32, u64, ctypes.POINTER(vp)]),
+            "tfs_crc_group_host_free": (ctypes.c_int, [vp, u32, vp]),
+            "tfs_crc_group_blocks_verify": (ctypes.c_int, [vp, vp, u32]),
+            "tfs_crc_group_blocks_compact": (ctypes.c_int, [vp, vp, vp, u32]),
             "tfs_packet_verify": (ctypes.c_int, [vp, vp, u32, vp, u64, vp, vp, vp]),
             "tfs_packet_verify_device": (ctypes.c_int, [vp, vp, u32, vp, vp, vp, vp, vp]),
             "tfs_packet_seal": (ctypes.c_int, [vp, vp, u32, vp, u64, vp, vp]),
@@ -170,7 +188,15 @@ def _as_u8(data):
 class Context:
     """One per GPU: wraps tfs_crc_ctx (device tables, stream, staging pools)."""
 
+    @classmethod
+    def wrap(cls, handle, device):
+        """A non-owning view of a context owned elsewhere (a Group member)."""
+        c = cls.__new__(cls)
+        c.handle, c.device, c._owned = ctypes.c_void_p(handle), device, False
+        return c
+
     def __init__(self, device=0):
+        self._owned = True
         h = ctypes.c_void_p()
         rc = lib().tfs_crc32_ctx_create(device, ctypes.byref(h))
         if rc != TFS_SUCCESS:
@@ -182,7 +208,7 @@ class Context:
         self.device = device
 
     def close(self):
-        if self.handle is not None and self.handle.value:
+        if getattr(self, "_owned", True) and self.handle is not None and self.handle.value:
             lib().tfs_crc32_ctx_destroy(self.handle)
         self.handle = None
 
@@ -209,6 +235,10 @@ class Context:
 
     def sync(self):
         self._check(lib().tfs_crc32_sync(self.handle), "sync")
+
+    def inject_device_error(self, skip=0, count=1):
+        """Fault injection: the next `count` host submissions after `skip` fail with -20001."""
+        self._check(lib().tfs_crc32_inject_device_error(self.handle, skip, count), "inject_device_error")
 
     def stream_create(self):
         p = ctypes.c_void_p()
@@ -396,6 +426,80 @@ class Context:
         return dest[:dlen.value], dmetas[:nlive.value], ok, rc
 
 
+class BlockVerifyJob(ctypes.Structure):
+    """tfs_block_verify_job (include/tfs_crc.h)."""
+    _fields_ = [("block_id", ctypes.c_uint32), ("image", ctypes.c_void_p), ("image_len", ctypes.c_uint64),
+                ("metas", ctypes.c_void_p), ("n", ctypes.c_uint32), ("out_crc", ctypes.c_void_p),
+                ("out_status", ctypes.c_void_p), ("n_bad", ctypes.c_uint32), ("status", ctypes.c_int)]
+
+
+class Group:
+    """tfs_crc_group: one context per GPU, blocks routed by block id (block_id % size)."""
+
+    def __init__(self, devices=None):
+        h = ctypes.c_void_p()
+        arr = (ctypes.c_int * len(devices))(*devices) if devices else None
+        rc = lib().tfs_crc_group_create(arr, len(devices) if devices else 0, ctypes.byref(h))
+        if rc != TFS_SUCCESS:
+            msg = lib().tfs_crc_group_last_error(h).decode() if h.value else "group_create failed"
+            if h.value:
+                lib().tfs_crc_group_destroy(h)
+            raise TfsCrcError(rc, "tfs_crc_group_create: %s" % msg)
+        self.handle = h
+        self.devices = list(devices) if devices else list(range(lib().tfs_crc_group_size(h)))
+
+    def close(self):
+        if self.handle is not None and self.handle.value:
+            lib().tfs_crc_group_destroy(self.handle)
+        self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what, ok=(TFS_SUCCESS,)):
+        if rc not in ok:
+            raise TfsCrcError(rc, "%s: %s" % (what, lib().tfs_crc_group_last_error(self.handle).decode()))
+        return rc
+
+    def size(self):
+        return lib().tfs_crc_group_size(self.handle)
+
+    def ctx(self, i):
+        return Context.wrap(lib().tfs_crc_group_ctx(self.handle, i), self.devices[i])
+
+    def member_of(self, block_id):
+        return lib().tfs_crc_group_member_of(self.handle, block_id)
+
+    def ctx_for_block(self, block_id):
+        return self.ctx(self.member_of(block_id))
+
+    def numa_node(self, i):
+        return lib().tfs_crc_group_numa_node(self.handle, i)
+
+    def member_bound(self, i):
+        return bool(lib().tfs_crc_group_member_bound(self.handle, i))
+
+    def host_malloc(self, i, nbytes):
+        """Page-locked memory on member i's NUMA node, as a PinnedBuffer."""
+        p = ctypes.c_void_p()
+        self._check(lib().tfs_crc_group_host_malloc(self.handle, i, nbytes, ctypes.byref(p)), "group_host_malloc")
+        return PinnedBuffer.adopt(self.ctx(i), p.value, nbytes,
+                                  lambda ptr, g=self.handle, m=i: lib().tfs_crc_group_host_free(g, m, ptr))
+
+    def blocks_verify(self, jobs):
+        rc = lib().tfs_crc_group_blocks_verify(self.handle, ctypes.cast(jobs, ctypes.c_void_p), len(jobs))
+        return self._check(rc, "group_blocks_verify", ok=(TFS_SUCCESS, TFS_EXIT_CHECK_CRC_ERROR))
+
+    def blocks_compact(self, block_ids, jobs):
+        ids = np.ascontiguousarray(block_ids, np.uint32)
+        rc = lib().tfs_crc_group_blocks_compact(self.handle, ids.ctypes.data, ctypes.cast(jobs, ctypes.c_void_p),
+                                                len(jobs))
+        return self._check(rc, "group_blocks_compact", ok=(TFS_SUCCESS, TFS_EXIT_CHECK_CRC_ERROR))
+
+
 class DeviceBuffer:
     """Device memory owned through the C ABI (tfs_crc32_dev_malloc)."""
 
@@ -442,11 +546,19 @@ class PinnedBuffer:
         ctx._check(lib().tfs_crc32_host_malloc_pinned(ctx.handle, nbytes, ctypes.byref(p)), "host_malloc_pinned")
         self.ctx, self.ptr, self.nbytes = ctx, p.value, nbytes
         self.array = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p.value))
+        self._free = lambda ptr: lib().tfs_crc32_host_free_pinned(self.ctx.handle, ptr)
+
+    @classmethod
+    def adopt(cls, ctx, ptr, nbytes, free_fn):
+        b = cls.__new__(cls)
+        b.ctx, b.ptr, b.nbytes, b._free = ctx, ptr, nbytes, free_fn
+        b.array = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(ptr))
+        return b
 
     def free(self):
         if self.ptr:
             self.array = None
-            lib().tfs_crc32_host_free_pinned(self.ctx.handle, self.ptr)
+            self._free(self.ptr)
             self.ptr = None
 
 

@@ -177,6 +177,7 @@ struct tfs_crc_ctx {
   std::atomic<uint32_t> flag_seq{0};  // completion-flag values of zero-copy launches
   int compact_slots = 8;  // blocks in flight in tfs_blocks_compact (TFS_CRC_COMPACT_SLOTS, 1..8)
   int variant = 0;  // kernel variant (TFS_CRC_VARIANT, measurement knob; 0 = product default)
+  std::atomic<uint32_t> inject_skip{0}, inject_count{0};  // tfs_crc32_inject_device_error
   DevBuf packet_scratch;  // device-resident packet calls (parse descriptors, verdicts)
   hipStream_t packet_scratch_stream = nullptr;
 };
@@ -302,6 +303,19 @@ int wait_flag(tfs_crc_ctx* ctx, Slot& s) {
   return TFS_SUCCESS;
 }
 
+// An armed tfs_crc32_inject_device_error: this submission fails as a device error would.
+int injected_fault(tfs_crc_ctx* ctx) {
+  if (ctx->inject_count.load() == 0) return TFS_SUCCESS;
+  uint32_t k = ctx->inject_skip.load();
+  while (k > 0)
+    if (ctx->inject_skip.compare_exchange_weak(k, k - 1)) return TFS_SUCCESS;
+  uint32_t c = ctx->inject_count.load();
+  while (c > 0)
+    if (ctx->inject_count.compare_exchange_weak(c, c - 1))
+      return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "injected device error (tfs_crc32_inject_device_error)");
+  return TFS_SUCCESS;
+}
+
 Slot* free_slot(tfs_crc_ctx* ctx) {
   for (auto& s : ctx->slots)
     if (!s.busy) return &s;
@@ -312,6 +326,7 @@ Slot* free_slot(tfs_crc_ctx* ctx) {
 // land in the slot's pinned buffers when s.done fires.
 int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint32_t n, const void* base,
                        uint64_t base_len) {
+  if (const int f = injected_fault(ctx)) return f;
   uint64_t lo = 0, hi = 0;
   const Desc* dd = static_cast<const Desc*>(d);
   if (!span_of(dd, n, base_len, &lo, &hi))
@@ -654,6 +669,7 @@ int tfs_block_verify(tfs_crc_ctx* ctx, const void* image, uint64_t image_len, co
     return TFS_SUCCESS;
   }
   std::lock_guard<std::mutex> g(ctx->mu);
+  if (const int f = injected_fault(ctx)) return f;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   Slot* s = free_slot(ctx);
   if (!s) return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "all %d slots busy", kSlots);
@@ -710,6 +726,7 @@ static int compact_enqueue(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job
   job->status = TFS_SUCCESS;
   job->dest_len = 0;
   job->n_live = 0;
+  if (const int f = injected_fault(ctx)) return f;
   if (n && (!job->src_image || !job->metas || !job->flags || !job->dest_image))
     return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "null block job pointer");
   // Host: new offsets in iteration order (task.cpp:753-768).
@@ -965,6 +982,7 @@ static int packet_host(tfs_crc_ctx* ctx, int mode, const tfs_packet_desc* d, uin
   if (n_bad) *n_bad = 0;
   if (n == 0) return TFS_SUCCESS;
   std::lock_guard<std::mutex> g(ctx->mu);
+  if (const int f = injected_fault(ctx)) return f;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   Slot* s = free_slot(ctx);
   if (!s) return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "all %d slots busy with async submissions", kSlots);
@@ -1163,6 +1181,14 @@ int tfs_crc32_sync(tfs_crc_ctx* ctx) {
   if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_inject_device_error(tfs_crc_ctx* ctx, uint32_t skip, uint32_t count) {
+  if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
+  ctx->inject_count = 0;
+  ctx->inject_skip = skip;
+  ctx->inject_count = count;
   return TFS_SUCCESS;
 }
 

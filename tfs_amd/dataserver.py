@@ -75,6 +75,12 @@ def lib():
                                                          ctypes.POINTER(u32), vp]),
             "tfs_ds_decode": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, u32, ctypes.POINTER(u32),
                                              ctypes.POINTER(i64)]),
+            "tfs_ds_service_new": (vp, [vp, u32, ctypes.c_int]),
+            "tfs_ds_service_free": (None, [vp]),
+            "tfs_ds_service_ctx_for_block": (vp, [vp, u32]),
+            "tfs_ds_service_close": (ctypes.c_int, [vp, vp, u64, u32, vp]),
+            "tfs_ds_service_verify_blocks": (ctypes.c_int, [vp, vp, u32, vp]),
+            "tfs_ds_service_loopback": (ctypes.c_int, [vp, vp, u32, u32, i32, vp, ctypes.c_int, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -195,6 +201,48 @@ class CloseBatcher:
         if self.h:
             lib().tfs_ds_batcher_free(self.h)
             self.h = None
+
+
+class CrcService:
+    """DataService's CRC side on a multi-GPU node: a device group and one CloseBatcher
+    per member; DataFiles, closes and block verifies are routed by block id."""
+
+    def __init__(self, group, max_batch=8, max_wait_us=100):
+        self.group = group
+        self.h = lib().tfs_ds_service_new(group.handle, max_batch, max_wait_us)
+
+    def ctx_for_block(self, block_id):
+        return _crc.Context.wrap(lib().tfs_ds_service_ctx_for_block(self.h, block_id), -1)
+
+    def close(self, block, file_id, client_crc, df):
+        return lib().tfs_ds_service_close(self.h, block.h, file_id, client_crc, df.h)
+
+    def verify_blocks(self, blocks):
+        arr = (ctypes.c_void_p * len(blocks))(*[b.h for b in blocks])
+        nb = np.zeros(len(blocks), np.uint32)
+        rc = lib().tfs_ds_service_verify_blocks(self.h, arr, len(blocks), nb.ctypes.data)
+        return rc, nb
+
+    def loopback(self, payloads, files_per_block, length, client_crc, nthreads, blocks):
+        p = np.ascontiguousarray(payloads, dtype=np.uint8)
+        c = np.ascontiguousarray(client_crc, dtype=np.uint32)
+        n = len(blocks) * files_per_block
+        if p.size < n * length or c.size < n:
+            raise ValueError("payloads/client_crc too small")
+        arr = (ctypes.c_void_p * len(blocks))(*[b.h for b in blocks])
+        return lib().tfs_ds_service_loopback(self.h, p.ctypes.data, len(blocks), files_per_block, length,
+                                             c.ctypes.data, nthreads, arr)
+
+    def free(self):
+        if self.h:
+            lib().tfs_ds_service_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 class BlockCrcChecker:

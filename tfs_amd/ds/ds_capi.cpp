@@ -182,6 +182,79 @@ int tfs_ds_loopback_block(tfs_crc_ctx* ctx, const char* payloads, uint32_t n, in
   return nb < 0 ? nb : bad.load() + nb;
 }
 
+// ---- multi-GPU service (CrcService over a tfs_crc_group) --------------------
+
+void* tfs_ds_service_new(tfs_crc_group* group, uint32_t max_batch, int max_wait_us) {
+  return group ? new CrcService(group, max_batch, max_wait_us) : nullptr;
+}
+void tfs_ds_service_free(void* s) { delete static_cast<CrcService*>(s); }
+tfs_crc_ctx* tfs_ds_service_ctx_for_block(void* s, uint32_t block_id) {
+  return static_cast<CrcService*>(s)->ctx_for_block(block_id);
+}
+int tfs_ds_service_close(void* s, void* block, uint64_t file_id, uint32_t client_crc, void* df) {
+  CloseFileInfo info;
+  info.block_id_ = static_cast<LogicBlockImage*>(block)->block_id();
+  info.file_id_ = file_id;
+  info.crc_ = client_crc;
+  return static_cast<CrcService*>(s)->close_write_file(info, *static_cast<DataFile*>(df),
+                                                       *static_cast<LogicBlockImage*>(block));
+}
+int tfs_ds_service_verify_blocks(void* s, void** blocks, uint32_t n, uint32_t* nbad) {
+  std::vector<const LogicBlockImage*> b(n);
+  for (uint32_t i = 0; i < n; ++i) b[i] = static_cast<const LogicBlockImage*>(blocks[i]);
+  std::vector<uint32_t> nb;
+  const int rc = static_cast<CrcService*>(s)->verify_blocks(b, &nb);
+  for (uint32_t i = 0; nbad && i < n; ++i) nbad[i] = nb[i];
+  return rc;
+}
+
+// BASELINE configs[0]'s loop over several blocks on a multi-GPU node: worker
+// threads write file k of block b (block ids blocks[b]->block_id()) through a
+// DataFile on that block's GPU and close it through the service (routed by
+// block id), then every block is verified on its GPU, members concurrently.
+// Returns the number of files that failed either check, or a negative status.
+int tfs_ds_service_loopback(void* service, const char* payloads, uint32_t nblocks, uint32_t files_per_block,
+                            int32_t len, const uint32_t* client_crc, int nthreads, void** blocks) {
+  auto* svc = static_cast<CrcService*>(service);
+  if (!svc || !blocks || len < 0) return TFS_EXIT_PARAMETER_ERROR;
+  if (nthreads < 1) nthreads = 1;
+  const uint32_t n = nblocks * files_per_block;
+  for (uint32_t b = 0; b < nblocks; ++b) {
+    auto* blk = static_cast<LogicBlockImage*>(blocks[b]);
+    blk->reserve(blk->data_size() + int64_t(files_per_block) * (int64_t(len) + TFS_FILEINFO_SIZE));
+  }
+  std::atomic<int> bad{0}, err{0};
+  std::vector<std::thread> workers;
+  for (int t = 0; t < nthreads; ++t)
+    workers.emplace_back([&, t] {
+      for (uint32_t i = uint32_t(t); i < n; i += uint32_t(nthreads)) {
+        auto* blk = static_cast<LogicBlockImage*>(blocks[i % nblocks]);
+        DataFile df(i + 1, "/tmp", svc->ctx_for_block(blk->block_id()));
+        if (df.set_data(payloads + size_t(i) * size_t(len), len, 0) < 0) {
+          err = TFS_EXIT_PARAMETER_ERROR;
+          continue;
+        }
+        CloseFileInfo info;
+        info.block_id_ = blk->block_id();
+        info.file_id_ = i + 1;
+        info.crc_ = client_crc[i];
+        const int rc = svc->close_write_file(info, df, *blk);
+        if (rc == TFS_EXIT_DATA_FILE_ERROR) ++bad;
+        else if (rc != TFS_SUCCESS) err = rc;
+      }
+    });
+  for (auto& w : workers) w.join();
+  if (err.load() != 0) return err.load();
+  std::vector<const LogicBlockImage*> all(nblocks);
+  for (uint32_t b = 0; b < nblocks; ++b) all[b] = static_cast<const LogicBlockImage*>(blocks[b]);
+  std::vector<uint32_t> nb;
+  const int rc = svc->verify_blocks(all, &nb);
+  if (rc != TFS_SUCCESS && rc != TFS_EXIT_CHECK_CRC_ERROR) return rc;
+  int total = bad.load();
+  for (uint32_t x : nb) total += int(x);
+  return total;
+}
+
 }  // extern "C"
 
 // ---- packet codec (packet_codec.h) ----------------------------------------

@@ -372,6 +372,43 @@ void CloseBatcher::flush(std::vector<Req*>& reqs) {
   }
 }
 
+// ---------------- CrcService (DataService's CRC side, multi-GPU) ----------------
+
+CrcService::CrcService(tfs_crc_group* group, size_t max_batch, int max_wait_us) : group_(group) {
+  for (uint32_t i = 0; i < tfs_crc_group_size(group); ++i)
+    batchers_.emplace_back(new CloseBatcher(tfs_crc_group_ctx(group, i), max_batch, max_wait_us));
+}
+
+CrcService::~CrcService() = default;
+
+int CrcService::close_write_file(const CloseFileInfo& info, DataFile& df, LogicBlockImage& block) {
+  if (batchers_.empty()) return TFS_EXIT_PARAMETER_ERROR;
+  return batchers_[tfs_crc_group_member_of(group_, info.block_id_)]->close(info, df, block);
+}
+
+int CrcService::verify_blocks(const std::vector<const LogicBlockImage*>& blocks, std::vector<uint32_t>* nbad) {
+  std::vector<std::vector<tfs_raw_meta>> live(blocks.size());
+  std::vector<tfs_block_verify_job> jobs(blocks.size());
+  for (size_t i = 0; i < blocks.size(); ++i) {
+    const LogicBlockImage& b = *blocks[i];
+    for (auto& m : b.sorted_metas())
+      if (!(b.flag_of(m.file_id) & (TFS_FI_DELETED | TFS_FI_INVALID))) live[i].push_back(m);
+    tfs_block_verify_job& j = jobs[i];
+    memset(&j, 0, sizeof j);
+    j.block_id = b.block_id();
+    j.image = b.data().data();
+    j.image_len = uint64_t(b.data_size());
+    j.metas = live[i].data();
+    j.n = uint32_t(live[i].size());
+  }
+  const int rc = tfs_crc_group_blocks_verify(group_, jobs.data(), uint32_t(jobs.size()));
+  if (nbad) {
+    nbad->resize(blocks.size());
+    for (size_t i = 0; i < blocks.size(); ++i) (*nbad)[i] = jobs[i].n_bad;
+  }
+  return rc;
+}
+
 // ---------------- verify / checker / compact ----------------
 
 void BlockCrcChecker::add_crc_error(uint32_t block_id, uint64_t file_id) {

@@ -180,6 +180,29 @@ class CloseBatcher {
   std::thread worker_;
 };
 
+// The CRC side of DataService on a multi-GPU node (dataservice.cpp:151-377
+// creates it): a device group (include/tfs_crc.h, one context per GPU) and one
+// CloseBatcher per member.  Every call is routed by block id -- the lease's
+// DataFile, its close, a block's verify -- so a block's files stay on one GPU
+// and nothing crosses between GPUs.
+class CrcService {
+ public:
+  CrcService(tfs_crc_group* group, size_t max_batch, int max_wait_us);
+  ~CrcService();
+  tfs_crc_ctx* ctx_for_block(uint32_t block_id) const { return tfs_crc_group_ctx_for_block(group_, block_id); }
+  uint32_t members() const { return tfs_crc_group_size(group_); }
+  // DataManagement::close_write_file through the block's GPU batcher.
+  int close_write_file(const CloseFileInfo& info, DataFile& df, LogicBlockImage& block);
+  // Verify-on-read of whole blocks, each on its GPU, members concurrently
+  // (tfs_crc_group_blocks_verify).  nbad[i]: bad files of blocks[i].  Returns
+  // TFS_SUCCESS, TFS_EXIT_CHECK_CRC_ERROR or a device error.
+  int verify_blocks(const std::vector<const LogicBlockImage*>& blocks, std::vector<uint32_t>* nbad);
+
+ private:
+  tfs_crc_group* group_;
+  std::vector<std::unique_ptr<CloseBatcher>> batchers_;
+};
+
 // BlockChecker's CRC-error accounting (block_checker.cpp:58-182, block_status.h:40-52):
 // per-block crc_error_ counter; >= max_crc_error_nums_ (parameter.cpp:256, default 4)
 // marks the block for repair.
