@@ -1224,6 +1224,46 @@ def ec_cpu_baseline(d, k, m, seconds, chunk=4 << 20):
                       "w=8 ps=128, single thread, %.1f s" % (reps, k, chunk >> 20, dt)}
 
 
+def _ref_crc_fn():
+    """Address of the reference's own Func::crc (oracle/_ref/libref_crc.so, built from
+    src/common/func.{h,cpp}) or, without it, the oracle restatement's."""
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "libref_crc.so")
+    if os.path.exists(ref_so):
+        L = ctypes.CDLL(ref_so)
+        _ref_crc_fn.keep = L
+        return ctypes.cast(L.ref_func_crc, ctypes.c_void_p).value, "reference"
+    L = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle_crc.so"))
+    _ref_crc_fn.keep = L
+    return ctypes.cast(L.oracle_crc, ctypes.c_void_p).value, "port"
+
+
+_PCIE = {}
+
+
+def pcie_ceiling(ctx, nbytes=256 << 20):
+    """The link's measured DMA ceiling, this run: best of 3 pinned hipMemcpyAsync
+    of 256 MiB host->device and device->host (the `peak` of the PCIe-bound lines)."""
+    if _PCIE:
+        return _PCIE
+    import tfs_amd.crc as crc
+    h = crc.PinnedBuffer(ctx, nbytes)
+    h.array[:] = 1
+    d = crc.DeviceBuffer(ctx, nbytes)
+    out = {}
+    for name, dst, src in (("h2d_GBs", d.ptr, h.ptr), ("d2h_GBs", h.ptr, d.ptr)):
+        best = 0.0
+        for _ in range(3):
+            t0 = time.perf_counter()
+            ctx._check(crc.lib().tfs_crc32_memcpy(ctx.handle, dst, src, nbytes, None), "memcpy")
+            best = max(best, nbytes / (time.perf_counter() - t0) / 1e9)
+        out[name] = best
+    h.free()
+    d.free()
+    out["source"] = "measured: best of 3 pinned 256 MiB hipMemcpy per direction, this run"
+    _PCIE.update(out)
+    return _PCIE
+
+
 def _cpu_budget():
     """Host CPUs this process may use: the scheduler affinity capped by the cgroup
     quota (cpu.max) -- on the GPU box 16 of the machine's 256 hardware threads."""
@@ -1278,14 +1318,30 @@ def bench_loopback(args):
         return ora.oracle_loopback_block(pay.ctypes.data, n, L, client.ctypes.data, stage.ctypes.data,
                                          image.ctypes.data, stored.ctypes.data)
 
+    ora.oracle_loopback_block_fn.restype = ctypes.c_int32
+    ora.oracle_loopback_block_fn.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint32, ctypes.c_int32] + \
+        [ctypes.c_void_p] * 4
+
+    def cpu_once_fn(fn, stage, image, stored):
+        return ora.oracle_loopback_block_fn(fn, pay.ctypes.data, n, L, client.ctypes.data, stage.ctypes.data,
+                                            image.ctypes.data, stored.ctypes.data)
+
     bufs = (np.zeros(L, np.uint8), np.zeros(n * (L + FILEINFO), np.uint8), np.zeros(n, np.uint32))
     if cpu_once(*bufs) != 0:
         raise SystemExit("loopback: CPU restatement rejects the GPU client CRCs")
     cpu_image = bufs[1].copy()
 
+    # The block's storage: page-locked buffers allocated once (a dataserver
+    # preallocates its blocks), so the final verify reads the block in place.
+    pool = ds.BlockImagePool(ctx, 2, n * (L + FILEINFO) + 4096)
+
+    # One CloseBatcher per thread count, created once (DataService::initialize).
+    batchers = {8: ds.CloseBatcher(ctx, max_batch=8, max_wait_us=100),
+                64: ds.CloseBatcher(ctx, max_batch=64, max_wait_us=100)}
+
     def gpu_once(threads=8):
-        blk = ds.LogicBlock(1)
-        bad = ds.loopback_block(ctx, pay, n, L, client, threads, blk)
+        blk = ds.LogicBlock(1, pool=pool)
+        bad = ds.loopback_block(ctx, pay, n, L, client, threads, blk, batchers[threads])
         return bad, blk
 
     bad, blk = gpu_once()
@@ -1341,37 +1397,71 @@ def bench_loopback(args):
         "dtype": "u8", "data": "synthetic (splitmix64) 1024 x 64 KiB payloads",
         "config": {"workload": "configs[0]: DataFile set_data -> close (CloseBatcher, 8 worker threads) -> "
                                "FileInfo|payload append; then verify_block of the whole block",
+                   "block_storage": "page-locked, allocated once (%d buffers)" % pool.size(),
                    "files": n, "file_size": L},
         "threads64_GiBs": reps * n * L / el64 / 2**30,
         "phases_ms": {"verify_block": verify_ms, "append_only_python": append_ms},
     }
+    # Write-path latency (SURVEY §7 "Batching vs. latency"): the scalar drop-in on
+    # one 64 KiB payload, and a CloseBatcher close with 1, 8 and 64 leases closing
+    # at once (the reference's close is one RPC per file on thread_count workers).
+    lat = {}
+    sl = ds.scalar_latency(300)
+    lat["scalar_tfs_crc32_64KiB"] = {"p50_us": float(np.percentile(sl, 50)), "p99_us": float(np.percentile(sl, 99)),
+                                     "calls": int(sl.size)}
+    for nl, it in ((1, 300), (8, 64), (64, 8)):
+        cl = ds.close_latency(ctx, nl, it)
+        lat["close_%d_leases" % nl] = {"p50_us": float(np.percentile(cl, 50)), "p99_us": float(np.percentile(cl, 99)),
+                                       "closes": int(cl.size)}
+    res["latency"] = lat
+    # PCIe bytes of one loopback: every payload crosses once for the close check
+    # (zero-copy reads of the lease buffers) and once for the whole-block verify.
+    pcie_bytes = 2.0 * n * L
+    ceil = pcie_ceiling(ctx)
+    res["roofline"] = {"bound": "pcie", "achieved": reps * pcie_bytes / el / 1e9, "peak": ceil["h2d_GBs"],
+                       "unit": "GB/s (per GPU)", "frac": reps * pcie_bytes / el / 1e9 / ceil["h2d_GBs"],
+                       "traffic": None, "peak_source": ceil["source"],
+                       "kernel": "crc_wg_kernel<1> (close batches) + block_verify_kernel (zero-copy)",
+                       "note": "latency-bound: one GPU round trip per batch of concurrent closes"}
     if rank == 0 and world == 1 and not args.no_cpu:
+        # CPU legs (test infrastructure): the restated loop of config 1 with the
+        # reference's own Func::crc text inside (oracle/_ref, built from
+        # src/common/func.{h,cpp}); one thread, then one block per thread on every
+        # core this process may use.
+        fn, kind = _ref_crc_fn()
         secs = min(args.cpu_seconds, 10.0)
         t0, k = time.perf_counter(), 0
         while True:
-            cpu_once(*bufs)
+            if cpu_once_fn(fn, *bufs) != 0:
+                raise SystemExit("loopback: CPU loop rejects the client CRCs")
             k += 1
             if time.perf_counter() - t0 >= secs:
                 break
         one = k * n * L / (time.perf_counter() - t0) / 2**30
-        threads = min(16, os.cpu_count() or 1)
+        threads = _cpu_budget()
         tb = [(np.zeros(L, np.uint8), np.zeros(n * (L + FILEINFO), np.uint8), np.zeros(n, np.uint32))
               for _ in range(threads)]
         with cf.ThreadPoolExecutor(threads) as ex:
+            list(ex.map(lambda b: cpu_once_fn(fn, *b), tb))
             t0 = time.perf_counter()
             rounds = 0
             while time.perf_counter() - t0 < min(secs, 5.0):
-                list(ex.map(lambda b: cpu_once(*b), tb))
+                list(ex.map(lambda b: cpu_once_fn(fn, *b), tb))
                 rounds += 1
             allc = rounds * threads * n * L / (time.perf_counter() - t0) / 2**30
         res["cpu_baseline"] = {
-            "value": one, "unit": "GiB/s", "cores": 1, "kind": "port",
+            "value": one, "unit": "GiB/s", "cores": 1, "kind": kind,
             "sample": "%d loopbacks of the 1024 x 64 KiB block (stage, crc, compare, append, then re-CRC verify), "
-                      "oracle restatement of Func::crc, single thread, %.1f s" % (k, secs),
-            "allcore": {"value": allc, "cores": threads, "nproc": os.cpu_count(), "cpu_model": _cpu_model()},
+                      "restated loop around the reference's Func::crc text, single thread, %.1f s" % (k, secs),
+            "allcore": {"value": allc, "cores": threads, "nproc": os.cpu_count(), "cpu_model": _cpu_model(),
+                        "cores_source": "sched affinity capped by the cgroup cpu.max quota"},
         }
+        res["vs_cpu_allcore"] = res["value"] / allc
     if rank == 0:
         print(json.dumps(res), flush=True)
+    for b in batchers.values():
+        b.free()
+    pool.free()
     ctx.close()
     if dist:
         dist.destroy_process_group()

@@ -105,42 +105,52 @@ void oracle_crc_batch(const oracle_desc* d, uint32_t n, const char* base, uint32
   for (uint32_t i = 0; i < n; ++i) out[i] = oracle_crc(d[i].seed, base + d[i].offset, (int32_t)d[i].len);
 }
 
+/* A Func::crc implementation: this restatement, or the reference's own text
+ * (oracle/_ref/libref_crc.so ref_func_crc) passed in by the caller. */
+typedef uint32_t (*oracle_crc_fn)(uint32_t, const char*, int32_t);
+
 typedef struct {
   const oracle_desc* d;
   const char* base;
   uint32_t* out;
   uint32_t begin, end;
+  oracle_crc_fn fn;
 } mt_job;
 
 static void* mt_worker(void* arg) {
   mt_job* j = (mt_job*)arg;
   for (uint32_t i = j->begin; i < j->end; ++i)
-    j->out[i] = oracle_crc(j->d[i].seed, j->base + j->d[i].offset, (int32_t)j->d[i].len);
+    j->out[i] = j->fn(j->d[i].seed, j->base + j->d[i].offset, (int32_t)j->d[i].len);
   return NULL;
 }
 
-/* All-core variant: one file per task, contiguous ranges per thread. */
-int oracle_crc_batch_mt(const oracle_desc* d, uint32_t n, const char* base, uint32_t* out, int nthreads) {
+/* All-core variant with a caller-supplied Func::crc (NULL = this restatement):
+ * one file per task, contiguous ranges per thread. */
+int oracle_crc_batch_mt_fn(oracle_crc_fn fn, const oracle_desc* d, uint32_t n, const char* base, uint32_t* out,
+                           int nthreads) {
+  if (!fn) fn = oracle_crc;
   if (nthreads < 1) nthreads = 1;
   if (nthreads > 256) nthreads = 256;
   pthread_t th[256];
   mt_job jobs[256];
+  int ok[256];
   uint32_t per = (n + (uint32_t)nthreads - 1) / (uint32_t)nthreads;
-  int started = 0;
   for (int t = 0; t < nthreads; ++t) {
     uint32_t b = (uint32_t)t * per, e = b + per;
     if (b > n) b = n;
     if (e > n) e = n;
-    jobs[t] = (mt_job){d, base, out, b, e};
-    if (pthread_create(&th[t], NULL, mt_worker, &jobs[t]) != 0) {
-      mt_worker(&jobs[t]);
-      continue;
-    }
-    ++started;
-    (void)started;
+    jobs[t] = (mt_job){d, base, out, b, e, fn};
+    ok[t] = pthread_create(&th[t], NULL, mt_worker, &jobs[t]) == 0;
+    if (!ok[t]) mt_worker(&jobs[t]);
   }
-  for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+  for (int t = 0; t < nthreads; ++t)
+    if (ok[t]) pthread_join(th[t], NULL);
   return 0;
+}
+
+/* All-core variant: one file per task, contiguous ranges per thread. */
+int oracle_crc_batch_mt(const oracle_desc* d, uint32_t n, const char* base, uint32_t* out, int nthreads) {
+  return oracle_crc_batch_mt_fn(oracle_crc, d, n, base, out, nthreads);
 }
 
 /* DataFile::get_crc -- src/dataserver/data_file.cpp:168-194.  The >2 MiB branch
@@ -175,14 +185,25 @@ uint32_t oracle_datafile_get_crc(const char* data, int32_t length) {
  * per file (tfs_file.cpp:962-963).  image: out, >= n*(36+len) bytes.
  * Returns the number of files that failed either check.
  */
+int32_t oracle_loopback_block_fn(oracle_crc_fn fn, const char* payloads, uint32_t n, int32_t len,
+                                 const uint32_t* client_crc, char* stage, char* image, uint32_t* stored_crc);
 int32_t oracle_loopback_block(const char* payloads, uint32_t n, int32_t len, const uint32_t* client_crc,
                               char* stage, char* image, uint32_t* stored_crc) {
+  return oracle_loopback_block_fn(oracle_crc, payloads, n, len, client_crc, stage, image, stored_crc);
+}
+
+/* The same loop with a caller-supplied Func::crc (the reference text for the CPU
+ * baseline; NULL = this restatement).  Payloads <= 2 MiB, as in config 1. */
+int32_t oracle_loopback_block_fn(oracle_crc_fn fn, const char* payloads, uint32_t n, int32_t len,
+                                 const uint32_t* client_crc, char* stage, char* image, uint32_t* stored_crc) {
+  if (!fn) fn = oracle_crc;
   int32_t bad = 0;
   int64_t woff = 0;
   uint32_t written = 0;
   for (uint32_t i = 0; i < n; ++i) {
     memcpy(stage, payloads + (int64_t)i * len, (size_t)len);       /* DataFile::set_data */
-    uint32_t crc = oracle_datafile_get_crc(stage, len);            /* DataFile::get_crc */
+    uint32_t crc = len > ORACLE_TMPBUF_SIZE ? oracle_datafile_get_crc(stage, len)
+                                            : fn(0, stage, len);   /* DataFile::get_crc, data_file.cpp:190 */
     if (crc != client_crc[i]) { ++bad; continue; }                  /* EXIT_DATA_FILE_ERROR */
     oracle_file_info fi;
     memset(&fi, 0, sizeof fi);
@@ -204,7 +225,7 @@ int32_t oracle_loopback_block(const char* payloads, uint32_t n, int32_t len, con
     oracle_file_info fi;
     memcpy(&fi, image + roff, ORACLE_FILEINFO_SIZE);
     int32_t plen = fi.size_ - ORACLE_FILEINFO_SIZE;
-    uint32_t crc = oracle_crc(0, image + roff + ORACLE_FILEINFO_SIZE, plen);
+    uint32_t crc = fn(0, image + roff + ORACLE_FILEINFO_SIZE, plen);
     if (crc != fi.crc_) ++bad;
     roff += fi.size_;
   }

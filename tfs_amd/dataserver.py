@@ -34,6 +34,10 @@ def lib():
             "tfs_ds_datafile_length": (i32, [vp]),
             "tfs_ds_datafile_get_crc": (u32, [vp, ctypes.POINTER(ctypes.c_int)]),
             "tfs_ds_block_new": (vp, [u32, i64]),
+            "tfs_ds_pool_new": (vp, [vp, u32, u64]),
+            "tfs_ds_pool_free": (None, [vp]),
+            "tfs_ds_pool_size": (u32, [vp]),
+            "tfs_ds_block_new_in": (vp, [vp, u32, i64]),
             "tfs_ds_block_free": (None, [vp]),
             "tfs_ds_block_size": (i64, [vp]),
             "tfs_ds_block_data": (vp, [vp]),
@@ -52,6 +56,7 @@ def lib():
             "tfs_ds_verify_block": (ctypes.c_int, [vp, vp, vp, u32, vp]),
             "tfs_ds_compact_block": (ctypes.c_int, [vp, vp, vp, vp, u32]),
             "tfs_ds_loopback_block": (ctypes.c_int, [vp, vp, u32, i32, vp, ctypes.c_int, vp]),
+            "tfs_ds_loopback_block_with": (ctypes.c_int, [vp, vp, vp, u32, i32, vp, ctypes.c_int, vp]),
             "tfs_ds_block_read_file": (ctypes.c_int, [vp, u64, vp, ctypes.POINTER(i32), i32, ctypes.c_int]),
             "tfs_ds_recombine_block": (ctypes.c_int, [vp, vp, vp, ctypes.POINTER(ctypes.c_int)]),
             "tfs_ds_read_file_verified": (ctypes.c_int, [vp, vp, u64, vp, i32, ctypes.POINTER(i32), vp]),
@@ -75,6 +80,8 @@ def lib():
                                                          ctypes.POINTER(u32), vp]),
             "tfs_ds_decode": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, u32, ctypes.POINTER(u32),
                                              ctypes.POINTER(i64)]),
+            "tfs_ds_close_latency": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, i32, vp]),
+            "tfs_ds_scalar_latency": (ctypes.c_int, [ctypes.c_int, i32, vp]),
             "tfs_ds_service_new": (vp, [vp, u32, ctypes.c_int]),
             "tfs_ds_service_free": (None, [vp]),
             "tfs_ds_service_ctx_for_block": (vp, [vp, u32]),
@@ -122,12 +129,29 @@ class DataFile:
             pass
 
 
+class BlockImagePool:
+    """Page-locked block buffers allocated once and lent to LogicBlocks (a dataserver's
+    preallocated blocks); a page-locked image is verified in place (zero-copy)."""
+
+    def __init__(self, ctx, count, nbytes):
+        self.h = lib().tfs_ds_pool_new(ctx.handle, count, nbytes)
+
+    def size(self):
+        return lib().tfs_ds_pool_size(self.h)
+
+    def free(self):
+        if self.h:
+            lib().tfs_ds_pool_free(self.h)
+            self.h = None
+
+
 class LogicBlock:
     """One logical block: FileInfo|payload records + index (logic_block.cpp)."""
 
-    def __init__(self, block_id, capacity=1 << 40):
+    def __init__(self, block_id, capacity=1 << 40, pool=None):
         self.block_id = block_id
-        self.h = lib().tfs_ds_block_new(block_id, capacity)
+        self.h = lib().tfs_ds_block_new_in(pool.h, block_id, capacity) if pool else \
+            lib().tfs_ds_block_new(block_id, capacity)
 
     def close_write_file(self, file_id, client_crc, df):
         """DataManagement::close_write_file: 0, or EXIT_DATA_FILE_ERROR (-8013) on crc mismatch."""
@@ -387,15 +411,35 @@ def compact_block(ctx, src, dest):
     return rc, ok[:len(m)]
 
 
-def loopback_block(ctx, payloads, n, length, client_crc, nthreads, block):
+def loopback_block(ctx, payloads, n, length, client_crc, nthreads, block, batcher=None):
     """BASELINE configs[0] through the harness: n payloads written by `nthreads`
     worker threads (DataFile -> CloseBatcher close), then the whole block verified.
-    Returns the number of files that failed either check (or a negative status)."""
+    `batcher`: a long-lived CloseBatcher (else one per call).  Returns the number
+    of files that failed either check (or a negative status)."""
     p = np.ascontiguousarray(payloads, dtype=np.uint8)
     c = np.ascontiguousarray(client_crc, dtype=np.uint32)
     if p.size < n * length or c.size < n:
         raise ValueError("payloads/client_crc too small")
-    return lib().tfs_ds_loopback_block(ctx.handle, p.ctypes.data, n, length, c.ctypes.data, nthreads, block.h)
+    return lib().tfs_ds_loopback_block_with(ctx.handle, batcher.h if batcher else None, p.ctypes.data, n, length,
+                                            c.ctypes.data, nthreads, block.h)
+
+
+def close_latency(ctx, nleases, iters, length=65536):
+    """Microseconds per CloseBatcher close with `nleases` leases closing concurrently."""
+    out = np.zeros(nleases * iters, np.float64)
+    rc = lib().tfs_ds_close_latency(ctx.handle, nleases, iters, length, out.ctypes.data)
+    if rc != 0:
+        raise _crc.TfsCrcError(rc, "close_latency")
+    return out
+
+
+def scalar_latency(iters, length=65536):
+    """Microseconds per tfs_crc32(0, data, length) call (pageable data, default context)."""
+    out = np.zeros(iters, np.float64)
+    rc = lib().tfs_ds_scalar_latency(iters, length, out.ctypes.data)
+    if rc != 0:
+        raise _crc.TfsCrcError(rc, "scalar_latency")
+    return out
 
 
 def recombine_block(ctx, src, dest):

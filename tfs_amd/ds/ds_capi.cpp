@@ -33,6 +33,15 @@ uint32_t tfs_ds_datafile_get_crc(void* df, int* status) {
 }
 
 void* tfs_ds_block_new(uint32_t block_id, int64_t capacity) { return new LogicBlockImage(block_id, capacity); }
+// Page-locked block buffers lent to LogicBlockImages (a dataserver's preallocated blocks).
+void* tfs_ds_pool_new(tfs_crc_ctx* ctx, uint32_t count, uint64_t bytes) {
+  return new BlockImagePool(ctx, count, size_t(bytes));
+}
+void tfs_ds_pool_free(void* pool) { delete static_cast<BlockImagePool*>(pool); }
+uint32_t tfs_ds_pool_size(void* pool) { return uint32_t(static_cast<BlockImagePool*>(pool)->size()); }
+void* tfs_ds_block_new_in(void* pool, uint32_t block_id, int64_t capacity) {
+  return new LogicBlockImage(block_id, capacity, pool ? static_cast<BlockImagePool*>(pool)->take() : nullptr);
+}
 void tfs_ds_block_free(void* b) { delete static_cast<LogicBlockImage*>(b); }
 int64_t tfs_ds_block_size(void* b) { return static_cast<LogicBlockImage*>(b)->data_size(); }
 const char* tfs_ds_block_data(void* b) { return static_cast<LogicBlockImage*>(b)->data().data(); }
@@ -126,8 +135,17 @@ int tfs_ds_compact_block(tfs_crc_ctx* ctx, void* src, void* dest, uint8_t* crc_o
 // 196-198, then FileInfo|payload appended, logic_block.cpp:171-178).  Then
 // verify-on-read of the whole block (sync_backup.cpp:383-429).  Returns the
 // number of files that failed either check, or a negative status.
+int tfs_ds_loopback_block_with(tfs_crc_ctx* ctx, void* batcher, const char* payloads, uint32_t n, int32_t len,
+                               const uint32_t* client_crc, int nthreads, void* block);
 int tfs_ds_loopback_block(tfs_crc_ctx* ctx, const char* payloads, uint32_t n, int32_t len, const uint32_t* client_crc,
                           int nthreads, void* block) {
+  return tfs_ds_loopback_block_with(ctx, nullptr, payloads, n, len, client_crc, nthreads, block);
+}
+
+// The same with a long-lived CloseBatcher (DataService creates it once, at
+// initialize); NULL = one for this call.
+int tfs_ds_loopback_block_with(tfs_crc_ctx* ctx, void* batcher, const char* payloads, uint32_t n, int32_t len,
+                               const uint32_t* client_crc, int nthreads, void* block) {
   if (!ctx || !block || len < 0 || (n && (!payloads || !client_crc))) return TFS_EXIT_PARAMETER_ERROR;
   LogicBlockImage& blk = *static_cast<LogicBlockImage*>(block);
   if (nthreads < 1) nthreads = 1;
@@ -140,7 +158,9 @@ int tfs_ds_loopback_block(tfs_crc_ctx* ctx, const char* payloads, uint32_t n, in
   auto us = [](auto a, auto b) { return int64_t(std::chrono::duration_cast<std::chrono::microseconds>(b - a).count()); };
   const auto t_begin = now();
   {
-    CloseBatcher batcher(ctx, size_t(nthreads), 100);
+    std::unique_ptr<CloseBatcher> own;
+    if (!batcher) own.reset(new CloseBatcher(ctx, size_t(nthreads), 100));
+    CloseBatcher& bat = batcher ? *static_cast<CloseBatcher*>(batcher) : *own;
     std::vector<std::thread> workers;
     for (int t = 0; t < nthreads; ++t)
       workers.emplace_back([&, t] {
@@ -157,7 +177,7 @@ int tfs_ds_loopback_block(tfs_crc_ctx* ctx, const char* payloads, uint32_t n, in
           info.block_id_ = blk.block_id();
           info.file_id_ = i + 1;
           info.crc_ = client_crc[i];
-          const int rc = batcher.close(info, *df, blk);
+          const int rc = bat.close(info, *df, blk);
           const auto t3 = now();
           df.reset();
           if (trace) {
@@ -180,6 +200,65 @@ int tfs_ds_loopback_block(tfs_crc_ctx* ctx, const char* payloads, uint32_t n, in
             (long long)us(t_begin, t_writes), (long long)us(t_writes, now()), (long long)t_new.load(),
             (long long)t_set.load(), (long long)t_close.load(), (long long)t_free.load());
   return nb < 0 ? nb : bad.load() + nb;
+}
+
+// ---- write-path latency (SURVEY §7 "Batching vs. latency") ------------------
+
+// Per-close latency of DataManagement::close_write_file through the CloseBatcher:
+// `nleases` worker threads (concurrent leases) each close `iters` files of `len`
+// bytes; a close is timed from the call to its return (GPU check of the client
+// CRC + FileInfo|payload append).  out_us receives nleases*iters microseconds.
+int tfs_ds_close_latency(tfs_crc_ctx* ctx, int nleases, int iters, int32_t len, double* out_us) {
+  if (!ctx || nleases < 1 || iters < 1 || len < 0 || !out_us) return TFS_EXIT_PARAMETER_ERROR;
+  std::vector<char> payload(size_t(len) + 1);
+  for (int32_t i = 0; i < len; ++i) payload[size_t(i)] = char((i * 2654435761u) >> 11);
+  uint32_t client = 0;
+  int rc = tfs_datafile_get_crc(ctx, payload.data(), len, &client);  // the client's Func::crc
+  if (rc != TFS_SUCCESS) return rc;
+  LogicBlockImage blk(1, int64_t(INT32_MAX));
+  const int64_t total = int64_t(nleases) * iters * (int64_t(len) + TFS_FILEINFO_SIZE);
+  if (total > int64_t(INT32_MAX)) return TFS_EXIT_PARAMETER_ERROR;
+  blk.reserve(total);
+  std::atomic<int> err{0};
+  {
+    CloseBatcher batcher(ctx, size_t(nleases), 100);
+    std::vector<std::thread> workers;
+    for (int t = 0; t < nleases; ++t)
+      workers.emplace_back([&, t] {
+        for (int k = 0; k < iters; ++k) {
+          const uint64_t fid = uint64_t(t) * uint64_t(iters) + uint64_t(k) + 1;
+          DataFile df(fid, "/tmp", ctx);
+          df.set_data(payload.data(), len, 0);
+          CloseFileInfo info;
+          info.block_id_ = 1;
+          info.file_id_ = fid;
+          info.crc_ = client;
+          const auto t0 = std::chrono::steady_clock::now();
+          const int r = batcher.close(info, df, blk);
+          const auto t1 = std::chrono::steady_clock::now();
+          out_us[size_t(t) * size_t(iters) + size_t(k)] = std::chrono::duration<double, std::micro>(t1 - t0).count();
+          if (r != TFS_SUCCESS) err = r;
+        }
+      });
+    for (auto& w : workers) w.join();
+  }
+  return err.load();
+}
+
+// The scalar drop-in: tfs_crc32(0, data, len) on a pageable buffer, timed per call.
+int tfs_ds_scalar_latency(int iters, int32_t len, double* out_us) {
+  if (iters < 1 || len < 0 || !out_us) return TFS_EXIT_PARAMETER_ERROR;
+  std::vector<char> payload(size_t(len) + 1);
+  for (int32_t i = 0; i < len; ++i) payload[size_t(i)] = char((i * 40503u) >> 5);
+  int err = TFS_SUCCESS;
+  for (int k = 0; k < iters; ++k) {
+    const auto t0 = std::chrono::steady_clock::now();
+    (void)tfs_crc32_e(0, payload.data(), len, &err);
+    const auto t1 = std::chrono::steady_clock::now();
+    out_us[k] = std::chrono::duration<double, std::micro>(t1 - t0).count();
+    if (err != TFS_SUCCESS) return err;
+  }
+  return TFS_SUCCESS;
 }
 
 // ---- multi-GPU service (CrcService over a tfs_crc_group) --------------------

@@ -124,7 +124,28 @@ uint32_t DataFile::get_crc() {
 
 // ---------------- LogicBlockImage (logic_block.cpp) ----------------
 
-LogicBlockImage::LogicBlockImage(uint32_t block_id, int64_t capacity) : block_id_(block_id), capacity_(capacity) {}
+LogicBlockImage::LogicBlockImage(uint32_t block_id, int64_t capacity, ImageArena* arena)
+    : block_id_(block_id), capacity_(capacity), data_(ImageAlloc<char>(arena)) {}
+
+BlockImagePool::BlockImagePool(tfs_crc_ctx* ctx, size_t count, size_t bytes) : ctx_(ctx) {
+  for (size_t i = 0; i < count; ++i) {
+    void* p = nullptr;
+    if (tfs_crc32_host_malloc_pinned(ctx, bytes, &p) != TFS_SUCCESS) break;
+    arenas_.emplace_back(new ImageArena());
+    arenas_.back()->p = static_cast<char*>(p);
+    arenas_.back()->cap = bytes;
+  }
+}
+
+BlockImagePool::~BlockImagePool() {
+  for (auto& a : arenas_) tfs_crc32_host_free_pinned(ctx_, a->p);
+}
+
+ImageArena* BlockImagePool::take() {
+  for (auto& a : arenas_)
+    if (!a->in_use.load()) return a.get();  // claimed by the image's first allocation
+  return nullptr;
+}
 
 int LogicBlockImage::append_record(uint64_t file_id, const char* payload, int32_t len, uint32_t crc) {
   if (len < 0) return TFS_EXIT_PARAMETER_ERROR;
@@ -139,26 +160,34 @@ int LogicBlockImage::append_record(uint64_t file_id, const char* payload, int32_
   fi.crc_ = crc;                    // :177
   int64_t off;
   {
-    std::unique_lock<std::shared_mutex> g(mu_);
-    off = int64_t(data_.size());
+    // The record's range and index entry are taken under a short lock; the bytes
+    // are copied outside it, beside other writers (records are disjoint).
+    std::lock_guard<std::mutex> g(mu_);
+    off = used_.load();
     // Capacity and the int32 FileInfo/RawMeta offset are checked under the lock
     // that reserves the range, so batched and unbatched closes accept the same
     // writes and concurrent appends cannot overrun the block together.
     if (off + int64_t(fi.size_) > capacity_ || off + int64_t(fi.size_) > int64_t(INT32_MAX))
       return kExitBlockExhaust;
     fi.offset_ = int32_t(off);
-    data_.resize(size_t(off + fi.size_));  // moves the image only when past the reservation
+    if (size_t(off + fi.size_) > data_.capacity()) {  // moves the image: no copy may be in flight
+      std::unique_lock<std::shared_mutex> w(grow_mu_);
+      data_.reserve(std::max(data_.capacity() * 2, size_t(off + fi.size_)));
+    }
+    data_.resize(size_t(off + fi.size_));
+    used_.store(off + fi.size_, std::memory_order_release);
     index_[file_id] = tfs_raw_meta{file_id, int32_t(off), fi.size_};
     flags_[file_id] = 0;
   }
-  std::shared_lock<std::shared_mutex> g(mu_);
+  std::shared_lock<std::shared_mutex> g(grow_mu_);
   put_file_info(data_.data() + off, fi);
   if (len) memcpy(data_.data() + off + kFileInfoSize, payload, size_t(len));
   return TFS_SUCCESS;
 }
 
 void LogicBlockImage::reserve(int64_t bytes) {
-  std::unique_lock<std::shared_mutex> g(mu_);
+  std::lock_guard<std::mutex> g(mu_);
+  std::unique_lock<std::shared_mutex> w(grow_mu_);
   if (bytes <= int64_t(data_.capacity())) return;
   data_.reserve(size_t(bytes));
   const uintptr_t a = (reinterpret_cast<uintptr_t>(data_.data()) + (2u << 20) - 1) & ~uintptr_t((2u << 20) - 1);
@@ -180,6 +209,7 @@ int LogicBlockImage::close_write_file(uint64_t file_id, DataFile& df, uint32_t c
 }
 
 int LogicBlockImage::read_file(uint64_t file_id, std::vector<char>& out) const {
+  std::lock_guard<std::mutex> g(mu_);
   auto it = index_.find(file_id);
   if (it == index_.end()) return TFS_EXIT_FILE_INFO_ERROR;
   out.assign(data_.begin() + it->second.offset, data_.begin() + it->second.offset + it->second.size);
@@ -187,12 +217,16 @@ int LogicBlockImage::read_file(uint64_t file_id, std::vector<char>& out) const {
 }
 
 int LogicBlockImage::read_file(uint64_t file_id, char* buf, int32_t* nbytes, int32_t offset, bool force) const {
-  auto it = index_.find(file_id);
-  if (it == index_.end()) return kExitMetaNotFound;
-  const tfs_raw_meta& m = it->second;
+  tfs_raw_meta m;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = index_.find(file_id);
+    if (it == index_.end()) return kExitMetaNotFound;
+    m = it->second;
+  }
   if (offset + *nbytes > m.size) *nbytes = m.size - offset;  // truncate to the record (:388-391)
   if (*nbytes < 0) return kExitReadOffset;
-  if (int64_t(m.offset) + offset + *nbytes > int64_t(data_.size())) return TFS_EXIT_PARAMETER_ERROR;
+  if (int64_t(m.offset) + offset + *nbytes > data_size()) return TFS_EXIT_PARAMETER_ERROR;
   memcpy(buf, data_.data() + m.offset + offset, size_t(*nbytes));
   if (offset == 0) {  // :414-435
     if (*nbytes < kFileInfoSize) return TFS_EXIT_READ_FILE_SIZE_ERROR;
@@ -206,6 +240,7 @@ int LogicBlockImage::read_file(uint64_t file_id, char* buf, int32_t* nbytes, int
 }
 
 int LogicBlockImage::set_flag(uint64_t file_id, int32_t flag) {
+  std::lock_guard<std::mutex> g(mu_);
   auto it = flags_.find(file_id);
   if (it == flags_.end()) return TFS_EXIT_FILE_INFO_ERROR;
   it->second = flag;
@@ -213,14 +248,18 @@ int LogicBlockImage::set_flag(uint64_t file_id, int32_t flag) {
 }
 
 int32_t LogicBlockImage::flag_of(uint64_t file_id) const {
+  std::lock_guard<std::mutex> g(mu_);
   auto it = flags_.find(file_id);
   return it == flags_.end() ? TFS_FI_INVALID : it->second;
 }
 
 std::vector<tfs_raw_meta> LogicBlockImage::sorted_metas() const {
   std::vector<tfs_raw_meta> v;
-  v.reserve(index_.size());
-  for (auto& kv : index_) v.push_back(kv.second);
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    v.reserve(index_.size());
+    for (auto& kv : index_) v.push_back(kv.second);
+  }
   std::sort(v.begin(), v.end(), [](const tfs_raw_meta& a, const tfs_raw_meta& b) { return a.offset < b.offset; });
   return v;
 }
@@ -233,7 +272,10 @@ std::vector<int32_t> LogicBlockImage::sorted_flags() const {
 
 void LogicBlockImage::replace(ByteImage&& data, const std::vector<tfs_raw_meta>& metas,
                               const std::vector<int32_t>& flags) {
+  std::lock_guard<std::mutex> g(mu_);
+  std::unique_lock<std::shared_mutex> w(grow_mu_);
   data_ = std::move(data);
+  used_ = int64_t(data_.size());
   index_.clear();
   flags_.clear();
   for (size_t i = 0; i < metas.size(); ++i) {
@@ -251,125 +293,167 @@ int close_write_file(const CloseFileInfo& info, DataFile& df, LogicBlockImage& b
   return block.close_write_file(info.file_id_, df, datafile_crc);
 }
 
+namespace {
+// Wait for `pred` spinning (the verdict of a batch arrives in tens of
+// microseconds), yielding the CPU once the wait grows long.
+template <typename P>
+void spin_until(P pred) {
+  for (uint32_t i = 0; !pred(); ++i) {
+    if (i < 4096) __builtin_ia32_pause();
+    else std::this_thread::yield();
+  }
+}
+}  // namespace
+
 CloseBatcher::CloseBatcher(tfs_crc_ctx* ctx, size_t max_batch, int max_wait_us)
-    : ctx_(ctx), max_batch_(max_batch ? max_batch : 1), max_wait_us_(max_wait_us), worker_([this] { run(); }) {}
+    : ctx_(ctx), max_batch_(max_batch ? max_batch : 1), max_wait_us_(max_wait_us),
+      gather_cap_(std::min<size_t>(std::max<size_t>(max_batch_ * (256u << 10), 4u << 20), 16u << 20)),
+      trace_(getenv("TFS_DS_TRACE") != nullptr) {
+  // The gather buffers are page-locked once, here (DataService::initialize),
+  // never on a close.
+  for (Batch& b : batches_buf_) {
+    void* p = nullptr;
+    if (tfs_crc32_host_malloc_pinned(ctx_, gather_cap_, &p) == TFS_SUCCESS) {
+      b.gather = static_cast<char*>(p);
+    } else {
+      b.fallback.resize(gather_cap_);
+      b.gather = b.fallback.data();
+    }
+    b.desc.resize(max_batch_);
+    b.crc.resize(max_batch_);
+    b.ok.resize(max_batch_);
+  }
+}
 
 CloseBatcher::~CloseBatcher() {
+  for (Batch& b : batches_buf_)
+    if (b.gather && b.fallback.empty()) tfs_crc32_host_free_pinned(ctx_, b.gather);
+  if (getenv("TFS_DS_TRACE"))
+    fprintf(stderr,
+            "close batcher: %llu batches, verify %lld us; thread-us claim %lld copy %lld wait %lld (leader "
+            "pre-verify %lld) append %lld\n",
+            (unsigned long long)batches_.load(), (long long)verify_us_.load(), (long long)t_claim_.load(),
+            (long long)t_copy_.load(), (long long)t_wait_.load(), (long long)t_lead_wait_.load(),
+            (long long)t_append_.load());
+}
+
+CloseBatcher::Batch* CloseBatcher::take_batch(std::unique_lock<std::mutex>& lk) {
+  for (;;) {
+    for (Batch& b : batches_buf_) {
+      if (!b.free) continue;
+      b.free = false;
+      b.n = 0;
+      b.bytes = 0;
+      b.closed = false;
+      b.ready = 0;
+      b.left = 0;
+      b.done = 0;
+      b.rc = TFS_SUCCESS;
+      b.opened = std::chrono::steady_clock::now();
+      return &b;
+    }
+    free_cv_.wait(lk);
+  }
+}
+
+// The first member of a batch: close it (full, or max_wait_us after it opened),
+// wait for every member's payload, run the GPU verify, publish the verdicts.
+void CloseBatcher::lead(Batch* b) {
+  const auto deadline = b->opened + std::chrono::microseconds(max_wait_us_);
+  spin_until([&] { return b->closed.load(std::memory_order_acquire) || std::chrono::steady_clock::now() >= deadline; });
+  uint32_t n;
   {
     std::lock_guard<std::mutex> g(mu_);
-    stop_ = true;
+    if (!b->closed.load()) {
+      b->closed = true;
+      if (cur_ == b) cur_ = nullptr;
+    }
+    n = b->n;
   }
-  cv_.notify_all();
-  worker_.join();
-  if (gather_) tfs_crc32_host_free_pinned(ctx_, gather_);
-  if (getenv("TFS_DS_TRACE"))
-    fprintf(stderr, "close batcher: %llu batches, gather %lld us, verify %lld us\n", (unsigned long long)batches_,
-            (long long)gather_us_, (long long)verify_us_);
+  spin_until([&] { return b->ready.load(std::memory_order_acquire) == n; });
+  const auto t0 = std::chrono::steady_clock::now();
+  if (trace_) t_lead_wait_ += std::chrono::duration_cast<std::chrono::microseconds>(t0 - b->opened).count();
+  uint32_t nbad = 0;
+  b->rc = tfs_crc32_verify(ctx_, b->desc.data(), n, b->gather, b->bytes, b->crc.data(), b->ok.data(), &nbad);
+  verify_us_ += std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+  ++batches_;
+  b->done.store(1, std::memory_order_release);
 }
 
 int CloseBatcher::close(const CloseFileInfo& info, DataFile& df, LogicBlockImage& block) {
-  Req r;
-  r.info = &info;
-  r.df = &df;
-  r.block = &block;
+  const int32_t len = df.get_length();
+  if (len > kMaxBatched || size_t(len) > gather_cap_) return close_write_file(info, df, block);  // unbatched
+  using clk = std::chrono::steady_clock;
+  auto us = [](clk::time_point a, clk::time_point b2) {
+    return int64_t(std::chrono::duration_cast<std::chrono::microseconds>(b2 - a).count());
+  };
+  const auto c0 = trace_ ? clk::now() : clk::time_point();
+  Batch* b;
+  uint32_t slot;
+  uint64_t off;
   {
     std::unique_lock<std::mutex> lk(mu_);
-    queue_.push_back(&r);
-    if (queue_.size() >= max_batch_) cv_.notify_all();
-    done_cv_.wait(lk, [&] { return r.done; });
+    if (cur_ && cur_->bytes + uint64_t(len) > gather_cap_) {  // no room: close it, its leader fires it
+      cur_->closed = true;
+      cur_ = nullptr;
+    }
+    if (!cur_) cur_ = take_batch(lk);
+    b = cur_;
+    slot = b->n++;
+    off = b->bytes;
+    b->bytes += uint64_t(len);
+    b->left.fetch_add(1);
+    if (b->n == max_batch_) {
+      b->closed.store(true, std::memory_order_release);
+      cur_ = nullptr;
+    }
   }
-  if (r.status != kAppend) return r.status;
+  const auto c1 = trace_ ? clk::now() : clk::time_point();
+  // This lease's payload into the batch's gather buffer (data_file.cpp:115-166).
+  int32_t got = 0;
+  while (got < len) {
+    int32_t rl = len - got;
+    if (!df.get_data(b->gather + off + got, &rl, got) || rl <= 0) break;
+    got += rl;
+  }
+  // An unreadable lease (spill-file I/O error) gets an empty descriptor and fails
+  // with TFS_ERROR as LogicBlock::close_write_file would (logic_block.cpp:264-270).
+  const bool readable = got == len;
+  b->desc[slot] = tfs_crc_vdesc{off, readable ? uint32_t(len) : 0u, info.crc_};
+  b->ready.fetch_add(1, std::memory_order_release);
+  const auto c2 = trace_ ? clk::now() : clk::time_point();
+  if (slot == 0) lead(b);
+  else spin_until([&] { return b->done.load(std::memory_order_acquire) != 0; });
+  if (trace_) {
+    const auto c3 = clk::now();
+    t_claim_ += us(c0, c1);
+    t_copy_ += us(c1, c2);
+    t_wait_ += us(c2, c3);
+  }
+  int status;
+  uint32_t crc = 0;
+  if (!readable) {
+    status = kTfsError;
+  } else if (b->rc != TFS_SUCCESS && b->rc != TFS_EXIT_CHECK_CRC_ERROR) {
+    status = b->rc;  // device failure: reported as such, never as client corruption
+  } else if (!b->ok[slot]) {
+    status = TFS_EXIT_DATA_FILE_ERROR;  // data_management.cpp:198
+  } else {
+    status = kAppend;
+    crc = b->crc[slot];
+  }
+  if (b->left.fetch_sub(1) == 1) {  // last reader: the batch is free again
+    std::lock_guard<std::mutex> g(mu_);
+    b->free = true;
+    free_cv_.notify_one();
+  }
+  if (status != kAppend) return status;
   // Checked: persist from this thread (LogicBlock::close_write_file runs on the
   // worker, logic_block.cpp:156-372), so the appends of a batch run side by side.
-  return block.close_write_file(info.file_id_, df, r.crc);
-}
-
-void CloseBatcher::run() {
-  std::unique_lock<std::mutex> lk(mu_);
-  for (;;) {
-    cv_.wait_for(lk, std::chrono::microseconds(max_wait_us_), [&] { return stop_ || queue_.size() >= max_batch_; });
-    if (queue_.empty()) {
-      if (stop_) return;
-      continue;
-    }
-    std::vector<Req*> reqs;
-    reqs.swap(queue_);
-    lk.unlock();
-    flush(reqs);
-    lk.lock();
-    for (Req* r : reqs) r->done = true;
-    ++batches_;
-    done_cv_.notify_all();
-  }
-}
-
-void CloseBatcher::flush(std::vector<Req*>& reqs) {
-  // Gather every payload into one buffer, one GPU verify for the whole batch
-  // (expected = the client's CloseFileInfo.crc_).
-  const auto t0 = std::chrono::steady_clock::now();
-  std::vector<tfs_crc_vdesc> d(reqs.size());
-  uint64_t total = 0;
-  for (size_t i = 0; i < reqs.size(); ++i) total += uint64_t(reqs[i]->df->get_length());
-  if (total + 16 > gather_cap_) {
-    if (gather_) tfs_crc32_host_free_pinned(ctx_, gather_);
-    gather_ = nullptr;
-    gather_cap_ = 0;
-    void* p = nullptr;
-    const size_t want = size_t(total) + 16 + size_t(total) / 2;
-    if (tfs_crc32_host_malloc_pinned(ctx_, want, &p) == TFS_SUCCESS) {
-      gather_ = static_cast<char*>(p);
-      gather_cap_ = want;
-    }
-  }
-  std::vector<char> pageable;  // only if the pinned allocation failed
-  char* gathered = gather_;
-  if (!gathered) {
-    pageable.resize(size_t(total) + 16);
-    gathered = pageable.data();
-  }
-  // A lease whose payload cannot be read back (spill-file I/O error) is not
-  // verified: it fails with TFS_ERROR as LogicBlock::close_write_file would
-  // (logic_block.cpp:264-270), instead of checking stale gather-buffer bytes.
-  std::vector<size_t> which;  // request index of each descriptor
-  which.reserve(reqs.size());
-  uint64_t off = 0;
-  for (size_t i = 0; i < reqs.size(); ++i) {
-    DataFile& df = *reqs[i]->df;
-    const int32_t n = df.get_length();
-    int32_t got = 0;
-    while (got < n) {
-      int32_t rl = n - got;
-      if (!df.get_data(gathered + off + got, &rl, got) || rl <= 0) break;
-      got += rl;
-    }
-    if (got < n) {
-      reqs[i]->status = kTfsError;
-      continue;
-    }
-    d[which.size()] = tfs_crc_vdesc{off, uint32_t(n), reqs[i]->info->crc_};
-    which.push_back(i);
-    off += uint64_t(n);
-  }
-  const uint32_t nv = uint32_t(which.size());
-  std::vector<uint32_t> crc(nv);
-  std::vector<uint8_t> ok(nv);
-  uint32_t nbad = 0;
-  const auto t1 = std::chrono::steady_clock::now();
-  const int rc = nv ? tfs_crc32_verify(ctx_, d.data(), nv, gathered, off, crc.data(), ok.data(), &nbad) : TFS_SUCCESS;
-  const auto t2 = std::chrono::steady_clock::now();
-  gather_us_ += std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count();
-  verify_us_ += std::chrono::duration_cast<std::chrono::microseconds>(t2 - t1).count();
-  for (size_t k = 0; k < nv; ++k) {
-    Req& r = *reqs[which[k]];
-    if (rc != TFS_SUCCESS && rc != TFS_EXIT_CHECK_CRC_ERROR) {
-      r.status = rc;  // device failure: reported as such, never as client corruption
-    } else if (!ok[k]) {
-      r.status = TFS_EXIT_DATA_FILE_ERROR;  // data_management.cpp:198
-    } else {
-      r.status = kAppend;
-      r.crc = crc[k];
-    }
-  }
+  const auto c4 = trace_ ? clk::now() : clk::time_point();
+  const int rc = block.close_write_file(info.file_id_, df, crc);
+  if (trace_) t_append_ += us(c4, clk::now());
+  return rc;
 }
 
 // ---------------- CrcService (DataService's CRC side, multi-GPU) ----------------

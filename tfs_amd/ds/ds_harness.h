@@ -12,6 +12,8 @@
 //   BlockCrcChecker       src/dataserver/block_checker.cpp:58-182, block_status.h:40-52
 //   compact_block         src/dataserver/task.cpp:713-836 (+ re-CRC verify)
 #pragma once
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <cstdio>
@@ -77,15 +79,37 @@ struct CloseFileInfo {  // internal.h:716-726
 // DataHandle presents them: data_handle.cpp:103-141) plus its index.
 // Block bytes: a vector whose growth does not zero-fill (every byte below size()
 // belongs to a record that its writer fills), so appends touch each page once.
+// Its storage may be a page-locked arena from a BlockImagePool: a dataserver
+// preallocates its blocks (BlockFileManager::bootstrap), and a page-locked image
+// is verified in place -- only the named records cross PCIe, no staging copy.
+struct ImageArena {
+  char* p = nullptr;
+  size_t cap = 0;
+  std::atomic<bool> in_use{false};
+};
+
 template <typename T>
-struct DefaultInitAlloc : std::allocator<T> {
+struct ImageAlloc {
+  using value_type = T;
+  using propagate_on_container_move_assignment = std::true_type;
+  using propagate_on_container_swap = std::true_type;
+  using propagate_on_container_copy_assignment = std::true_type;
+  ImageArena* arena = nullptr;
+  ImageAlloc() = default;
+  explicit ImageAlloc(ImageArena* a) : arena(a) {}
   template <typename U>
-  struct rebind {
-    using other = DefaultInitAlloc<U>;
-  };
-  DefaultInitAlloc() = default;
-  template <typename U>
-  DefaultInitAlloc(const DefaultInitAlloc<U>&) noexcept {}
+  ImageAlloc(const ImageAlloc<U>& o) noexcept : arena(o.arena) {}
+  T* allocate(size_t n) {
+    if (arena && n * sizeof(T) <= arena->cap && !arena->in_use.exchange(true)) return reinterpret_cast<T*>(arena->p);
+    return static_cast<T*>(::operator new(n * sizeof(T)));
+  }
+  void deallocate(T* p, size_t) noexcept {
+    if (arena && reinterpret_cast<char*>(p) == arena->p) {
+      arena->in_use = false;
+      return;
+    }
+    ::operator delete(p);
+  }
   template <typename U>
   void construct(U* p) noexcept {
     ::new (static_cast<void*>(p)) U;
@@ -94,12 +118,30 @@ struct DefaultInitAlloc : std::allocator<T> {
   void construct(U* p, A&&... a) {
     ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
   }
+  template <typename U>
+  bool operator==(const ImageAlloc<U>& o) const noexcept { return arena == o.arena; }
+  template <typename U>
+  bool operator!=(const ImageAlloc<U>& o) const noexcept { return arena != o.arena; }
 };
-using ByteImage = std::vector<char, DefaultInitAlloc<char>>;
+using ByteImage = std::vector<char, ImageAlloc<char>>;
+
+// Page-locked block buffers (tfs_crc32_host_malloc_pinned on one context),
+// allocated once and lent to LogicBlockImages.
+class BlockImagePool {
+ public:
+  BlockImagePool(tfs_crc_ctx* ctx, size_t count, size_t bytes);
+  ~BlockImagePool();
+  ImageArena* take();  // a free arena, or nullptr (the image then lives in pageable memory)
+  size_t size() const { return arenas_.size(); }
+
+ private:
+  tfs_crc_ctx* ctx_;
+  std::vector<std::unique_ptr<ImageArena>> arenas_;
+};
 
 class LogicBlockImage {
  public:
-  explicit LogicBlockImage(uint32_t block_id, int64_t capacity = 64LL * 1024 * 1024);
+  explicit LogicBlockImage(uint32_t block_id, int64_t capacity = 64LL * 1024 * 1024, ImageArena* arena = nullptr);
   uint32_t block_id() const { return block_id_; }
   // LogicBlock::close_write_file (logic_block.cpp:156-372), insert path:
   // FileInfo{id, offset=data_offset, size=len+36, usize, mtime, ctime, flag=0, crc}|payload.
@@ -124,60 +166,77 @@ class LogicBlockImage {
   std::vector<int32_t> sorted_flags() const;
   const ByteImage& data() const { return data_; }
   ByteImage& data() { return data_; }
-  int64_t data_size() const {
-    std::shared_lock<std::shared_mutex> g(mu_);
-    return int64_t(data_.size());
-  }
+  int64_t data_size() const { return used_.load(std::memory_order_acquire); }
   void replace(ByteImage&& data, const std::vector<tfs_raw_meta>& metas, const std::vector<int32_t>& flags);
 
  private:
   uint32_t block_id_;
   int64_t capacity_;
   ByteImage data_;
+  std::atomic<int64_t> used_{0};  // == data_.size() once every append has returned
   std::map<uint64_t, tfs_raw_meta> index_;
   std::map<uint64_t, int32_t> flags_;
-  mutable std::shared_mutex mu_;  // exclusive: layout/index changes; shared: filling a record
+  mutable std::mutex mu_;                // record ranges, index and flags
+  mutable std::shared_mutex grow_mu_;    // exclusive only to move the image (growth past the reservation)
 };
 
 // DataManagement::close_write_file (data_management.cpp:173-236): CRC compare
 // then persist with the computed crc.  EXIT_DATA_FILE_ERROR on mismatch.
 int close_write_file(const CloseFileInfo& info, DataFile& df, LogicBlockImage& block);
 
-// Batched closes across leases: many worker threads submit, one GPU batch
-// verifies all client CRCs (tfs_crc32_verify over the gathered payloads), then
-// each waiter gets the status close_write_file would have returned.
+// Batched closes across leases.  Leader-based: the first lease of a batch leads
+// it -- it waits until max_batch leases have joined (or max_wait_us passed),
+// then runs one GPU verify of every member's client CRC (tfs_crc32_verify, a
+// zero-copy launch over the page-locked gather buffer).  Each member copies its
+// own payload into the gather buffer (the copies run side by side) and waits
+// spinning for the verdict -- no hand-off thread, no condition-variable wake-up
+// on the critical path.  Up to kBatches batches are in use at once, so the next
+// batch forms while one is on the GPU.  Each member then gets the status
+// close_write_file would have returned and persists its own record.  Payloads
+// larger than kMaxBatched take the unbatched close.
 class CloseBatcher {
  public:
   CloseBatcher(tfs_crc_ctx* ctx, size_t max_batch, int max_wait_us);
   ~CloseBatcher();
   // Blocks until this close has been checked (and persisted on success).
   int close(const CloseFileInfo& info, DataFile& df, LogicBlockImage& block);
-  uint64_t batches() const { return batches_; }
+  uint64_t batches() const { return batches_.load(); }
+
+  static constexpr int kBatches = 4;
+  static constexpr int32_t kMaxBatched = 2 * 1024 * 1024;  // DataFile's in-memory limit (data_file.h:78)
 
  private:
-  struct Req {
-    const CloseFileInfo* info;
-    DataFile* df;
-    LogicBlockImage* block;
-    int status = 1;
-    uint32_t crc = 0;
-    bool done = false;
+  struct Batch {
+    char* gather = nullptr;  // page-locked (pageable `fallback` if that allocation failed)
+    std::vector<char> fallback;
+    std::vector<tfs_crc_vdesc> desc;
+    std::vector<uint32_t> crc;
+    std::vector<uint8_t> ok;
+    uint32_t n = 0;           // members (under mu_)
+    uint64_t bytes = 0;       // gather bytes claimed (under mu_)
+    bool free = true;         // (under mu_)
+    std::atomic<bool> closed{false};
+    std::atomic<uint32_t> ready{0};  // members whose payload and descriptor are in place
+    std::atomic<uint32_t> left{0};   // members that have not read their verdict yet
+    std::atomic<int> done{0};
+    int rc = TFS_SUCCESS;
+    std::chrono::steady_clock::time_point opened;
   };
   static constexpr int kAppend = 1;  // checked, the closing thread persists it
-  void run();
-  void flush(std::vector<Req*>& reqs);
+  Batch* take_batch(std::unique_lock<std::mutex>& lk);
+  void lead(Batch* b);
   tfs_crc_ctx* ctx_;
   size_t max_batch_;
   int max_wait_us_;
+  size_t gather_cap_;  // per batch: max_batch x 256 KiB, within [4 MiB, 16 MiB]
   std::mutex mu_;
-  std::condition_variable cv_, done_cv_;
-  std::vector<Req*> queue_;
-  char* gather_ = nullptr;  // page-locked gather buffer (the verify DMA reads it directly)
-  size_t gather_cap_ = 0;
-  bool stop_ = false;
-  uint64_t batches_ = 0;
-  int64_t gather_us_ = 0, verify_us_ = 0;  // TFS_DS_TRACE diagnostics
-  std::thread worker_;
+  std::condition_variable free_cv_;
+  Batch batches_buf_[kBatches];
+  Batch* cur_ = nullptr;  // the batch taking members (under mu_)
+  std::atomic<uint64_t> batches_{0};
+  std::atomic<int64_t> verify_us_{0};  // TFS_DS_TRACE diagnostics
+  std::atomic<int64_t> t_claim_{0}, t_copy_{0}, t_wait_{0}, t_append_{0}, t_lead_wait_{0};
+  bool trace_ = false;
 };
 
 // The CRC side of DataService on a multi-GPU node (dataservice.cpp:151-377
