@@ -61,7 +61,8 @@ def parse():
     p.add_argument("--ec-mib", type=int, default=1536,
                    help="member size in MiB for --workload ec (< 2048: ErasureCode sizes are int)")
     p.add_argument("--membench", action="store_true", help="also time raw streaming reads (stderr)")
-    p.add_argument("--workload", default="verify", choices=["verify", "zipf", "compact", "e2e", "packet", "compact_device", "ec", "loopback", "block_verify"],
+    p.add_argument("--workload", default="verify", choices=["verify", "zipf", "compact", "e2e", "packet", "compact_device", "ec", "loopback", "block_verify",
+                            "block_verify_device"],
                    help="verify = BASELINE configs[1] (the headline line); zipf = configs[2]; "
                         "compact = configs[3]; e2e = pinned-host verify incl. H2D (configs[4] end-to-end)")
     p.add_argument("--ab", default="", help="comma list of TFS_CRC_VARIANT ids: interleaved A/B timing (stderr)")
@@ -98,34 +99,35 @@ def cpu_baseline(sample_u8, offs, lens, expected, seconds, what="64 KiB payloads
         if time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
-    # all-core variant through the oracle's pthread batch (one file per task)
+    # All-core variant: the same Func::crc (the reference text when built) on every
+    # CPU this process may use, one file per task (oracle_crc_batch_mt_fn's pthreads).
     allcore = None
     try:
-        if seed != 0:  # the oracle's pthread batch computes seed-0 CRCs only
-            raise StopIteration
         O = ctypes.CDLL(ora_so)
-        O.oracle_crc_batch_mt.restype = ctypes.c_int
-        O.oracle_crc_batch_mt.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
-                                          ctypes.c_int]
+        O.oracle_crc_batch_mt_fn.restype = ctypes.c_int
+        O.oracle_crc_batch_mt_fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_int]
         import tfs_amd.crc as crc
         d = np.zeros(len(offs), crc.DESC_DTYPE)
         d["offset"] = offs
         d["len"] = lens
+        d["aux"] = seed
         out = np.zeros(len(offs), np.uint32)
-        threads = min(16, os.cpu_count() or 1)
+        fn, _ = _ref_crc_fn()
+        threads = _cpu_budget()
+        O.oracle_crc_batch_mt_fn(fn, d.ctypes.data, len(offs), base, out.ctypes.data, threads)
         t1 = time.perf_counter()
         reps = 0
         while True:
-            O.oracle_crc_batch_mt(d.ctypes.data, len(offs), base, out.ctypes.data, threads)
+            O.oracle_crc_batch_mt_fn(fn, d.ctypes.data, len(offs), base, out.ctypes.data, threads)
             reps += 1
             if time.perf_counter() - t1 >= min(3.0, seconds):
                 break
         ad = time.perf_counter() - t1
         assert (out == expected).all()
         allcore = {"value": reps * float(np.sum(lens)) / ad / 2**30, "cores": threads, "nproc": os.cpu_count(),
-                   "cpu_model": _cpu_model()}
-    except StopIteration:
-        allcore = None
+                   "cpu_model": _cpu_model(), "kind": kind,
+                   "cores_source": "sched affinity capped by the cgroup cpu.max quota"}
     except Exception as e:  # reported, never fatal
         allcore = {"error": str(e)}
     return {
@@ -136,7 +138,7 @@ def cpu_baseline(sample_u8, offs, lens, expected, seconds, what="64 KiB payloads
         "sample": "%d passes over %d x %s (%.0f MiB) copied from the GPU-resident batch; "
                   "Func::crc(%s, payload) vs stored crc, single thread, %.1f s" % (
                       passes, len(offs), what, float(np.sum(lens)) / 2**20, "0" if seed == 0 else hex(seed), dt),
-        **({"allcore": allcore} if allcore is not None else {}),
+        "allcore": allcore,
     }
 
 
@@ -145,7 +147,8 @@ def main():
     if args.workload != "verify":
         return {"zipf": bench_zipf, "compact": bench_compact, "e2e": bench_e2e,
                 "packet": bench_packet, "compact_device": bench_compact_device, "ec": bench_ec,
-                "loopback": bench_loopback, "block_verify": bench_block_verify}[args.workload](args)
+                "loopback": bench_loopback, "block_verify": bench_block_verify,
+                "block_verify_device": bench_block_verify_device}[args.workload](args)
     world, rank, local, dist = _dist_init()
     import tfs_amd.crc as crc
     from tfs_amd.synth import synth_bytes
@@ -352,10 +355,14 @@ def main():
         # configs[4] asks for device-resident AND end-to-end at every N: the same
         # job's PCIe-inclusive rate, reported beside `value` (never as `value`).
         gibs, pcie, el = e2e_blocks(ctx, dist, world, rank, args.e2e_blocks)
+        ceil = pcie_ceiling(ctx)
         result["end_to_end"] = {
             "value": gibs, "unit": "GiB/s", "pcie_GBs": pcie, "ms_per_block": el / args.e2e_blocks * 1e3,
             "workload": "%d pinned host 64 MiB block images per GPU -> H2D -> verify -> verdicts back, "
-                        "3 in flight, max over ranks" % args.e2e_blocks}
+                        "3 in flight, max over ranks" % args.e2e_blocks,
+            "roofline": {"bound": "pcie", "achieved": pcie / world, "peak": ceil["h2d_GBs"], "unit": "GB/s (per GPU)",
+                         "frac": pcie / world / ceil["h2d_GBs"], "peak_source": ceil["source"],
+                         "traffic": "whole block images host->device (64 MiB + 36 B headers per 1,024 files)"}}
     if rank == 0:
         print(json.dumps(result), flush=True)
     del ev
@@ -789,12 +796,16 @@ def bench_compact(args):
     if rc != 0 or any(jobs[j].status != 0 for j in range(nblocks)):
         raise SystemExit("compact: unexpected CRC mismatches on clean blocks")
     src_total = float(world) * nblocks * blk_bytes
+    live_total = float(world) * nblocks * live * psize
     # Zero-copy form: the kernel reads only the live records from the pinned
     # source image and writes the new block into the pinned destination.
     pcie_block = 2 * live * rec
+    ceil = pcie_ceiling(ctx)
+    pcie_gbs = float(nblocks) * pcie_block / el / 1e9
     res = {
-        "metric": "GiB/s block compaction (re-read + re-CRC + repack), host block images, PCIe transfers included",
-        "value": src_total / el / 2**30, "unit": "GiB/s of source block bytes", "n_gpus": world,
+        "metric": "GiB/s of live payload compacted (re-read + re-CRC + repack), host block images, PCIe included",
+        "value": live_total / el / 2**30, "unit": "GiB/s of live payload", "n_gpus": world,
+        "source_block_GiBs": src_total / el / 2**30,
         "steps": nblocks, "warmup": len(warm), "ms_per_step": el / nblocks * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic 64 KiB files, 1024 per block, evens + every 3rd of the rest deleted (%d live)" % live,
@@ -804,6 +815,11 @@ def bench_compact(args):
             "transfer": "zero-copy: fused kernel reads live records from pinned host memory and writes the "
                         "new block to pinned host memory"},
         "pcie_GBs": float(world) * nblocks * pcie_block / el / 1e9,
+        "roofline": {"bound": "pcie", "achieved": pcie_gbs, "peak": ceil["h2d_GBs"] + ceil["d2h_GBs"],
+                     "unit": "GB/s (per GPU, both directions)", "frac": pcie_gbs / (ceil["h2d_GBs"] + ceil["d2h_GBs"]),
+                     "peak_source": ceil["source"] + " (H2D + D2H: the link is full duplex)",
+                     "traffic": "live records read over PCIe + the new block written back (%d B per block)" %
+                                pcie_block},
         "ab": dict(ab, speedup=ab["dma_ms_per_block"] / ab["zero_copy_ms_per_block"], blocks=nab),
     }
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -821,8 +837,8 @@ def bench_compact(args):
                 break
         dt = time.perf_counter() - t0
         res["cpu_baseline"] = {
-            "value": reps * blk_bytes / dt / 2**30, "unit": "GiB/s of source block bytes", "cores": 1,
-            "kind": "port",
+            "value": reps * live * psize / dt / 2**30, "unit": "GiB/s of live payload", "cores": 1,
+            "kind": "port", "source_block_GiBs": reps * blk_bytes / dt / 2**30,
             "sample": "%d compactions of the %d pinned source block images (re-CRC of %d live files + repack), "
                       "oracle_compact single thread, %.1f s" % (reps, ndistinct, live, dt)}
     if rank == 0:
@@ -894,15 +910,21 @@ def bench_block_verify(args):
         out[name] = (_max_over_ranks(dist, time.perf_counter() - t0), nb)
     ctx_dma.close()
     el, nb = out["zero_copy"]
+    ceil = pcie_ceiling(ctx)
+    pcie_gbs = float(nb) * live.size * rec / el / 1e9
     res = {
-        "metric": "GiB/s verify-on-read of fragmented blocks in page-locked host memory (source block bytes)",
-        "value": float(world) * nb * blk_bytes / el / 2**30, "unit": "GiB/s", "n_gpus": world, "steps": nb,
+        "metric": "GiB/s of live payload verified on read from fragmented blocks in page-locked host memory",
+        "value": float(world) * nb * live.size * FILE_SIZE / el / 2**30, "unit": "GiB/s of live payload",
+        "source_block_GiBs": float(world) * nb * blk_bytes / el / 2**30, "n_gpus": world, "steps": nb,
         "warmup": 1, "ms_per_step": el / nb * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8",
         "data": "synthetic 64 KiB files, 1024 per block, evens + every 3rd of the rest deleted (%d live)" % live.size,
         "config": {"workload": "one tfs_block_verify per block over its live records, %d blocks" % nb,
                    "live_payload_GiBs": float(world) * nb * live.size * FILE_SIZE / el / 2**30},
         "ab": {"zero_copy_ms_per_block": el / nb * 1e3, "dma_ms_per_block": out["dma"][0] / out["dma"][1] * 1e3},
+        "roofline": {"bound": "pcie", "achieved": pcie_gbs, "peak": ceil["h2d_GBs"], "unit": "GB/s (per GPU)",
+                     "frac": pcie_gbs / ceil["h2d_GBs"], "peak_source": ceil["source"],
+                     "traffic": "the live records (FileInfo + payload) read in place over PCIe"},
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         # the reference CRC over the live payloads of the same page-locked image, checked against the
@@ -917,6 +939,148 @@ def bench_block_verify(args):
     for b in srcs:
         b.free()
     for b in (d_img, d_desc, d_crc, d_off, d_len):
+        b.free()
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+def bench_block_verify_device(args):
+    """Device-resident verify-on-read of block images (sync_backup.cpp:345-435 /
+    block_console.cpp:543-577 shape): per record the FileInfo is read, its id and
+    size checked against the index entry, the payload re-CRC'd and compared with
+    the stored crc_.  The resident set is the headline's (1,024 blocks x 1,024
+    records of 64 KiB), all records in one launch (tfs_blocks_verify_device)."""
+    import tfs_amd.crc as crc
+    world, rank, local, dist = _dist_init()
+    ctx = crc.Context(local)
+    nblocks = args.blocks
+    nfiles = nblocks * FILES_PER_BLOCK
+    rec = FILEINFO + FILE_SIZE
+    total = nfiles * rec
+    img = crc.DeviceBuffer(ctx, (total + 4095) // 4096 * 4096)
+    gblocks = rank_blocks(nblocks * world, world, rank)
+    block_bytes = FILES_PER_BLOCK * rec
+    for i, g in enumerate(gblocks):
+        ctx.synth_fill_device(img.ptr + i * block_bytes, block_bytes, 0x9E3779B97F4A7C15, int(g) * (block_bytes // 8))
+    rec_off = np.arange(nfiles, dtype=np.uint64) * rec
+    desc = np.zeros(nfiles, crc.DESC_DTYPE)
+    desc["offset"], desc["len"] = rec_off + FILEINFO, FILE_SIZE
+    d_desc = crc.DeviceBuffer(ctx, desc.nbytes).upload(desc)
+    d_crc = crc.DeviceBuffer(ctx, 4 * nfiles)
+    ctx.batch_device(d_desc, nfiles, img, d_crc)
+    d_off = crc.DeviceBuffer(ctx, 8 * nfiles).upload(rec_off)
+    d_len = crc.DeviceBuffer(ctx, 4 * nfiles).upload(np.full(nfiles, FILE_SIZE, np.uint32))
+    ctx.write_headers_device(img, d_off, d_len, d_crc, 1, nfiles)   # FileInfo{id = 1 + k, crc_}
+    ctx.sync()
+    expected = d_crc.download(np.uint32)
+    for b in (d_desc, d_off, d_len):
+        b.free()
+    jobs = np.zeros(nfiles, crc.COMPACT_JOB_DTYPE)
+    jobs["src_offset"], jobs["file_id"], jobs["size"] = rec_off, 1 + np.arange(nfiles, dtype=np.uint64), rec
+    d_jobs = crc.DeviceBuffer(ctx, jobs.nbytes).upload(jobs)
+    d_out = crc.DeviceBuffer(ctx, 4 * nfiles)
+    d_st = crc.DeviceBuffer(ctx, 4 * nfiles)
+    d_bad = crc.DeviceBuffer(ctx, 4)
+    d_bad.zero()
+
+    def step(c=ctx):
+        c.blocks_verify_device(img, total, d_jobs, nfiles, d_out, d_st, d_bad)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    ctx.sync()
+    # parity (test infrastructure): every status 0, every CRC equal to the write pass's,
+    # and one block in every --parity-every against the oracle's verify of the same bytes
+    if int(d_bad.download(np.uint32, 1)[0]) or (d_st.download(np.int32) != 0).any():
+        raise SystemExit("block_verify_device: bad statuses on clean blocks")
+    if (d_out.download(np.uint32) != expected).any():
+        raise SystemExit("block_verify_device: CRCs differ from the write pass")
+    ora = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle_crc.so"))
+    ora.oracle_verify_file.restype = ctypes.c_int32
+    ora.oracle_verify_file.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
+                                       ctypes.POINTER(ctypes.c_uint32)]
+    checked = 0
+    for b in range(0, nblocks, max(1, args.parity_every)):
+        host = img.download(np.uint8, block_bytes, b * block_bytes)
+        for k in range(0, FILES_PER_BLOCK, 64):
+            oc = ctypes.c_uint32()
+            code = ora.oracle_verify_file(host.ctypes.data, block_bytes, k * rec, rec, ctypes.byref(oc))
+            if code != 0 or oc.value != int(expected[b * FILES_PER_BLOCK + k]):
+                raise SystemExit("block_verify_device: oracle disagrees at block %d record %d" % (b, k))
+            checked += 1
+    # A/B in one process (measurement): round 1's static grid-stride block_verify_kernel
+    # over 34 windows of 31 blocks (int32 RawMeta offsets), TFS_CRC_VARIANT=24.
+    os.environ["TFS_CRC_VARIANT"] = "24"
+    c24 = crc.Context(local)
+    os.environ["TFS_CRC_VARIANT"] = "0"
+    W = 31
+    wins = []
+    for w0 in range(0, nblocks, W):
+        nb = min(W, nblocks - w0)
+        m = np.zeros(nb * FILES_PER_BLOCK, crc.META_DTYPE)
+        m["file_id"] = 1 + w0 * FILES_PER_BLOCK + np.arange(m.size)
+        m["offset"] = np.arange(m.size) * rec
+        m["size"] = rec
+        wins.append((img.ptr + w0 * block_bytes, nb * block_bytes, crc.DeviceBuffer(c24, m.nbytes).upload(m), m.size))
+
+    def step_windows(c):
+        for base, ln, dm, nm in wins:
+            c.block_verify_device(base, ln, dm, nm, None, d_st, d_bad)
+
+    def timed(c, fn):
+        e0, e1 = crc.Event(c), crc.Event(c)
+        if dist:
+            dist.barrier()
+        c.sync()
+        t0 = time.perf_counter()
+        e0.record()
+        for _ in range(args.steps):
+            fn(c)
+        e1.record()
+        c.sync()
+        if dist:
+            dist.barrier()
+        return _max_over_ranks(dist, time.perf_counter() - t0), e0.elapsed_ms(e1) / args.steps
+
+    step_windows(c24)
+    c24.sync()
+    _, kms_old = timed(c24, step_windows)
+    step_windows(ctx)
+    ctx.sync()
+    _, kms_win = timed(ctx, step_windows)
+    el, kms = timed(ctx, step)
+    for w in wins:
+        w[2].free()
+    c24.close()
+    algo_per_rec = FILEINFO + FILE_SIZE + 40 + 4 + 4   # header + payload + job read, crc + status written
+    achieved = nfiles * algo_per_rec / (kms / 1e3) / 1e9
+    res = {
+        "metric": "GiB/s payload verified on read from device-resident block images (FileInfo checks + re-CRC)",
+        "value": world * args.steps * nfiles * FILE_SIZE / el / 2**30, "unit": "GiB/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (splitmix64) 64 KiB payloads behind FileInfo headers, generated on device",
+        "config": {"workload": "%d resident blocks x %d records of 64 KiB (%.1f GiB), one launch per pass" % (
+            nblocks, FILES_PER_BLOCK, nfiles * FILE_SIZE / 2**30), "files_per_gpu": nfiles,
+            "algorithmic_bytes_per_record": algo_per_rec},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "compact_pipe_kernel<true,true,true> (verify form)", "kernel_ms_avg": kms},
+        "parity": {"statuses_all_ok": True, "crcs_equal_write_pass": nfiles, "oracle_checked": checked},
+        "ab": {"pipelined_one_launch_ms": kms, "pipelined_31_block_windows_ms": kms_win,
+               "round1_block_verify_kernel_windows_ms": kms_old, "speedup_vs_round1": kms_old / kms},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        # the reference's Func::crc over the payloads of resident block 0 copied to host,
+        # against the stored crc_ (the loop of sync_backup.cpp:383-435 without the pread)
+        host = img.download(np.uint8, block_bytes)
+        cb = cpu_baseline(host, np.arange(FILES_PER_BLOCK) * rec + FILEINFO, np.full(FILES_PER_BLOCK, FILE_SIZE),
+                          expected[:FILES_PER_BLOCK], args.cpu_seconds, "64 KiB payloads of resident block 0")
+        res["cpu_baseline"] = cb
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    for b in (img, d_crc, d_jobs, d_out, d_st, d_bad):
         b.free()
     ctx.close()
     if dist:
@@ -1048,7 +1212,7 @@ def bench_compact_device(args):
     if args.membench:  # streaming-copy ceiling for the same number of live bytes
         nb = int(live_bytes_total(windows, rec)) // 16 * 16
         cdst = crc.DeviceBuffer(ctx, nb + 64)
-        for pat in (50000, 51000):
+        for pat in (50000, 51000, 52001, 52004, 52008, 52104, 52114, 52014, 52118, 52108):
             e0, e1 = crc.Event(ctx), crc.Event(ctx)
             ctx.membench_device(pat, img, None, 0, nb, cdst)
             e0.record()
@@ -1060,13 +1224,29 @@ def bench_compact_device(args):
         cdst.free()
     el_w, kms_w = timed(ctx)
     el2, kms2 = timed(ctx2)
+    os.environ["TFS_CRC_VARIANT"] = "22"   # A/B: the unpipelined fused kernel (round 1's product)
+    ctx22 = crc.Context(local)
+    os.environ["TFS_CRC_VARIANT"] = "0"
+    step_jobs(ctx22)
+    ctx22.sync()
+    _, kms22 = timed(ctx22, step_jobs)
+    ctx22.close()
+    os.environ["TFS_CRC_VARIANT"] = "23"   # A/B: the pipelined kernel with ds_bpermute lane shifts
+    ctx23 = crc.Context(local)
+    os.environ["TFS_CRC_VARIANT"] = "0"
+    step_jobs(ctx23)
+    ctx23.sync()
+    _, kms23 = timed(ctx23, step_jobs)
+    ctx23.close()
     el, kms = timed(ctx, step_jobs)
     nlive = sum(w["n"] for w in windows)
     live_bytes = float(nlive) * rec
     algo = 2 * live_bytes + nlive * (16 + 4 + 8 + 4)  # read + write live records, metas/flags/offsets/status
+    live_payload = float(nlive) * FILE_SIZE
     res = {
-        "metric": "GiB/s device-resident compaction (re-CRC + repack of live files), source block bytes",
-        "value": world * args.steps * float(total) / el / 2**30, "unit": "GiB/s", "n_gpus": world,
+        "metric": "GiB/s of live payload compacted on the device (re-CRC + repack of live files)",
+        "value": world * args.steps * live_payload / el / 2**30, "unit": "GiB/s of live payload", "n_gpus": world,
+        "source_block_GiBs": world * args.steps * float(total) / el / 2**30,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic 64 KiB files, 1024 per block, evens + every 3rd of the rest deleted",
@@ -1077,7 +1257,9 @@ def bench_compact_device(args):
                      "kernel": "compact_fused_kernel<WIDE> (one launch)", "kernel_ms_avg": kms},
         "membench": extra,
         "ab": {"fused_one_launch_ms": kms, "fused_windows_ms": kms_w, "unfused_windows_ms": kms2,
-               "windows": len(windows), "speedup_vs_unfused": kms2 / kms},
+               "unpipelined_fused_one_launch_ms": kms22, "pipelined_bpermute_one_launch_ms": kms23,
+               "windows": len(windows), "speedup_vs_unfused": kms2 / kms,
+               "speedup_vs_unpipelined": kms22 / kms},
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         # CPU restatement of real_compact + re-CRC (oracle_compact) over block 0 of the same image, one thread
@@ -1102,7 +1284,8 @@ def bench_compact_device(args):
         if not (ook[flags1 == 0] == 1).all():
             raise SystemExit("compact_device: oracle re-CRC disagrees with the GPU-written headers")
         res["cpu_baseline"] = {
-            "value": reps * blk / dt / 2**30, "unit": "GiB/s of source block bytes", "cores": 1, "kind": "port",
+            "value": reps * len(live1) * FILE_SIZE / dt / 2**30, "unit": "GiB/s of live payload", "cores": 1,
+            "kind": "port", "source_block_GiBs": reps * blk / dt / 2**30,
             "sample": "%d compactions of resident block 0 copied to host (re-CRC of %d live files + repack), "
                       "oracle_compact single thread, %.1f s" % (reps, len(live1), dt)}
     if rank == 0:
@@ -1534,6 +1717,9 @@ def bench_e2e(args):
         "config": {"workload": "pinned host blocks -> GPU verify, %d in flight, %d blocks" % (inflight, nsub)},
         "pcie_GBs": pcie,
     }
+    ceil = pcie_ceiling(ctx)
+    res["roofline"] = {"bound": "pcie", "achieved": pcie / world, "peak": ceil["h2d_GBs"], "unit": "GB/s (per GPU)",
+                       "frac": pcie / world / ceil["h2d_GBs"], "peak_source": ceil["source"], "traffic": None}
     if rank == 0:
         print(json.dumps(res), flush=True)
     ctx.close()

@@ -227,6 +227,14 @@ int tfs_compact_jobs_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_le
                             uint32_t n, void* d_dest, uint32_t* d_out_crc, int32_t* d_out_status, uint32_t* d_n_bad,
                             void* stream);
 
+/* Verify-on-read of the records of many device-resident blocks in one launch
+ * (64-bit offsets): per job, the FileInfo at d_src + src_offset is checked
+ * against file_id and size and the payload CRC against its crc_, statuses as
+ * tfs_block_verify.  The dest_offset / flag / new_offset fields of the jobs are
+ * not used.  Asynchronous on `stream`; d_n_bad accumulated into. */
+int tfs_blocks_verify_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_len, const tfs_compact_job* d_jobs,
+                             uint32_t n, uint32_t* d_out_crc, int32_t* d_out_status, uint32_t* d_n_bad, void* stream);
+
 /* Many blocks in one call (the compaction task thread's queue): each job is
  * tfs_block_compact's arguments plus its outputs.  Jobs are pipelined over
  * several streams so the H2D copy of one block, the verify/repack kernels of

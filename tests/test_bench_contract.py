@@ -36,8 +36,14 @@ def test_default_line_contract_small():
     assert rf["traffic"] is None  # PMC traffic is only quoted for the full-size launch it was measured on
     cb = res["cpu_baseline"]
     assert cb["value"] > 0 and cb["cores"] == 1 and cb["kind"] in ("reference", "port")
+    ac = cb["allcore"]
+    assert ac["value"] > cb["value"] and ac["cores"] >= 1 and ac["kind"] == cb["kind"]
     e2e = res["end_to_end"]
     assert 0 < e2e["value"] < res["value"] and e2e["pcie_GBs"] > 0
+    er = e2e["roofline"]
+    assert er["bound"] == "pcie" and 0 < er["frac"] < 1.2 and er["peak"] > 10
+    par = res["parity"]
+    assert par["files_checked"] >= 1024 and par["mismatches"] == 0 and par["verdicts_all_ok"]
 
 
 @pytest.mark.gpu
@@ -46,6 +52,8 @@ def test_zipf_and_compact_lines_carry_cpu_baseline():
     assert z["roofline"]["bound"] == "hbm" and z["cpu_baseline"]["value"] > 0
     c = _run(["--workload", "compact", "--compact-blocks", "16", "--cpu-seconds", "0.3"])
     assert c["value"] > 0 and c["cpu_baseline"]["kind"] == "port" and c["ab"]["speedup"] > 0
+    assert c["unit"] == "GiB/s of live payload" and c["source_block_GiBs"] > c["value"]
+    assert c["roofline"]["bound"] == "pcie" and 0 < c["roofline"]["frac"] < 1.2
 
 
 @pytest.mark.gpu
@@ -68,3 +76,17 @@ def test_packet_and_compact_device_lines_carry_cpu_baseline():
 def test_block_verify_line_carries_cpu_baseline():
     b = _run(["--workload", "block_verify", "--compact-blocks", "16", "--cpu-seconds", "0.3"])
     assert b["value"] > 0 and b["cpu_baseline"]["source_block_GiBs"] > b["cpu_baseline"]["value"] > 0
+    assert b["source_block_GiBs"] > b["value"] and b["roofline"]["bound"] == "pcie"
+
+
+@pytest.mark.gpu
+def test_block_verify_device_and_loopback_lines():
+    d = _run(["--workload", "block_verify_device", "--blocks", "8", "--steps", "2", "--warmup", "1",
+              "--cpu-seconds", "0.3", "--parity-every", "4"])
+    assert d["roofline"]["bound"] == "hbm" and d["value"] > 0 and d["cpu_baseline"]["value"] > 0
+    assert d["parity"]["oracle_checked"] > 0
+    lb = _run(["--workload", "loopback", "--steps", "1", "--cpu-seconds", "0.5"])
+    assert lb["value"] > 0 and lb["roofline"]["bound"] == "pcie"
+    for k in ("scalar_tfs_crc32_64KiB", "close_1_leases", "close_8_leases", "close_64_leases"):
+        assert 0 < lb["latency"][k]["p50_us"] <= lb["latency"][k]["p99_us"], k
+    assert lb["cpu_baseline"]["allcore"]["value"] > 0

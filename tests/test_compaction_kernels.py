@@ -1,0 +1,239 @@
+"""The compaction data pass under every kernel form: the product
+pipelined kernel (dynamic tickets, next-record prefetch, DPP lane shifts), the
+same with ds_bpermute lane shifts (TFS_CRC_VARIANT=23) and round 1's
+unpipelined fused kernel (22).  Each must produce the oracle's real_compact
+bytes and statuses exactly, for every destination shift class, tiny and large
+records, rejected records (size, range, id, CRC), device-resident single-block
+and many-block forms, and zero-copy host images."""
+import numpy as np
+import pytest
+
+from test_gpu_parity import _block_image, _oracle_compact
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(params=[0, 22, 23])
+def vctx(request, monkeypatch):
+    import tfs_amd.crc as crc
+    monkeypatch.setenv("TFS_CRC_VARIANT", str(request.param))
+    ctx = crc.Context(0)
+    monkeypatch.setenv("TFS_CRC_VARIANT", "0")
+    yield ctx
+    ctx.close()
+
+
+def _shift_class_block(oracle, seed, n=200):
+    rng = np.random.default_rng(seed)
+    sizes, flags = [], []
+    for k in range(n):
+        sizes.append(int(rng.choice([1, 3, 17, 31, 32, 33, 100, 1023, 1024, 1025, 2049, 5000, 65536, 70001,
+                                     200000])))
+        flags.append(1 if k % 3 == 1 else 0)
+        if flags[-1]:
+            sizes[-1] = 16 + (k % 16 - 36) % 16 + 16 * int(rng.integers(0, 4))
+    img, metas = _block_image(oracle, sizes, seed=seed)
+    return img, metas, np.array(flags, np.int32)
+
+
+def test_host_compaction_all_shift_classes(vctx, oracle):
+    img, metas, fl = _shift_class_block(oracle, 301)
+    assert fl[9] == 0
+    img[int(metas[9]["offset"]) + 36 + 3] ^= 0x80     # a live record with a bad payload
+    dest, dmetas, ok, rc = vctx.block_compact(img, metas, fl)
+    odest, doff, ook = _oracle_compact(oracle, img, metas, fl)
+    assert dest.size == odest.size and (dest == odest).all()
+    assert (ok == ook).all() and rc == -1010
+
+
+def test_device_compaction_statuses(vctx, oracle):
+    """tfs_block_compact_device with rejected records mixed in: too short, past the
+    image, wrong FileInfo id, wrong FileInfo size, bad CRC -- statuses in the
+    reference's order (id, size, crc), good records repacked byte-exact."""
+    import tfs_amd.crc as crc
+    img, metas, fl = _shift_class_block(oracle, 302, 120)
+    live = np.nonzero(fl == 0)[0]
+    lm = np.ascontiguousarray(metas[live])
+    odest, doff, ook = _oracle_compact(oracle, img, metas, fl)
+    ld = np.concatenate([[0], np.cumsum(lm["size"].astype(np.int64))[:-1]]).astype(np.int64)
+    bad = {}
+    lm[3]["size"] = 36                       # too short
+    bad[3] = -8034
+    lm[5]["offset"] = img.size - 8           # runs past the image
+    bad[5] = -1016
+    lm[7]["file_id"] = 123456789             # FileInfo id != index
+    bad[7] = -8016
+    img2 = img.copy()
+    img2[int(lm[9]["offset"]) + 12] ^= 1     # FileInfo.size_ != index size
+    bad[9] = -8038
+    img2[int(lm[11]["offset"]) + 36] ^= 1    # payload corrupted
+    bad[11] = -1010
+    n = len(lm)
+    d_src = crc.DeviceBuffer(vctx, img2.size + 64).upload(img2)
+    d_m = crc.DeviceBuffer(vctx, lm.nbytes).upload(lm)
+    d_f = crc.DeviceBuffer(vctx, 4 * n).upload(np.zeros(n, np.int32))
+    d_o = crc.DeviceBuffer(vctx, 8 * n).upload(ld)
+    d_dst = crc.DeviceBuffer(vctx, odest.size + 64)
+    d_dst.zero()
+    d_st = crc.DeviceBuffer(vctx, 4 * n)
+    d_bad = crc.DeviceBuffer(vctx, 4)
+    d_bad.zero()
+    vctx.block_compact_device(d_src, img2.size, d_m, d_f, d_o, n, d_dst, None, d_st, d_bad)
+    vctx.sync()
+    st = d_st.download(np.int32, n)
+    out = d_dst.download(np.uint8, odest.size)
+    for k in range(n):
+        assert st[k] == bad.get(k, 0), (k, st[k])
+        if k in bad:
+            continue
+        o, sz = int(ld[k]), int(lm[k]["size"])
+        assert (out[o:o + sz] == odest[o:o + sz]).all(), k
+    assert int(d_bad.download(np.uint32, 1)[0]) == len(bad)
+
+
+def test_jobs_device_many_blocks_shuffled(vctx, oracle):
+    import tfs_amd.crc as crc
+    rng = np.random.default_rng(303)
+    blocks, jobs, expect = [], [], []
+    src_base = dst_base = 0
+    for b in range(6):
+        img, metas, fl = _shift_class_block(oracle, 310 + b, 60)
+        odest, doff, ook = _oracle_compact(oracle, img, metas, fl)
+        for i in np.nonzero((fl & 3) == 0)[0]:
+            jobs.append((src_base + int(metas[i]["offset"]), dst_base + int(doff[i]), int(metas[i]["file_id"]),
+                         int(metas[i]["size"]), 0, int(doff[i]), 0))
+        blocks.append(img[:int(metas["size"].astype(np.int64).sum())])
+        expect.append((dst_base, odest))
+        src_base += blocks[-1].size
+        dst_base += odest.size + (b * 5) % 16
+    src = np.concatenate(blocks)
+    j = np.array(jobs, dtype=crc.COMPACT_JOB_DTYPE)
+    rng.shuffle(j)
+    d_src = crc.DeviceBuffer(vctx, src.size + 64).upload(src)
+    d_j = crc.DeviceBuffer(vctx, j.nbytes).upload(j)
+    d_dst = crc.DeviceBuffer(vctx, dst_base + 64)
+    d_dst.zero()
+    d_st = crc.DeviceBuffer(vctx, 4 * len(j))
+    d_bad = crc.DeviceBuffer(vctx, 4)
+    d_bad.zero()
+    for rep in range(3):   # repeated launches on one stream: tickets reset by each launch
+        vctx.compact_jobs_device(d_src, src.size, d_j, len(j), d_dst, None, d_st, d_bad)
+    vctx.sync()
+    out = d_dst.download(np.uint8, dst_base)
+    for base, od in expect:
+        assert (out[base:base + od.size] == od).all()
+    assert int(d_bad.download(np.uint32, 1)[0]) == 0 and (d_st.download(np.int32, len(j)) == 0).all()
+
+
+def test_zero_copy_host_images(vctx, oracle):
+    import tfs_amd.crc as crc
+    img, metas = _block_image(oracle, [65536] * 40 + [4 * 777, 4 * 1001], seed=320)
+    fl = np.zeros(len(metas), np.int32)
+    fl[::2] = 1
+    src = crc.PinnedBuffer(vctx, img.size)
+    cap = int(metas["size"].astype(np.int64).sum()) + 64
+    dst = crc.PinnedBuffer(vctx, cap)
+    try:
+        src.array[:] = img
+        dst.array[:] = 0
+        jobs = (crc.BlockJob * 1)()
+        ok = np.zeros(len(metas), np.uint8)
+        j = jobs[0]
+        j.src_image, j.src_len, j.metas, j.flags, j.n = src.ptr, img.size, metas.ctypes.data, fl.ctypes.data, len(metas)
+        j.dest_image, j.dest_cap, j.crc_ok = dst.ptr, cap, ok.ctypes.data
+        assert vctx.blocks_compact(jobs) == 0
+        odest, doff, ook = _oracle_compact(oracle, img, metas, fl)
+        assert (dst.array[:odest.size] == odest).all() and (ok == ook).all()
+    finally:
+        src.free()
+        dst.free()
+
+
+@pytest.fixture(params=[0, 24])
+def vfy_ctx(request, monkeypatch):
+    """Verify-on-read forms: the pipelined record kernel (product) and round 1's
+    grid-stride block_verify_kernel (TFS_CRC_VARIANT=24)."""
+    import tfs_amd.crc as crc
+    monkeypatch.setenv("TFS_CRC_VARIANT", str(request.param))
+    ctx = crc.Context(0)
+    monkeypatch.setenv("TFS_CRC_VARIANT", "0")
+    yield ctx
+    ctx.close()
+
+
+def _statuses_case(oracle):
+    img, metas, fl = _shift_class_block(oracle, 330, 160)
+    m = np.ascontiguousarray(metas.copy())
+    img = img.copy()
+    m[2]["size"] = 20                                 # too short      -> -8034
+    m[4]["offset"] = img.size - 10                    # past the image -> -1016
+    m[6]["file_id"] = 999                             # id mismatch    -> -8016
+    img[int(m[8]["offset"]) + 12] ^= 2                # size mismatch  -> -8038
+    img[int(m[10]["offset"]) + 36 + int(m[10]["size"]) // 2 - 18] ^= 1   # bad payload -> -1010
+    want = {2: -8034, 4: -1016, 6: -8016, 8: -8038, 10: -1010}
+    return img, m, want
+
+
+def test_block_verify_forms_statuses(vfy_ctx, oracle):
+    import tfs_amd.crc as crc
+    img, m, want = _statuses_case(oracle)
+    for k in range(len(m)):
+        if k in want:
+            continue
+        o, sz = int(m[k]["offset"]), int(m[k]["size"])
+        assert oracle.oracle_verify_file(img.ctypes.data, img.size, o, sz, None) == 0
+    # host form
+    c, st, nbad, rc = vfy_ctx.block_verify(img, m)
+    assert rc == -1010 and nbad == len(want)
+    assert {k: int(st[k]) for k in range(len(m)) if st[k] != 0} == want
+    for k in range(len(m)):
+        if st[k] == 0:
+            o, sz = int(m[k]["offset"]), int(m[k]["size"])
+            oc = __import__("ctypes").c_uint32()
+            oracle.oracle_verify_file(img.ctypes.data, img.size, o, sz, __import__("ctypes").byref(oc))
+            assert int(c[k]) == oc.value
+    # device form
+    n = len(m)
+    d_img = crc.DeviceBuffer(vfy_ctx, img.size + 64).upload(img)
+    d_m = crc.DeviceBuffer(vfy_ctx, m.nbytes).upload(m)
+    d_c = crc.DeviceBuffer(vfy_ctx, 4 * n)
+    d_s = crc.DeviceBuffer(vfy_ctx, 4 * n)
+    d_b = crc.DeviceBuffer(vfy_ctx, 4)
+    d_b.zero()
+    vfy_ctx.block_verify_device(d_img, img.size, d_m, n, d_c, d_s, d_b)
+    vfy_ctx.sync()
+    assert (d_s.download(np.int32, n) == st).all() and (d_c.download(np.uint32, n)[st == 0] == c[st == 0]).all()
+    assert int(d_b.download(np.uint32, 1)[0]) == len(want)
+
+
+def test_blocks_verify_device_many_blocks(gpu_ctx, oracle):
+    """tfs_blocks_verify_device: records of several blocks (64-bit offsets, any order)
+    in one launch, statuses as the single-block form."""
+    import tfs_amd.crc as crc
+    imgs, jobs, want = [], [], []
+    base = 0
+    for b in range(4):
+        img, m, w = _statuses_case(oracle) if b == 2 else (*_shift_class_block(oracle, 340 + b, 80)[:2], {})
+        for k in range(len(m)):
+            jobs.append((base + max(int(m[k]["offset"]), 0) if int(m[k]["offset"]) >= 0 else 0, 0,
+                         int(m[k]["file_id"]), int(m[k]["size"]), 0, 0, 0))
+            want.append(w.get(k, 0))
+        imgs.append(img)
+        base += img.size
+    src = np.concatenate(imgs)
+    # the "past the image" record of block 2 must be past the whole buffer here
+    j = np.array(jobs, dtype=crc.COMPACT_JOB_DTYPE)
+    idx = [i for i, x in enumerate(want) if x == -1016]
+    j["src_offset"][idx] = src.size - 10
+    order = np.random.default_rng(5).permutation(len(j))
+    j, want = j[order], np.array(want, np.int32)[order]
+    n = len(j)
+    d_src = crc.DeviceBuffer(gpu_ctx, src.size + 64).upload(src)
+    d_j = crc.DeviceBuffer(gpu_ctx, j.nbytes).upload(j)
+    d_s = crc.DeviceBuffer(gpu_ctx, 4 * n)
+    d_b = crc.DeviceBuffer(gpu_ctx, 4)
+    d_b.zero()
+    gpu_ctx.blocks_verify_device(d_src, src.size, d_j, n, None, d_s, d_b)
+    gpu_ctx.sync()
+    assert (d_s.download(np.int32, n) == want).all()
+    assert int(d_b.download(np.uint32, 1)[0]) == int((want != 0).sum())

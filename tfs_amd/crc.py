@@ -64,7 +64,7 @@ EXPORTED = [
     "tfs_crc_group_create", "tfs_crc_group_destroy", "tfs_crc_group_last_error", "tfs_crc_group_size",
     "tfs_crc_group_ctx", "tfs_crc_group_member_of", "tfs_crc_group_ctx_for_block", "tfs_crc_group_numa_node",
     "tfs_crc_group_member_bound", "tfs_crc_group_host_malloc", "tfs_crc_group_host_free",
-    "tfs_crc_group_blocks_verify", "tfs_crc_group_blocks_compact",
+    "tfs_crc_group_blocks_verify", "tfs_crc_group_blocks_compact", "tfs_blocks_verify_device",
     "tfs_packet_verify", "tfs_packet_verify_device", "tfs_packet_seal", "tfs_packet_seal_device",
     "tfs_crc32_write_packet_headers_device", "tfs_block_compact_device", "tfs_compact_jobs_device",
 ]
@@ -115,6 +115,7 @@ def lib():
             "tfs_blocks_compact": (ctypes.c_int, [vp, vp, u32]),
             "tfs_block_compact_device": (ctypes.c_int, [vp, vp, u64, vp, vp, vp, u32, vp, vp, vp, vp, vp]),
             "tfs_compact_jobs_device": (ctypes.c_int, [vp, vp, u64, vp, u32, vp, vp, vp, vp, vp]),
+            "tfs_blocks_verify_device": (ctypes.c_int, [vp, vp, u64, vp, u32, vp, vp, vp, vp]),
             "tfs_crc32_synth_fill_device": (ctypes.c_int, [vp, vp, u64, u64, u64, vp]),
             "tfs_crc32_write_headers_device": (ctypes.c_int, [vp, vp, vp, vp, vp, u64, u32, vp]),
             "tfs_crc32_membench_device": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, u32, u64, vp, ctypes.c_uint, vp]),
@@ -345,6 +346,11 @@ class Context:
         self._check(lib().tfs_compact_jobs_device(self.handle, _ptr(d_src), src_len, _ptr(d_jobs), n, _ptr(d_dest),
                                                   _ptr(d_crc), _ptr(d_status), _ptr(d_nbad), stream),
                     "compact_jobs_device")
+
+    def blocks_verify_device(self, d_src, src_len, d_jobs, n, d_crc=None, d_status=None, d_nbad=None, stream=None):
+        """Verify-on-read of records of many device-resident blocks (tfs_compact_job layout)."""
+        self._check(lib().tfs_blocks_verify_device(self.handle, _ptr(d_src), src_len, _ptr(d_jobs), n, _ptr(d_crc),
+                                                   _ptr(d_status), _ptr(d_nbad), stream), "blocks_verify_device")
 
     def blocks_compact(self, jobs):
         """Pipelined compaction of many blocks; `jobs` is a ctypes array of BlockJob."""

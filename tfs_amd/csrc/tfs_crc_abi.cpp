@@ -33,14 +33,19 @@ hipError_t launch_packet_finish(uint8_t* base, const PacketDesc* pd, const Desc*
 hipError_t launch_block_verify(const uint8_t* image, uint64_t image_len, const RawMeta* metas, uint32_t n,
                                const Tables* tg, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
                                hipStream_t stream);
+hipError_t launch_block_verify_pipe(const uint8_t* image, uint64_t image_len, const RawMeta* metas,
+                                    const CompactJob* jobs, uint32_t n, const Tables* tg, uint32_t* out_crc,
+                                    int32_t* out_status, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
+                                    int variant);
 hipError_t launch_compact_copy(const uint8_t* src, const RawMeta* metas, const int32_t* flags, const int64_t* dest_off,
                                uint32_t n, uint8_t* dst, hipStream_t stream);
 hipError_t launch_compact_fused(const uint8_t* src, uint64_t src_len, const RawMeta* metas, const int32_t* flags,
                                 const int64_t* dest_off, uint32_t n, uint8_t* dst, const Tables* tg, uint32_t* out_crc,
-                                int32_t* out_status, uint32_t* n_bad, hipStream_t stream);
+                                int32_t* out_status, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
+                                int variant);
 hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const CompactJob* jobs, uint32_t n, uint8_t* dst,
                                const Tables* tg, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
-                               hipStream_t stream);
+                               uint32_t* sched, hipStream_t stream, int variant);
 hipError_t launch_synth_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, uint64_t first_word, hipStream_t stream);
 hipError_t launch_write_headers(uint8_t* image, const uint64_t* rec_off, const uint32_t* len, const uint32_t* crc,
                                 uint64_t first_id, uint32_t n, hipStream_t stream);
@@ -655,9 +660,24 @@ int tfs_block_verify_device(tfs_crc_ctx* ctx, const void* d_image, uint64_t imag
   if (!ctx || (n && (!d_image || !d_metas))) return TFS_EXIT_PARAMETER_ERROR;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  HIP_TRY(ctx, launch_block_verify(static_cast<const uint8_t*>(d_image), image_len,
-                                   reinterpret_cast<const RawMeta*>(d_metas), n, ctx->d_tables, d_out_crc,
-                                   d_out_status, d_n_bad, st));
+  uint32_t* sched = nullptr;
+  HIP_TRY(ctx, sched_slot(ctx, st, &sched));
+  HIP_TRY(ctx, launch_block_verify_pipe(static_cast<const uint8_t*>(d_image), image_len,
+                                        reinterpret_cast<const RawMeta*>(d_metas), nullptr, n, ctx->d_tables, d_out_crc,
+                                        d_out_status, d_n_bad, sched, st, ctx->variant));
+  return TFS_SUCCESS;
+}
+
+int tfs_blocks_verify_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_len, const tfs_compact_job* d_jobs,
+                             uint32_t n, uint32_t* d_out_crc, int32_t* d_out_status, uint32_t* d_n_bad, void* stream) {
+  if (!ctx || (n && (!d_src || !d_jobs))) return TFS_EXIT_PARAMETER_ERROR;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  uint32_t* sched = nullptr;
+  HIP_TRY(ctx, sched_slot(ctx, st, &sched));
+  HIP_TRY(ctx, launch_block_verify_pipe(static_cast<const uint8_t*>(d_src), src_len, nullptr,
+                                        reinterpret_cast<const CompactJob*>(d_jobs), n, ctx->d_tables, d_out_crc,
+                                        d_out_status, d_n_bad, sched, st, ctx->variant));
   return TFS_SUCCESS;
 }
 
@@ -695,9 +715,12 @@ int tfs_block_verify(tfs_crc_ctx* ctx, const void* image, uint64_t image_len, co
   HIP_TRY(ctx, s->h_bad.reserve(4));
   HIP_TRY(ctx, hipMemcpyAsync(s->d_desc.p, metas, size_t(n) * sizeof(RawMeta), hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(ctx, hipMemsetAsync(s->d_bad.p, 0, 4, ctx->stream));
-  HIP_TRY(ctx, launch_block_verify(d_base, image_len, static_cast<const RawMeta*>(s->d_desc.p), n, ctx->d_tables,
-                                   static_cast<uint32_t*>(s->d_crc.p), static_cast<int32_t*>(s->d_ok.p),
-                                   static_cast<uint32_t*>(s->d_bad.p), ctx->stream));
+  uint32_t* sched = nullptr;
+  HIP_TRY(ctx, sched_slot(ctx, ctx->stream, &sched));
+  HIP_TRY(ctx, launch_block_verify_pipe(d_base, image_len, static_cast<const RawMeta*>(s->d_desc.p), nullptr, n,
+                                        ctx->d_tables, static_cast<uint32_t*>(s->d_crc.p),
+                                        static_cast<int32_t*>(s->d_ok.p), static_cast<uint32_t*>(s->d_bad.p), sched,
+                                        ctx->stream, ctx->variant));
   HIP_TRY(ctx, hipMemcpyAsync(s->h_crc.p, s->d_crc.p, size_t(n) * 4, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipMemcpyAsync(s->h_ok.p, s->d_ok.p, size_t(n) * 4, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipMemcpyAsync(s->h_bad.p, s->d_bad.p, 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -788,9 +811,11 @@ static int compact_enqueue(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job
   HIP_TRY(ctx, cs.h_status.reserve(fb + 4));
   if (zc) {
     HIP_TRY(ctx, hipMemcpyAsync(da, ha, ob + mb + fb, hipMemcpyHostToDevice, cs.stream));
+    uint32_t* sched = nullptr;
+    HIP_TRY(ctx, sched_slot(ctx, cs.stream, &sched));
     HIP_TRY(ctx, launch_compact_fused(static_cast<const uint8_t*>(zc_src), job->src_len, d_metas, d_flags, d_doff, nl,
-                                      static_cast<uint8_t*>(zc_dst), ctx->d_tables, d_crc, d_status, nullptr,
-                                      cs.stream));
+                                      static_cast<uint8_t*>(zc_dst), ctx->d_tables, d_crc, d_status, nullptr, sched,
+                                      cs.stream, ctx->variant));
     HIP_TRY(ctx, hipMemcpyAsync(cs.h_status.p, d_status, fb, hipMemcpyDeviceToHost, cs.stream));
   } else {
     const int rc = compact_dma(ctx, cs, job, nl, w, da, ha, ob + mb + fb, d_metas, d_flags, d_doff, d_crc, d_status);
@@ -827,9 +852,11 @@ static int compact_dma(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job, ui
     const uint8_t* d_src = static_cast<const uint8_t*>(cs.d_src.p);
     // One read of every live record: re-CRC (the verify the reference's
     // real_compact does not do) and repack from the same registers.
+    uint32_t* sched = nullptr;
+    HIP_TRY(ctx, sched_slot(ctx, cs.stream, &sched));
     HIP_TRY(ctx, launch_compact_fused(d_src, job->src_len, d_metas, d_flags, d_doff, nl,
-                                      static_cast<uint8_t*>(cs.d_dst.p), ctx->d_tables, d_crc, d_status, nullptr,
-                                      cs.stream));
+                                      static_cast<uint8_t*>(cs.d_dst.p), ctx->d_tables, d_crc, d_status, nullptr, sched,
+                                      cs.stream, ctx->variant));
     HIP_TRY(ctx, hipMemcpyAsync(cs.h_status.p, d_status, fb, hipMemcpyDeviceToHost, cs.stream));
     if (w) HIP_TRY(ctx, hipMemcpyAsync(job->dest_image, cs.d_dst.p, size_t(w), hipMemcpyDeviceToHost, cs.stream));
   }
@@ -892,10 +919,12 @@ int tfs_block_compact_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_l
                                      d_flags, d_dest_off, n, static_cast<uint8_t*>(d_dest), st));
     return TFS_SUCCESS;
   }
+  uint32_t* sched = nullptr;
+  HIP_TRY(ctx, sched_slot(ctx, st, &sched));
   HIP_TRY(ctx, launch_compact_fused(static_cast<const uint8_t*>(d_src), src_len,
                                     reinterpret_cast<const RawMeta*>(d_live_metas), d_flags, d_dest_off, n,
                                     static_cast<uint8_t*>(d_dest), ctx->d_tables, d_out_crc, d_out_status, d_n_bad,
-                                    st));
+                                    sched, st, ctx->variant));
   return TFS_SUCCESS;
 }
 
@@ -905,9 +934,11 @@ int tfs_compact_jobs_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_le
   if (!ctx || (n && (!d_src || !d_jobs || !d_dest))) return TFS_EXIT_PARAMETER_ERROR;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  uint32_t* sched = nullptr;
+  HIP_TRY(ctx, sched_slot(ctx, st, &sched));
   HIP_TRY(ctx, launch_compact_jobs(static_cast<const uint8_t*>(d_src), src_len,
                                    reinterpret_cast<const CompactJob*>(d_jobs), n, static_cast<uint8_t*>(d_dest),
-                                   ctx->d_tables, d_out_crc, d_out_status, d_n_bad, st));
+                                   ctx->d_tables, d_out_crc, d_out_status, d_n_bad, sched, st, ctx->variant));
   return TFS_SUCCESS;
 }
 

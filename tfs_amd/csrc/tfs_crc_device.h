@@ -42,6 +42,7 @@ constexpr int kFileInfoSize = 36;  // sizeof(FileInfo), internal.h:432-446
 constexpr uint32_t kSchedStride = 64;                    // u32 between counters
 constexpr uint32_t kSchedDone = 8u * kSchedStride;       // index of the finished-waves counter
 constexpr uint32_t kSchedSlotBytes = 9u * kSchedStride * 4u;  // 2.25 KiB per stream
+constexpr uint32_t kDynMinPerWave = 16;  // dynamic tickets only for launches of >= 16 files per wave
 
 // Latency form (small batches): one workgroup of kWgWaves waves per file; wave w
 // takes stripes w, w+16, ... of the file, so a 64 KiB file is 4-5 stripes per

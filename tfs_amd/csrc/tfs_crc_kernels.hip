@@ -306,9 +306,20 @@ struct ShiftCarry {
   uint32_t y, z, w;
   bool valid;
 };
+// DPP: lane l-1's dwords by a wave_shr:1 DPP move (VALU) instead of ds_bpermute
+// (__shfl_up), which goes through the LDS crossbar beside the table lookups.
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) {
+  return __builtin_amdgcn_update_dpp(0u, v, 0x138 /* wave_shr:1 */, 0xf, 0xf, false);
+}
+template <bool DPP = true>
 __device__ __forceinline__ void store_shifted(uintptr_t chunk, const uint4& v, uint32_t k, int lane, ShiftCarry& cr,
                                               bool store, bool flush) {
-  uint32_t p1 = __shfl_up(v.w, 1, kWave), p2 = __shfl_up(v.z, 1, kWave), p3 = __shfl_up(v.y, 1, kWave);
+  uint32_t p1, p2, p3;
+  if (DPP) {
+    p1 = from_prev_lane(v.w), p2 = from_prev_lane(v.z), p3 = from_prev_lane(v.y);
+  } else {
+    p1 = __shfl_up(v.w, 1, kWave), p2 = __shfl_up(v.z, 1, kWave), p3 = __shfl_up(v.y, 1, kWave);
+  }
   if (lane == 0) {
     p1 = cr.w;
     p2 = cr.z;
@@ -348,7 +359,7 @@ __device__ __forceinline__ void store_shifted(uintptr_t chunk, const uint4& v, u
 // COPY: also store every payload byte of [start, B16) to dst = src + delta.
 // G (measurement knob): refill the ring G slots at a time, so each wave issues G
 // consecutive stripes (G KiB contiguous) back to back instead of one per stripe.
-template <int RUN, int PF, bool NT, bool S8, bool COPY = false, int G = 1>
+template <int RUN, int PF, bool NT, bool S8, bool COPY = false, int G = 1, bool DPPSH = false>
 __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase& lb, const FileGeo<RUN>& g,
                                                const Head<RUN>& h, uint4 (&buf)[PF][RUN / 16], int lane,
                                                uintptr_t junk, intptr_t delta = 0, bool copy_on = false) {
@@ -397,8 +408,8 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
       if (kshift == 0u) {
         if (valid) st128_nt(q + delta, v);
       } else {
-        store_shifted(q + uintptr_t(delta) - 4u * kshift, v, kshift, lane, carry, valid,
-                      st == last && uint32_t(lane) + 1u == g.nvalid);
+        store_shifted<DPPSH>(q + uintptr_t(delta) - 4u * kshift, v, kshift, lane, carry, valid,
+                             st == last && uint32_t(lane) + 1u == g.nvalid);
       }
     };
     uint32_t r = 1;
@@ -517,6 +528,16 @@ template <bool IL = false, int W = 1>
 struct Tickets {
   uint32_t* ctr;  // 8 zeroed counters for this launch, kSchedStride u32 apart (one per 256-byte line)
   uint32_t n, group;
+  // Short launches (fewer than kDynMinPerWave files per wave) take files
+  // round-robin instead: atomics to one line serialise (~88 per us), which a
+  // launch of a few files per wave does not amortise (a 31-block window: ~40 us).
+  bool dyn = true;
+  uint32_t snext = 0, sstride = 0;
+  __device__ __forceinline__ void init_static(uint32_t waves_total, uint32_t global_wave) {
+    dyn = n >= kDynMinPerWave * waves_total;
+    snext = global_wave;
+    sstride = waves_total;
+  }
   __device__ __forceinline__ uint32_t gbegin(uint32_t g) const { return uint32_t((uint64_t(n) * g) >> 3); }
   __device__ __forceinline__ uint32_t gcount(uint32_t g) const {
     if constexpr (IL && W > 1) {
@@ -530,18 +551,34 @@ struct Tickets {
     return IL ? j * 8u + g : gbegin(g) + j;
   }
   // Issue the atomic of the home group in lane 0; the result stays in lane 0's register.
-  __device__ __forceinline__ uint32_t issue(int lane) const {
+  __device__ __forceinline__ uint32_t issue(int lane) {
+    if (!dyn) {
+      const uint32_t j = snext;
+      snext += sstride;
+      return j;
+    }
     uint32_t j = 0;
     if (lane == 0) j = atomicAdd(&ctr[group * kSchedStride], 1u);
     return j;
   }
-  // Turn an issued ticket into a file index (n = no work left).
+  // Turn an issued ticket into a file index (n = no work left).  A group whose
+  // counter is already past its count is skipped after a plain load: at the end
+  // of a launch every wave walks the other groups, and atomics on one line
+  // serialise (~88 per us) -- 8 per wave cost tens of microseconds per launch.
   __device__ __forceinline__ uint32_t resolve(uint32_t jv, int lane) {
+    if (!dyn) return jv < n ? jv : n;
     uint32_t j = __builtin_amdgcn_readlane(jv, 0);
     for (uint32_t tries = 0;; ++tries) {
       if (j < gcount(group)) return file_of(group, j);
-      if (tries == 7) return n;
-      group = (group + 1) & 7u;  // steal
+      for (;;) {
+        if (tries == 7) return n;
+        group = (group + 1) & 7u;  // steal
+        ++tries;
+        uint32_t seen = 0;
+        if (lane == 0) seen = __hip_atomic_load(&ctr[group * kSchedStride], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__builtin_amdgcn_readlane(seen, 0) < gcount(group)) break;
+      }
+      --tries;
       uint32_t k = 0;
       if (lane == 0) k = atomicAdd(&ctr[group * kSchedStride], 1u);
       j = __builtin_amdgcn_readlane(k, 0);
@@ -590,6 +627,7 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t stride = gridDim.x * wpb;
   Tickets<IL, W> tk{sched, n, blockIdx.x & 7u};
+  tk.init_static(stride, blockIdx.x * wpb + wave);
   uint32_t bad = 0;
   do {  // `break` = this wave has no (more) files; every wave reaches launch_exit
   uint32_t f, fn;
@@ -1104,6 +1142,186 @@ __global__ void __launch_bounds__(kBlock) compact_fused_kernel(const uint8_t* __
   if (lane == 0 && bad && n_bad) atomicAdd(n_bad, bad);
 }
 
+// ---------------------------------------------------------------------------
+// Pipelined compaction (task.cpp:713-836): the crc_files_kernel
+// schedule applied to the fused re-CRC + repack.  Records are taken by dynamic
+// tickets (Tickets<kIL>, stream-bound slot, launch_exit), and the next record's
+// descriptor, FileInfo, head and first PF stripes are in flight while the current
+// one is finished (tail and header stores, combine, checks).  The 36-byte
+// FileInfo is read with one byte load per lane (lanes 0..35) and written with one
+// byte store per lane (offset_/size_/usize_/flag_ rewritten); the fields the
+// checks need come out of those registers by readlane.  Payload bytes take the
+// copy-through of lane_chain (whole dwordx4 stores for a destination congruent
+// mod 4); other shifts copy bytes after the CRC, as in compact_fused_kernel.
+// ---------------------------------------------------------------------------
+struct CRec {
+  uint64_t soff, doff, fid;
+  int32_t size, flag, new_off;
+  int32_t pre;  // kSuccess, or the status decided before reading (size / range)
+};
+
+template <bool WIDE, bool VERIFY = false>
+__device__ __forceinline__ CRec load_crec(uint32_t f, uint64_t src_len, const RawMeta* __restrict__ metas,
+                                          const int32_t* __restrict__ flags, const int64_t* __restrict__ dest_off,
+                                          const CompactJob* __restrict__ jobs) {
+  CRec r;
+  bool range_ok;
+  if (VERIFY && !WIDE) {
+    const RawMeta m = metas[f];
+    r.soff = uint64_t(int64_t(m.offset)), r.doff = 0, r.fid = m.file_id;
+    r.size = m.size, r.flag = 0, r.new_off = 0;
+    range_ok = m.offset >= 0 && uint64_t(m.offset) + uint64_t(uint32_t(m.size)) <= src_len;
+  } else if (WIDE) {
+    const CompactJob j = jobs[f];
+    r.soff = j.src_offset, r.doff = j.dest_offset, r.fid = j.file_id;
+    r.size = j.size, r.flag = j.flag, r.new_off = j.new_offset;
+    range_ok = r.soff + uint64_t(uint32_t(r.size)) <= src_len;
+  } else {
+    const RawMeta m = metas[f];
+    const int64_t d = dest_off[f];
+    r.soff = uint64_t(int64_t(m.offset)), r.doff = uint64_t(d), r.fid = m.file_id;
+    r.size = m.size, r.flag = flags[f], r.new_off = int32_t(d);
+    range_ok = m.offset >= 0 && d >= 0 && uint64_t(m.offset) + uint64_t(uint32_t(m.size)) <= src_len;
+  }
+  r.pre = r.size <= kFileInfoSize ? kExitReadFileSizeError : (range_ok ? kSuccess : kExitParameterError);
+  return r;
+}
+
+// A record's registers issued ahead of its compute.
+struct CState {
+  FileGeo<kRun> g;
+  Head<kRun> h;
+  uint32_t hb;  // this lane's FileInfo byte (lanes 0..35)
+  intptr_t delta;
+};
+
+__device__ __forceinline__ CState issue_crec(const CRec& r, const uint8_t* src, uint8_t* dst, int lane,
+                                             uintptr_t junk) {
+  CState s;
+  if (r.pre == kSuccess) {
+    const uint8_t* rec = src + r.soff;
+    s.hb = lane < kFileInfoSize ? uint32_t(rec[lane]) : 0u;
+    s.g = make_geo<kRun>(rec + kFileInfoSize, uint32_t(r.size - kFileInfoSize), 0u);
+    s.h = load_head<kRun>(s.g, lane);
+    s.delta = intptr_t(dst + r.doff) - intptr_t(rec);
+  } else {  // nothing is read for a record rejected up front
+    s.hb = 0u;
+    s.g = make_geo<kRun>(reinterpret_cast<const uint8_t*>(junk), 0u, 0u);
+    s.h = Head<kRun>{};
+    s.delta = 0;
+  }
+  return s;
+}
+
+// FileInfo dword k (bytes 4k..4k+3, k < 9) from the lanes' header bytes.
+__device__ __forceinline__ uint32_t hdr_dword(uint32_t hb, uint32_t k) {
+  return __builtin_amdgcn_readlane(hb, 4 * k) | __builtin_amdgcn_readlane(hb, 4 * k + 1) << 8 |
+         __builtin_amdgcn_readlane(hb, 4 * k + 2) << 16 | __builtin_amdgcn_readlane(hb, 4 * k + 3) << 24;
+}
+
+// VERIFY: the verify-on-read form (sync_backup.cpp:345-435, block_console.cpp:
+// 543-577) -- the same schedule and checks, no stores: `metas` (RawMeta, !WIDE)
+// or `jobs` (CompactJob with the dest fields unused, WIDE: many blocks, 64-bit
+// offsets) name the records, dst is unused.
+template <bool WIDE, bool DPPSH = true, bool VERIFY = false>
+__global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __restrict__ src, uint64_t src_len,
+                                                              const RawMeta* __restrict__ metas,
+                                                              const int32_t* __restrict__ flags,
+                                                              const int64_t* __restrict__ dest_off,
+                                                              const CompactJob* __restrict__ jobs, uint32_t n,
+                                                              uint8_t* __restrict__ dst, const Tables* __restrict__ tg,
+                                                              uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
+                                                              uint32_t* sched) {
+  __shared__ uint32_t lds_tables[LdsLayout<kS8>::bytes / 4];
+  load_tables<kRun, kPAR, kS8>(lds_tables, tg);
+  const int lane = threadIdx.x & (kWave - 1);
+  const LaneBase lb = lane_base_of(lane);
+  const uint32_t wpb = kBlock / kWave;
+  const uintptr_t junk = reinterpret_cast<uintptr_t>(tg->slice);
+  Tickets<kIL> tk{sched, n, blockIdx.x & 7u};
+  tk.init_static(gridDim.x * wpb, blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave));
+  uint32_t bad = 0;
+  do {
+    uint32_t f = tk.resolve(tk.issue(lane), lane);
+    if (f >= n) break;
+    uint32_t fn = tk.resolve(tk.issue(lane), lane);
+    CRec cur = load_crec<WIDE, VERIFY>(f, src_len, metas, flags, dest_off, jobs);
+    CState st = issue_crec(cur, src, dst, lane, junk);
+    uint4 buf[kPF][kRun / 16];
+    load_ring<kRun, kPF, kNT>(st.g, lane, buf, junk);
+    CRec nxt = fn < n ? load_crec<WIDE, VERIFY>(fn, src_len, metas, flags, dest_off, jobs) : CRec{};
+    uint32_t jv = fn < n ? tk.issue(lane) : 0u;
+    for (;;) {
+      const bool fused = (st.delta & 3) == 0;
+      uint32_t c = st.g.nstripes ? lane_chain<kRun, kPF, kNT, kS8, !VERIFY, 1, DPPSH>(lds_tables, lb, st.g, st.h, buf,
+                                                                                       lane, junk, st.delta, fused)
+                                 : 0u;
+      // The next record's loads go out before this one is finished.
+      const bool more = fn < n;
+      const CRec ncur = nxt;
+      CState ns = st;
+      uint32_t fnn = n;
+      if (more) {
+        ns = issue_crec(ncur, src, dst, lane, junk);
+        load_ring<kRun, kPF, kNT>(ns.g, lane, buf, junk);
+        fnn = tk.resolve(jv, lane);
+        if (fnn < n) {
+          nxt = load_crec<WIDE, VERIFY>(fnn, src_len, metas, flags, dest_off, jobs);
+          jv = tk.issue(lane);
+        }
+      }
+      int32_t status = cur.pre;
+      if (status == kSuccess) {
+        const uint8_t* rec = src + cur.soff;
+        uint8_t* drec = dst + cur.doff;
+        const uint32_t len = uint32_t(cur.size - kFileInfoSize);
+        // FileInfo with offset_(8) size_(12) usize_(16) flag_(28) rewritten, the rest copied (task.cpp:753-759)
+        if (!VERIFY && lane < kFileInfoSize) {
+          const int fld = lane >> 2, sh = 8 * (lane & 3);
+          uint32_t b = st.hb;
+          if (fld == 2) b = uint32_t(cur.new_off) >> sh;
+          else if (fld == 3 || fld == 4) b = uint32_t(cur.size) >> sh;
+          else if (fld == 7) b = uint32_t(cur.flag) >> sh;
+          drec[lane] = uint8_t(b);
+        }
+        if (VERIFY) {
+        } else if (fused && st.g.nstripes) {
+          if (lane == 0) {  // tail [B16, end) from lane 0's registers
+            const uint32_t ntw = uint32_t((st.g.end & ~uintptr_t(3)) - st.g.B16) / 4u;
+            for (uint32_t i = 0; i < 3u; ++i)
+              if (i < ntw) st32(st.g.B16 + 4u * i + st.delta, st.h.tw[i]);
+            const uintptr_t B = st.g.end & ~uintptr_t(3);
+            for (uint32_t i = 0; i < 3u; ++i)
+              if (B + i < st.g.end) *reinterpret_cast<uint8_t*>(B + i + st.delta) = uint8_t(st.h.tb[i]);
+          }
+        } else {  // tiny payload, or a destination not congruent mod 4: byte copy
+          const uint8_t* p = rec + kFileInfoSize;
+          for (uint32_t i = lane; i < len; i += kWave) drec[kFileInfoSize + i] = p[i];
+        }
+        c = finish_file<kRun, kS8>(lds_tables, lb, st.g, st.h, c, lane);
+        const uint64_t hid = uint64_t(hdr_dword(st.hb, 0)) | uint64_t(hdr_dword(st.hb, 1)) << 32;
+        if (hid != cur.fid) status = kExitFileInfoError;
+        else if (int32_t(hdr_dword(st.hb, 3)) != cur.size) status = kExitSyncFileError;
+        else if (c != hdr_dword(st.hb, 8)) status = kExitCheckCrcError;
+      } else {
+        c = 0u;
+      }
+      if (lane == 0) {
+        if (out_crc) out_crc[f] = c;
+        if (out_status) out_status[f] = status;
+        bad += status != kSuccess ? 1u : 0u;
+      }
+      if (!more) break;
+      f = fn;
+      fn = fnn;
+      cur = ncur;
+      st = ns;
+    }
+  } while (false);
+  if (lane == 0 && bad && n_bad) atomicAdd(n_bad, bad);
+  if (lane == 0) launch_exit(sched, gridDim.x * wpb, nullptr, 0u);
+}
+
 // Synthetic payload bytes: word i = splitmix64(seed + (first_word + i + 1) * GOLDEN)
 // (same stream as tfs_amd/synth.py).
 __global__ void synth_fill_kernel(uint64_t* __restrict__ dst, uint64_t nwords, uint64_t seed, uint64_t first_word) {
@@ -1211,6 +1429,34 @@ __global__ void __launch_bounds__(kBlock) membench_copy_kernel(const uint8_t* __
       const u32x4 w = {v.x, v.y, v.z, v.w};
       *reinterpret_cast<gu128wp>(d + 16 * i) = w;
     }
+  }
+}
+
+// Calibration: copy with U 16-byte chunks per lane in flight per iteration
+// (U loads, then U stores); LNT = nt loads; SK = store kind (0 plain, 1 nt).
+template <bool LNT, int SK, int U>
+__global__ void __launch_bounds__(kBlock) membench_copy2_kernel(const uint8_t* __restrict__ src,
+                                                                uint8_t* __restrict__ dst, uint64_t nbytes) {
+  const uint64_t nv = nbytes / 16;
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  const uintptr_t s = reinterpret_cast<uintptr_t>(src), d = reinterpret_cast<uintptr_t>(dst);
+  uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (; i + uint64_t(U - 1) * stride < nv; i += uint64_t(U) * stride) {
+    uint4 v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) v[k] = ld128s<LNT>(s + 16 * (i + uint64_t(k) * stride));
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const u32x4 w = {v[k].x, v[k].y, v[k].z, v[k].w};
+      gu128wp a = reinterpret_cast<gu128wp>(d + 16 * (i + uint64_t(k) * stride));
+      if (SK == 1) __builtin_nontemporal_store(w, a);
+      else *a = w;
+    }
+  }
+  for (; i < nv; i += stride) {
+    const uint4 v = ld128s<LNT>(s + 16 * i);
+    const u32x4 w = {v.x, v.y, v.z, v.w};
+    *reinterpret_cast<gu128wp>(d + 16 * i) = w;
   }
 }
 
@@ -1326,21 +1572,57 @@ hipError_t launch_block_verify(const uint8_t* image, uint64_t image_len, const R
   return hipGetLastError();
 }
 
+// Product: compact_pipe_kernel (dynamic tickets on the stream's slot, next-record
+// prefetch).  variant 22 (measurement): the unpipelined compact_fused_kernel.
 hipError_t launch_compact_fused(const uint8_t* src, uint64_t src_len, const RawMeta* metas, const int32_t* flags,
                                 const int64_t* dest_off, uint32_t n, uint8_t* dst, const Tables* tg, uint32_t* out_crc,
-                                int32_t* out_status, uint32_t* n_bad, hipStream_t stream) {
+                                int32_t* out_status, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
+                                int variant) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(compact_fused_kernel<false>, dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len, metas,
-                     flags, dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad);
+  if (variant == 22 || !sched)
+    hipLaunchKernelGGL(compact_fused_kernel<false>, dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len, metas,
+                       flags, dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad);
+  else if (variant == 23)
+    hipLaunchKernelGGL((compact_pipe_kernel<false, false>), dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len,
+                       metas, flags, dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched);
+  else
+    hipLaunchKernelGGL(compact_pipe_kernel<false>, dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len, metas,
+                       flags, dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched);
   return hipGetLastError();
 }
 
 hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const CompactJob* jobs, uint32_t n, uint8_t* dst,
                                const Tables* tg, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
-                               hipStream_t stream) {
+                               uint32_t* sched, hipStream_t stream, int variant) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(compact_fused_kernel<true>, dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len, nullptr,
-                     nullptr, nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad);
+  if (variant == 22 || !sched)
+    hipLaunchKernelGGL(compact_fused_kernel<true>, dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len, nullptr,
+                       nullptr, nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad);
+  else if (variant == 23)
+    hipLaunchKernelGGL((compact_pipe_kernel<true, false>), dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len,
+                       nullptr, nullptr, nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad, sched);
+  else
+    hipLaunchKernelGGL(compact_pipe_kernel<true>, dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len, nullptr,
+                       nullptr, nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad, sched);
+  return hipGetLastError();
+}
+
+// Verify-on-read of block records: the pipelined form (product) or the
+// static grid-stride block_verify_kernel (TFS_CRC_VARIANT=24, round 1's).
+hipError_t launch_block_verify_pipe(const uint8_t* image, uint64_t image_len, const RawMeta* metas,
+                                    const CompactJob* jobs, uint32_t n, const Tables* tg, uint32_t* out_crc,
+                                    int32_t* out_status, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
+                                    int variant) {
+  if (n == 0) return hipSuccess;
+  if (jobs)
+    hipLaunchKernelGGL((compact_pipe_kernel<true, true, true>), dim3(grid_for(n)), dim3(kBlock), 0, stream, image,
+                       image_len, nullptr, nullptr, nullptr, jobs, n, nullptr, tg, out_crc, out_status, n_bad, sched);
+  else if (variant == 24 || !sched)
+    hipLaunchKernelGGL(block_verify_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, image, image_len, metas, n, tg,
+                       out_crc, out_status, n_bad);
+  else
+    hipLaunchKernelGGL((compact_pipe_kernel<false, true, true>), dim3(grid_for(n)), dim3(kBlock), 0, stream, image,
+                       image_len, metas, nullptr, nullptr, nullptr, n, nullptr, tg, out_crc, out_status, n_bad, sched);
   return hipGetLastError();
 }
 
@@ -1365,6 +1647,18 @@ hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, u
   // pattern: 0 = coalesced, 16 = stripe pattern (run 16); +1000 = non-temporal loads;
   // +10000 = stripes anchored at 128-byte boundaries (else 16);
   // 50000 / 51000 = streaming copy of nbytes into `out` (default / non-temporal)
+  if (pattern >= 52000 && pattern < 53000) {
+    // 52LSU: L = nt loads (0/1), S = store kind (0 plain, 1 nt), U = chunks in flight (1, 4, 8)
+    const int L = (pattern / 100) % 10, S = (pattern / 10) % 10, U = pattern % 10;
+    const dim3 g(grid ? grid : 2048u);
+    uint8_t* d = reinterpret_cast<uint8_t*>(out);
+#define TFS_COPY2(LL, SS, UU) \
+  if (L == LL && S == SS && U == UU) hipLaunchKernelGGL((membench_copy2_kernel<LL == 1, SS, UU>), g, dim3(kBlock), 0, stream, base, d, nbytes)
+    TFS_COPY2(0, 0, 1); TFS_COPY2(0, 0, 4); TFS_COPY2(0, 0, 8); TFS_COPY2(1, 0, 4); TFS_COPY2(1, 1, 4);
+    TFS_COPY2(0, 1, 4); TFS_COPY2(1, 1, 8); TFS_COPY2(1, 0, 8);
+#undef TFS_COPY2
+    return hipGetLastError();
+  }
   if (pattern == 50000 || pattern == 51000) {
     const dim3 g(grid ? grid : 2048u);
     if (pattern == 51000)
