@@ -561,24 +561,18 @@ struct Tickets {
     if (lane == 0) j = atomicAdd(&ctr[group * kSchedStride], 1u);
     return j;
   }
-  // Turn an issued ticket into a file index (n = no work left).  A group whose
-  // counter is already past its count is skipped after a plain load: at the end
-  // of a launch every wave walks the other groups, and atomics on one line
-  // serialise (~88 per us) -- 8 per wave cost tens of microseconds per launch.
+  // Turn an issued ticket into a file index (n = no work left).  (Skipping an
+  // exhausted group after a plain load of its counter, instead of an atomic,
+  // measured 4-7 % slower on the headline: DESIGN.md §4.)
   __device__ __forceinline__ uint32_t resolve(uint32_t jv, int lane) {
-    if (!dyn) return jv < n ? jv : n;
+    // readlane keeps the file index wave-uniform (SGPR) in both modes, so the
+    // descriptor loads stay scalar loads and the geometry stays in SGPRs.
     uint32_t j = __builtin_amdgcn_readlane(jv, 0);
+    if (!dyn) return j < n ? j : n;
     for (uint32_t tries = 0;; ++tries) {
       if (j < gcount(group)) return file_of(group, j);
-      for (;;) {
-        if (tries == 7) return n;
-        group = (group + 1) & 7u;  // steal
-        ++tries;
-        uint32_t seen = 0;
-        if (lane == 0) seen = __hip_atomic_load(&ctr[group * kSchedStride], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (__builtin_amdgcn_readlane(seen, 0) < gcount(group)) break;
-      }
-      --tries;
+      if (tries == 7) return n;
+      group = (group + 1) & 7u;  // steal
       uint32_t k = 0;
       if (lane == 0) k = atomicAdd(&ctr[group * kSchedStride], 1u);
       j = __builtin_amdgcn_readlane(k, 0);
