@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--stats", required=True, help="kernel_stats.csv of rocprofv3 --stats on the same command")
     ap.add_argument("--out", required=True)
     ap.add_argument("--latest", action="store_true")
+    ap.add_argument("--work", default="1,048,576 files x 64 KiB payload (block images, FileInfo|payload)")
     ap.add_argument("csvs", nargs="+", help="counter_collection.csv of each --pmc pass")
     a = ap.parse_args()
     c = counters(a.csvs, a.kernel)
@@ -48,7 +49,7 @@ def main():
     write = c.get("WRITE_SIZE", 0.0) * 1024.0
     res = {
         "kernel": a.kernel, "tag": a.tag,
-        "launch_work": "1,048,576 files x 64 KiB payload (block images, FileInfo|payload)",
+        "launch_work": a.work,
         "rocprof_kernel_stats": ks, "counters_median": c,
         "read_bytes_corrected": read,
         "read_bytes_from_rdreq_x128": c["TCC_EA0_RDREQ_sum"] * 128.0 if "TCC_EA0_RDREQ_sum" in c else None,

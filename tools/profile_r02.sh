@@ -1,0 +1,38 @@
+#!/usr/bin/env bash
+# tools/profile_r02.sh -- rocprofv3 passes for the round-2 profiles (run on the
+# GPU box through gpurun): kernel trace + stats of each bench command, then each
+# PMC group in its own pass (FETCH_SIZE and WRITE_SIZE cannot share one; counters
+# never combined with other trace domains).  Outputs under gpurun_out/prof_r02/;
+# tools/pmc_summary.py folds them into profiles/r02/.
+set -euo pipefail
+OUT=gpurun_out/prof_r02
+mkdir -p "$OUT"
+ROOT=$(pwd)
+cd /tmp && export TMPDIR=/tmp && cd "$ROOT"
+run_trace() {  # name, bench args...
+  local name=$1; shift
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/$name/trace" -o run --output-format csv -- \
+    python bench.py "$@" > "$OUT/$name/bench_trace.json" 2> "$OUT/$name/trace.err"
+}
+run_pmc() {  # name, counters, kernel regex, bench args...
+  local name=$1 ctrs=$2 kre=$3; shift 3
+  local tag
+  tag=$(echo "$ctrs" | cut -d' ' -f1 | tr 'A-Z' 'a-z')
+  timeout -s KILL 120 rocprofv3 --pmc $ctrs --kernel-include-regex "$kre" -d "$OUT/$name/pmc_$tag" -o run \
+    --output-format csv -- python bench.py "$@" > "$OUT/$name/pmc_$tag.json" 2> "$OUT/$name/pmc_$tag.err"
+}
+mkdir -p "$OUT/verify" "$OUT/compact" "$OUT/bverify"
+H=(--steps 8 --warmup 2 --no-cpu --e2e-blocks 0 --parity-every 1024)
+run_trace verify "${H[@]}"
+for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" \
+           "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
+           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"; do
+  run_pmc verify "$grp" "crc_files_kernel<1" --steps 2 --warmup 1 --no-cpu --e2e-blocks 0 --parity-every 1024
+done
+C=(--workload compact_device --no-cpu --steps 4 --warmup 1)
+run_trace compact "${C[@]}"
+for grp in FETCH_SIZE WRITE_SIZE; do run_pmc compact "$grp" "compact_pipe_kernel<true, true, false>" --workload compact_device --no-cpu --steps 1 --warmup 1; done
+B=(--workload block_verify_device --no-cpu --steps 4 --warmup 1)
+run_trace bverify "${B[@]}"
+for grp in FETCH_SIZE WRITE_SIZE; do run_pmc bverify "$grp" "compact_pipe_kernel<true, true, true>" --workload block_verify_device --no-cpu --steps 1 --warmup 1; done
+echo "profile_r02 done"
