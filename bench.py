@@ -840,7 +840,9 @@ def bench_compact(args):
             "value": reps * live * psize / dt / 2**30, "unit": "GiB/s of live payload", "cores": 1,
             "kind": "port", "source_block_GiBs": reps * blk_bytes / dt / 2**30,
             "sample": "%d compactions of the %d pinned source block images (re-CRC of %d live files + repack), "
-                      "oracle_compact single thread, %.1f s" % (reps, ndistinct, live, dt)}
+                      "oracle_compact single thread, %.1f s" % (reps, ndistinct, live, dt),
+            "allcore": _compact_allcore(ora, [b.ptr for b in srcs], mo, ms, flags, nfiles, odest.size, w,
+                                        live * psize, blk_bytes, min(3.0, args.cpu_seconds))}
     if rank == 0:
         print(json.dumps(res), flush=True)
     for b in srcs + dests:
@@ -850,6 +852,32 @@ def bench_compact(args):
     ctx.close()
     if dist:
         dist.destroy_process_group()
+
+
+def _compact_allcore(ora, src_ptrs, mo, ms, flags, nfiles, dest_cap, expect_len, live_bytes, blk_bytes, seconds):
+    """oracle_compact on every CPU this process may use: thread i compacts source
+    image i % len(src_ptrs) into its own destination (reported, never fatal)."""
+    try:
+        def make(i):
+            odest = np.zeros(dest_cap, np.uint8)
+            doff = np.zeros(nfiles, np.int64)
+            dsz = np.zeros(nfiles, np.int32)
+            ook = np.zeros(nfiles, np.uint8)
+            src = src_ptrs[i % len(src_ptrs)]
+
+            def run():
+                wc = ora.oracle_compact(src, mo.ctypes.data, ms.ctypes.data, flags.ctypes.data, nfiles,
+                                        odest.ctypes.data, doff.ctypes.data, dsz.ctypes.data, ook.ctypes.data)
+                if (expect_len is not None and wc != expect_len) or not ook[flags == 0].all():
+                    raise SystemExit("compact: all-core oracle baseline disagrees")
+            return run
+        calls, dt, threads = _allcore_threads(make, seconds)
+        return {"value": calls * live_bytes / dt / 2**30, "source_block_GiBs": calls * blk_bytes / dt / 2**30,
+                "cores": threads, "nproc": os.cpu_count(), "cpu_model": _cpu_model(), "kind": "port",
+                "cores_source": "sched affinity capped by the cgroup cpu.max quota",
+                "sample": "%d compactions over %d threads, %.1f s" % (calls, threads, dt)}
+    except Exception as e:  # reported, never fatal
+        return {"error": str(e)}
 
 
 def bench_block_verify(args):
@@ -1254,7 +1282,7 @@ def bench_compact_device(args):
             nblocks, nlive, live_bytes / 2**30)},
         "roofline": {"bound": "hbm", "achieved": algo / (kms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": algo / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "compact_fused_kernel<WIDE> (one launch)", "kernel_ms_avg": kms},
+                     "kernel": "compact_pipe_kernel<WIDE> (one launch)", "kernel_ms_avg": kms},
         "membench": extra,
         "ab": {"fused_one_launch_ms": kms, "fused_windows_ms": kms_w, "unfused_windows_ms": kms2,
                "unpipelined_fused_one_launch_ms": kms22, "pipelined_bpermute_one_launch_ms": kms23,
@@ -1287,7 +1315,9 @@ def bench_compact_device(args):
             "value": reps * len(live1) * FILE_SIZE / dt / 2**30, "unit": "GiB/s of live payload", "cores": 1,
             "kind": "port", "source_block_GiBs": reps * blk / dt / 2**30,
             "sample": "%d compactions of resident block 0 copied to host (re-CRC of %d live files + repack), "
-                      "oracle_compact single thread, %.1f s" % (reps, len(live1), dt)}
+                      "oracle_compact single thread, %.1f s" % (reps, len(live1), dt),
+            "allcore": _compact_allcore(ora, [src.ctypes.data], mo, ms, flags1, nfiles, blk, None,
+                                        len(live1) * FILE_SIZE, blk, min(3.0, args.cpu_seconds))}
     if rank == 0:
         print(json.dumps(res), flush=True)
     for w in windows:
@@ -1402,9 +1432,46 @@ def ec_cpu_baseline(d, k, m, seconds, chunk=4 << 20):
     for i in range(k, k + m):
         if not (d[i].download(np.uint8, chunk) == host[i]).all():
             raise SystemExit("ec: CPU baseline parity disagrees with the GPU")
+    try:
+        # jerasure keeps process-wide byte counters (jerasure.cpp:42-44, bumped per
+        # packet at :336-340) that every encoding thread writes: threads of one
+        # library copy serialise on that cache line.  Each thread here runs its own
+        # loaded copy of the library (as separate dataserver processes would).
+        import shutil
+        import tempfile
+        tmpd = tempfile.mkdtemp(prefix="tfs_ec_ref_")
+
+        def make(i):
+            par = [np.zeros(chunk, np.uint8) for _ in range(m)]
+            ptrs = (ctypes.c_void_p * (k + m))(*([h.ctypes.data for h in host[:k]] + [p.ctypes.data for p in par]))
+            make.keep.append((par, ptrs))
+            if kind != "reference":
+                return lambda: run(ptrs)
+            cp = os.path.join(tmpd, "libref_ec_%d.so" % i)
+            shutil.copyfile(ref_so, cp)
+            Li = ctypes.CDLL(cp, mode=os.RTLD_LOCAL)
+            Li.ref_ec_encode.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+            make.libs.append(Li)
+            return lambda: Li.ref_ec_encode(k, m, ptrs, chunk)
+        make.keep, make.libs = [], []
+        try:
+            calls, adt, threads = _allcore_threads(make, min(3.0, seconds))
+        finally:
+            shutil.rmtree(tmpd, ignore_errors=True)
+        for par, _ in make.keep:
+            if not all((par[j] == host[k + j]).all() for j in range(m)):
+                raise SystemExit("ec: all-core CPU parity disagrees with the GPU")
+        allcore = {"value": calls * k * chunk / adt / 2**30, "cores": threads, "nproc": os.cpu_count(),
+                   "cpu_model": _cpu_model(), "kind": kind,
+                   "cores_source": "sched affinity capped by the cgroup cpu.max quota",
+                   "sample": "%d encodes over %d threads, one loaded copy of the library per thread, %.1f s" % (
+                       calls, threads, adt)}
+    except Exception as e:  # reported, never fatal
+        allcore = {"error": str(e)}
     return {"value": reps * k * chunk / dt / 2**30, "unit": "GiB/s", "cores": 1, "kind": kind,
             "sample": "%d encodes of k=%d x %d MiB (first bytes of the same members), jerasure_bitmatrix_encode "
-                      "w=8 ps=128, single thread, %.1f s" % (reps, k, chunk >> 20, dt)}
+                      "w=8 ps=128, single thread, %.1f s" % (reps, k, chunk >> 20, dt),
+            "allcore": allcore}
 
 
 def _ref_crc_fn():
@@ -1459,6 +1526,34 @@ def _cpu_budget():
     except (OSError, ValueError):
         pass
     return n
+
+
+def _allcore_threads(make_worker, seconds):
+    """All-core CPU leg for the oracle routines that have no pthread driver: one
+    Python thread per CPU this process may use, each calling `make_worker(i)()`
+    (a ctypes call into the oracle, which releases the GIL) on its own output
+    buffers until `seconds` have passed.  Returns (calls, elapsed s, threads)."""
+    import threading
+    threads = _cpu_budget()
+    workers = [make_worker(i) for i in range(threads)]
+    counts = [0] * threads
+    stop = [False]
+
+    def body(i):
+        w = workers[i]
+        while not stop[0]:
+            w()
+            counts[i] += 1
+
+    ts = [threading.Thread(target=body, args=(i,)) for i in range(threads)]
+    t0 = time.perf_counter()
+    for t in ts:
+        t.start()
+    time.sleep(seconds)
+    stop[0] = True
+    for t in ts:
+        t.join()
+    return sum(counts), time.perf_counter() - t0, threads
 
 
 def _cpu_model():
@@ -1650,7 +1745,7 @@ def bench_loopback(args):
         dist.destroy_process_group()
 
 
-def e2e_blocks(ctx, dist, world, rank, nsub, inflight=3):
+def e2e_blocks(ctx, dist, world, rank, nsub, inflight=3, cpu=None):
     """configs[4] end-to-end leg: pinned host block images -> H2D -> verify ->
     verdicts back, `inflight` blocks in flight (submit/wait), timed between
     barriers, max over ranks.  Returns (payload GiB/s over all ranks, PCIe GB/s,
@@ -1693,6 +1788,8 @@ def e2e_blocks(ctx, dist, world, rank, nsub, inflight=3):
     el = _max_over_ranks(dist, time.perf_counter() - t0)
     if bad:
         raise SystemExit("e2e: mismatches on clean data")
+    if cpu is not None:
+        cpu(srcs[0].array, offs, lens, exps[0])
     for b in srcs:
         b.free()
     for b in (d_img, d_desc, d_crc):
@@ -1708,7 +1805,14 @@ def bench_e2e(args):
     world, rank, local, dist = _dist_init()
     ctx = crc.Context(local)
     nsub, inflight = args.compact_blocks, 3
-    gibs, pcie, el = e2e_blocks(ctx, dist, world, rank, nsub, inflight)
+    cpu_res = {}
+
+    def cpu(arr, offs, lens, exp):
+        # the same verify of one page-locked block image on the host CPU
+        cpu_res["v"] = cpu_baseline(arr, offs, lens, exp, args.cpu_seconds,
+                                    "64 KiB payloads of a page-locked block image")
+    gibs, pcie, el = e2e_blocks(ctx, dist, world, rank, nsub, inflight,
+                                cpu if rank == 0 and world == 1 and not args.no_cpu else None)
     res = {
         "metric": "GiB/s CRC32 verify end-to-end from pinned host block images (H2D included)",
         "value": gibs, "unit": "GiB/s", "n_gpus": world, "steps": nsub, "warmup": 2,
@@ -1720,6 +1824,8 @@ def bench_e2e(args):
     ceil = pcie_ceiling(ctx)
     res["roofline"] = {"bound": "pcie", "achieved": pcie / world, "peak": ceil["h2d_GBs"], "unit": "GB/s (per GPU)",
                        "frac": pcie / world / ceil["h2d_GBs"], "peak_source": ceil["source"], "traffic": None}
+    if "v" in cpu_res:
+        res["cpu_baseline"] = cpu_res["v"]
     if rank == 0:
         print(json.dumps(res), flush=True)
     ctx.close()

@@ -54,6 +54,7 @@ def test_zipf_and_compact_lines_carry_cpu_baseline():
     assert c["value"] > 0 and c["cpu_baseline"]["kind"] == "port" and c["ab"]["speedup"] > 0
     assert c["unit"] == "GiB/s of live payload" and c["source_block_GiBs"] > c["value"]
     assert c["roofline"]["bound"] == "pcie" and 0 < c["roofline"]["frac"] < 1.2
+    assert c["cpu_baseline"]["allcore"]["value"] > 0 and c["cpu_baseline"]["allcore"]["cores"] >= 1
 
 
 @pytest.mark.gpu
@@ -61,6 +62,10 @@ def test_ec_line_carries_cpu_baseline():
     e = _run(["--workload", "ec", "--ec-mib", "16", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0.3"])
     assert e["roofline"]["bound"] == "hbm" and e["value"] > 0
     assert e["cpu_baseline"]["value"] > 0 and e["cpu_baseline"]["kind"] in ("reference", "port")
+    assert e["cpu_baseline"]["allcore"]["value"] > 0
+    t = _run(["--workload", "e2e", "--compact-blocks", "8", "--cpu-seconds", "0.3"])
+    assert t["roofline"]["bound"] == "pcie" and t["cpu_baseline"]["value"] > 0
+    assert t["cpu_baseline"]["allcore"]["value"] > 0
 
 
 @pytest.mark.gpu
@@ -70,6 +75,7 @@ def test_packet_and_compact_device_lines_carry_cpu_baseline():
     c = _run(["--workload", "compact_device", "--blocks", "8", "--steps", "2", "--warmup", "1",
               "--cpu-seconds", "0.3"])
     assert c["cpu_baseline"]["value"] > 0 and c["cpu_baseline"]["kind"] == "port"
+    assert c["cpu_baseline"]["allcore"]["value"] > 0
 
 
 @pytest.mark.gpu

@@ -180,7 +180,7 @@ struct FileGeo {
 };
 
 template <int RUN>
-__device__ __forceinline__ FileGeo<RUN> make_geo(const uint8_t* p, uint32_t len, uint32_t seed) {
+__device__ __forceinline__ FileGeo<RUN> make_geo(const uint8_t* p, uint32_t len, uint32_t seed, uint32_t aoff = 0u) {
   constexpr uint32_t kStripe = 64u * RUN;
   FileGeo<RUN> g;
   g.start = reinterpret_cast<uintptr_t>(p);
@@ -194,8 +194,11 @@ __device__ __forceinline__ FileGeo<RUN> make_geo(const uint8_t* p, uint32_t len,
   // stripe is exactly eight whole lines -- with non-temporal loads a line split
   // between two stripes was fetched twice (+2 % HBM traffic).  Runs in
   // [B16, E) lie in the same line as payload bytes (safe to read) and are
-  // excluded from their lanes' chains (`nvalid`).
-  g.E = RUN == 16 ? ((g.B16 + 127) & ~uintptr_t(127)) : g.B16;
+  // excluded from their lanes' chains (`nvalid`).  `aoff` (16-byte multiple,
+  // record kernel only): anchor the grid at 128k + aoff instead, so that the
+  // copy-through writes whole destination lines; the caller checks that the
+  // last stripe's up to 112 bytes past B16 stay inside the source.
+  g.E = RUN == 16 ? (((g.B16 - aoff + 127) & ~uintptr_t(127)) + aoff) : g.B16;
   g.nvalid = 64u - uint32_t(g.E - g.B16) / RUN;
   const uint32_t body = len >= kMinParallelLen ? uint32_t(g.E - g.A) : 0u;
   g.nstripes = (body + kStripe - 1) / kStripe;
@@ -285,10 +288,14 @@ __device__ __forceinline__ void load_ring(const FileGeo<RUN>& g, int lane, uint4
 typedef __attribute__((address_space(1))) uint32_t* gu32wp;
 typedef __attribute__((address_space(1))) u32x4* gu128wp;
 __device__ __forceinline__ void st32(uintptr_t a, uint32_t v) { *reinterpret_cast<gu32wp>(a) = v; }
+// NTS = false (measurement, TFS_CRC_VARIANT=25): plain stores, so partial lines
+// at record and stripe edges can merge in L2 before they are written back.
+template <bool NTS = true>
 __device__ __forceinline__ void st128_nt(uintptr_t a, const uint4& v) {
   u32x4 w = {v.x, v.y, v.z, v.w};
   if ((a & 15u) == 0) {
-    __builtin_nontemporal_store(w, reinterpret_cast<gu128wp>(a));
+    if (NTS) __builtin_nontemporal_store(w, reinterpret_cast<gu128wp>(a));
+    else *reinterpret_cast<gu128wp>(a) = w;
   } else {  // 4-aligned: four dword stores
     st32(a, v.x); st32(a + 4, v.y); st32(a + 8, v.z); st32(a + 12, v.w);
   }
@@ -311,7 +318,7 @@ struct ShiftCarry {
 __device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) {
   return __builtin_amdgcn_update_dpp(0u, v, 0x138 /* wave_shr:1 */, 0xf, 0xf, false);
 }
-template <bool DPP = true>
+template <bool DPP = true, bool NTS = true>
 __device__ __forceinline__ void store_shifted(uintptr_t chunk, const uint4& v, uint32_t k, int lane, ShiftCarry& cr,
                                               bool store, bool flush) {
   uint32_t p1, p2, p3;
@@ -337,7 +344,7 @@ __device__ __forceinline__ void store_shifted(uintptr_t chunk, const uint4& v, u
     } else {
       const uint4 o = k == 1 ? make_uint4(p1, v.x, v.y, v.z)
                              : (k == 2 ? make_uint4(p2, p1, v.x, v.y) : make_uint4(p3, p2, p1, v.x));
-      st128_nt(chunk, o);
+      st128_nt<NTS>(chunk, o);
     }
     if (flush) {
       if (k == 1) {
@@ -359,7 +366,11 @@ __device__ __forceinline__ void store_shifted(uintptr_t chunk, const uint4& v, u
 // COPY: also store every payload byte of [start, B16) to dst = src + delta.
 // G (measurement knob): refill the ring G slots at a time, so each wave issues G
 // consecutive stripes (G KiB contiguous) back to back instead of one per stripe.
-template <int RUN, int PF, bool NT, bool S8, bool COPY = false, int G = 1, bool DPPSH = false>
+// NTS: non-temporal copy-through stores (product).  NOCRC (measurement only,
+// TFS_CRC_VARIANT=26: wrong CRCs): skip the payload steps, so the record kernel
+// runs its own load/store schedule without the table lookups.
+template <int RUN, int PF, bool NT, bool S8, bool COPY = false, int G = 1, bool DPPSH = false, bool NTS = true,
+          bool NOCRC = false>
 __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase& lb, const FileGeo<RUN>& g,
                                                const Head<RUN>& h, uint4 (&buf)[PF][RUN / 16], int lane,
                                                uintptr_t junk, intptr_t delta = 0, bool copy_on = false) {
@@ -406,9 +417,9 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
       const bool valid = !(st == last && !lane_in_last);
       const uintptr_t q = g.sb0 + uintptr_t(st) * kStripe + uintptr_t(lane) * RUN;
       if (kshift == 0u) {
-        if (valid) st128_nt(q + delta, v);
+        if (valid) st128_nt<NTS>(q + delta, v);
       } else {
-        store_shifted<DPPSH>(q + uintptr_t(delta) - 4u * kshift, v, kshift, lane, carry, valid,
+        store_shifted<DPPSH, NTS>(q + uintptr_t(delta) - 4u * kshift, v, kshift, lane, carry, valid,
                              st == last && uint32_t(lane) + 1u == g.nvalid);
       }
     };
@@ -423,7 +434,7 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
           inj = 0;
         }
 #pragma unroll
-        for (int v = 0; v < kVec; ++v) c = steps16(T, lb, c, buf[f][v]);
+        for (int v = 0; v < kVec; ++v) c = NOCRC ? c ^ buf[f][v].x : steps16(T, lb, c, buf[f][v]);
         c = (r + f == last && !lane_in_last) ? c_old : c;  // run past B16: not part of the chain
         if (COPY && copy_on) copy_stripe(r + f, buf[f][0]);
         if ((f + 1) % G == 0) {
@@ -444,7 +455,7 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
         c = shift_stripe<S8>(T, c);
         if (f == 0) c ^= inj;
 #pragma unroll
-        for (int v = 0; v < kVec; ++v) c = steps16(T, lb, c, buf[f][v]);
+        for (int v = 0; v < kVec; ++v) c = NOCRC ? c ^ buf[f][v].x : steps16(T, lb, c, buf[f][v]);
         c = (r + f == last && !lane_in_last) ? c_old : c;
         if (COPY && copy_on) copy_stripe(r + f, buf[f][0]);
       }
@@ -1189,15 +1200,24 @@ struct CState {
   intptr_t delta;
 };
 
-__device__ __forceinline__ CState issue_crec(const CRec& r, const uint8_t* src, uint8_t* dst, int lane,
-                                             uintptr_t junk) {
+// DA: anchor the record's stripe grid on destination lines (make_geo's `aoff`):
+// every stripe's copy-through store then covers eight whole 128-byte lines of the
+// new block instead of splitting two lines with its neighbours (a split line
+// leaves the chip as two partial writes).  Needs a destination congruent to the
+// source mod 4 and 128 readable bytes past the record inside the source.
+template <bool DA>
+__device__ __forceinline__ CState issue_crec(const CRec& r, const uint8_t* src, uint64_t src_len, uint8_t* dst,
+                                             int lane, uintptr_t junk) {
   CState s;
   if (r.pre == kSuccess) {
     const uint8_t* rec = src + r.soff;
     s.hb = lane < kFileInfoSize ? uint32_t(rec[lane]) : 0u;
-    s.g = make_geo<kRun>(rec + kFileInfoSize, uint32_t(r.size - kFileInfoSize), 0u);
-    s.h = load_head<kRun>(s.g, lane);
     s.delta = intptr_t(dst + r.doff) - intptr_t(rec);
+    uint32_t aoff = 0u;
+    if (DA && (s.delta & 3) == 0 && r.soff + uint64_t(uint32_t(r.size)) + 128u <= src_len)
+      aoff = uint32_t(-(s.delta & ~intptr_t(15))) & 127u;
+    s.g = make_geo<kRun>(rec + kFileInfoSize, uint32_t(r.size - kFileInfoSize), 0u, aoff);
+    s.h = load_head<kRun>(s.g, lane);
   } else {  // nothing is read for a record rejected up front
     s.hb = 0u;
     s.g = make_geo<kRun>(reinterpret_cast<const uint8_t*>(junk), 0u, 0u);
@@ -1217,7 +1237,16 @@ __device__ __forceinline__ uint32_t hdr_dword(uint32_t hb, uint32_t k) {
 // 543-577) -- the same schedule and checks, no stores: `metas` (RawMeta, !WIDE)
 // or `jobs` (CompactJob with the dest fields unused, WIDE: many blocks, 64-bit
 // offsets) name the records, dst is unused.
-template <bool WIDE, bool DPPSH = true, bool VERIFY = false>
+// DIAG bits: 2 stripe grid anchored on destination lines (issue_crec<DA>), 3
+// temporal payload loads (with the destination-anchored grid a source line is
+// split between two stripes of the same wave; a temporal load keeps it in L2
+// for the second).  The product is both (kCompactDiag).  Measurement only: bit
+// 0 plain copy-through stores (variant 25), bit 1 no payload CRC steps (variant
+// 26, wrong CRCs and statuses); variant 27 = DIAG 0 (source-anchored grid,
+// non-temporal loads: the round-2 baseline), 29 = the anchored grid with
+// non-temporal loads.
+constexpr int kCompactDiag = 4 | 8;
+template <bool WIDE, bool DPPSH = true, bool VERIFY = false, int DIAG = kCompactDiag>
 __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __restrict__ src, uint64_t src_len,
                                                               const RawMeta* __restrict__ metas,
                                                               const int32_t* __restrict__ flags,
@@ -1226,6 +1255,8 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
                                                               uint8_t* __restrict__ dst, const Tables* __restrict__ tg,
                                                               uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
                                                               uint32_t* sched) {
+  constexpr bool DA = !VERIFY && (DIAG & 4) != 0;
+  constexpr bool LNT = (DIAG & 8) && !VERIFY ? false : kNT;  // the verify form keeps the headline's loads
   __shared__ uint32_t lds_tables[LdsLayout<kS8>::bytes / 4];
   load_tables<kRun, kPAR, kS8>(lds_tables, tg);
   const int lane = threadIdx.x & (kWave - 1);
@@ -1240,15 +1271,15 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
     if (f >= n) break;
     uint32_t fn = tk.resolve(tk.issue(lane), lane);
     CRec cur = load_crec<WIDE, VERIFY>(f, src_len, metas, flags, dest_off, jobs);
-    CState st = issue_crec(cur, src, dst, lane, junk);
+    CState st = issue_crec<DA>(cur, src, src_len, dst, lane, junk);
     uint4 buf[kPF][kRun / 16];
-    load_ring<kRun, kPF, kNT>(st.g, lane, buf, junk);
+    load_ring<kRun, kPF, LNT>(st.g, lane, buf, junk);
     CRec nxt = fn < n ? load_crec<WIDE, VERIFY>(fn, src_len, metas, flags, dest_off, jobs) : CRec{};
     uint32_t jv = fn < n ? tk.issue(lane) : 0u;
     for (;;) {
       const bool fused = (st.delta & 3) == 0;
-      uint32_t c = st.g.nstripes ? lane_chain<kRun, kPF, kNT, kS8, !VERIFY, 1, DPPSH>(lds_tables, lb, st.g, st.h, buf,
-                                                                                       lane, junk, st.delta, fused)
+      uint32_t c = st.g.nstripes ? lane_chain<kRun, kPF, LNT, kS8, !VERIFY, 1, DPPSH, !(DIAG & 1), (DIAG & 2) != 0>(
+                                     lds_tables, lb, st.g, st.h, buf, lane, junk, st.delta, fused)
                                  : 0u;
       // The next record's loads go out before this one is finished.
       const bool more = fn < n;
@@ -1256,8 +1287,8 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
       CState ns = st;
       uint32_t fnn = n;
       if (more) {
-        ns = issue_crec(ncur, src, dst, lane, junk);
-        load_ring<kRun, kPF, kNT>(ns.g, lane, buf, junk);
+        ns = issue_crec<DA>(ncur, src, src_len, dst, lane, junk);
+        load_ring<kRun, kPF, LNT>(ns.g, lane, buf, junk);
         fnn = tk.resolve(jv, lane);
         if (fnn < n) {
           nxt = load_crec<WIDE, VERIFY>(fnn, src_len, metas, flags, dest_off, jobs);
@@ -1579,6 +1610,9 @@ hipError_t launch_compact_fused(const uint8_t* src, uint64_t src_len, const RawM
   else if (variant == 23)
     hipLaunchKernelGGL((compact_pipe_kernel<false, false>), dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len,
                        metas, flags, dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched);
+  else if (variant == 27)
+    hipLaunchKernelGGL((compact_pipe_kernel<false, true, false, 0>), dim3(grid_for(n)), dim3(kBlock), 0, stream, src,
+                       src_len, metas, flags, dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched);
   else
     hipLaunchKernelGGL(compact_pipe_kernel<false>, dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len, metas,
                        flags, dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched);
@@ -1589,15 +1623,19 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
                                const Tables* tg, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
                                uint32_t* sched, hipStream_t stream, int variant) {
   if (n == 0) return hipSuccess;
+#define TFS_CJ(...)                                                                                                \
+  hipLaunchKernelGGL((compact_pipe_kernel<__VA_ARGS__>), dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len, \
+                     nullptr, nullptr, nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad, sched)
   if (variant == 22 || !sched)
     hipLaunchKernelGGL(compact_fused_kernel<true>, dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len, nullptr,
                        nullptr, nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad);
-  else if (variant == 23)
-    hipLaunchKernelGGL((compact_pipe_kernel<true, false>), dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len,
-                       nullptr, nullptr, nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad, sched);
-  else
-    hipLaunchKernelGGL(compact_pipe_kernel<true>, dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len, nullptr,
-                       nullptr, nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad, sched);
+  else if (variant == 23) TFS_CJ(true, false);
+  else if (variant == 25) TFS_CJ(true, true, false, kCompactDiag | 1);
+  else if (variant == 26) TFS_CJ(true, true, false, kCompactDiag | 2);
+  else if (variant == 27) TFS_CJ(true, true, false, 0);
+  else if (variant == 29) TFS_CJ(true, true, false, 4);
+  else TFS_CJ(true);
+#undef TFS_CJ
   return hipGetLastError();
 }
 

@@ -1,0 +1,131 @@
+#!/usr/bin/env python3
+"""Same-process A/B of the device compaction kernel (measurement
+only).  Builds bench.py's compact_device workload once (1,024 resident blocks,
+341 of every 1,024 records live, one job per live record), then interleaves, round
+by round, launches of
+
+  * kernel variants on the packed destination (product 0: stripe grid anchored
+    on destination lines, temporal payload loads; 27 the source-anchored grid
+    with non-temporal loads (the earlier product); 29 the anchored grid with
+    non-temporal loads; 25 plain copy-through stores; 26 no payload CRC steps
+    -- the kernel's own load/store schedule), and
+  * the product kernel on destinations congruent to the source mod 16 (no lane
+    shift) and mod 128 (whole destination lines per stripe),
+
+each timed with HIP events on its own context's stream.  The streaming-copy
+ceiling of the same bytes (membench pattern 52114) is timed in the same rounds.
+
+  python tools/ab_compact.py [ROUNDS] [NBLOCKS]
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+import tfs_amd.crc as crc  # noqa: E402
+
+
+def ctx_for(variant):
+    os.environ["TFS_CRC_VARIANT"] = str(variant)
+    c = crc.Context(0)
+    os.environ["TFS_CRC_VARIANT"] = "0"
+    return c
+
+
+def main():
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
+    nblocks = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+    ctx = crc.Context(0)
+    nfiles, rec = bench.FILES_PER_BLOCK, bench.FILEINFO + bench.FILE_SIZE
+    blk = nfiles * rec
+    total = nblocks * blk
+    img = crc.DeviceBuffer(ctx, (total + 4095) // 4096 * 4096)
+    ctx.synth_fill_device(img, (total + 7) // 8 * 8, 0xC0DE, 0)
+    n = nblocks * nfiles
+    desc = np.zeros(n, crc.DESC_DTYPE)
+    rec_off = np.arange(n, dtype=np.uint64) * rec
+    desc["offset"], desc["len"] = rec_off + bench.FILEINFO, bench.FILE_SIZE
+    d_desc = crc.DeviceBuffer(ctx, desc.nbytes).upload(desc)
+    d_crc = crc.DeviceBuffer(ctx, 4 * n)
+    ctx.batch_device(d_desc, n, img, d_crc)
+    d_roff = crc.DeviceBuffer(ctx, rec_off.nbytes).upload(rec_off)
+    d_len = crc.DeviceBuffer(ctx, 4 * n).upload(np.full(n, bench.FILE_SIZE, np.uint32))
+    ctx.write_headers_device(img, d_roff, d_len, d_crc, 1, n)
+    ctx.sync()
+    for b in (d_desc, d_roff, d_len, d_crc):
+        b.free()
+    live1 = np.nonzero(bench._fragmented_flags(nfiles) == 0)[0]
+    nl = live1.size
+    bidx = np.repeat(np.arange(nblocks, dtype=np.uint64), nl)
+    soff = bidx * blk + np.tile(live1.astype(np.uint64) * rec, nblocks)
+    k = np.arange(nblocks * nl, dtype=np.uint64)
+    dsts = {"packed": k * rec,                                   # the product workload (contiguous new blocks)
+            "dst16": k * 65584 + (soff & np.uint64(15)),         # delta == 0 mod 16: no lane shift
+            "dst128": k * 65664 + (soff & np.uint64(127))}       # delta == 0 mod 128: whole lines per stripe
+    d_dst = crc.DeviceBuffer(ctx, int(k.size) * 65664 + 256)
+    d_st = crc.DeviceBuffer(ctx, 4 * int(k.size))
+    d_bad = crc.DeviceBuffer(ctx, 4)
+    jobsets = {}
+    for name, do in dsts.items():
+        j = np.zeros(k.size, crc.COMPACT_JOB_DTYPE)
+        j["src_offset"], j["dest_offset"] = soff, do
+        j["file_id"] = 1 + bidx * nfiles + np.tile(live1.astype(np.uint64), nblocks)
+        j["size"] = rec
+        j["new_offset"] = (do % np.uint64(1 << 31)).astype(np.int32)
+        jobsets[name] = crc.DeviceBuffer(ctx, j.nbytes).upload(j)
+    ctxs = {0: ctx, 25: ctx_for(25), 26: ctx_for(26), 27: ctx_for(27), 29: ctx_for(29)}
+    cases = [(0, "packed"), (27, "packed"), (25, "packed"), (26, "packed"), (29, "packed"), (0, "dst128"),
+             (27, "dst128")]
+    nj = int(k.size)
+    live_bytes = float(nj) * rec
+    algo = 2 * live_bytes + nj * (40 + 4)
+    # correctness of the product cases (the diagnostic variant 26 computes no CRCs)
+    for v, js in cases:
+        if v == 26:
+            continue
+        d_bad.zero()
+        ctxs[v].compact_jobs_device(img, total, jobsets[js], nj, d_dst, None, d_st, d_bad)
+        ctxs[v].sync()
+        if int(d_bad.download(np.uint32, 1)[0]) != 0:
+            raise SystemExit("ab_compact: variant %d on %s reports bad records" % (v, js))
+    times = {"%d_%s" % c: [] for c in cases}
+    times["copy_52114"] = []
+    cb = int(live_bytes) // 16 * 16
+    for r in range(rounds):
+        for v, js in cases:
+            c = ctxs[v]
+            e0, e1 = crc.Event(c), crc.Event(c)
+            c.compact_jobs_device(img, total, jobsets[js], nj, d_dst, None, d_st, d_bad)
+            e0.record()
+            for _ in range(3):
+                c.compact_jobs_device(img, total, jobsets[js], nj, d_dst, None, d_st, d_bad)
+            e1.record()
+            c.sync()
+            times["%d_%s" % (v, js)].append(e0.elapsed_ms(e1) / 3)
+        e0, e1 = crc.Event(ctx), crc.Event(ctx)
+        ctx.membench_device(52114, img, None, 0, cb, d_dst)
+        e0.record()
+        for _ in range(3):
+            ctx.membench_device(52114, img, None, 0, cb, d_dst)
+        e1.record()
+        ctx.sync()
+        times["copy_52114"].append(e0.elapsed_ms(e1) / 3)
+        print("round %d done" % r, file=sys.stderr, flush=True)
+    res = {}
+    for name, v in times.items():
+        v = sorted(v)
+        med = v[len(v) // 2]
+        by = 2.0 * cb if name.startswith("copy") else algo
+        res[name] = {"median_ms": med, "min_ms": v[0], "max_ms": v[-1], "GBs": by / (med / 1e3) / 1e9,
+                     "frac_8TBs": by / (med / 1e3) / 1e9 / 8000.0}
+    print(json.dumps({"tool": "ab_compact", "rounds": rounds, "nblocks": nblocks, "records": nj,
+                      "algo_bytes": algo, "ab": res}))
+
+
+if __name__ == "__main__":
+    main()
