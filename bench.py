@@ -71,6 +71,22 @@ def parse():
     return p.parse_args()
 
 
+def _pmc_traffic(rel, kernel, applies):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary of this same
+    command at full size (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), or
+    (None, None) when the run is not the one profiled."""
+    if not applies or os.environ.get("TFS_CRC_VARIANT", "0") != "0":
+        return None, None
+    try:
+        with open(os.path.join(ROOT, rel)) as fh:
+            pmc = json.load(fh)
+    except (OSError, ValueError):
+        return None, None
+    if pmc.get("kernel") != kernel:
+        return None, None
+    return pmc.get("traffic_bytes_per_launch"), rel
+
+
 def cpu_baseline(sample_u8, offs, lens, expected, seconds, what="64 KiB payloads", seed=0):
     """Single-thread reference CRC over a bounded sample (test infrastructure)."""
     ref_so = os.path.join(ROOT, "oracle", "_ref", "libref_crc.so")
@@ -1083,6 +1099,8 @@ def bench_block_verify_device(args):
     c24.close()
     algo_per_rec = FILEINFO + FILE_SIZE + 40 + 4 + 4   # header + payload + job read, crc + status written
     achieved = nfiles * algo_per_rec / (kms / 1e3) / 1e9
+    bv_traffic, bv_src = _pmc_traffic("profiles/r02/block_verify_device/pmc_summary.json",
+                                      "compact_pipe_kernel<true, true, true, 12>", nblocks == 1024)
     res = {
         "metric": "GiB/s payload verified on read from device-resident block images (FileInfo checks + re-CRC)",
         "value": world * args.steps * nfiles * FILE_SIZE / el / 2**30, "unit": "GiB/s", "n_gpus": world,
@@ -1093,8 +1111,9 @@ def bench_block_verify_device(args):
             nblocks, FILES_PER_BLOCK, nfiles * FILE_SIZE / 2**30), "files_per_gpu": nfiles,
             "algorithmic_bytes_per_record": algo_per_rec},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "compact_pipe_kernel<true,true,true> (verify form)", "kernel_ms_avg": kms},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": bv_traffic, "traffic_source": bv_src,
+                     "kernel": "compact_pipe_kernel<true,true,true> (verify form)", "kernel_ms_avg": kms,
+                     "algorithmic_bytes_per_launch": nfiles * algo_per_rec},
         "parity": {"statuses_all_ok": True, "crcs_equal_write_pass": nfiles, "oracle_checked": checked},
         "ab": {"pipelined_one_launch_ms": kms, "pipelined_31_block_windows_ms": kms_win,
                "round1_block_verify_kernel_windows_ms": kms_old, "speedup_vs_round1": kms_old / kms},
@@ -1269,8 +1288,10 @@ def bench_compact_device(args):
     el, kms = timed(ctx, step_jobs)
     nlive = sum(w["n"] for w in windows)
     live_bytes = float(nlive) * rec
-    algo = 2 * live_bytes + nlive * (16 + 4 + 8 + 4)  # read + write live records, metas/flags/offsets/status
+    algo = 2 * live_bytes + nlive * (40 + 4)  # read + write live records, 40 B CompactJob + 4 B status
     live_payload = float(nlive) * FILE_SIZE
+    cd_traffic, cd_src = _pmc_traffic("profiles/r02/compact_device_anchored/pmc_summary.json",
+                                      "compact_pipe_kernel<true, true, false, 12>", nblocks == 1024)
     res = {
         "metric": "GiB/s of live payload compacted on the device (re-CRC + repack of live files)",
         "value": world * args.steps * live_payload / el / 2**30, "unit": "GiB/s of live payload", "n_gpus": world,
@@ -1281,8 +1302,9 @@ def bench_compact_device(args):
         "config": {"workload": "SURVEY §8 f3: %d resident blocks, %d live files (%.1f GiB live)" % (
             nblocks, nlive, live_bytes / 2**30)},
         "roofline": {"bound": "hbm", "achieved": algo / (kms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": algo / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "compact_pipe_kernel<WIDE> (one launch)", "kernel_ms_avg": kms},
+                     "frac": algo / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": cd_traffic, "traffic_source": cd_src,
+                     "kernel": "compact_pipe_kernel<WIDE> (one launch)", "kernel_ms_avg": kms,
+                     "algorithmic_bytes_per_launch": algo},
         "membench": extra,
         "ab": {"fused_one_launch_ms": kms, "fused_windows_ms": kms_w, "unfused_windows_ms": kms2,
                "unpipelined_fused_one_launch_ms": kms22, "pipelined_bpermute_one_launch_ms": kms23,

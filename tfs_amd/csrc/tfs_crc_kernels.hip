@@ -370,7 +370,7 @@ __device__ __forceinline__ void store_shifted(uintptr_t chunk, const uint4& v, u
 // TFS_CRC_VARIANT=26: wrong CRCs): skip the payload steps, so the record kernel
 // runs its own load/store schedule without the table lookups.
 template <int RUN, int PF, bool NT, bool S8, bool COPY = false, int G = 1, bool DPPSH = false, bool NTS = true,
-          bool NOCRC = false>
+          bool NOCRC = false, bool HEADST = true>
 __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase& lb, const FileGeo<RUN>& g,
                                                const Head<RUN>& h, uint4 (&buf)[PF][RUN / 16], int lane,
                                                uintptr_t junk, intptr_t delta = 0, bool copy_on = false) {
@@ -391,7 +391,7 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
     for (int i = 0; i < RUN / 4; ++i) {
       const uintptr_t q = lo + 4u * i;
       uint32_t w = h.w[i];
-      if (COPY && copy_on) {
+      if (COPY && HEADST && copy_on) {
         if (q >= g.start && q < g.B16) {
           st32(q + delta, w);
         } else if (q == g.A && g.s) {  // the dword holding `start`: its payload bytes only
@@ -1244,7 +1244,8 @@ __device__ __forceinline__ uint32_t hdr_dword(uint32_t hb, uint32_t k) {
 // 0 plain copy-through stores (variant 25), bit 1 no payload CRC steps (variant
 // 26, wrong CRCs and statuses); variant 27 = DIAG 0 (source-anchored grid,
 // non-temporal loads: the round-2 baseline), 29 = the anchored grid with
-// non-temporal loads.
+// non-temporal loads, 30 = the product without the stripe-0, FileInfo and tail
+// stores (DIAG bit 4; wrong output).
 constexpr int kCompactDiag = 4 | 8;
 template <bool WIDE, bool DPPSH = true, bool VERIFY = false, int DIAG = kCompactDiag>
 __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __restrict__ src, uint64_t src_len,
@@ -1278,7 +1279,7 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
     uint32_t jv = fn < n ? tk.issue(lane) : 0u;
     for (;;) {
       const bool fused = (st.delta & 3) == 0;
-      uint32_t c = st.g.nstripes ? lane_chain<kRun, kPF, LNT, kS8, !VERIFY, 1, DPPSH, !(DIAG & 1), (DIAG & 2) != 0>(
+      uint32_t c = st.g.nstripes ? lane_chain<kRun, kPF, LNT, kS8, !VERIFY, 1, DPPSH, !(DIAG & 1), (DIAG & 2) != 0, !(DIAG & 16)>(
                                      lds_tables, lb, st.g, st.h, buf, lane, junk, st.delta, fused)
                                  : 0u;
       // The next record's loads go out before this one is finished.
@@ -1301,7 +1302,7 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
         uint8_t* drec = dst + cur.doff;
         const uint32_t len = uint32_t(cur.size - kFileInfoSize);
         // FileInfo with offset_(8) size_(12) usize_(16) flag_(28) rewritten, the rest copied (task.cpp:753-759)
-        if (!VERIFY && lane < kFileInfoSize) {
+        if (!VERIFY && !(DIAG & 16) && lane < kFileInfoSize) {
           const int fld = lane >> 2, sh = 8 * (lane & 3);
           uint32_t b = st.hb;
           if (fld == 2) b = uint32_t(cur.new_off) >> sh;
@@ -1311,7 +1312,7 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
         }
         if (VERIFY) {
         } else if (fused && st.g.nstripes) {
-          if (lane == 0) {  // tail [B16, end) from lane 0's registers
+          if (lane == 0 && !(DIAG & 16)) {  // tail [B16, end) from lane 0's registers
             const uint32_t ntw = uint32_t((st.g.end & ~uintptr_t(3)) - st.g.B16) / 4u;
             for (uint32_t i = 0; i < 3u; ++i)
               if (i < ntw) st32(st.g.B16 + 4u * i + st.delta, st.h.tw[i]);
@@ -1634,6 +1635,7 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
   else if (variant == 26) TFS_CJ(true, true, false, kCompactDiag | 2);
   else if (variant == 27) TFS_CJ(true, true, false, 0);
   else if (variant == 29) TFS_CJ(true, true, false, 4);
+  else if (variant == 30) TFS_CJ(true, true, false, kCompactDiag | 16);
   else TFS_CJ(true);
 #undef TFS_CJ
   return hipGetLastError();

@@ -8,7 +8,8 @@ by round, launches of
     on destination lines, temporal payload loads; 27 the source-anchored grid
     with non-temporal loads (the earlier product); 29 the anchored grid with
     non-temporal loads; 25 plain copy-through stores; 26 no payload CRC steps
-    -- the kernel's own load/store schedule), and
+    -- the kernel's own load/store schedule; 30 no stripe-0/FileInfo/tail
+    stores), and
   * the product kernel on destinations congruent to the source mod 16 (no lane
     shift) and mod 128 (whole destination lines per stripe),
 
@@ -78,15 +79,16 @@ def main():
         j["size"] = rec
         j["new_offset"] = (do % np.uint64(1 << 31)).astype(np.int32)
         jobsets[name] = crc.DeviceBuffer(ctx, j.nbytes).upload(j)
-    ctxs = {0: ctx, 25: ctx_for(25), 26: ctx_for(26), 27: ctx_for(27), 29: ctx_for(29)}
-    cases = [(0, "packed"), (27, "packed"), (25, "packed"), (26, "packed"), (29, "packed"), (0, "dst128"),
-             (27, "dst128")]
+    ctxs = {0: ctx, 25: ctx_for(25), 26: ctx_for(26), 27: ctx_for(27), 29: ctx_for(29), 30: ctx_for(30)}
+    cases = [(0, "packed"), (27, "packed"), (25, "packed"), (26, "packed"), (29, "packed"), (30, "packed"),
+             (0, "dst128"), (27, "dst128")]
     nj = int(k.size)
     live_bytes = float(nj) * rec
     algo = 2 * live_bytes + nj * (40 + 4)
-    # correctness of the product cases (the diagnostic variant 26 computes no CRCs)
+    # correctness of the product cases (the diagnostic variants 26 and 30 compute
+    # no CRCs / skip stores)
     for v, js in cases:
-        if v == 26:
+        if v in (26, 30):
             continue
         d_bad.zero()
         ctxs[v].compact_jobs_device(img, total, jobsets[js], nj, d_dst, None, d_st, d_bad)

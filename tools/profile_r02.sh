@@ -4,8 +4,10 @@
 # PMC group in its own pass (FETCH_SIZE and WRITE_SIZE cannot share one; counters
 # never combined with other trace domains).  Outputs under gpurun_out/prof_r02/;
 # tools/pmc_summary.py folds them into profiles/r02/.
+# Usage: tools/profile_r02.sh [all|compact|verify|bverify] [outdir]
 set -euo pipefail
-OUT=gpurun_out/prof_r02
+PART=${1:-all}
+OUT=${2:-gpurun_out/prof_r02}
 mkdir -p "$OUT"
 ROOT=$(pwd)
 cd /tmp && export TMPDIR=/tmp && cd "$ROOT"
@@ -23,16 +25,23 @@ run_pmc() {  # name, counters, kernel regex, bench args...
 }
 mkdir -p "$OUT/verify" "$OUT/compact" "$OUT/bverify"
 H=(--steps 8 --warmup 2 --no-cpu --e2e-blocks 0 --parity-every 1024)
+if [[ $PART == all || $PART == verify ]]; then
 run_trace verify "${H[@]}"
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" \
            "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"; do
   run_pmc verify "$grp" "crc_files_kernel<1" --steps 2 --warmup 1 --no-cpu --e2e-blocks 0 --parity-every 1024
 done
+fi
+# the record kernel's product instantiations carry DIAG = kCompactDiag (12)
+if [[ $PART == all || $PART == compact ]]; then
 C=(--workload compact_device --no-cpu --steps 4 --warmup 1)
 run_trace compact "${C[@]}"
-for grp in FETCH_SIZE WRITE_SIZE; do run_pmc compact "$grp" "compact_pipe_kernel<true, true, false>" --workload compact_device --no-cpu --steps 1 --warmup 1; done
+for grp in FETCH_SIZE WRITE_SIZE; do run_pmc compact "$grp" "compact_pipe_kernel<true, true, false, 12>" --workload compact_device --no-cpu --steps 1 --warmup 1; done
+fi
+if [[ $PART == all || $PART == bverify ]]; then
 B=(--workload block_verify_device --no-cpu --steps 4 --warmup 1)
 run_trace bverify "${B[@]}"
-for grp in FETCH_SIZE WRITE_SIZE; do run_pmc bverify "$grp" "compact_pipe_kernel<true, true, true>" --workload block_verify_device --no-cpu --steps 1 --warmup 1; done
+for grp in FETCH_SIZE WRITE_SIZE; do run_pmc bverify "$grp" "compact_pipe_kernel<true, true, true, 12>" --workload block_verify_device --no-cpu --steps 1 --warmup 1; done
+fi
 echo "profile_r02 done"
