@@ -288,6 +288,21 @@ __device__ __forceinline__ void load_ring(const FileGeo<RUN>& g, int lane, uint4
 typedef __attribute__((address_space(1))) uint32_t* gu32wp;
 typedef __attribute__((address_space(1))) u32x4* gu128wp;
 __device__ __forceinline__ void st32(uintptr_t a, uint32_t v) { *reinterpret_cast<gu32wp>(a) = v; }
+// Stores at any byte address (HSA unaligned access mode: one global_store_dword
+// / _dwordx4 whatever the alignment), for destinations not congruent to the
+// source mod 4.
+typedef uint32_t __attribute__((aligned(1))) u32u;
+typedef u32x4 __attribute__((aligned(1))) u32x4u;
+typedef __attribute__((address_space(1))) u32u* gu32up;
+typedef __attribute__((address_space(1))) u32x4u* gu128up;
+__device__ __forceinline__ void st32u(uintptr_t a, uint32_t v) { *reinterpret_cast<gu32up>(a) = v; }
+template <bool NTS = true>
+__device__ __forceinline__ void st128u(uintptr_t a, const uint4& v) {
+  const u32x4 w = {v.x, v.y, v.z, v.w};
+  if (NTS) __builtin_nontemporal_store(w, reinterpret_cast<gu128up>(a));
+  else *reinterpret_cast<gu128up>(a) = w;
+}
+
 // NTS = false (measurement, TFS_CRC_VARIANT=25): plain stores, so partial lines
 // at record and stripe edges can merge in L2 before they are written back.
 template <bool NTS = true>
@@ -312,6 +327,7 @@ __device__ __forceinline__ void st128_nt(uintptr_t a, const uint4& v) {
 struct ShiftCarry {
   uint32_t y, z, w;
   bool valid;
+  uint32_t x;  // byte shifts only (store_bshift)
 };
 // DPP: lane l-1's dwords by a wave_shr:1 DPP move (VALU) instead of ds_bpermute
 // (__shfl_up), which goes through the LDS crossbar beside the table lookups.
@@ -362,6 +378,49 @@ __device__ __forceinline__ void store_shifted(uintptr_t chunk, const uint4& v, u
   cr.valid = true;
 }
 
+// Copy-through of one stripe to dst = src + delta with a byte shift
+// (delta = 16m + 4K + b, b in 1..3): the aligned 16-byte destination chunk under
+// lane l (`chunk` = q + delta - 4K - b, the stripe grid anchored so that lane 0's
+// chunk starts a 128-byte line) holds the last 4K + b bytes of lane l-1's run and
+// the first 16 - 4K - b of lane l's: with S = lane l-1's four dwords followed by
+// lane l's, dword i of the chunk is alignbyte(S[4-K+i], S[3-K+i], 4-b).  Lane 0
+// takes the previous stripe's lane-63 dwords; right after stripe 0 (stored dword
+// by dword) it stores only its own 16 bytes, unaligned (`own`), and so does the
+// record's last valid lane (`flush`) for the bytes past its chunk.  The byte
+// ranges those extra stores share with a neighbouring chunk hold the same values.
+template <int K, bool NTS>
+__device__ __forceinline__ void store_bshift(uintptr_t chunk, uintptr_t own, const uint4& v, uint32_t sh, int lane,
+                                             ShiftCarry& cr, bool store, bool flush) {
+  uint32_t p0 = 0u, p1 = 0u, p2 = 0u, p3 = from_prev_lane(v.w);
+  if (K >= 1) p2 = from_prev_lane(v.z);
+  if (K >= 2) p1 = from_prev_lane(v.y);
+  if (K >= 3) p0 = from_prev_lane(v.x);
+  if (lane == 0) {
+    p0 = cr.x;
+    p1 = cr.y;
+    p2 = cr.z;
+    p3 = cr.w;
+  }
+  if (store) {
+    if (lane == 0 && !cr.valid) {
+      st128u<NTS>(own, v);
+    } else {
+      const uint32_t S[8] = {p0, p1, p2, p3, v.x, v.y, v.z, v.w};
+      const uint4 o = make_uint4(__builtin_amdgcn_alignbyte(S[4 - K], S[3 - K], sh),
+                                 __builtin_amdgcn_alignbyte(S[5 - K], S[4 - K], sh),
+                                 __builtin_amdgcn_alignbyte(S[6 - K], S[5 - K], sh),
+                                 __builtin_amdgcn_alignbyte(S[7 - K], S[6 - K], sh));
+      st128_nt<NTS>(chunk, o);
+    }
+    if (flush) st128u<NTS>(own, v);
+  }
+  cr.x = __builtin_amdgcn_readlane(v.x, kWave - 1);
+  cr.y = __builtin_amdgcn_readlane(v.y, kWave - 1);
+  cr.z = __builtin_amdgcn_readlane(v.z, kWave - 1);
+  cr.w = __builtin_amdgcn_readlane(v.w, kWave - 1);
+  cr.valid = true;
+}
+
 // The lane's chain over stripes 0..nstripes-1 (before the final combine).
 // COPY: also store every payload byte of [start, B16) to dst = src + delta.
 // G (measurement knob): refill the ring G slots at a time, so each wave issues G
@@ -370,7 +429,7 @@ __device__ __forceinline__ void store_shifted(uintptr_t chunk, const uint4& v, u
 // TFS_CRC_VARIANT=26: wrong CRCs): skip the payload steps, so the record kernel
 // runs its own load/store schedule without the table lookups.
 template <int RUN, int PF, bool NT, bool S8, bool COPY = false, int G = 1, bool DPPSH = false, bool NTS = true,
-          bool NOCRC = false, bool HEADST = true>
+          bool NOCRC = false, bool HEADST = true, bool BSU = false>
 __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase& lb, const FileGeo<RUN>& g,
                                                const Head<RUN>& h, uint4 (&buf)[PF][RUN / 16], int lane,
                                                uintptr_t junk, intptr_t delta = 0, bool copy_on = false) {
@@ -393,7 +452,7 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
       uint32_t w = h.w[i];
       if (COPY && HEADST && copy_on) {
         if (q >= g.start && q < g.B16) {
-          st32(q + delta, w);
+          st32u(q + delta, w);
         } else if (q == g.A && g.s) {  // the dword holding `start`: its payload bytes only
           for (uint32_t k = g.s; k < 4u; ++k) *reinterpret_cast<uint8_t*>(q + k + delta) = uint8_t(w >> (8 * k));
         }
@@ -411,12 +470,23 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
     // Copy-through of stripe st (COPY only): whole dwordx4 stores at any
     // destination shift congruent mod 4 (store_shifted).
     const uint32_t kshift = uint32_t(delta >> 2) & 3u;
-    ShiftCarry carry{0u, 0u, 0u, false};
+    const bool bshift = (delta & 3) != 0;  // wave-uniform
+    ShiftCarry carry{0u, 0u, 0u, false, 0u};
     static_assert(!COPY || RUN == 16, "copy-through assumes one 16-byte run per lane");
     auto copy_stripe = [&](uint32_t st, const uint4& v) {
       const bool valid = !(st == last && !lane_in_last);
       const uintptr_t q = g.sb0 + uintptr_t(st) * kStripe + uintptr_t(lane) * RUN;
-      if (kshift == 0u) {
+      if (bshift && !BSU) {  // byte shift: line-aligned chunks built by alignbyte
+        const uintptr_t chunk = q + uintptr_t(delta & ~intptr_t(15));
+        const uint32_t sh = 4u - uint32_t(delta & 3);
+        const bool fl = st == last && uint32_t(lane) + 1u == g.nvalid;
+        if (kshift == 0u) store_bshift<0, NTS>(chunk, q + delta, v, sh, lane, carry, valid, fl);
+        else if (kshift == 1u) store_bshift<1, NTS>(chunk, q + delta, v, sh, lane, carry, valid, fl);
+        else if (kshift == 2u) store_bshift<2, NTS>(chunk, q + delta, v, sh, lane, carry, valid, fl);
+        else store_bshift<3, NTS>(chunk, q + delta, v, sh, lane, carry, valid, fl);
+      } else if (bshift) {  // BSU (measurement): the lane's 16 bytes at their byte address
+        if (valid) st128u<NTS>(q + delta, v);
+      } else if (kshift == 0u) {
         if (valid) st128_nt<NTS>(q + delta, v);
       } else {
         store_shifted<DPPSH, NTS>(q + uintptr_t(delta) - 4u * kshift, v, kshift, lane, carry, valid,
@@ -1156,8 +1226,9 @@ __global__ void __launch_bounds__(kBlock) compact_fused_kernel(const uint8_t* __
 // FileInfo is read with one byte load per lane (lanes 0..35) and written with one
 // byte store per lane (offset_/size_/usize_/flag_ rewritten); the fields the
 // checks need come out of those registers by readlane.  Payload bytes take the
-// copy-through of lane_chain (whole dwordx4 stores for a destination congruent
-// mod 4); other shifts copy bytes after the CRC, as in compact_fused_kernel.
+// copy-through of lane_chain at every shift: whole aligned dwordx4 stores for a
+// destination congruent mod 4, one unaligned dwordx4 per lane otherwise;
+// payloads too short for stripes take copy_unaligned.
 // ---------------------------------------------------------------------------
 struct CRec {
   uint64_t soff, doff, fid;
@@ -1214,7 +1285,7 @@ __device__ __forceinline__ CState issue_crec(const CRec& r, const uint8_t* src, 
     s.hb = lane < kFileInfoSize ? uint32_t(rec[lane]) : 0u;
     s.delta = intptr_t(dst + r.doff) - intptr_t(rec);
     uint32_t aoff = 0u;
-    if (DA && (s.delta & 3) == 0 && r.soff + uint64_t(uint32_t(r.size)) + 128u <= src_len)
+    if (DA && r.soff + uint64_t(uint32_t(r.size)) + 128u <= src_len)
       aoff = uint32_t(-(s.delta & ~intptr_t(15))) & 127u;
     s.g = make_geo<kRun>(rec + kFileInfoSize, uint32_t(r.size - kFileInfoSize), 0u, aoff);
     s.h = load_head<kRun>(s.g, lane);
@@ -1237,6 +1308,36 @@ __device__ __forceinline__ uint32_t hdr_dword(uint32_t hb, uint32_t k) {
 // 543-577) -- the same schedule and checks, no stores: `metas` (RawMeta, !WIDE)
 // or `jobs` (CompactJob with the dest fields unused, WIDE: many blocks, 64-bit
 // offsets) name the records, dst is unused.
+// Payload copy for a destination not congruent to the source mod 4 (and tiny
+// payloads), after the record's CRC pass: whole dwordx4 stores at 16-aligned
+// destination chunks, each from ONE unaligned 16-byte load of the source (the
+// HSA unaligned access mode: one global_load_dwordx4 at any byte address; the
+// lines were just read by the CRC pass, so the re-read is mostly served by the
+// caches).  At most 15 head and 15 tail bytes go byte by byte.
+__device__ __forceinline__ void copy_unaligned(const uint8_t* s, uint8_t* d, uint32_t len, int lane) {
+  const uintptr_t d0 = reinterpret_cast<uintptr_t>(d);
+  const uintptr_t da = (d0 + 15u) & ~uintptr_t(15);
+  const uint32_t head = uint32_t(da - d0) < len ? uint32_t(da - d0) : len;
+  const uint32_t nch = (len - head) / 16u;
+  const uint32_t t0 = head + 16u * nch;
+  if (uint32_t(lane) < head) d[lane] = s[lane];
+  if (uint32_t(lane) < len - t0) d[t0 + lane] = s[t0 + lane];
+  const uint8_t* sa = s + head;
+  uint32_t c = uint32_t(lane);
+  for (; c + 3u * kWave < nch; c += 4u * kWave) {
+    uint4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) __builtin_memcpy(&v[k], sa + 16u * (c + uint32_t(k) * kWave), 16);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) st128_nt(da + 16u * (c + uint32_t(k) * kWave), v[k]);
+  }
+  for (; c < nch; c += kWave) {
+    uint4 v;
+    __builtin_memcpy(&v, sa + 16u * c, 16);
+    st128_nt(da + 16u * c, v);
+  }
+}
+
 // DIAG bits: 2 stripe grid anchored on destination lines (issue_crec<DA>), 3
 // temporal payload loads (with the destination-anchored grid a source line is
 // split between two stripes of the same wave; a temporal load keeps it in L2
@@ -1245,7 +1346,10 @@ __device__ __forceinline__ uint32_t hdr_dword(uint32_t hb, uint32_t k) {
 // 26, wrong CRCs and statuses); variant 27 = DIAG 0 (source-anchored grid,
 // non-temporal loads: the round-2 baseline), 29 = the anchored grid with
 // non-temporal loads, 30 = the product without the stripe-0, FileInfo and tail
-// stores (DIAG bit 4; wrong output).
+// stores (DIAG bit 4; wrong output), 31 = byte-shifted records copied after the
+// CRC by copy_unaligned instead of through the chain (DIAG bit 5), 32 = byte-
+// shifted records stored as each lane's 16 bytes at their byte address instead
+// of line-aligned alignbyte chunks (DIAG bit 6).
 constexpr int kCompactDiag = 4 | 8;
 template <bool WIDE, bool DPPSH = true, bool VERIFY = false, int DIAG = kCompactDiag>
 __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __restrict__ src, uint64_t src_len,
@@ -1278,9 +1382,11 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
     CRec nxt = fn < n ? load_crec<WIDE, VERIFY>(fn, src_len, metas, flags, dest_off, jobs) : CRec{};
     uint32_t jv = fn < n ? tk.issue(lane) : 0u;
     for (;;) {
-      const bool fused = (st.delta & 3) == 0;
-      uint32_t c = st.g.nstripes ? lane_chain<kRun, kPF, LNT, kS8, !VERIFY, 1, DPPSH, !(DIAG & 1), (DIAG & 2) != 0, !(DIAG & 16)>(
-                                     lds_tables, lb, st.g, st.h, buf, lane, junk, st.delta, fused)
+      // DIAG bit 5 (variant 31, measurement): byte-shifted records copy after the CRC (copy_unaligned)
+      const bool chain_copy = !(DIAG & 32) || (st.delta & 3) == 0;
+      uint32_t c = st.g.nstripes ? lane_chain<kRun, kPF, LNT, kS8, !VERIFY, 1, DPPSH, !(DIAG & 1), (DIAG & 2) != 0, !(DIAG & 16),
+                                            (DIAG & 64) != 0>(
+                                     lds_tables, lb, st.g, st.h, buf, lane, junk, st.delta, chain_copy)
                                  : 0u;
       // The next record's loads go out before this one is finished.
       const bool more = fn < n;
@@ -1311,18 +1417,17 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
           drec[lane] = uint8_t(b);
         }
         if (VERIFY) {
-        } else if (fused && st.g.nstripes) {
+        } else if (chain_copy && st.g.nstripes) {
           if (lane == 0 && !(DIAG & 16)) {  // tail [B16, end) from lane 0's registers
             const uint32_t ntw = uint32_t((st.g.end & ~uintptr_t(3)) - st.g.B16) / 4u;
             for (uint32_t i = 0; i < 3u; ++i)
-              if (i < ntw) st32(st.g.B16 + 4u * i + st.delta, st.h.tw[i]);
+              if (i < ntw) st32u(st.g.B16 + 4u * i + st.delta, st.h.tw[i]);
             const uintptr_t B = st.g.end & ~uintptr_t(3);
             for (uint32_t i = 0; i < 3u; ++i)
               if (B + i < st.g.end) *reinterpret_cast<uint8_t*>(B + i + st.delta) = uint8_t(st.h.tb[i]);
           }
-        } else {  // tiny payload, or a destination not congruent mod 4: byte copy
-          const uint8_t* p = rec + kFileInfoSize;
-          for (uint32_t i = lane; i < len; i += kWave) drec[kFileInfoSize + i] = p[i];
+        } else {  // tiny payload, or a destination not congruent mod 4
+          copy_unaligned(rec + kFileInfoSize, drec + kFileInfoSize, len, lane);
         }
         c = finish_file<kRun, kS8>(lds_tables, lb, st.g, st.h, c, lane);
         const uint64_t hid = uint64_t(hdr_dword(st.hb, 0)) | uint64_t(hdr_dword(st.hb, 1)) << 32;
@@ -1636,6 +1741,8 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
   else if (variant == 27) TFS_CJ(true, true, false, 0);
   else if (variant == 29) TFS_CJ(true, true, false, 4);
   else if (variant == 30) TFS_CJ(true, true, false, kCompactDiag | 16);
+  else if (variant == 31) TFS_CJ(true, true, false, kCompactDiag | 32);
+  else if (variant == 32) TFS_CJ(true, true, false, kCompactDiag | 64);
   else TFS_CJ(true);
 #undef TFS_CJ
   return hipGetLastError();

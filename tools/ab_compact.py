@@ -9,9 +9,11 @@ by round, launches of
     with non-temporal loads (the earlier product); 29 the anchored grid with
     non-temporal loads; 25 plain copy-through stores; 26 no payload CRC steps
     -- the kernel's own load/store schedule; 30 no stripe-0/FileInfo/tail
-    stores), and
+    stores; 31 byte-shifted records copied after the CRC; 32 byte-shifted
+    records stored unaligned, lane by lane), and
   * the product kernel on destinations congruent to the source mod 16 (no lane
-    shift) and mod 128 (whole destination lines per stripe),
+    shift) and mod 128 (whole destination lines per stripe), and on
+    destinations one byte off (every record takes the unaligned copy),
 
 each timed with HIP events on its own context's stream.  The streaming-copy
 ceiling of the same bytes (membench pattern 52114) is timed in the same rounds.
@@ -67,7 +69,8 @@ def main():
     k = np.arange(nblocks * nl, dtype=np.uint64)
     dsts = {"packed": k * rec,                                   # the product workload (contiguous new blocks)
             "dst16": k * 65584 + (soff & np.uint64(15)),         # delta == 0 mod 16: no lane shift
-            "dst128": k * 65664 + (soff & np.uint64(127))}       # delta == 0 mod 128: whole lines per stripe
+            "dst128": k * 65664 + (soff & np.uint64(127)),       # delta == 0 mod 128: whole lines per stripe
+            "shift1": k * rec + np.uint64(1)}                    # delta == 1 mod 4: the unaligned copy
     d_dst = crc.DeviceBuffer(ctx, int(k.size) * 65664 + 256)
     d_st = crc.DeviceBuffer(ctx, 4 * int(k.size))
     d_bad = crc.DeviceBuffer(ctx, 4)
@@ -79,9 +82,10 @@ def main():
         j["size"] = rec
         j["new_offset"] = (do % np.uint64(1 << 31)).astype(np.int32)
         jobsets[name] = crc.DeviceBuffer(ctx, j.nbytes).upload(j)
-    ctxs = {0: ctx, 25: ctx_for(25), 26: ctx_for(26), 27: ctx_for(27), 29: ctx_for(29), 30: ctx_for(30)}
+    ctxs = {0: ctx, 25: ctx_for(25), 26: ctx_for(26), 27: ctx_for(27), 29: ctx_for(29), 30: ctx_for(30),
+            31: ctx_for(31), 32: ctx_for(32)}
     cases = [(0, "packed"), (27, "packed"), (25, "packed"), (26, "packed"), (29, "packed"), (30, "packed"),
-             (0, "dst128"), (27, "dst128")]
+             (0, "dst128"), (27, "dst128"), (0, "shift1"), (31, "shift1"), (32, "shift1")]
     nj = int(k.size)
     live_bytes = float(nj) * rec
     algo = 2 * live_bytes + nj * (40 + 4)
