@@ -778,13 +778,10 @@ static int compact_enqueue(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job
   // live records straight out of the source image over PCIe and writes the new
   // block straight into the destination image, so only live bytes cross the
   // link (the deleted records of a fragmented block never leave host memory).
-  // It needs every live record's source and destination congruent mod 4;
-  // otherwise the kernel's byte-copy fallback would re-read the record over
-  // PCIe, and the whole-block DMA form below is used instead.
+  // Every destination shift copies through the kernel's CRC chain (only payloads
+  // shorter than one stripe are read a second time), so any layout qualifies.
   bool zc = nl && ctx->variant != kVariantDmaCompact && is_pinned_host(job->src_image) &&
             is_pinned_host(job->dest_image);
-  const uintptr_t src_a = reinterpret_cast<uintptr_t>(job->src_image);
-  const uintptr_t dst_a = reinterpret_cast<uintptr_t>(job->dest_image);
   int64_t off = 0;
   for (uint32_t k = 0; k < nl; ++k) {
     const uint32_t i = cs.live_idx[k];
@@ -792,7 +789,6 @@ static int compact_enqueue(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job
     h_metas[k] = RawMeta{job->metas[i].file_id, job->metas[i].offset, job->metas[i].size};
     h_flags[k] = job->flags[i];
     if (job->dest_metas) job->dest_metas[k] = tfs_raw_meta{job->metas[i].file_id, int32_t(off), job->metas[i].size};
-    if (((src_a + uint64_t(job->metas[i].offset)) ^ (dst_a + uint64_t(off))) & 3u) zc = false;
     off += job->metas[i].size;
   }
   void* zc_src = nullptr;
