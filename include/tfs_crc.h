@@ -202,7 +202,9 @@ int tfs_block_compact(tfs_crc_ctx* ctx, const void* src_image, uint64_t src_len,
  * offset order), re-CRC each payload against its stored crc_ and write
  * FileInfo{offset_ = d_dest_off[i], size_ = usize_ = meta.size, flag_ =
  * d_flags[i], rest copied} | payload at d_dest + d_dest_off[i].  Per-file
- * status as tfs_block_verify; d_n_bad (may be NULL) accumulated into.  The
+ * status as tfs_block_verify, except that an empty file (meta.size == 36) is
+ * copied like any other (real_compact does; only meta.size < 36 is
+ * TFS_EXIT_READ_FILE_SIZE_ERROR); d_n_bad (may be NULL) accumulated into.  The
  * caller computes d_dest_off (the running sum of live sizes, task.cpp:753-768)
  * and d_dest must hold sum(size).  Several blocks can share one call when
  * their images are concatenated in d_src.  Asynchronous on `stream`. */
@@ -239,10 +241,10 @@ int tfs_blocks_verify_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_l
  * tfs_block_compact's arguments plus its outputs.  Jobs are pipelined over
  * several streams so the H2D copy of one block, the verify/repack kernels of
  * the next and the D2H copy of another overlap.  When both source and dest
- * images are page-locked (tfs_crc32_host_malloc_pinned / hipHostRegister) and
- * every live record keeps its alignment mod 4, the kernel reads the live
- * records from, and writes the new block to, host memory directly (zero-copy:
- * only live bytes cross PCIe, no whole-block copies).  Otherwise page-locked
+ * images are page-locked (tfs_crc32_host_malloc_pinned / hipHostRegister), the
+ * kernel reads the live records from, and writes the new block to, host memory
+ * directly (zero-copy: only live bytes cross PCIe, no whole-block copies).
+ * Otherwise page-locked
  * images are copied directly (whole block H2D, new block D2H); pageable ones are
  * staged.  Returns the worst job status (TFS_EXIT_CHECK_CRC_ERROR if only CRC
  * mismatches were found). */
@@ -388,6 +390,9 @@ int tfs_crc32_dev_malloc(tfs_crc_ctx* ctx, uint64_t bytes, void** d_ptr);
 int tfs_crc32_dev_free(tfs_crc_ctx* ctx, void* d_ptr);
 int tfs_crc32_host_malloc_pinned(tfs_crc_ctx* ctx, uint64_t bytes, void** h_ptr);
 int tfs_crc32_host_free_pinned(tfs_crc_ctx* ctx, void* h_ptr);
+/* Device address of page-locked host memory (hipHostGetDevicePointer), for
+ * passing host buffers to the *_device calls (zero-copy over PCIe). */
+int tfs_crc32_host_device_ptr(tfs_crc_ctx* ctx, const void* h_ptr, void** d_ptr);
 int tfs_crc32_memcpy(tfs_crc_ctx* ctx, void* dst, const void* src, uint64_t bytes, void* stream);
 int tfs_crc32_memset_device(tfs_crc_ctx* ctx, void* d_ptr, int value, uint64_t bytes, void* stream);
 int tfs_crc32_event_create(tfs_crc_ctx* ctx, void** ev);

@@ -177,3 +177,88 @@ def test_gpu_verify_block_files(ds, oracle, gpu_ctx, tmp_path):
         stored = struct.unpack_from("<I", img, o + 32)[0]
         exp = 0 if ocrc(oracle, 0, img[o + 36:o + sz]) == stored else -1010
         assert st[k] == exp
+
+
+def _flip_on_disk(mount, chain, main_size, ext_size, logic_off, mask=0x40):
+    """Flip bits of one byte at a logic data offset, in the physical block that holds it."""
+    base = 0
+    for k, pid in enumerate(chain):
+        area = (main_size if k == 0 else ext_size) - 512
+        if logic_off < base + area:
+            path = os.path.join(mount, str(pid)) if k == 0 else os.path.join(mount, "extend", str(pid))
+            with open(path, "r+b") as f:
+                f.seek(512 + logic_off - base)
+                b = f.read(1)
+                f.seek(512 + logic_off - base)
+                f.write(bytes([b[0] ^ mask]))
+            return
+        base += area
+    raise AssertionError("offset past the chain")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("windows_per_launch", [1, 3])
+def test_gpu_compact_block_files(ds, oracle, gpu_ctx, tmp_path, windows_per_launch):
+    """real_compact from block files on disk through 8 MiB windows (FileIterator,
+    logic_block.cpp:1132-1329; task.cpp:713-836): arbitrary sizes (every
+    destination shift), two files larger than a window (write_big_file), files
+    deleted and concealed through the index, a FileInfo that disagrees with its
+    index entry (FI_INVALID, skipped), a corrupted live payload in an extension
+    block (copied, reported -1010).  The new block files must hold exactly the
+    oracle's real_compact output of the stitched source, and the new index the
+    new metas and BlockInfo."""
+    from test_gpu_parity import _oracle_compact
+    rng = np.random.default_rng(1234)
+    sizes = [int(x) for x in rng.integers(0, 300_000, 150)]
+    sizes[20] = 9 * MiB + 77          # big files: more than one window each
+    sizes[90] = 17 * MiB + 3
+    sizes[5], sizes[6], sizes[7] = 0, 1, 35
+    flags = {3: 1, 4: 1, 30: 1, 31: 4, 60: 5, 93: 1, 120: 1}
+    blk = make_block(ds, oracle, 606, sizes, seed=7, flags=flags)
+    main_size, ext_size = 16 * MiB, 8 * MiB
+    src, dst = str(tmp_path / "src"), str(tmp_path / "dst")
+    ds.write_block_files(blk, src, 12, 300, bucket_size=17, main_size=main_size, ext_size=ext_size)
+    lb0 = ds.LoadedBlock(None, src, 12, main_size=main_size, ext_size=ext_size)
+    m0 = lb0.metas
+    # FileInfo id of file 50 rewritten on disk: index and header disagree -> FI_INVALID
+    o50 = int(m0["offset"][np.nonzero(m0["file_id"] == 50)[0][0]])
+    _flip_on_disk(src, lb0.chain, main_size, ext_size, o50, 0x01)
+    # a live payload byte corrupted where it lies in an extension block
+    k = next(i for i in range(len(m0)) if int(m0["offset"][i]) > main_size and int(m0["size"][i]) > 1000
+             and int(m0["file_id"][i]) not in flags and int(m0["file_id"][i]) != 50)
+    bad_id = int(m0["file_id"][k])
+    _flip_on_disk(src, lb0.chain, main_size, ext_size, int(m0["offset"][k]) + 36 + 700)
+    lb = ds.LoadedBlock(None, src, 12, main_size=main_size, ext_size=ext_size)
+    img = lb.data()
+    odest, doff, ook = _oracle_compact(oracle, img, lb.metas, lb.flags)
+    live = np.nonzero((lb.flags & 3) == 0)[0]
+    assert lb.flags[np.nonzero(lb.metas["file_id"] == 50)[0][0]] == 2
+    rc, dmetas, st, ext, cnt = ds.compact_block_files(gpu_ctx, src, 12, dst, 40, 700, bucket_size=0,
+                                                      windows_per_launch=windows_per_launch,
+                                                      main_size=main_size, ext_size=ext_size)
+    exp_st = np.where(ook[live] == 1, 0, -1010)
+    assert cnt["n_live"] == len(live) and cnt["big_files"] == 2 and cnt["windows"] > 4, cnt
+    assert np.array_equal(st, exp_st), (np.nonzero(st != exp_st)[0][:10], np.nonzero(exp_st)[0], cnt)
+    assert rc == -1010 and cnt["n_bad"] == 1, (rc, cnt)
+    assert cnt["dest_size"] == odest.size
+    assert np.array_equal(dmetas["file_id"], lb.metas["file_id"][live])
+    assert np.array_equal(dmetas["size"], lb.metas["size"][live])
+    assert np.array_equal(dmetas["offset"].astype(np.int64), doff[live])
+    assert int(st[list(dmetas["file_id"]).index(bad_id)]) == -1010
+    out = ds.LoadedBlock(None, dst, 40, main_size=main_size, ext_size=ext_size)
+    assert out.rc == 0 and out.logic_block_id == 606 and out.chain == [40] + ext
+    assert np.array_equal(out.data(), odest)
+    assert np.array_equal(out.metas, dmetas)
+    h, h0 = out.header[0], lb.header[0]
+    assert h["file_count"] == len(live) and h["size"] == odest.size and h["data_file_offset"] == odest.size
+    assert h["del_file_count"] == 0 and h["del_size"] == 0 and h["version"] == h0["version"] + 1
+    assert h["seq_no"] == h0["seq_no"] and h["bucket_size"] == 17
+    # the concealed file keeps its flag in the new FileInfo; the corrupted one keeps its stored crc_
+    assert out.flags[list(out.metas["file_id"]).index(31)] == 4
+    # verify-on-read of the new block: the corrupted file fails its CRC; the empty
+    # file (id 6) is rejected as the reference's sync_backup rejects it
+    # (read length <= sizeof(FileInfo), sync_backup.cpp:348-351)
+    rc2, st2 = ds.verify_block_files(gpu_ctx, dst, 40, main_size=main_size, ext_size=ext_size)
+    ids = list(out.metas["file_id"])
+    assert rc2 == 2 and st2[ids.index(bad_id)] == -1010 and st2[ids.index(6)] == -8034
+    assert int((st2 != 0).sum()) == 2

@@ -57,7 +57,7 @@ def test_device_compaction_statuses(vctx, oracle):
     odest, doff, ook = _oracle_compact(oracle, img, metas, fl)
     ld = np.concatenate([[0], np.cumsum(lm["size"].astype(np.int64))[:-1]]).astype(np.int64)
     bad = {}
-    lm[3]["size"] = 36                       # too short
+    lm[3]["size"] = 35                       # shorter than its FileInfo
     bad[3] = -8034
     lm[5]["offset"] = img.size - 8           # runs past the image
     bad[5] = -1016

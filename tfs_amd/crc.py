@@ -58,6 +58,7 @@ EXPORTED = [
     "tfs_block_verify", "tfs_block_verify_device", "tfs_block_compact", "tfs_blocks_compact",
     "tfs_crc32_synth_fill_device", "tfs_crc32_write_headers_device", "tfs_crc32_membench_device",
     "tfs_crc32_dev_malloc", "tfs_crc32_dev_free", "tfs_crc32_host_malloc_pinned", "tfs_crc32_host_free_pinned",
+    "tfs_crc32_host_device_ptr",
     "tfs_crc32_memcpy", "tfs_crc32_memset_device", "tfs_crc32_event_create", "tfs_crc32_event_record",
     "tfs_crc32_event_elapsed_ms", "tfs_crc32_event_destroy",
     "tfs_crc32_stream", "tfs_crc32_sync", "tfs_crc32_stream_create", "tfs_crc32_stream_sync",
@@ -124,6 +125,7 @@ def lib():
             "tfs_crc32_dev_free": (ctypes.c_int, [vp, vp]),
             "tfs_crc32_host_malloc_pinned": (ctypes.c_int, [vp, u64, ctypes.POINTER(vp)]),
             "tfs_crc32_host_free_pinned": (ctypes.c_int, [vp, vp]),
+            "tfs_crc32_host_device_ptr": (ctypes.c_int, [vp, vp, ctypes.POINTER(vp)]),
             "tfs_crc32_memcpy": (ctypes.c_int, [vp, vp, vp, u64, vp]),
             "tfs_crc32_memset_device": (ctypes.c_int, [vp, vp, ctypes.c_int, u64, vp]),
             "tfs_crc32_event_create": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),

@@ -756,7 +756,7 @@ static int compact_enqueue(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job
   int64_t w = 0;
   for (uint32_t i = 0; i < n; ++i) {
     const tfs_raw_meta& m = job->metas[i];
-    if (m.size <= TFS_FILEINFO_SIZE || m.offset < 0 || uint64_t(m.offset) + uint64_t(m.size) > job->src_len)
+    if (m.size < TFS_FILEINFO_SIZE || m.offset < 0 || uint64_t(m.offset) + uint64_t(m.size) > job->src_len)
       return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "meta %u out of range", i);
     if (job->flags[i] & (TFS_FI_DELETED | TFS_FI_INVALID)) continue;
     cs.live_idx.push_back(i);
@@ -1153,6 +1153,14 @@ int tfs_crc32_host_free_pinned(tfs_crc_ctx* ctx, void* h_ptr) {
   if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
   if (!h_ptr) return TFS_SUCCESS;
   HIP_TRY(ctx, hipHostFree(h_ptr));
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_host_device_ptr(tfs_crc_ctx* ctx, const void* h_ptr, void** d_ptr) {
+  if (!ctx || !h_ptr || !d_ptr) return TFS_EXIT_PARAMETER_ERROR;
+  *d_ptr = nullptr;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  HIP_TRY(ctx, hipHostGetDevicePointer(d_ptr, const_cast<void*>(h_ptr), 0));
   return TFS_SUCCESS;
 }
 

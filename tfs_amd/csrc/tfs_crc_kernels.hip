@@ -1259,7 +1259,10 @@ __device__ __forceinline__ CRec load_crec(uint32_t f, uint64_t src_len, const Ra
     r.size = m.size, r.flag = flags[f], r.new_off = int32_t(d);
     range_ok = m.offset >= 0 && d >= 0 && uint64_t(m.offset) + uint64_t(uint32_t(m.size)) <= src_len;
   }
-  r.pre = r.size <= kFileInfoSize ? kExitReadFileSizeError : (range_ok ? kSuccess : kExitParameterError);
+  // Verify rejects a record with no payload byte (sync_backup.cpp:348-351); the
+  // compaction copies an empty file like any other (task.cpp:753-798).
+  const bool short_rec = VERIFY ? r.size <= kFileInfoSize : r.size < kFileInfoSize;
+  r.pre = short_rec ? kExitReadFileSizeError : (range_ok ? kSuccess : kExitParameterError);
   return r;
 }
 

@@ -78,6 +78,9 @@ def lib():
             "tfs_ds_loaded_metas": (u32, [vp, vp, vp, u32, vp, u32, ctypes.POINTER(u32), vp]),
             "tfs_ds_verify_block_files": (ctypes.c_int, [vp, ctypes.c_char_p, i32, i32, u32, vp, u32,
                                                          ctypes.POINTER(u32), vp]),
+            "tfs_ds_compact_block_files": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_char_p, i32, i32, u32, u32,
+                                                          u32, i32, ctypes.c_int, vp, vp, u32, vp, u32,
+                                                          ctypes.POINTER(u32), vp]),
             "tfs_ds_decode": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, u32, ctypes.POINTER(u32),
                                              ctypes.POINTER(i64)]),
             "tfs_ds_close_latency": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, i32, vp]),
@@ -394,6 +397,25 @@ def verify_block_files(ctx, mount, main_id, checker=None, main_size=MAIN_BLOCK_S
     rc = lib().tfs_ds_verify_block_files(ctx.handle, mount.encode(), main_size, ext_size, main_id, st.ctypes.data,
                                          st.size, ctypes.byref(nl), checker.h if checker else None)
     return rc, st[:nl.value]
+
+
+def compact_block_files(ctx, src_mount, src_main_id, dst_mount, dst_main_id, first_ext_id, bucket_size=0,
+                        windows_per_launch=4, main_size=MAIN_BLOCK_SIZE, ext_size=EXT_BLOCK_SIZE, cap=1 << 20):
+    """real_compact from block files on disk through 8 MiB windows (block_store.h
+    compact_block_files).  Returns (rc, dest metas, statuses, ext ids, counters)
+    with counters {n_live, dest_size, windows, launches, big_files, n_bad}."""
+    metas = np.zeros(cap, _crc.META_DTYPE)
+    st = np.zeros(cap, np.int32)
+    ext = np.zeros(64, np.uint32)
+    next_ = ctypes.c_uint32()
+    cnt = np.zeros(6, np.int64)
+    rc = lib().tfs_ds_compact_block_files(ctx.handle, src_mount.encode(), dst_mount.encode(), main_size, ext_size,
+                                          src_main_id, dst_main_id, first_ext_id, bucket_size, windows_per_launch,
+                                          metas.ctypes.data, st.ctypes.data, cap, ext.ctypes.data, 64,
+                                          ctypes.byref(next_), cnt.ctypes.data)
+    n = int(cnt[0])
+    keys = ("n_live", "dest_size", "windows", "launches", "big_files", "n_bad")
+    return rc, metas[:n], st[:n], ext[:next_.value].tolist(), dict(zip(keys, (int(x) for x in cnt)))
 
 
 def verify_block(ctx, block, checker=None):

@@ -72,6 +72,36 @@ struct BlockStore {
   int32_t ext_block_size = 32 * 1024 * 1024;   // extblock_size (config_item.h:133)
 };
 
+// A logic block being written: physical blocks are created as the data grows
+// (main block first, then extension blocks first_ext_id, first_ext_id+1, ...;
+// LogicBlock::extend_block, logic_block.cpp:1066-1113), each preallocated to
+// its block length with its prefix chained to the previous one.  write() takes
+// logic data offsets (DataHandle::write_segment_data, data_handle.cpp:103-141).
+class ChainWriter {
+ public:
+  ChainWriter(const BlockStore& st, uint32_t main_id, uint32_t first_ext_id, uint32_t logic_id);
+  ~ChainWriter();
+  ChainWriter(const ChainWriter&) = delete;
+  ChainWriter& operator=(const ChainWriter&) = delete;
+  int write(const char* src, int64_t len, int64_t off);
+  int status() const { return rc_; }
+  const std::vector<uint32_t>& chain() const { return chain_; }
+
+ private:
+  int add_block(uint32_t id);
+  BlockStore st_;
+  uint32_t first_ext_id_, logic_id_;
+  std::vector<uint32_t> chain_;
+  std::vector<int> fds_;
+  int rc_ = 0;
+};
+
+// The index file of a logic block: header with `info`, bucket_size empty slots,
+// one MetaInfo per meta in the given order (hash_insert, index_handle.cpp:
+// 1015-1060); unlink_flags (empty, or one per meta) go into the index entries.
+int write_index(const BlockStore& st, uint32_t main_id, const BlockInfo& info, const std::vector<tfs_raw_meta>& metas,
+                const std::vector<int32_t>& unlink_flags, int32_t bucket_size, int32_t data_size);
+
 // Write `img` as logic block `img.block_id()`: main block <main_id>, extension
 // blocks first_ext_id, first_ext_id+1, ... as needed (ids returned in
 // *ext_ids), prefixes in-file, and the index with every file inserted in offset
@@ -85,6 +115,13 @@ int load_chain(const BlockStore& st, uint32_t main_id, std::vector<uint32_t>* ch
 int load_index(const BlockStore& st, uint32_t main_id, IndexHeader* header, std::vector<tfs_raw_meta>* metas);
 // The logic block's data bytes [0, size) stitched from the chain into dst.
 int read_data(const BlockStore& st, const std::vector<uint32_t>& chain, char* dst, int64_t size);
+// Data bytes [off, off + len) (LogicBlock::read_raw_data).
+int read_range(const BlockStore& st, const std::vector<uint32_t>& chain, char* dst, int64_t off, int64_t len);
+// A file's flag as FileIterator reports it (logic_block.cpp:1250-1273):
+// FI_INVALID when the FileInfo disagrees with the index entry, else
+// LogicBlock::get_real_flag (:996-1009) -- the entry's unlink bits when its
+// use-index bit is set, the FileInfo's flag_ otherwise.  m.size already masked.
+int32_t real_flag(const tfs_raw_meta& m, int32_t raw_size, const tfs_file_info& fi);
 
 // A block loaded for the GPU: index, chain, the FileInfo flag of every meta
 // (FileIterator, logic_block.cpp:1273) and the data in page-locked memory
@@ -115,6 +152,37 @@ class LoadedBlock {
 // `checker` (may be NULL).  Returns the number of bad files or < 0.
 int verify_block_files(tfs_crc_ctx* ctx, const BlockStore& st, uint32_t main_id, std::vector<int32_t>* status,
                        BlockCrcChecker* checker);
+
+// CompactTask::real_compact over block files on disk (task.cpp:713-836) with
+// the build's re-CRC: the source logic block is walked in offset order through
+// windows of MAX_COMPACT_READ_SIZE (8 MiB, dataserver_define.h:41) as
+// FileIterator does (logic_block.cpp:1132-1329); each window is read into
+// page-locked memory, and its live records are verified and repacked on the GPU
+// straight into a page-locked write buffer (tfs_compact_jobs_device, zero-copy)
+// whose bytes are then appended to the destination logic block
+// (write_raw_data).  `windows_per_launch` windows go to the GPU in one launch,
+// and the next group is read from disk while it runs.  Files larger than a
+// window take write_big_file's path (task.cpp:838-880): window-sized pieces,
+// their CRC chained piece to piece.  Records are copied whatever their CRC (the
+// reference copies, it never verifies); status[i] is the verdict of the i-th
+// file of the new block (TFS_SUCCESS or TFS_EXIT_CHECK_CRC_ERROR).  The
+// destination index gets the new metas and BlockInfo{file_count_, size_ of the
+// live files, del_* 0, version_ + 1 (VERSION_INC_STEP_DEFAULT), the rest
+// copied} (batch_write_meta, logic_block.cpp:817-857).  Returns TFS_SUCCESS,
+// TFS_EXIT_CHECK_CRC_ERROR when some file failed its CRC, or an error
+// (EXIT_META_OFFSET_ERROR -8027 for a meta past the data, as FileIterator::next).
+struct CompactFilesResult {
+  std::vector<tfs_raw_meta> dest_metas;
+  std::vector<int32_t> status;
+  std::vector<uint32_t> ext_ids;
+  int64_t dest_size = 0;
+  uint32_t windows = 0, launches = 0, big_files = 0, n_bad = 0;
+};
+constexpr int32_t kMaxCompactReadSize = 8388608;  // MAX_COMPACT_READ_SIZE, dataserver_define.h:41
+constexpr int kExitMetaOffsetError = -8027;       // EXIT_META_OFFSET_ERROR, error_msg.h:163
+int compact_block_files(tfs_crc_ctx* ctx, const BlockStore& src, uint32_t src_main_id, const BlockStore& dst,
+                        uint32_t dst_main_id, uint32_t first_ext_id, int32_t bucket_size, int windows_per_launch,
+                        CompactFilesResult* out);
 
 }  // namespace dataserver
 }  // namespace tfs

@@ -417,6 +417,34 @@ uint32_t tfs_ds_loaded_metas(void* b, tfs_raw_meta* metas, int32_t* flags, uint3
   return uint32_t(lb->metas.size());
 }
 
+// compact_block_files: the new block's metas / statuses (cap entries), ext ids
+// (ext_cap), and counters[6] = {n_live, dest_size, windows, launches, big_files, n_bad}.
+int tfs_ds_compact_block_files(tfs_crc_ctx* ctx, const char* src_mount, const char* dst_mount, int32_t main_size,
+                               int32_t ext_size, uint32_t src_main_id, uint32_t dst_main_id, uint32_t first_ext_id,
+                               int32_t bucket_size, int windows_per_launch, tfs_raw_meta* dest_metas,
+                               int32_t* status, uint32_t cap, uint32_t* ext_ids, uint32_t ext_cap, uint32_t* n_ext,
+                               int64_t* counters) {
+  tfs::dataserver::CompactFilesResult r;
+  const int rc = tfs::dataserver::compact_block_files(ctx, make_store(src_mount, main_size, ext_size), src_main_id,
+                                                      make_store(dst_mount, main_size, ext_size), dst_main_id,
+                                                      first_ext_id, bucket_size, windows_per_launch, &r);
+  for (size_t i = 0; i < r.dest_metas.size() && i < cap; ++i) {
+    if (dest_metas) dest_metas[i] = r.dest_metas[i];
+    if (status) status[i] = r.status[i];
+  }
+  if (n_ext) *n_ext = uint32_t(r.ext_ids.size());
+  for (size_t i = 0; ext_ids && i < r.ext_ids.size() && i < ext_cap; ++i) ext_ids[i] = r.ext_ids[i];
+  if (counters) {
+    counters[0] = int64_t(r.dest_metas.size());
+    counters[1] = r.dest_size;
+    counters[2] = r.windows;
+    counters[3] = r.launches;
+    counters[4] = r.big_files;
+    counters[5] = r.n_bad;
+  }
+  return rc;
+}
+
 int tfs_ds_verify_block_files(tfs_crc_ctx* ctx, const char* mount, int32_t main_size, int32_t ext_size,
                               uint32_t main_id, int32_t* status, uint32_t cap, uint32_t* n_live, void* checker) {
   std::vector<int32_t> st;
