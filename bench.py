@@ -1636,8 +1636,11 @@ def bench_loopback(args):
     pool = ds.BlockImagePool(ctx, 2, n * (L + FILEINFO) + 4096)
 
     # One CloseBatcher per thread count, created once (DataService::initialize).
-    batchers = {8: ds.CloseBatcher(ctx, max_batch=8, max_wait_us=100),
-                64: ds.CloseBatcher(ctx, max_batch=64, max_wait_us=100)}
+    # Batches of about half the closing threads (8 of 64): several batches are in
+    # flight at once, their round trips overlapping (tools/loopback_probe.py,
+    # profiles/r02/loopback_probe.json).
+    close_batch = {8: 4, 64: 8}
+    batchers = {t: ds.CloseBatcher(ctx, max_batch=b, max_wait_us=100) for t, b in close_batch.items()}
 
     def gpu_once(threads=8):
         blk = ds.LogicBlock(1, pool=pool)
@@ -1698,7 +1701,7 @@ def bench_loopback(args):
         "config": {"workload": "configs[0]: DataFile set_data -> close (CloseBatcher, 8 worker threads) -> "
                                "FileInfo|payload append; then verify_block of the whole block",
                    "block_storage": "page-locked, allocated once (%d buffers)" % pool.size(),
-                   "files": n, "file_size": L},
+                   "files": n, "file_size": L, "close_batch": close_batch},
         "threads64_GiBs": reps * n * L / el64 / 2**30,
         "phases_ms": {"verify_block": verify_ms, "append_only_python": append_ms},
     }

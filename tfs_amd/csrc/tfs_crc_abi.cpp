@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -137,6 +138,7 @@ struct Slot {
 };
 
 constexpr int kSlots = 4;
+constexpr int kSyncSlots = 8;
 
 struct CompactSlot {
   hipStream_t stream = nullptr;
@@ -168,8 +170,13 @@ struct tfs_crc_ctx {
   hipStream_t stream = nullptr;
   Tables* d_tables = nullptr;
   std::mutex mu;
-  std::string last_error = "no error";
-  Slot slots[kSlots];
+  std::mutex err_mu;
+  char last_error[512] = "no error";
+  Slot slots[kSlots];  // async submissions, block verify, packets
+  // Synchronous host calls (tfs_crc32_batch / _verify and the scalar drop-in):
+  // their own slots, taken and launched under `mu`, waited on outside it.
+  Slot sync_slots[kSyncSlots];
+  std::condition_variable sync_cv;
   CompactSlot cslots[kCompactSlots];
   uint64_t next_ticket = 1;
   // Work-distribution counters: kSchedSlots slots of 8 ticket counters and a
@@ -195,7 +202,10 @@ int set_err(tfs_crc_ctx* ctx, int code, const char* fmt, ...) {
   va_start(ap, fmt);
   vsnprintf(buf, sizeof buf, fmt, ap);
   va_end(ap);
-  if (ctx) ctx->last_error = buf;
+  if (ctx) {
+    std::lock_guard<std::mutex> g(ctx->err_mu);
+    memcpy(ctx->last_error, buf, sizeof buf);
+  }
   return code;
 }
 
@@ -503,6 +513,7 @@ int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx) {
   if (ctx->device >= 0) (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   for (auto& s : ctx->slots) s.release();
+  for (auto& s : ctx->sync_slots) s.release();
   for (auto& cs : ctx->cslots) {
     if (cs.stream) (void)hipStreamSynchronize(cs.stream);
     cs.release();
@@ -517,23 +528,58 @@ int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx) {
 
 const char* tfs_crc32_last_error(const tfs_crc_ctx* ctx) {
   if (!ctx) {
-    if (g_default) return g_default->last_error.c_str();
+    if (g_default) return g_default->last_error;
     return g_default_err.c_str();
   }
-  return ctx->last_error.c_str();
+  return ctx->last_error;
 }
+
+namespace {
+
+// A synchronous host call: its slot is taken and its launch queued under
+// ctx->mu, and the wait for the result (the completion-flag spin of a
+// zero-copy batch) runs outside it, so calls from several threads -- the
+// close path's batches -- overlap their round trips; their kernels queue back
+// to back on the ctx stream.
+int sync_host_call(tfs_crc_ctx* ctx, int mode, const void* d, uint32_t n, const void* base, uint64_t base_len,
+                   uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad) {
+  Slot* s = nullptr;
+  {
+    std::unique_lock<std::mutex> lk(ctx->mu);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    for (;;) {
+      for (Slot& x : ctx->sync_slots)
+        if (!x.busy) {
+          s = &x;
+          break;
+        }
+      if (s) break;
+      ctx->sync_cv.wait(lk);
+    }
+    s->busy = true;
+    const int rc = enqueue_host_batch(ctx, *s, mode, d, n, base, base_len);
+    if (rc) {
+      s->busy = false;
+      ctx->sync_cv.notify_one();
+      return rc;
+    }
+  }
+  const int rc = finish_slot(ctx, *s, mode, n, out_crc, out_ok, n_bad);
+  {
+    std::lock_guard<std::mutex> g(ctx->mu);
+    s->busy = false;
+  }
+  ctx->sync_cv.notify_one();
+  return rc;
+}
+
+}  // namespace
 
 int tfs_crc32_batch(tfs_crc_ctx* ctx, const tfs_crc_desc* d, uint32_t n, const void* base, uint64_t base_len,
                     uint32_t* out_crc) {
   if (!ctx || (n && (!d || !out_crc || !base))) return TFS_EXIT_PARAMETER_ERROR;
   if (n == 0) return TFS_SUCCESS;
-  std::lock_guard<std::mutex> g(ctx->mu);
-  HIP_TRY(ctx, hipSetDevice(ctx->device));
-  Slot* s = free_slot(ctx);
-  if (!s) return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "all %d slots busy with async submissions", kSlots);
-  int rc = enqueue_host_batch(ctx, *s, 0, d, n, base, base_len);
-  if (rc) return rc;
-  return finish_slot(ctx, *s, 0, n, out_crc, nullptr, nullptr);
+  return sync_host_call(ctx, 0, d, n, base, base_len, out_crc, nullptr, nullptr);
 }
 
 int tfs_crc32_verify(tfs_crc_ctx* ctx, const tfs_crc_vdesc* d, uint32_t n, const void* base, uint64_t base_len,
@@ -543,13 +589,7 @@ int tfs_crc32_verify(tfs_crc_ctx* ctx, const tfs_crc_vdesc* d, uint32_t n, const
     if (n_bad) *n_bad = 0;
     return TFS_SUCCESS;
   }
-  std::lock_guard<std::mutex> g(ctx->mu);
-  HIP_TRY(ctx, hipSetDevice(ctx->device));
-  Slot* s = free_slot(ctx);
-  if (!s) return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "all %d slots busy with async submissions", kSlots);
-  int rc = enqueue_host_batch(ctx, *s, 1, d, n, base, base_len);
-  if (rc) return rc;
-  return finish_slot(ctx, *s, 1, n, out_crc, out_ok, n_bad);
+  return sync_host_call(ctx, 1, d, n, base, base_len, out_crc, out_ok, n_bad);
 }
 
 int tfs_crc32_submit_verify(tfs_crc_ctx* ctx, const tfs_crc_vdesc* d, uint32_t n, const void* base,

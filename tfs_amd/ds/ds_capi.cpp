@@ -216,7 +216,8 @@ int tfs_ds_close_latency(tfs_crc_ctx* ctx, int nleases, int iters, int32_t len, 
   int rc = tfs_datafile_get_crc(ctx, payload.data(), len, &client);  // the client's Func::crc
   if (rc != TFS_SUCCESS) return rc;
   LogicBlockImage blk(1, int64_t(INT32_MAX));
-  const int64_t total = int64_t(nleases) * iters * (int64_t(len) + TFS_FILEINFO_SIZE);
+  constexpr int kWarm = 8;  // untimed closes per lease first: steady state, not first-use allocations
+  const int64_t total = int64_t(nleases) * (iters + kWarm) * (int64_t(len) + TFS_FILEINFO_SIZE);
   if (total > int64_t(INT32_MAX)) return TFS_EXIT_PARAMETER_ERROR;
   blk.reserve(total);
   std::atomic<int> err{0};
@@ -225,8 +226,8 @@ int tfs_ds_close_latency(tfs_crc_ctx* ctx, int nleases, int iters, int32_t len, 
     std::vector<std::thread> workers;
     for (int t = 0; t < nleases; ++t)
       workers.emplace_back([&, t] {
-        for (int k = 0; k < iters; ++k) {
-          const uint64_t fid = uint64_t(t) * uint64_t(iters) + uint64_t(k) + 1;
+        for (int k = -kWarm; k < iters; ++k) {
+          const uint64_t fid = uint64_t(t) * uint64_t(iters + kWarm) + uint64_t(k + kWarm) + 1;
           DataFile df(fid, "/tmp", ctx);
           df.set_data(payload.data(), len, 0);
           CloseFileInfo info;
@@ -236,7 +237,8 @@ int tfs_ds_close_latency(tfs_crc_ctx* ctx, int nleases, int iters, int32_t len, 
           const auto t0 = std::chrono::steady_clock::now();
           const int r = batcher.close(info, df, blk);
           const auto t1 = std::chrono::steady_clock::now();
-          out_us[size_t(t) * size_t(iters) + size_t(k)] = std::chrono::duration<double, std::micro>(t1 - t0).count();
+          if (k >= 0)
+            out_us[size_t(t) * size_t(iters) + size_t(k)] = std::chrono::duration<double, std::micro>(t1 - t0).count();
           if (r != TFS_SUCCESS) err = r;
         }
       });
@@ -251,6 +253,7 @@ int tfs_ds_scalar_latency(int iters, int32_t len, double* out_us) {
   std::vector<char> payload(size_t(len) + 1);
   for (int32_t i = 0; i < len; ++i) payload[size_t(i)] = char((i * 40503u) >> 5);
   int err = TFS_SUCCESS;
+  for (int k = 0; k < 8 && err == TFS_SUCCESS; ++k) (void)tfs_crc32_e(0, payload.data(), len, &err);  // untimed
   for (int k = 0; k < iters; ++k) {
     const auto t0 = std::chrono::steady_clock::now();
     (void)tfs_crc32_e(0, payload.data(), len, &err);

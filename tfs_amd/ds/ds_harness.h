@@ -202,7 +202,7 @@ class CloseBatcher {
   int close(const CloseFileInfo& info, DataFile& df, LogicBlockImage& block);
   uint64_t batches() const { return batches_.load(); }
 
-  static constexpr int kBatches = 4;
+  static constexpr int kBatches = 8;
   static constexpr int32_t kMaxBatched = 2 * 1024 * 1024;  // DataFile's in-memory limit (data_file.h:78)
 
  private:
