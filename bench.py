@@ -337,6 +337,7 @@ def main():
             "layout": "block image, FileInfo(36 B)|payload, payload 4-byte aligned",
             "partition": "by block id across ranks, no collective",
             "partition_check": partition,
+            "host_numa": dict(_NUMA),
         },
         "parity": {"files_checked": checked, "mismatches": mism, "verdicts_all_ok": all_ok,
                    "method": "every %d-th resident block of every rank: all 1,024 CRCs recomputed by the oracle "
@@ -459,7 +460,35 @@ def _dist_init():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group(backend="gloo")
+    _bind_numa(local)
     return world, rank, local, dist
+
+
+_NUMA = {}
+
+
+def _bind_numa(device):
+    """Keep this rank's threads (and so its page-locked buffers, placed where they
+    are first touched) on the NUMA node of its GPU (tfs_crc32_device_numa_node),
+    as the device group's workers are: with 8 GPUs over two sockets, half the
+    ranks would otherwise stage host data across the socket link."""
+    import tfs_amd.crc as crc
+    node = crc.lib().tfs_crc32_device_numa_node(device)
+    _NUMA.update(node=node, bound=False)
+    if node < 0:
+        return
+    try:
+        with open("/sys/devices/system/node/node%d/cpulist" % node) as fh:
+            cpus = set()
+            for part in fh.read().strip().split(","):
+                a, _, b = part.partition("-")
+                cpus.update(range(int(a), int(b or a) + 1))
+        mine = cpus & os.sched_getaffinity(0)
+        if mine:
+            os.sched_setaffinity(0, mine)
+            _NUMA.update(bound=True, cpus=len(mine))
+    except (OSError, ValueError):
+        pass
 
 
 def _max_over_ranks(dist, v):

@@ -101,6 +101,10 @@ int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx);
 const char* tfs_crc32_last_error(const tfs_crc_ctx* ctx);
 /* Number of HIP devices visible to this process (0 when none). */
 int tfs_crc32_device_count(void);
+/* NUMA node of HIP device `device` (its PCI device's sysfs numa_node), -1 when
+ * unknown: where a process serving that GPU should keep its threads and
+ * page-locked buffers. */
+int tfs_crc32_device_numa_node(int device);
 
 /* ---- scalar drop-in --------------------------------------------------- */
 

@@ -53,6 +53,7 @@ assert DESC_DTYPE.itemsize == 16 and META_DTYPE.itemsize == 16 and FILEINFO_DTYP
 # Every symbol include/tfs_crc.h declares (checked by tests/test_abi.py).
 EXPORTED = [
     "tfs_crc32_ctx_create", "tfs_crc32_ctx_destroy", "tfs_crc32_last_error", "tfs_crc32_device_count",
+    "tfs_crc32_device_numa_node",
     "tfs_crc32", "tfs_crc32_e", "tfs_datafile_get_crc", "tfs_crc32_batch", "tfs_crc32_verify",
     "tfs_crc32_batch_device", "tfs_crc32_verify_device", "tfs_crc32_submit_verify", "tfs_crc32_wait",
     "tfs_block_verify", "tfs_block_verify_device", "tfs_block_compact", "tfs_blocks_compact",
@@ -102,6 +103,7 @@ def lib():
             "tfs_crc32_ctx_destroy": (ctypes.c_int, [vp]),
             "tfs_crc32_last_error": (ctypes.c_char_p, [vp]),
             "tfs_crc32_device_count": (ctypes.c_int, []),
+            "tfs_crc32_device_numa_node": (ctypes.c_int, [ctypes.c_int]),
             "tfs_crc32": (u32, [u32, ctypes.c_char_p, i32]),
             "tfs_crc32_e": (u32, [u32, ctypes.c_char_p, i32, ctypes.POINTER(ctypes.c_int)]),
             "tfs_datafile_get_crc": (ctypes.c_int, [vp, ctypes.c_char_p, i32, ctypes.POINTER(u32)]),

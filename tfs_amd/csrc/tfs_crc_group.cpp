@@ -146,6 +146,8 @@ struct tfs_crc_group {
 
 extern "C" {
 
+int tfs_crc32_device_numa_node(int device) { return device_numa_node(device); }
+
 int tfs_crc_group_create(const int* devices, uint32_t n, tfs_crc_group** out) {
   if (!out) return TFS_EXIT_PARAMETER_ERROR;
   *out = nullptr;
