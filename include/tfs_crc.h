@@ -418,6 +418,16 @@ int tfs_crc32_inject_device_error(tfs_crc_ctx* ctx, uint32_t skip, uint32_t coun
 int tfs_crc32_stream_create(tfs_crc_ctx* ctx, void** stream);
 int tfs_crc32_stream_sync(tfs_crc_ctx* ctx, void* stream);
 int tfs_crc32_stream_destroy(tfs_crc_ctx* ctx, void* stream);
+/* Resident form of the synchronous small batches (tfs_crc32_batch / _verify /
+ * the scalar drop-in with <= 256 files read in place from page-locked memory,
+ * i.e. every close batch of DataManagement::close_write_file,
+ * data_management.cpp:173-236): a kernel that stays on the GPU between batches
+ * takes them from a page-locked ring, so a batch costs no launch; it leaves
+ * after TFS_CRC_RESIDENT_IDLE_US (200) without work and is relaunched on the
+ * next batch.  on = 0 launches every batch instead (also TFS_CRC_RESIDENT=0).
+ * Stats: kernel launches made and files taken through the ring so far. */
+int tfs_crc32_set_resident(tfs_crc_ctx* ctx, int on);
+int tfs_crc32_resident_stats(tfs_crc_ctx* ctx, uint64_t* launches, uint64_t* files);
 
 #ifdef __cplusplus
 }

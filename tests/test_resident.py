@@ -1,0 +1,144 @@
+"""The resident form: synchronous small batches taken by a
+kernel that stays on the GPU, from a page-locked ring, instead of a launch per
+batch.  Every output is checked against the oracle; the stats show the ring was
+used (and, with short idle/lifetime limits, that the kernel was relaunched)."""
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from conftest import ocrc
+from test_latency_form import _oracle_batch
+from tfs_amd.synth import synth_bytes
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx(monkeypatch, **env):
+    import tfs_amd.crc as crc
+    for k, v in env.items():
+        monkeypatch.setenv(k, str(v))
+    ctx = crc.Context(0)
+    for k in env:
+        monkeypatch.delenv(k)
+    return ctx
+
+
+def _random_batch(rng, n, maxlen=70000, seed=0):
+    lens = rng.integers(0, maxlen, n).astype(np.uint32)
+    offs = np.cumsum(np.concatenate([[0], lens[:-1]]).astype(np.uint64) + rng.integers(0, 9, n).astype(np.uint64))
+    buf = synth_bytes(seed, int(offs[-1] + lens[-1]) + 64)
+    return buf, offs, lens
+
+
+def test_resident_batches_match_oracle(monkeypatch, oracle):
+    """Compute with seeds and verify (with mismatches) through the ring, batch sizes
+    1..256, pageable and page-locked; the same calls with the ring off agree."""
+    import tfs_amd.crc as crc
+    ctx = _ctx(monkeypatch, TFS_CRC_RESIDENT=1)
+    try:
+        rng = np.random.default_rng(31)
+        ring_files = 0
+        for it, n in enumerate((1, 2, 3, 8, 17, 64, 200, 256)):
+            buf, offs, lens = _random_batch(rng, n, maxlen=70000 if n <= 64 else 30000, seed=500 + n)
+            ring_files += 3 * n  # spans <= 8 MiB: read in place, so through the ring
+            seeds = rng.integers(0, 2**32, n).astype(np.uint32)
+            exp = _oracle_batch(oracle, buf, offs, lens, seeds)
+            assert (ctx.batch(buf, offs, lens, seeds) == exp).all(), n
+            zexp = _oracle_batch(oracle, buf, offs, lens, np.zeros(n, np.uint32))
+            want = zexp.copy()
+            flip = rng.integers(0, n)
+            want[flip] ^= 0x10
+            c, ok, nbad, rc = ctx.verify(buf, offs, lens, want)
+            assert (c == zexp).all() and nbad == 1 and rc == -1010 and int(np.argmin(ok)) == flip, n
+            pin = crc.PinnedBuffer(ctx, buf.size)
+            try:
+                pin.array[:] = buf
+                assert (ctx.batch(pin.array, offs, lens, seeds) == exp).all(), n
+            finally:
+                pin.free()
+        launches, files = ctx.resident_stats()
+        assert launches >= 1 and files == ring_files, (launches, files, ring_files)
+        ctx.set_resident(False)
+        buf, offs, lens = _random_batch(rng, 40, seed=77)
+        seeds = rng.integers(0, 2**32, 40).astype(np.uint32)
+        assert (ctx.batch(buf, offs, lens, seeds) == _oracle_batch(oracle, buf, offs, lens, seeds)).all()
+        assert ctx.resident_stats()[1] == files  # the ring was not used
+    finally:
+        ctx.close()
+
+
+def test_resident_idle_exit_and_relaunch(monkeypatch, oracle):
+    """The kernel leaves after its idle time; the next batch relaunches it."""
+    ctx = _ctx(monkeypatch, TFS_CRC_RESIDENT=1, TFS_CRC_RESIDENT_IDLE_US=50)
+    try:
+        rng = np.random.default_rng(32)
+        for it in range(12):
+            buf, offs, lens = _random_batch(rng, 4, seed=600 + it)
+            seeds = rng.integers(0, 2**32, 4).astype(np.uint32)
+            assert (ctx.batch(buf, offs, lens, seeds) == _oracle_batch(oracle, buf, offs, lens, seeds)).all(), it
+            time.sleep(0.003)
+        launches, files = ctx.resident_stats()
+        assert files == 48 and launches >= 6, (launches, files)
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("life_us", [10000, 300])
+def test_resident_concurrent_threads(monkeypatch, oracle, life_us):
+    """8 threads of synchronous verifies (1-8 files each, one wrong expected CRC per
+    call) in flight together; with a 300 us lifetime the kernel is relaunched many
+    times under load.  Every CRC and verdict of every call is checked."""
+    import tfs_amd.crc as crc
+    ctx = _ctx(monkeypatch, TFS_CRC_RESIDENT=1, TFS_CRC_RESIDENT_LIFE_US=life_us)
+    errors = []
+    nthreads, calls = 8, 150
+    try:
+        pins = [crc.PinnedBuffer(ctx, 8 * 65536 + 64) for _ in range(nthreads)]
+
+        def worker(t):
+            try:
+                rng = np.random.default_rng(1000 + t)
+                pin = pins[t]
+                for it in range(calls):
+                    n = int(rng.integers(1, 9))
+                    lens = rng.integers(0, 65536, n).astype(np.uint32)
+                    offs = np.arange(n, dtype=np.uint64) * 65536 + rng.integers(0, 8, n).astype(np.uint64)
+                    pin.array[:] = rng.integers(0, 256, pin.array.size, dtype=np.uint8)
+                    exp = _oracle_batch(oracle, pin.array, offs, lens, np.zeros(n, np.uint32))
+                    want = exp.copy()
+                    flip = it % n
+                    want[flip] ^= 1
+                    c, ok, nbad, rc = ctx.verify(pin.array, offs, lens, want)
+                    if not ((c == exp).all() and nbad == 1 and rc == -1010 and int(np.argmin(ok)) == flip):
+                        errors.append((t, it, n))
+                        return
+            except Exception as e:  # noqa: BLE001
+                errors.append((t, repr(e)))
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(nthreads)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        launches, files = ctx.resident_stats()
+        for p in pins:
+            p.free()
+    finally:
+        ctx.close()
+    assert not errors, errors[:5]
+    assert files > 0
+    if life_us == 300:
+        assert launches > 2, launches
+
+
+def test_resident_scalar_drop_in(oracle):
+    """tfs_crc32 (the Func::crc drop-in, default context) goes through the ring."""
+    import tfs_amd.crc as crc
+    rng = np.random.default_rng(33)
+    for it in range(300):
+        n = int(rng.integers(0, 70000))
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        s = int(rng.integers(0, 2**32))
+        assert crc.func_crc(s, d) == ocrc(oracle, s, d), it

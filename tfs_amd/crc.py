@@ -63,7 +63,8 @@ EXPORTED = [
     "tfs_crc32_memcpy", "tfs_crc32_memset_device", "tfs_crc32_event_create", "tfs_crc32_event_record",
     "tfs_crc32_event_elapsed_ms", "tfs_crc32_event_destroy",
     "tfs_crc32_stream", "tfs_crc32_sync", "tfs_crc32_stream_create", "tfs_crc32_stream_sync",
-    "tfs_crc32_stream_destroy", "tfs_crc32_inject_device_error",
+    "tfs_crc32_stream_destroy", "tfs_crc32_inject_device_error", "tfs_crc32_set_resident",
+    "tfs_crc32_resident_stats",
     "tfs_crc_group_create", "tfs_crc_group_destroy", "tfs_crc_group_last_error", "tfs_crc_group_size",
     "tfs_crc_group_ctx", "tfs_crc_group_member_of", "tfs_crc_group_ctx_for_block", "tfs_crc_group_numa_node",
     "tfs_crc_group_member_bound", "tfs_crc_group_host_malloc", "tfs_crc_group_host_free",
@@ -140,6 +141,9 @@ def lib():
             "tfs_crc32_stream_sync": (ctypes.c_int, [vp, vp]),
             "tfs_crc32_stream_destroy": (ctypes.c_int, [vp, vp]),
             "tfs_crc32_inject_device_error": (ctypes.c_int, [vp, u32, u32]),
+            "tfs_crc32_set_resident": (ctypes.c_int, [vp, ctypes.c_int]),
+            "tfs_crc32_resident_stats": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64),
+                                                        ctypes.POINTER(ctypes.c_uint64)]),
             "tfs_crc_group_create": (ctypes.c_int, [vp, u32, ctypes.POINTER(vp)]),
             "tfs_crc_group_destroy": (ctypes.c_int, [vp]),
             "tfs_crc_group_last_error": (ctypes.c_char_p, [vp]),
@@ -250,6 +254,16 @@ class Context:
     def inject_device_error(self, skip=0, count=1):
         """Fault injection: the next `count` host submissions after `skip` fail with -20001."""
         self._check(lib().tfs_crc32_inject_device_error(self.handle, skip, count), "inject_device_error")
+
+    def set_resident(self, on):
+        """Small synchronous batches through the resident kernel (on) or a launch each (off)."""
+        self._check(lib().tfs_crc32_set_resident(self.handle, 1 if on else 0), "set_resident")
+
+    def resident_stats(self):
+        """(launches of the resident kernel, files taken through its ring) so far."""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(lib().tfs_crc32_resident_stats(self.handle, ctypes.byref(a), ctypes.byref(b)), "resident_stats")
+        return a.value, b.value
 
     def stream_create(self):
         p = ctypes.c_void_p()

@@ -54,6 +54,8 @@ hipError_t launch_write_packet_headers(uint8_t* base, const uint64_t* rec_off, c
                                        int32_t pcode, int32_t version, uint64_t first_id, hipStream_t stream);
 hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, uint32_t n, uint64_t nbytes,
                            uint32_t* out, unsigned grid, hipStream_t stream);
+hipError_t launch_resident(const Tables* tg, const ResHost* hs, uint32_t* dstate, unsigned grid, uint32_t idle_ticks,
+                           uint32_t life_ticks, uint32_t gen, hipStream_t stream);
 }  // namespace tfscrc
 
 static_assert(sizeof(tfs_crc_desc) == 16 && sizeof(tfs_crc_vdesc) == 16, "descriptor ABI");
@@ -116,14 +118,17 @@ struct PinBuf {
 struct Slot {
   DevBuf d_data, d_desc, d_crc, d_ok, d_bad, d_aux;
   PinBuf h_data, h_crc, h_ok, h_bad, h_desc, h_flag;
+  PinBuf h_res;  // resident form: one {crc, seq} result word per file
   hipEvent_t done = nullptr;
   bool busy = false;
   uint64_t ticket = 0;
   int status = TFS_SUCCESS;
   bool count_bad = false;  // zero-copy launch: n_bad is counted from h_ok
   bool spin = false;       // zero-copy launch: completion = h_flag reaching `seq`
+  bool resident = false;   // posted to the resident kernel's ring (no launch, no s.done)
+  uint32_t res_first = 0;  // ... as units [res_first, res_first + n)
   uint32_t seq = 0;
-  Slot() { h_crc.coherent = h_ok.coherent = h_bad.coherent = h_flag.coherent = true; }
+  Slot() { h_crc.coherent = h_ok.coherent = h_bad.coherent = h_flag.coherent = h_res.coherent = true; }
   // user outputs for the async path
   uint32_t n = 0;
   uint32_t* out_crc = nullptr;
@@ -132,6 +137,7 @@ struct Slot {
   void release() {
     d_data.release(); d_desc.release(); d_crc.release(); d_ok.release(); d_bad.release(); d_aux.release();
     h_data.release(); h_crc.release(); h_ok.release(); h_bad.release(); h_desc.release(); h_flag.release();
+    h_res.release();
     if (done) (void)hipEventDestroy(done);
     done = nullptr;
   }
@@ -192,6 +198,21 @@ struct tfs_crc_ctx {
   std::atomic<uint32_t> inject_skip{0}, inject_count{0};  // tfs_crc32_inject_device_error
   DevBuf packet_scratch;  // device-resident packet calls (parse descriptors, verdicts)
   hipStream_t packet_scratch_stream = nullptr;
+  // Resident form for the synchronous zero-copy batches of at
+  // most kWgMaxFiles files: ring in page-locked fine-grained memory, device
+  // cursor/counters, its own stream.  All fields under `mu`.
+  bool resident = true;  // TFS_CRC_RESIDENT=0 launches every batch instead
+  unsigned res_grid = 16;  // workgroups of the resident kernel (TFS_CRC_RESIDENT_WGS)
+  uint32_t res_idle_us = 200, res_life_us = 10000;  // TFS_CRC_RESIDENT_IDLE_US / _LIFE_US
+  ResHost* res_host = nullptr;
+  ResHost* res_host_d = nullptr;  // its device-visible address
+  uint32_t* res_state = nullptr;
+  hipStream_t res_stream = nullptr;
+  hipEvent_t res_event = nullptr;
+  bool res_running = false;  // a launch was made and res_event recorded behind it
+  uint32_t res_published = 0;
+  uint32_t res_idle_ticks = 0, res_life_ticks = 0;
+  uint64_t res_launches = 0, res_files = 0;
 };
 
 namespace {
@@ -318,6 +339,133 @@ int wait_flag(tfs_crc_ctx* ctx, Slot& s) {
   return TFS_SUCCESS;
 }
 
+// ---- resident form -------------------------------------------------------------
+// (Caller holds ctx->mu.)  Ring, device state, stream and event, made on first use.
+int resident_setup(tfs_crc_ctx* ctx) {
+  if (ctx->res_host) return TFS_SUCCESS;
+  int khz = 0;
+  HIP_TRY(ctx, hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device));
+  if (khz <= 0) khz = 100000;
+  ctx->res_idle_ticks = uint32_t(uint64_t(ctx->res_idle_us) * uint64_t(khz) / 1000u);
+  ctx->res_life_ticks = uint32_t(std::min<uint64_t>(uint64_t(ctx->res_life_us) * uint64_t(khz) / 1000u, 0x7fffffffu));
+  void* h = nullptr;
+  HIP_TRY(ctx, hipHostMalloc(&h, sizeof(ResHost), hipHostMallocCoherent | hipHostMallocMapped));
+  memset(h, 0, sizeof(ResHost));
+  void* hd = nullptr;
+  if (hipHostGetDevicePointer(&hd, h, 0) != hipSuccess) {
+    (void)hipHostFree(h);
+    return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "resident ring: hipHostGetDevicePointer failed");
+  }
+  void* st = nullptr;
+  if (hipMalloc(&st, kResStateBytes) != hipSuccess || hipMemset(st, 0, kResStateBytes) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->res_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->res_event, hipEventDisableTiming) != hipSuccess) {
+    (void)hipHostFree(h);
+    if (st) (void)hipFree(st);
+    return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "resident ring: device state allocation failed");
+  }
+  ctx->res_host = static_cast<ResHost*>(h);
+  ctx->res_host_d = static_cast<ResHost*>(hd);
+  ctx->res_state = static_cast<uint32_t*>(st);
+  ctx->res_published = 0;
+  return TFS_SUCCESS;
+}
+
+// (Caller holds ctx->mu.)  Launch the resident kernel unless one is running.
+// Only one is ever in flight: a new one is launched only after the event behind
+// the previous one has completed, i.e. every workgroup of it has left.
+int resident_ensure_running(tfs_crc_ctx* ctx) {
+  if (ctx->res_running) {
+    const hipError_t e = hipEventQuery(ctx->res_event);
+    if (e == hipErrorNotReady) return TFS_SUCCESS;
+    if (e != hipSuccess) return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "resident kernel failed: %s", hipGetErrorString(e));
+    ctx->res_running = false;
+  }
+  HIP_TRY(ctx, launch_resident(ctx->d_tables, ctx->res_host_d, ctx->res_state, ctx->res_grid, ctx->res_idle_ticks,
+                               ctx->res_life_ticks, uint32_t(ctx->res_launches + 1u), ctx->res_stream));
+  HIP_TRY(ctx, hipEventRecord(ctx->res_event, ctx->res_stream));
+  ctx->res_running = true;
+  ++ctx->res_launches;
+  return TFS_SUCCESS;
+}
+
+// (Caller holds ctx->mu.)  Post a zero-copy batch (device-visible base `zb`)
+// as units [P, P + n), one per file, each with its result word in s.h_res; then
+// `published`; the kernel is (re)launched if gone.  Returns 1 (nothing posted)
+// when the ring has no room: a unit of a batch still outstanding would be
+// rewritten.
+int resident_post(tfs_crc_ctx* ctx, Slot& s, int mode, const uint8_t* zb, const Desc* d, uint32_t n) {
+  if (const int rc = resident_setup(ctx)) return rc;
+  ResHost* H = ctx->res_host;
+  const uint32_t P = ctx->res_published;
+  for (const Slot& x : ctx->sync_slots)
+    if (&x != &s && x.busy && x.resident && int32_t(P + n - kResUnits - x.res_first) > 0) return 1;
+  HIP_TRY(ctx, s.h_res.reserve(size_t(n) * 8));
+  void* zres = nullptr;
+  HIP_TRY(ctx, hipHostGetDevicePointer(&zres, s.h_res.p, 0));
+  for (uint32_t i = 0; i < n; ++i) {
+    ResUnit& u = H->units[(P + i) % kResUnits];
+    u.addr = uint64_t(reinterpret_cast<uintptr_t>(zb + d[i].offset));
+    u.out = uint64_t(reinterpret_cast<uintptr_t>(zres)) + 8u * i;
+    u.len = d[i].len;
+    u.seed = mode == 0 ? d[i].aux : 0u;
+    u.seq = s.seq;
+    u.reserved = 0;
+  }
+  s.res_first = P;
+  ctx->res_published = P + n;
+  ctx->res_files += n;
+  __atomic_store_n(&H->published, uint64_t(ctx->res_published), __ATOMIC_RELEASE);
+  return resident_ensure_running(ctx);
+}
+
+// Completion of a resident batch: spin until every file's result word carries
+// this batch's seq; now and then check that the kernel is still there, and
+// relaunch it (under mu) when it left with this batch outstanding (idle or
+// lifetime exit racing the post).  Then the CRCs and verdicts go where
+// finish_slot reads them (the expected CRCs are in s.h_desc).
+int wait_resident(tfs_crc_ctx* ctx, Slot& s, int mode, uint32_t n) {
+  const volatile uint64_t* res = static_cast<const volatile uint64_t*>(s.h_res.p);
+  uint32_t i = 0, relaunches = 0;
+  for (uint32_t spins = 1;; ++spins) {
+    while (i < n && uint32_t(res[i] >> 32) == s.seq) ++i;
+    if (i == n) break;
+    __builtin_ia32_pause();
+    if ((spins & 255u) == 0) {
+      const hipError_t e = hipEventQuery(ctx->res_event);
+      if (e == hipErrorNotReady) continue;
+      std::lock_guard<std::mutex> g(ctx->mu);
+      const uint64_t before = ctx->res_launches;
+      if (const int rc = resident_ensure_running(ctx)) return rc;
+      if (ctx->res_launches != before && ++relaunches > 100000u)
+        return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "resident kernel makes no progress (seq %u)", s.seq);
+    }
+  }
+  uint32_t* crc = static_cast<uint32_t*>(s.h_crc.p);
+  uint8_t* ok = static_cast<uint8_t*>(s.h_ok.p);
+  const Desc* d = static_cast<const Desc*>(s.h_desc.p);
+  for (uint32_t k = 0; k < n; ++k) {
+    crc[k] = uint32_t(res[k]);
+    if (mode == 1) ok[k] = crc[k] == d[k].aux ? 1 : 0;
+  }
+  return TFS_SUCCESS;
+}
+
+// (Caller holds no lock.)  Stop the resident kernel and free its ring.
+void resident_teardown(tfs_crc_ctx* ctx) {
+  if (!ctx->res_host) return;
+  __atomic_store_n(&ctx->res_host->published, uint64_t(ctx->res_published) | (uint64_t(1) << 32), __ATOMIC_RELEASE);
+  if (ctx->res_stream) (void)hipStreamSynchronize(ctx->res_stream);
+  if (ctx->res_event) (void)hipEventDestroy(ctx->res_event);
+  if (ctx->res_stream) (void)hipStreamDestroy(ctx->res_stream);
+  if (ctx->res_state) (void)hipFree(ctx->res_state);
+  (void)hipHostFree(ctx->res_host);
+  ctx->res_host = ctx->res_host_d = nullptr;
+  ctx->res_state = nullptr;
+  ctx->res_stream = nullptr;
+  ctx->res_event = nullptr;
+}
+
 // An armed tfs_crc32_inject_device_error: this submission fails as a device error would.
 int injected_fault(tfs_crc_ctx* ctx) {
   if (ctx->inject_count.load() == 0) return TFS_SUCCESS;
@@ -338,9 +486,12 @@ Slot* free_slot(tfs_crc_ctx* ctx) {
 }
 
 // Enqueue a host-memory batch on slot s (mode 0 compute, 1 verify).  Outputs
-// land in the slot's pinned buffers when s.done fires.
+// land in the slot's pinned buffers when s.done fires (or, s.spin, when the
+// completion flag reaches s.seq).  `job` >= 0: a synchronous slot whose small
+// zero-copy batch may go to the resident kernel as that job slot.
 int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint32_t n, const void* base,
-                       uint64_t base_len) {
+                       uint64_t base_len, int job = -1) {
+  s.resident = false;
   if (const int f = injected_fault(ctx)) return f;
   uint64_t lo = 0, hi = 0;
   const Desc* dd = static_cast<const Desc*>(d);
@@ -377,10 +528,21 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
         hipHostGetDevicePointer(&zcrc, s.h_crc.p, 0) == hipSuccess &&
         hipHostGetDevicePointer(&zok, s.h_ok.p, 0) == hipSuccess &&
         hipHostGetDevicePointer(&zflag, s.h_flag.p, 0) == hipSuccess) {
-      uint32_t* sched = nullptr;
-      HIP_TRY(ctx, sched_slot(ctx, ctx->stream, &sched));
       s.seq = ctx->flag_seq.fetch_add(1) + 1u;
       if (s.seq == 0) s.seq = ctx->flag_seq.fetch_add(1) + 1u;  // 0 is the flag's initial value
+      if (job >= 0 && ctx->resident && ctx->variant == 0 && n <= kWgMaxFiles) {
+        const int rc = resident_post(ctx, s, mode, static_cast<const uint8_t*>(zb) - lo, static_cast<const Desc*>(d), n);
+        if (rc < 0) return rc;
+        if (rc == 0) {
+          s.count_bad = true;
+          s.spin = true;
+          s.resident = true;
+          return TFS_SUCCESS;
+        }
+        // no room in the ring: launch this batch
+      }
+      uint32_t* sched = nullptr;
+      HIP_TRY(ctx, sched_slot(ctx, ctx->stream, &sched));
       // n_bad is counted from the verdicts on the host (no atomics on host memory)
       HIP_TRY(ctx, launch_crc_files(mode, static_cast<const uint8_t*>(zb) - lo, static_cast<const Desc*>(zd), n,
                                     ctx->d_tables, static_cast<uint32_t*>(zcrc), static_cast<uint8_t*>(zok), nullptr,
@@ -419,7 +581,7 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
 int finish_slot(tfs_crc_ctx* ctx, Slot& s, int mode, uint32_t n, uint32_t* out_crc, uint8_t* out_ok,
                 uint32_t* n_bad) {
   if (s.spin) {
-    const int rc = wait_flag(ctx, s);
+    const int rc = s.resident ? wait_resident(ctx, s, mode, n) : wait_flag(ctx, s);
     if (rc) return rc;
   } else {
     HIP_TRY(ctx, hipEventSynchronize(s.done));
@@ -479,6 +641,10 @@ int tfs_crc32_ctx_create(int device, tfs_crc_ctx** out) {
   ctx->device = device;
   if (const char* v = getenv("TFS_CRC_VARIANT")) ctx->variant = atoi(v);
   if (const char* v = getenv("TFS_CRC_COMPACT_SLOTS")) ctx->compact_slots = std::min(std::max(atoi(v), 1), kCompactSlots);
+  if (const char* v = getenv("TFS_CRC_RESIDENT")) ctx->resident = atoi(v) != 0;
+  if (const char* v = getenv("TFS_CRC_RESIDENT_WGS")) ctx->res_grid = unsigned(std::min(std::max(atoi(v), 1), 256));
+  if (const char* v = getenv("TFS_CRC_RESIDENT_IDLE_US")) ctx->res_idle_us = uint32_t(std::min(std::max(atoi(v), 1), 1000000));
+  if (const char* v = getenv("TFS_CRC_RESIDENT_LIFE_US")) ctx->res_life_us = uint32_t(std::min(std::max(atoi(v), 1), 10000000));
   int rc = TFS_SUCCESS;
   do {
     hipError_t e = hipSetDevice(device);
@@ -511,6 +677,7 @@ int tfs_crc32_ctx_create(int device, tfs_crc_ctx** out) {
 int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx) {
   if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
   if (ctx->device >= 0) (void)hipSetDevice(ctx->device);
+  resident_teardown(ctx);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   for (auto& s : ctx->slots) s.release();
   for (auto& s : ctx->sync_slots) s.release();
@@ -557,7 +724,7 @@ int sync_host_call(tfs_crc_ctx* ctx, int mode, const void* d, uint32_t n, const 
       ctx->sync_cv.wait(lk);
     }
     s->busy = true;
-    const int rc = enqueue_host_batch(ctx, *s, mode, d, n, base, base_len);
+    const int rc = enqueue_host_batch(ctx, *s, mode, d, n, base, base_len, int(s - ctx->sync_slots));
     if (rc) {
       s->busy = false;
       ctx->sync_cv.notify_one();
@@ -1264,6 +1431,21 @@ int tfs_crc32_inject_device_error(tfs_crc_ctx* ctx, uint32_t skip, uint32_t coun
   ctx->inject_count = 0;
   ctx->inject_skip = skip;
   ctx->inject_count = count;
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_set_resident(tfs_crc_ctx* ctx, int on) {
+  if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  ctx->resident = on != 0;
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_resident_stats(tfs_crc_ctx* ctx, uint64_t* launches, uint64_t* files) {
+  if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (launches) *launches = ctx->res_launches;
+  if (files) *files = ctx->res_files;
   return TFS_SUCCESS;
 }
 

@@ -57,6 +57,34 @@ constexpr uint32_t kWgJumpOff = 4u * 256u * 32u * 4u;             // after the r
 constexpr uint32_t kWgLevelOff = kWgJumpOff + 1024u;
 constexpr uint32_t kWgLdsBytes = kWgLevelOff + uint32_t(kWgLevels) * 1024u;  // 140 KiB
 
+// Resident form (small synchronous host batches without a launch per batch):
+// the host appends one ResUnit per file to ResHost, in page-locked fine-grained
+// memory the kernel reads over PCIe, and bumps `published`.  Unit u belongs to
+// workgroup u % grid (no claiming); each workgroup keeps the count of units it
+// has done on its own device line across launches.  A file's result is one
+// 8-byte store {crc, seq << 32} into the batch's page-locked result words, which
+// the host spins on -- no counters, no flag.  A unit is never rewritten before
+// its file is done: the host posts units [P, P + n) only while
+// P + n - kResUnits <= the first unit of every batch still outstanding
+// (tfs_crc_abi.cpp resident_post), otherwise it launches instead.
+constexpr uint32_t kResUnits = 4096;            // ring of units
+constexpr uint32_t kResMaxGrid = 256;           // workgroups of the resident kernel, at most
+constexpr uint32_t kResExitLine = kResMaxGrid * kSchedStride;  // dstate: generation of the launch that is leaving
+constexpr uint32_t kResStateBytes = (kResMaxGrid + 1u) * kSchedStride * 4u;  // a line per workgroup + the exit line
+constexpr uint32_t kResMaxPolls = 1u << 22;     // hard bound on one workgroup's idle polls
+struct ResUnit {         // one file
+  uint64_t addr;         // device-visible address of its first byte
+  uint64_t out;          // device-visible address of its result word
+  uint32_t len, seed;    // seed 0 for a verify (the host compares)
+  uint32_t seq, reserved;
+};
+struct ResHost {
+  uint64_t published;    // low 32 bits: units published (wrapping); high 32 bits: stop
+  uint64_t pad[31];
+  ResUnit units[kResUnits];
+};
+static_assert(sizeof(ResUnit) == 32, "resident ring layout");
+
 // TFS status codes (src/common/error_msg.h)
 constexpr int32_t kSuccess = 0;
 constexpr int32_t kExitCheckCrcError = -1010;

@@ -799,38 +799,25 @@ __device__ __forceinline__ uintptr_t wg_run_addr(const FileGeo<16>& g, uint32_t 
   return (s >= 1u && s < g.nstripes ? g.sb0 + uintptr_t(s) * 1024u : junk) + uintptr_t(lane) * 16u;
 }
 
-template <int MODE>
-__global__ void __launch_bounds__(kBlock) crc_wg_kernel(const uint8_t* __restrict__ base,
-                                                        const Desc* __restrict__ desc, uint32_t n,
-                                                        const Tables* __restrict__ tg, uint32_t* out_crc,
-                                                        uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched,
-                                                        uint32_t vseed, uint32_t* done_flag, uint32_t seq) {
-  __shared__ uint32_t lds_tables[kWgLdsBytes / 4];
-  __shared__ uint32_t part[kWgWaves];
-  const int lane = threadIdx.x & (kWave - 1);
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const LaneBase lb = lane_base_of(lane);
-  const uintptr_t junk = reinterpret_cast<uintptr_t>(tg->slice);
-  uint32_t f = blockIdx.x;
-  Desc cur{0, 0, 0};
-  FileGeo<16> g{};
-  Head<16> h{};
-  uint4 buf[kWgPF];
-  // Issue a file's loads: descriptor, then (wave 0) the head stripe and tail
-  // words, and this wave's first kWgPF stripes.
-  auto issue = [&](uint32_t ff) {
-    cur = desc[ff];
-    g = make_geo<16>(base + cur.offset, cur.len, MODE == 0 ? cur.aux : vseed);
-    if (wave == 0) h = load_head<16>(g, lane);
+// Issue one file's loads for the latency form: (wave 0) the head stripe and tail
+// words, and this wave's first kWgPF stripes.
+__device__ __forceinline__ void wg_issue(const FileGeo<16>& g, Head<16>& h, uint4 (&buf)[kWgPF], uint32_t wave, int lane,
+                                         uintptr_t junk) {
+  if (wave == 0) h = load_head<16>(g, lane);
 #pragma unroll
-    for (int k = 0; k < kWgPF; ++k) buf[k] = ld128s<true>(wg_run_addr(g, wave + 16u * uint32_t(k), lane, junk));
-  };
-  // The first file's loads are in flight while the tables are staged.
-  if (f < n) issue(f);
-  load_wg_tables(lds_tables, tg);
-  __syncthreads();
-  uint32_t bad = 0;
-  while (f < n) {
+  for (int k = 0; k < kWgPF; ++k) buf[k] = ld128s<true>(wg_run_addr(g, wave + 16u * uint32_t(k), lane, junk));
+}
+
+// One file by the whole workgroup (its loads issued by wg_issue): wave w's lane
+// chains over stripes w, w+16, ..., moved to the end of the body, reduced in
+// the wave and across waves through `part`.  The CRC is returned in wave 0
+// (undefined in the other waves); `part` must not be rewritten before the
+// caller's next __syncthreads.
+__device__ __forceinline__ uint32_t wg_file_crc(const uint32_t* lds_tables, uint32_t* part, const LaneBase& lb,
+                                                const FileGeo<16>& g, const Head<16>& h, uint4 (&buf)[kWgPF],
+                                                uint32_t wave, int lane, uintptr_t junk) {
+  uint32_t crc = 0;
+  {
     // ---- this wave's lane chains over stripes wave, wave+16, ...
     const uint32_t K = g.nstripes > wave ? (g.nstripes - 1u - wave) / 16u + 1u : 0u;
     const uint32_t last = g.nstripes - 1u;
@@ -882,7 +869,6 @@ __global__ void __launch_bounds__(kBlock) crc_wg_kernel(const uint8_t* __restric
     if (lane == 0) part[wave] = c;
     __syncthreads();
     if (wave == 0) {
-      uint32_t crc;
       if (g.nstripes == 0) {  // tiny (< kMinParallelLen): the byte loop of func.cpp:429-433
         crc = g.seed;
         for (uint32_t i = 0; i < g.len; ++i) crc = step1(lds_tables, lb, crc, ld8(g.start + i));
@@ -899,13 +885,46 @@ __global__ void __launch_bounds__(kBlock) crc_wg_kernel(const uint8_t* __restric
         for (int i = 0; i < 3; ++i)
           if (uint32_t(i) < ntb) crc = step1(lds_tables, lb, crc, h.tb[i]);
       }
-      if (lane == 0) {
-        if (out_crc) out_crc[f] = crc;
-        if (MODE == 1) {
-          const bool ok = crc == cur.aux;
-          if (out_ok) out_ok[f] = ok ? 1 : 0;
-          bad += ok ? 0u : 1u;
-        }
+    }
+  }
+  return crc;
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(kBlock) crc_wg_kernel(const uint8_t* __restrict__ base,
+                                                        const Desc* __restrict__ desc, uint32_t n,
+                                                        const Tables* __restrict__ tg, uint32_t* out_crc,
+                                                        uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched,
+                                                        uint32_t vseed, uint32_t* done_flag, uint32_t seq) {
+  __shared__ uint32_t lds_tables[kWgLdsBytes / 4];
+  __shared__ uint32_t part[kWgWaves];
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const LaneBase lb = lane_base_of(lane);
+  const uintptr_t junk = reinterpret_cast<uintptr_t>(tg->slice);
+  uint32_t f = blockIdx.x;
+  Desc cur{0, 0, 0};
+  FileGeo<16> g{};
+  Head<16> h{};
+  uint4 buf[kWgPF];
+  auto issue = [&](uint32_t ff) {
+    cur = desc[ff];
+    g = make_geo<16>(base + cur.offset, cur.len, MODE == 0 ? cur.aux : vseed);
+    wg_issue(g, h, buf, wave, lane, junk);
+  };
+  // The first file's loads are in flight while the tables are staged.
+  if (f < n) issue(f);
+  load_wg_tables(lds_tables, tg);
+  __syncthreads();
+  uint32_t bad = 0;
+  while (f < n) {
+    const uint32_t crc = wg_file_crc(lds_tables, part, lb, g, h, buf, wave, lane, junk);
+    if (wave == 0 && lane == 0) {
+      if (out_crc) out_crc[f] = crc;
+      if (MODE == 1) {
+        const bool ok = crc == cur.aux;
+        if (out_ok) out_ok[f] = ok ? 1 : 0;
+        bad += ok ? 0u : 1u;
       }
     }
     f += gridDim.x;
@@ -916,6 +935,96 @@ __global__ void __launch_bounds__(kBlock) crc_wg_kernel(const uint8_t* __restric
     if (MODE == 1 && bad && n_bad) atomicAdd(n_bad, bad);
     launch_exit(sched, gridDim.x, done_flag, seq);
   }
+}
+
+// ---------------------------------------------------------------------------
+// Resident form: the latency form's workgroup-per-file body in
+// a kernel that stays on the GPU and takes files from a page-locked ring that
+// the host appends to (ResHost), so a close batch costs no launch.  Unit u is
+// workgroup (u % grid)'s: thread 0 polls `published` (the host's count of
+// units, over PCIe) until its next unit is there, reads it (32 bytes, one round
+// trip) and the workgroup CRCs the file; thread 0 stores {crc, seq} as one
+// 8-byte system-scope store into the file's result word, which the host spins
+// on.  The kernel leaves when `published` has not moved for `idle_ticks` of the
+// 100 MHz wall clock, after `life_ticks` in all, when the host sets `stop`, or
+// after kResMaxPolls polls: the first workgroup to decide so stores the launch's
+// generation into the exit line, and the others, which poll it, follow at once
+// (so a unit posted to a workgroup that has left waits for a relaunch, not for
+// the others' timers).  Each workgroup saves its count of units done for the
+// next launch; the host relaunches the kernel when it finds it gone with work
+// pending.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t ld_sys64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void __launch_bounds__(kBlock) crc_resident_kernel(const Tables* __restrict__ tg, const ResHost* hs,
+                                                              uint32_t* dstate, uint32_t idle_ticks,
+                                                              uint32_t life_ticks, uint32_t gen) {
+  __shared__ uint32_t lds_tables[kWgLdsBytes / 4];
+  __shared__ uint32_t part[kWgWaves];
+  __shared__ uint64_t claim[4];  // go, then the unit's addr, out, len | seed << 32 (seq kept by thread 0)
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const LaneBase lb = lane_base_of(lane);
+  const uintptr_t junk = reinterpret_cast<uintptr_t>(tg->slice);
+  uint32_t* mine = &dstate[blockIdx.x * kSchedStride];
+  uint32_t done = 0, seq = 0;  // thread 0: units this workgroup has done (all launches)
+  if (threadIdx.x == 0) done = __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  load_wg_tables(lds_tables, tg);
+  const uint64_t t0 = wall_clock64();
+  uint64_t last = t0;
+  uint32_t seen = 0;  // thread 0: `published` when last looked
+  if (threadIdx.x == 0) seen = uint32_t(ld_sys64(&hs->published));
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const uint32_t want = blockIdx.x + done * gridDim.x;  // this workgroup's next unit
+      uint32_t go = 0;
+      for (uint32_t it = 0;; ++it) {
+        const uint64_t ps = ld_sys64(&hs->published);  // published | stop << 32
+        if (int32_t(uint32_t(ps) - want) > 0) {
+          go = 1;
+          break;
+        }
+        if (__hip_atomic_load(&dstate[kResExitLine], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) break;
+        const uint64_t now = wall_clock64();
+        if (uint32_t(ps) != seen) {  // units posted (to any workgroup): not idle
+          seen = uint32_t(ps);
+          last = now;
+        }
+        if (uint32_t(ps >> 32) || now - last > idle_ticks || now - t0 > life_ticks || it >= kResMaxPolls) {
+          __hip_atomic_store(&dstate[kResExitLine], gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (go) {
+        const uint64_t* u = reinterpret_cast<const uint64_t*>(&hs->units[want % kResUnits]);
+        claim[1] = ld_sys64(u);
+        claim[2] = ld_sys64(u + 1);
+        claim[3] = ld_sys64(u + 2);
+        seq = uint32_t(ld_sys64(u + 3));
+        ++done;
+      }
+      claim[0] = go;
+    }
+    __syncthreads();
+    if (!claim[0]) break;
+    // The payload sits in page-locked memory the host rewrote since this
+    // workgroup last looked: drop stale cached lines, as a launch would.
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    const FileGeo<16> g = make_geo<16>(reinterpret_cast<const uint8_t*>(uintptr_t(claim[1])), uint32_t(claim[3]),
+                                       uint32_t(claim[3] >> 32));
+    Head<16> h{};
+    uint4 buf[kWgPF];
+    wg_issue(g, h, buf, wave, lane, junk);
+    const uint32_t crc = wg_file_crc(lds_tables, part, lb, g, h, buf, wave, lane, junk);
+    if (threadIdx.x == 0)
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(uintptr_t(claim[2])), uint64_t(crc) | uint64_t(seq) << 32,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();  // claim[] and part[] are rewritten for the next file
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(mine, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // The FileInfo fields the checks need (id_ +0, size_ +12, crc_ +32), read from a
@@ -1679,6 +1788,13 @@ hipError_t launch_crc_files(int mode, const uint8_t* base, const Desc* desc, uin
   if (mode == 0)
     return launch_variant<0>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, sched, stream, vseed, done_flag, seq);
   return launch_variant<1>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, sched, stream, vseed, done_flag, seq);
+}
+
+hipError_t launch_resident(const Tables* tg, const ResHost* hs, uint32_t* dstate, unsigned grid, uint32_t idle_ticks,
+                           uint32_t life_ticks, uint32_t gen, hipStream_t stream) {
+  hipLaunchKernelGGL(crc_resident_kernel, dim3(grid), dim3(kBlock), 0, stream, tg, hs, dstate, idle_ticks, life_ticks,
+                     gen);
+  return hipGetLastError();
 }
 
 hipError_t launch_packet_parse(const uint8_t* base, const PacketDesc* pd, uint32_t n, int mode, Desc* desc,
