@@ -1665,10 +1665,11 @@ def bench_loopback(args):
     pool = ds.BlockImagePool(ctx, 2, n * (L + FILEINFO) + 4096)
 
     # One CloseBatcher per thread count, created once (DataService::initialize).
-    # Batches of about half the closing threads (8 of 64): several batches are in
-    # flight at once, their round trips overlapping (tools/loopback_probe.py,
-    # profiles/r02/loopback_probe.json).
-    close_batch = {8: 4, 64: 8}
+    # Batches of a quarter of the closing threads (2 of 8, 4 of 64): several
+    # batches are in flight at once, their round trips overlapping; with the
+    # resident kernel a batch costs no launch, so smaller batches pay
+    # (tools/loopback_probe.py, profiles/r02/resident/loopback_probe.json).
+    close_batch = {8: 2, 64: 4}
     batchers = {t: ds.CloseBatcher(ctx, max_batch=b, max_wait_us=100) for t, b in close_batch.items()}
 
     def gpu_once(threads=8):

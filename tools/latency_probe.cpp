@@ -9,6 +9,7 @@
 #include <cstring>
 #include <functional>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../include/tfs_crc.h"
@@ -91,6 +92,31 @@ int main(int argc, char** argv) {
     tfs_crc32_batch(ctx, &d, 1, pageable.data(), 4, &tiny.expected);
   }
   run("verify_pinned_4B", [&] { return tfs_crc32_verify(ctx, &tiny, 1, pinned, 4, nullptr, ok.data(), &nbad); });
+  // A call after 1 ms without work: the resident kernel has left (idle exit)
+  // and is relaunched by this call.
+  {
+    std::vector<double> us;
+    int bad = 0;
+    for (int i = 0; i < iters / 4; ++i) {
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      const auto t0 = std::chrono::steady_clock::now();
+      bad |= tfs_crc32_verify(ctx, vd.data(), 1, pinned, size_t(kMax) * kFile, crc.data(), ok.data(), &nbad);
+      const auto t1 = std::chrono::steady_clock::now();
+      us.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
+    }
+    char b[256];
+    snprintf(b, sizeof b, ", \"verify_pinned_n1_after_1ms_idle\": {\"p50_us\": %.1f, \"p99_us\": %.1f, \"status\": %d}",
+             pct(us, 0.5), pct(us, 0.99), bad);
+    out += b;
+  }
+  uint64_t launches = 0, files = 0;
+  tfs_crc32_resident_stats(ctx, &launches, &files);
+  {
+    char b[160];
+    snprintf(b, sizeof b, ", \"resident\": {\"launches\": %llu, \"files\": %llu}", (unsigned long long)launches,
+             (unsigned long long)files);
+    out += b;
+  }
   out += "}";
   printf("%s\n", out.c_str());
   tfs_crc32_host_free_pinned(ctx, pinned);

@@ -29,7 +29,7 @@ def main():
     pay = synth_bytes(0x9E3779B97F4A7C15, n * L)
     client = ctx.batch(pay, np.arange(n, dtype=np.uint64) * L, np.full(n, L, np.uint32))
     pool = ds.BlockImagePool(ctx, 2, n * (L + 36) + 4096)
-    cases = [(8, 8), (8, 4), (8, 3), (64, 16), (64, 8), (64, 4)]
+    cases = [(8, 8), (8, 4), (8, 2), (8, 1), (64, 16), (64, 8), (64, 4), (64, 2)]
     batchers = {c: ds.CloseBatcher(ctx, max_batch=c[1], max_wait_us=100) for c in cases}
     times = {"%d_threads_batch_%d" % c: [] for c in cases}
     for _ in range(2):  # warm-up
