@@ -96,3 +96,11 @@ def test_block_verify_device_and_loopback_lines():
     for k in ("scalar_tfs_crc32_64KiB", "close_1_leases", "close_8_leases", "close_64_leases"):
         assert 0 < lb["latency"][k]["p50_us"] <= lb["latency"][k]["p99_us"], k
     assert lb["cpu_baseline"]["allcore"]["value"] > 0
+
+
+@pytest.mark.gpu
+def test_compact_files_line():
+    c = _run(["--workload", "compact_files", "--file-blocks", "2", "--cpu-seconds", "0.5"])
+    assert c["value"] > 0 and c["source_block_GiBs"] > c["value"]
+    assert c["roofline"]["bound"] == "host-io" and 0 < c["roofline"]["frac"]
+    assert c["cpu_baseline"]["value"] > 0 and c["cpu_baseline"]["kind"] == "port"

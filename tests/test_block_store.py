@@ -262,3 +262,51 @@ def test_gpu_compact_block_files(ds, oracle, gpu_ctx, tmp_path, windows_per_laun
     ids = list(out.metas["file_id"])
     assert rc2 == 2 and st2[ids.index(bad_id)] == -1010 and st2[ids.index(6)] == -8034
     assert int((st2 != 0).sum()) == 2
+
+
+@pytest.mark.gpu
+def test_gpu_compactor_reused_across_blocks(ds, oracle, gpu_ctx, tmp_path):
+    """One BlockFileCompactor (window buffers and streams kept) compacts three
+    different blocks in turn, one of them with a file over a window and one with
+    a corrupted payload; each new block equals the oracle's real_compact of its
+    source, and a failed call (missing source) leaves the compactor usable."""
+    from test_gpu_parity import _oracle_compact
+    main_size, ext_size = 16 * MiB, 8 * MiB
+    src, dst = str(tmp_path / "src"), str(tmp_path / "dst")
+    comp = ds.BlockFileCompactor(gpu_ctx, windows_per_launch=2)
+    rng = np.random.default_rng(99)
+    try:
+        for k in range(3):
+            sizes = [int(x) for x in rng.integers(0, 200_000, 90 + 20 * k)]
+            if k == 1:
+                sizes[10] = 9 * MiB + 5
+            flags = {int(i): 1 for i in rng.choice(len(sizes), 25, replace=False) + 1}
+            blk = make_block(ds, oracle, 700 + k, sizes, seed=40 + k, flags=flags)
+            ds.write_block_files(blk, src, 10 + k, 100 + 10 * k, bucket_size=31, main_size=main_size,
+                                 ext_size=ext_size)
+            lb0 = ds.LoadedBlock(None, src, 10 + k, main_size=main_size, ext_size=ext_size)
+            bad_id = None
+            if k == 2:
+                m0 = lb0.metas
+                j = next(i for i in range(len(m0)) if int(m0["size"][i]) > 1000 and int(m0["file_id"][i]) not in flags)
+                bad_id = int(m0["file_id"][j])
+                _flip_on_disk(src, lb0.chain, main_size, ext_size, int(m0["offset"][j]) + 36 + 500)
+            lb = ds.LoadedBlock(None, src, 10 + k, main_size=main_size, ext_size=ext_size)
+            odest, doff, ook = _oracle_compact(oracle, lb.data(), lb.metas, lb.flags)
+            live = np.nonzero((lb.flags & 3) == 0)[0]
+            rc, dmetas, st, ext, cnt = comp.compact(src, 10 + k, dst, 50 + k, 400 + 10 * k, main_size=main_size,
+                                                    ext_size=ext_size)
+            assert cnt["n_live"] == len(live) and cnt["dest_size"] == odest.size, (k, cnt)
+            assert rc == (-1010 if k == 2 else 0) and cnt["n_bad"] == (1 if k == 2 else 0), (k, rc, cnt)
+            assert cnt["big_files"] == (1 if k == 1 and 11 not in flags else 0), (k, cnt)
+            assert np.array_equal(dmetas["offset"].astype(np.int64), doff[live])
+            out = ds.LoadedBlock(None, dst, 50 + k, main_size=main_size, ext_size=ext_size)
+            assert out.rc == 0 and np.array_equal(out.data(), odest), k
+            if bad_id is not None:
+                assert int(st[list(dmetas["file_id"]).index(bad_id)]) == -1010
+        rc, _, _, _, _ = comp.compact(src, 99, dst, 90, 900, main_size=main_size, ext_size=ext_size)
+        assert rc != 0
+        rc, _, _, _, cnt = comp.compact(src, 10, dst, 91, 910, main_size=main_size, ext_size=ext_size)
+        assert rc == 0 and cnt["n_live"] > 0
+    finally:
+        comp.free()

@@ -81,6 +81,10 @@ def lib():
             "tfs_ds_compact_block_files": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_char_p, i32, i32, u32, u32,
                                                           u32, i32, ctypes.c_int, vp, vp, u32, vp, u32,
                                                           ctypes.POINTER(u32), vp]),
+            "tfs_ds_compactor_new": (vp, [vp, ctypes.c_int]),
+            "tfs_ds_compactor_free": (None, [vp]),
+            "tfs_ds_compactor_compact": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_char_p, i32, i32, u32, u32, u32,
+                                                        i32, vp, vp, u32, vp, u32, ctypes.POINTER(u32), vp]),
             "tfs_ds_decode": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, u32, ctypes.POINTER(u32),
                                              ctypes.POINTER(i64)]),
             "tfs_ds_close_latency": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, i32, vp]),
@@ -416,6 +420,46 @@ def compact_block_files(ctx, src_mount, src_main_id, dst_mount, dst_main_id, fir
     n = int(cnt[0])
     keys = ("n_live", "dest_size", "windows", "launches", "big_files", "n_bad")
     return rc, metas[:n], st[:n], ext[:next_.value].tolist(), dict(zip(keys, (int(x) for x in cnt)))
+
+
+class BlockFileCompactor:
+    """compact_block_files with its window buffers and streams kept across blocks
+    (block_store.h BlockFileCompactor: a compaction thread's state)."""
+
+    def __init__(self, ctx, windows_per_launch=4):
+        self.h = lib().tfs_ds_compactor_new(ctx.handle, windows_per_launch)
+        if not self.h:
+            raise _crc.TfsCrcError(-1016, "tfs_ds_compactor_new")
+        self.metas = np.zeros(1 << 16, _crc.META_DTYPE)
+        self.status = np.zeros(1 << 16, np.int32)
+        self.ext = np.zeros(64, np.uint32)
+        self.cnt = np.zeros(6, np.int64)
+
+    def compact(self, src_mount, src_main_id, dst_mount, dst_main_id, first_ext_id, bucket_size=0,
+                main_size=MAIN_BLOCK_SIZE, ext_size=EXT_BLOCK_SIZE):
+        """Returns (rc, dest metas, statuses, ext ids, counters) as compact_block_files (views valid
+        until the next call)."""
+        next_ = ctypes.c_uint32()
+        rc = lib().tfs_ds_compactor_compact(self.h, src_mount.encode(), dst_mount.encode(), main_size, ext_size,
+                                            src_main_id, dst_main_id, first_ext_id, bucket_size,
+                                            self.metas.ctypes.data, self.status.ctypes.data, self.metas.size,
+                                            self.ext.ctypes.data, self.ext.size, ctypes.byref(next_),
+                                            self.cnt.ctypes.data)
+        n = int(self.cnt[0])
+        keys = ("n_live", "dest_size", "windows", "launches", "big_files", "n_bad")
+        return (rc, self.metas[:n], self.status[:n], self.ext[:next_.value].tolist(),
+                dict(zip(keys, (int(x) for x in self.cnt))))
+
+    def free(self):
+        if self.h:
+            lib().tfs_ds_compactor_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 def verify_block(ctx, block, checker=None):

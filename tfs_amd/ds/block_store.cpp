@@ -428,11 +428,69 @@ struct WindowGroup {
 
 }  // namespace
 
+struct BlockFileCompactor::Impl {
+  tfs_crc_ctx* ctx;
+  int K;
+  int setup_rc = TFS_SUCCESS;
+  WindowGroup groups[2];
+  Impl(tfs_crc_ctx* c, int windows_per_launch) : ctx(c), K(std::max(1, std::min(windows_per_launch, 64))) {
+    if (!ctx) {
+      setup_rc = TFS_EXIT_PARAMETER_ERROR;
+      return;
+    }
+    const uint64_t kWin = uint64_t(kMaxCompactReadSize);
+    for (WindowGroup& g : groups) {
+      g.src.ctx = g.dst.ctx = g.jobs.ctx = g.status.ctx = g.d_status.ctx = ctx;
+      g.d_status.device = true;
+      // 128 bytes of slack past the last window: the record kernel's stripe grid
+      // may read up to 112 bytes past a record's payload (make_geo).
+      int rc;
+      if ((rc = g.src.grow(uint64_t(K) * kWin + 256)) || (rc = g.dst.grow(uint64_t(K) * kWin + 256)) ||
+          (rc = g.jobs.grow(4096 * sizeof(tfs_compact_job))) || (rc = g.status.grow(4096 * 4)) ||
+          (rc = g.d_status.grow(4096 * 4)) || (rc = tfs_crc32_stream_create(ctx, &g.stream))) {
+        setup_rc = rc;
+        return;
+      }
+    }
+  }
+  ~Impl() {
+    for (WindowGroup& g : groups)
+      if (g.stream) tfs_crc32_stream_destroy(ctx, g.stream);
+  }
+  int compact(const BlockStore& src, uint32_t src_main_id, const BlockStore& dst, uint32_t dst_main_id,
+              uint32_t first_ext_id, int32_t bucket_size, CompactFilesResult* out);
+};
+
+BlockFileCompactor::BlockFileCompactor(tfs_crc_ctx* ctx, int windows_per_launch)
+    : impl_(new Impl(ctx, windows_per_launch)) {}
+BlockFileCompactor::~BlockFileCompactor() { delete impl_; }
+int BlockFileCompactor::compact(const BlockStore& src, uint32_t src_main_id, const BlockStore& dst,
+                                uint32_t dst_main_id, uint32_t first_ext_id, int32_t bucket_size,
+                                CompactFilesResult* out) {
+  return impl_->compact(src, src_main_id, dst, dst_main_id, first_ext_id, bucket_size, out);
+}
+
 int compact_block_files(tfs_crc_ctx* ctx, const BlockStore& src, uint32_t src_main_id, const BlockStore& dst,
                         uint32_t dst_main_id, uint32_t first_ext_id, int32_t bucket_size, int windows_per_launch,
                         CompactFilesResult* out) {
-  if (!ctx || !out) return TFS_EXIT_PARAMETER_ERROR;
+  BlockFileCompactor c(ctx, windows_per_launch);
+  return c.compact(src, src_main_id, dst, dst_main_id, first_ext_id, bucket_size, out);
+}
+
+int BlockFileCompactor::Impl::compact(const BlockStore& src, uint32_t src_main_id, const BlockStore& dst,
+                                      uint32_t dst_main_id, uint32_t first_ext_id, int32_t bucket_size,
+                                      CompactFilesResult* out) {
+  if (!out) return TFS_EXIT_PARAMETER_ERROR;
   *out = CompactFilesResult();
+  if (setup_rc) return setup_rc;
+  for (WindowGroup& g : groups) {  // a previous call that failed part-way may have left a group queued
+    if (g.inflight) (void)tfs_crc32_stream_sync(ctx, g.stream);
+    g.wins.clear();
+    g.file_idx.clear();
+    g.src_used = g.dst_used = 0;
+    g.njobs = 0;
+    g.inflight = false;
+  }
   std::vector<uint32_t> chain;
   uint32_t logic_id = 0;
   int rc = load_chain(src, src_main_id, &chain, &logic_id);
@@ -442,20 +500,7 @@ int compact_block_files(tfs_crc_ctx* ctx, const BlockStore& src, uint32_t src_ma
   rc = load_index(src, src_main_id, &h, &metas);
   if (rc) return rc;
   const int64_t data_size = h.data_file_offset_;
-  const int K = std::max(1, std::min(windows_per_launch, 64));
   const uint64_t kWin = uint64_t(kMaxCompactReadSize);
-  WindowGroup groups[2];
-  for (WindowGroup& g : groups) {
-    g.src.ctx = g.dst.ctx = g.jobs.ctx = g.status.ctx = g.d_status.ctx = ctx;
-    g.d_status.device = true;
-    // 128 bytes of slack past the last window: the record kernel's stripe grid
-    // may read up to 112 bytes past a record's payload (make_geo).
-    if ((rc = g.src.grow(uint64_t(K) * kWin + 256)) || (rc = g.dst.grow(uint64_t(K) * kWin + 256)) ||
-        (rc = g.jobs.grow(4096 * sizeof(tfs_compact_job))) || (rc = g.status.grow(4096 * 4)) ||
-        (rc = g.d_status.grow(4096 * 4)) ||
-        (rc = tfs_crc32_stream_create(ctx, &g.stream)))
-      break;
-  }
   ChainWriter w(dst, dst_main_id, first_ext_id, logic_id);
   int64_t dest_off = 0;
   int cur = 0;
@@ -617,8 +662,6 @@ int compact_block_files(tfs_crc_ctx* ctx, const BlockStore& src, uint32_t src_ma
     const int r2 = drain(g);
     if (!rc) rc = r ? r : r2;
   }
-  for (WindowGroup& g : groups)
-    if (g.stream) tfs_crc32_stream_destroy(ctx, g.stream);
   if (rc) return rc;
   out->dest_size = dest_off;
   out->ext_ids.assign(w.chain().begin() + 1, w.chain().end());

@@ -184,5 +184,23 @@ int compact_block_files(tfs_crc_ctx* ctx, const BlockStore& src, uint32_t src_ma
                         uint32_t dst_main_id, uint32_t first_ext_id, int32_t bucket_size, int windows_per_launch,
                         CompactFilesResult* out);
 
+// The same walk with its page-locked window buffers and streams kept across
+// blocks (the compaction task thread's state, dataservice.cpp:2915-2918): what
+// a dataserver compacting block after block holds.  Not thread-safe; one per
+// compacting thread.
+class BlockFileCompactor {
+ public:
+  BlockFileCompactor(tfs_crc_ctx* ctx, int windows_per_launch);
+  ~BlockFileCompactor();
+  BlockFileCompactor(const BlockFileCompactor&) = delete;
+  BlockFileCompactor& operator=(const BlockFileCompactor&) = delete;
+  int compact(const BlockStore& src, uint32_t src_main_id, const BlockStore& dst, uint32_t dst_main_id,
+              uint32_t first_ext_id, int32_t bucket_size, CompactFilesResult* out);
+
+ private:
+  struct Impl;
+  Impl* impl_;
+};
+
 }  // namespace dataserver
 }  // namespace tfs

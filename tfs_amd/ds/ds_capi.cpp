@@ -420,17 +420,10 @@ uint32_t tfs_ds_loaded_metas(void* b, tfs_raw_meta* metas, int32_t* flags, uint3
   return uint32_t(lb->metas.size());
 }
 
-// compact_block_files: the new block's metas / statuses (cap entries), ext ids
-// (ext_cap), and counters[6] = {n_live, dest_size, windows, launches, big_files, n_bad}.
-int tfs_ds_compact_block_files(tfs_crc_ctx* ctx, const char* src_mount, const char* dst_mount, int32_t main_size,
-                               int32_t ext_size, uint32_t src_main_id, uint32_t dst_main_id, uint32_t first_ext_id,
-                               int32_t bucket_size, int windows_per_launch, tfs_raw_meta* dest_metas,
-                               int32_t* status, uint32_t cap, uint32_t* ext_ids, uint32_t ext_cap, uint32_t* n_ext,
-                               int64_t* counters) {
-  tfs::dataserver::CompactFilesResult r;
-  const int rc = tfs::dataserver::compact_block_files(ctx, make_store(src_mount, main_size, ext_size), src_main_id,
-                                                      make_store(dst_mount, main_size, ext_size), dst_main_id,
-                                                      first_ext_id, bucket_size, windows_per_launch, &r);
+namespace {
+int export_compact_result(int rc, const tfs::dataserver::CompactFilesResult& r, tfs_raw_meta* dest_metas,
+                          int32_t* status, uint32_t cap, uint32_t* ext_ids, uint32_t ext_cap, uint32_t* n_ext,
+                          int64_t* counters) {
   for (size_t i = 0; i < r.dest_metas.size() && i < cap; ++i) {
     if (dest_metas) dest_metas[i] = r.dest_metas[i];
     if (status) status[i] = r.status[i];
@@ -446,6 +439,38 @@ int tfs_ds_compact_block_files(tfs_crc_ctx* ctx, const char* src_mount, const ch
     counters[5] = r.n_bad;
   }
   return rc;
+}
+}  // namespace
+
+// compact_block_files: the new block's metas / statuses (cap entries), ext ids
+// (ext_cap), and counters[6] = {n_live, dest_size, windows, launches, big_files, n_bad}.
+int tfs_ds_compact_block_files(tfs_crc_ctx* ctx, const char* src_mount, const char* dst_mount, int32_t main_size,
+                               int32_t ext_size, uint32_t src_main_id, uint32_t dst_main_id, uint32_t first_ext_id,
+                               int32_t bucket_size, int windows_per_launch, tfs_raw_meta* dest_metas,
+                               int32_t* status, uint32_t cap, uint32_t* ext_ids, uint32_t ext_cap, uint32_t* n_ext,
+                               int64_t* counters) {
+  tfs::dataserver::CompactFilesResult r;
+  const int rc = tfs::dataserver::compact_block_files(ctx, make_store(src_mount, main_size, ext_size), src_main_id,
+                                                      make_store(dst_mount, main_size, ext_size), dst_main_id,
+                                                      first_ext_id, bucket_size, windows_per_launch, &r);
+  return export_compact_result(rc, r, dest_metas, status, cap, ext_ids, ext_cap, n_ext, counters);
+}
+
+// A BlockFileCompactor kept across blocks (window buffers and streams allocated once).
+void* tfs_ds_compactor_new(tfs_crc_ctx* ctx, int windows_per_launch) {
+  return ctx ? new tfs::dataserver::BlockFileCompactor(ctx, windows_per_launch) : nullptr;
+}
+void tfs_ds_compactor_free(void* h) { delete static_cast<tfs::dataserver::BlockFileCompactor*>(h); }
+int tfs_ds_compactor_compact(void* h, const char* src_mount, const char* dst_mount, int32_t main_size,
+                             int32_t ext_size, uint32_t src_main_id, uint32_t dst_main_id, uint32_t first_ext_id,
+                             int32_t bucket_size, tfs_raw_meta* dest_metas, int32_t* status, uint32_t cap,
+                             uint32_t* ext_ids, uint32_t ext_cap, uint32_t* n_ext, int64_t* counters) {
+  if (!h) return TFS_EXIT_PARAMETER_ERROR;
+  tfs::dataserver::CompactFilesResult r;
+  const int rc = static_cast<tfs::dataserver::BlockFileCompactor*>(h)->compact(
+      make_store(src_mount, main_size, ext_size), src_main_id, make_store(dst_mount, main_size, ext_size), dst_main_id,
+      first_ext_id, bucket_size, &r);
+  return export_compact_result(rc, r, dest_metas, status, cap, ext_ids, ext_cap, n_ext, counters);
 }
 
 int tfs_ds_verify_block_files(tfs_crc_ctx* ctx, const char* mount, int32_t main_size, int32_t ext_size,

@@ -11,5 +11,6 @@ run() {
 run default && run zipf --workload zipf && run packet --workload packet && run compact_device --workload compact_device \
   && run block_verify_device --workload block_verify_device && run compact --workload compact \
   && run block_verify --workload block_verify && run e2e --workload e2e && run ec --workload ec \
+  && run compact_files --workload compact_files \
   && run loopback --workload loopback
 echo "all_lines done"
