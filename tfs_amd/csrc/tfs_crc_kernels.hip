@@ -296,21 +296,33 @@ typedef u32x4 __attribute__((aligned(1))) u32x4u;
 typedef __attribute__((address_space(1))) u32u* gu32up;
 typedef __attribute__((address_space(1))) u32x4u* gu128up;
 __device__ __forceinline__ void st32u(uintptr_t a, uint32_t v) { *reinterpret_cast<gu32up>(a) = v; }
-template <bool NTS = true>
+// Copy-through store kinds (NTS): 1 non-temporal (product); measurement only:
+// 0 plain (TFS_CRC_VARIANT=25: partial lines at record and stripe edges can merge
+// in L2 before they are written back), 2 sc1 (variant 36: the line is dropped
+// from L2 as the store passes, MI355X_MICROARCH.md store flavours).
+template <int NTS>
+__device__ __forceinline__ void st128_kind(uintptr_t a, const u32x4& w) {
+  if (NTS == 1) {
+    __builtin_nontemporal_store(w, reinterpret_cast<gu128wp>(a));
+  } else if (NTS == 2) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(a), "v"(w) : "memory");
+  } else {
+    *reinterpret_cast<gu128wp>(a) = w;
+  }
+}
+template <int NTS = 1>
 __device__ __forceinline__ void st128u(uintptr_t a, const uint4& v) {
   const u32x4 w = {v.x, v.y, v.z, v.w};
-  if (NTS) __builtin_nontemporal_store(w, reinterpret_cast<gu128up>(a));
+  if (NTS == 1) __builtin_nontemporal_store(w, reinterpret_cast<gu128up>(a));
+  else if (NTS == 2) st128_kind<2>(a, w);  // the hardware takes any byte address (unaligned access mode)
   else *reinterpret_cast<gu128up>(a) = w;
 }
 
-// NTS = false (measurement, TFS_CRC_VARIANT=25): plain stores, so partial lines
-// at record and stripe edges can merge in L2 before they are written back.
-template <bool NTS = true>
+template <int NTS = 1>
 __device__ __forceinline__ void st128_nt(uintptr_t a, const uint4& v) {
   u32x4 w = {v.x, v.y, v.z, v.w};
   if ((a & 15u) == 0) {
-    if (NTS) __builtin_nontemporal_store(w, reinterpret_cast<gu128wp>(a));
-    else *reinterpret_cast<gu128wp>(a) = w;
+    st128_kind<NTS>(a, w);
   } else {  // 4-aligned: four dword stores
     st32(a, v.x); st32(a + 4, v.y); st32(a + 8, v.z); st32(a + 12, v.w);
   }
@@ -334,7 +346,7 @@ struct ShiftCarry {
 __device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) {
   return __builtin_amdgcn_update_dpp(0u, v, 0x138 /* wave_shr:1 */, 0xf, 0xf, false);
 }
-template <bool DPP = true, bool NTS = true>
+template <bool DPP = true, int NTS = 1>
 __device__ __forceinline__ void store_shifted(uintptr_t chunk, const uint4& v, uint32_t k, int lane, ShiftCarry& cr,
                                               bool store, bool flush) {
   uint32_t p1, p2, p3;
@@ -388,7 +400,7 @@ __device__ __forceinline__ void store_shifted(uintptr_t chunk, const uint4& v, u
 // by dword) it stores only its own 16 bytes, unaligned (`own`), and so does the
 // record's last valid lane (`flush`) for the bytes past its chunk.  The byte
 // ranges those extra stores share with a neighbouring chunk hold the same values.
-template <int K, bool NTS>
+template <int K, int NTS>
 __device__ __forceinline__ void store_bshift(uintptr_t chunk, uintptr_t own, const uint4& v, uint32_t sh, int lane,
                                              ShiftCarry& cr, bool store, bool flush) {
   uint32_t p0 = 0u, p1 = 0u, p2 = 0u, p3 = from_prev_lane(v.w);
@@ -428,7 +440,7 @@ __device__ __forceinline__ void store_bshift(uintptr_t chunk, uintptr_t own, con
 // NTS: non-temporal copy-through stores (product).  NOCRC (measurement only,
 // TFS_CRC_VARIANT=26: wrong CRCs): skip the payload steps, so the record kernel
 // runs its own load/store schedule without the table lookups.
-template <int RUN, int PF, bool NT, bool S8, bool COPY = false, int G = 1, bool DPPSH = false, bool NTS = true,
+template <int RUN, int PF, bool NT, bool S8, bool COPY = false, int G = 1, bool DPPSH = false, int NTS = 1,
           bool NOCRC = false, bool HEADST = true, bool BSU = false>
 __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase& lb, const FileGeo<RUN>& g,
                                                const Head<RUN>& h, uint4 (&buf)[PF][RUN / 16], int lane,
@@ -1461,9 +1473,10 @@ __device__ __forceinline__ void copy_unaligned(const uint8_t* s, uint8_t* d, uin
 // stores (DIAG bit 4; wrong output), 31 = byte-shifted records copied after the
 // CRC by copy_unaligned instead of through the chain (DIAG bit 5), 32 = byte-
 // shifted records stored as each lane's 16 bytes at their byte address instead
-// of line-aligned alignbyte chunks (DIAG bit 6).
+// of line-aligned alignbyte chunks (DIAG bit 6), 36 = sc1 copy-through stores
+// (DIAG bit 7).  CPF: stripes in flight per wave (variants 33-35, 37: 6, 7, 8, 4).
 constexpr int kCompactDiag = 4 | 8;
-template <bool WIDE, bool DPPSH = true, bool VERIFY = false, int DIAG = kCompactDiag>
+template <bool WIDE, bool DPPSH = true, bool VERIFY = false, int DIAG = kCompactDiag, int CPF = kPF>
 __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __restrict__ src, uint64_t src_len,
                                                               const RawMeta* __restrict__ metas,
                                                               const int32_t* __restrict__ flags,
@@ -1474,6 +1487,7 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
                                                               uint32_t* sched) {
   constexpr bool DA = !VERIFY && (DIAG & 4) != 0;
   constexpr bool LNT = (DIAG & 8) && !VERIFY ? false : kNT;  // the verify form keeps the headline's loads
+  constexpr int SK = (DIAG & 1) ? 0 : ((DIAG & 128) ? 2 : 1);  // copy-through store kind (st128_kind)
   __shared__ uint32_t lds_tables[LdsLayout<kS8>::bytes / 4];
   load_tables<kRun, kPAR, kS8>(lds_tables, tg);
   const int lane = threadIdx.x & (kWave - 1);
@@ -1489,14 +1503,14 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
     uint32_t fn = tk.resolve(tk.issue(lane), lane);
     CRec cur = load_crec<WIDE, VERIFY>(f, src_len, metas, flags, dest_off, jobs);
     CState st = issue_crec<DA>(cur, src, src_len, dst, lane, junk);
-    uint4 buf[kPF][kRun / 16];
-    load_ring<kRun, kPF, LNT>(st.g, lane, buf, junk);
+    uint4 buf[CPF][kRun / 16];
+    load_ring<kRun, CPF, LNT>(st.g, lane, buf, junk);
     CRec nxt = fn < n ? load_crec<WIDE, VERIFY>(fn, src_len, metas, flags, dest_off, jobs) : CRec{};
     uint32_t jv = fn < n ? tk.issue(lane) : 0u;
     for (;;) {
       // DIAG bit 5 (variant 31, measurement): byte-shifted records copy after the CRC (copy_unaligned)
       const bool chain_copy = !(DIAG & 32) || (st.delta & 3) == 0;
-      uint32_t c = st.g.nstripes ? lane_chain<kRun, kPF, LNT, kS8, !VERIFY, 1, DPPSH, !(DIAG & 1), (DIAG & 2) != 0, !(DIAG & 16),
+      uint32_t c = st.g.nstripes ? lane_chain<kRun, CPF, LNT, kS8, !VERIFY, 1, DPPSH, SK, (DIAG & 2) != 0, !(DIAG & 16),
                                             (DIAG & 64) != 0>(
                                      lds_tables, lb, st.g, st.h, buf, lane, junk, st.delta, chain_copy)
                                  : 0u;
@@ -1507,7 +1521,7 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
       uint32_t fnn = n;
       if (more) {
         ns = issue_crec<DA>(ncur, src, src_len, dst, lane, junk);
-        load_ring<kRun, kPF, LNT>(ns.g, lane, buf, junk);
+        load_ring<kRun, CPF, LNT>(ns.g, lane, buf, junk);
         fnn = tk.resolve(jv, lane);
         if (fnn < n) {
           nxt = load_crec<WIDE, VERIFY>(fnn, src_len, metas, flags, dest_off, jobs);
@@ -1862,6 +1876,11 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
   else if (variant == 30) TFS_CJ(true, true, false, kCompactDiag | 16);
   else if (variant == 31) TFS_CJ(true, true, false, kCompactDiag | 32);
   else if (variant == 32) TFS_CJ(true, true, false, kCompactDiag | 64);
+  else if (variant == 33) TFS_CJ(true, true, false, kCompactDiag, 6);
+  else if (variant == 34) TFS_CJ(true, true, false, kCompactDiag, 7);
+  else if (variant == 35) TFS_CJ(true, true, false, kCompactDiag, 8);
+  else if (variant == 36) TFS_CJ(true, true, false, kCompactDiag | 128);
+  else if (variant == 37) TFS_CJ(true, true, false, kCompactDiag, 4);
   else TFS_CJ(true);
 #undef TFS_CJ
   return hipGetLastError();

@@ -82,10 +82,13 @@ def main():
         j["size"] = rec
         j["new_offset"] = (do % np.uint64(1 << 31)).astype(np.int32)
         jobsets[name] = crc.DeviceBuffer(ctx, j.nbytes).upload(j)
-    ctxs = {0: ctx, 25: ctx_for(25), 26: ctx_for(26), 27: ctx_for(27), 29: ctx_for(29), 30: ctx_for(30),
-            31: ctx_for(31), 32: ctx_for(32)}
-    cases = [(0, "packed"), (27, "packed"), (25, "packed"), (26, "packed"), (29, "packed"), (30, "packed"),
-             (0, "dst128"), (27, "dst128"), (0, "shift1"), (31, "shift1"), (32, "shift1")]
+    want = [int(x) for x in os.environ.get("AB_VARIANTS", "27,25,26,29,30,31,32").split(",") if x]
+    ctxs = {0: ctx}
+    for v in want:
+        ctxs[v] = ctx_for(v)
+    cases = [(0, "packed")] + [(v, "packed") for v in want if v not in (31, 32)] + [(0, "dst128")]
+    if 31 in want or 32 in want:
+        cases += [(0, "shift1")] + [(v, "shift1") for v in want if v in (31, 32)]
     nj = int(k.size)
     live_bytes = float(nj) * rec
     algo = 2 * live_bytes + nj * (40 + 4)
