@@ -142,3 +142,18 @@ def test_resident_scalar_drop_in(oracle):
         d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
         s = int(rng.integers(0, 2**32))
         assert crc.func_crc(s, d) == ocrc(oracle, s, d), it
+
+
+def test_resident_process_exit_right_after_a_call():
+    """A process that makes one scalar call (default context, never destroyed) and
+    exits at once: the exit handler stops the resident kernel through host memory
+    before the runtime tears down; the process exits cleanly."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r); import tfs_amd.crc as c; "
+            "assert c.func_crc(0, bytes(range(256)) * 256) == c.func_crc(0, bytes(range(256)) * 256)" % root)
+    for _ in range(3):
+        r = subprocess.run([sys.executable, "-c", code], timeout=120, capture_output=True)
+        assert r.returncode == 0, r.stderr[-2000:]

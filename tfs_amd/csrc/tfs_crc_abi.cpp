@@ -340,9 +340,29 @@ int wait_flag(tfs_crc_ctx* ctx, Slot& s) {
 }
 
 // ---- resident form -------------------------------------------------------------
+// Contexts whose resident kernel may be running.  At process exit (a caller that
+// never destroys its context -- the scalar drop-in's default context) every such
+// kernel is stopped and waited for through host memory only, before the HIP
+// runtime tears down and unmaps its ring.
+std::mutex g_res_mu;
+std::vector<tfs_crc_ctx*> g_res_ctxs;
+
+void resident_atexit() {
+  std::lock_guard<std::mutex> g(g_res_mu);
+  for (tfs_crc_ctx* c : g_res_ctxs) {
+    ResHost* H = c->res_host;
+    if (!H || !c->res_running) continue;
+    const uint32_t gen = uint32_t(c->res_launches);
+    __atomic_store_n(&H->published, uint64_t(c->res_published) | (uint64_t(1) << 32), __ATOMIC_RELEASE);
+    for (int i = 0; i < 200000 && __atomic_load_n(&H->left, __ATOMIC_ACQUIRE) != gen; ++i) __builtin_ia32_pause();
+  }
+}
+
 // (Caller holds ctx->mu.)  Ring, device state, stream and event, made on first use.
 int resident_setup(tfs_crc_ctx* ctx) {
   if (ctx->res_host) return TFS_SUCCESS;
+  static std::once_flag atexit_once;
+  std::call_once(atexit_once, [] { std::atexit(resident_atexit); });
   int khz = 0;
   HIP_TRY(ctx, hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device));
   if (khz <= 0) khz = 100000;
@@ -368,6 +388,8 @@ int resident_setup(tfs_crc_ctx* ctx) {
   ctx->res_host_d = static_cast<ResHost*>(hd);
   ctx->res_state = static_cast<uint32_t*>(st);
   ctx->res_published = 0;
+  std::lock_guard<std::mutex> g(g_res_mu);
+  g_res_ctxs.push_back(ctx);
   return TFS_SUCCESS;
 }
 
@@ -454,6 +476,10 @@ int wait_resident(tfs_crc_ctx* ctx, Slot& s, int mode, uint32_t n) {
 // (Caller holds no lock.)  Stop the resident kernel and free its ring.
 void resident_teardown(tfs_crc_ctx* ctx) {
   if (!ctx->res_host) return;
+  {
+    std::lock_guard<std::mutex> g(g_res_mu);
+    g_res_ctxs.erase(std::remove(g_res_ctxs.begin(), g_res_ctxs.end(), ctx), g_res_ctxs.end());
+  }
   __atomic_store_n(&ctx->res_host->published, uint64_t(ctx->res_published) | (uint64_t(1) << 32), __ATOMIC_RELEASE);
   if (ctx->res_stream) (void)hipStreamSynchronize(ctx->res_stream);
   if (ctx->res_event) (void)hipEventDestroy(ctx->res_event);

@@ -70,7 +70,8 @@ constexpr uint32_t kWgLdsBytes = kWgLevelOff + uint32_t(kWgLevels) * 1024u;  // 
 constexpr uint32_t kResUnits = 4096;            // ring of units
 constexpr uint32_t kResMaxGrid = 256;           // workgroups of the resident kernel, at most
 constexpr uint32_t kResExitLine = kResMaxGrid * kSchedStride;  // dstate: generation of the launch that is leaving
-constexpr uint32_t kResStateBytes = (kResMaxGrid + 1u) * kSchedStride * 4u;  // a line per workgroup + the exit line
+constexpr uint32_t kResLeftLine = kResExitLine + kSchedStride;  // dstate: workgroups of this launch that have left
+constexpr uint32_t kResStateBytes = (kResMaxGrid + 2u) * kSchedStride * 4u;  // a line per workgroup + 2
 constexpr uint32_t kResMaxPolls = 1u << 22;     // hard bound on one workgroup's idle polls
 struct ResUnit {         // one file
   uint64_t addr;         // device-visible address of its first byte
@@ -80,9 +81,12 @@ struct ResUnit {         // one file
 };
 struct ResHost {
   uint64_t published;    // low 32 bits: units published (wrapping); high 32 bits: stop
-  uint64_t pad[31];
+  uint64_t pad0[15];
+  uint32_t left;         // generation of the last launch whose every workgroup has left (GPU-written)
+  uint32_t pad1[31];
   ResUnit units[kResUnits];
 };
+static_assert(sizeof(ResHost) == 256 + sizeof(ResUnit) * kResUnits, "resident ring header");
 static_assert(sizeof(ResUnit) == 32, "resident ring layout");
 
 // TFS status codes (src/common/error_msg.h)

@@ -1036,7 +1036,15 @@ __global__ void __launch_bounds__(kBlock) crc_resident_kernel(const Tables* __re
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __syncthreads();  // claim[] and part[] are rewritten for the next file
   }
-  if (threadIdx.x == 0) __hip_atomic_store(mine, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(mine, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // The last workgroup out tells the host (which may be exiting and waits on it
+    // without HIP calls, tfs_crc_abi.cpp resident_atexit).
+    if (atomicAdd(&dstate[kResLeftLine], 1u) + 1u == gridDim.x) {
+      atomicExch(&dstate[kResLeftLine], 0u);
+      __hip_atomic_store(const_cast<uint32_t*>(&hs->left), gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 // The FileInfo fields the checks need (id_ +0, size_ +12, crc_ +32), read from a
