@@ -438,7 +438,12 @@ int resident_post(tfs_crc_ctx* ctx, Slot& s, int mode, const uint8_t* zb, const 
   ctx->res_published = P + n;
   ctx->res_files += n;
   __atomic_store_n(&H->published, uint64_t(ctx->res_published), __ATOMIC_RELEASE);
-  return resident_ensure_running(ctx);
+  const int rc = resident_ensure_running(ctx);
+  // A launch that fails leaves units published that no kernel may ever take (or
+  // one taking them late, into result words since reused): the context stops
+  // using the ring and launches from then on.
+  if (rc) ctx->resident = false;
+  return rc;
 }
 
 // Completion of a resident batch: spin until every file's result word carries
@@ -458,9 +463,14 @@ int wait_resident(tfs_crc_ctx* ctx, Slot& s, int mode, uint32_t n) {
       if (e == hipErrorNotReady) continue;
       std::lock_guard<std::mutex> g(ctx->mu);
       const uint64_t before = ctx->res_launches;
-      if (const int rc = resident_ensure_running(ctx)) return rc;
-      if (ctx->res_launches != before && ++relaunches > 100000u)
+      if (const int rc = resident_ensure_running(ctx)) {
+        ctx->resident = false;  // as in resident_post
+        return rc;
+      }
+      if (ctx->res_launches != before && ++relaunches > 100000u) {
+        ctx->resident = false;
         return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "resident kernel makes no progress (seq %u)", s.seq);
+      }
     }
   }
   uint32_t* crc = static_cast<uint32_t*>(s.h_crc.p);
