@@ -1293,8 +1293,8 @@ def bench_block_verify_device(args):
     c24.close()
     algo_per_rec = FILEINFO + FILE_SIZE + 40 + 4 + 4   # header + payload + job read, crc + status written
     achieved = nfiles * algo_per_rec / (kms / 1e3) / 1e9
-    bv_traffic, bv_src = _pmc_traffic("profiles/r02/block_verify_device/pmc_summary.json",
-                                      "compact_pipe_kernel<true, true, true, 12>", nblocks == 1024)
+    bv_traffic, bv_src = _pmc_traffic("profiles/r02_final/block_verify_device/pmc_summary.json",
+                                      "compact_pipe_kernel<true, true, true, 12, 5>", nblocks == 1024)
     res = {
         "metric": "GiB/s payload verified on read from device-resident block images (FileInfo checks + re-CRC)",
         "value": world * args.steps * nfiles * FILE_SIZE / el / 2**30, "unit": "GiB/s", "n_gpus": world,
@@ -1484,8 +1484,8 @@ def bench_compact_device(args):
     live_bytes = float(nlive) * rec
     algo = 2 * live_bytes + nlive * (40 + 4)  # read + write live records, 40 B CompactJob + 4 B status
     live_payload = float(nlive) * FILE_SIZE
-    cd_traffic, cd_src = _pmc_traffic("profiles/r02/compact_device_anchored/pmc_summary.json",
-                                      "compact_pipe_kernel<true, true, false, 12>", nblocks == 1024)
+    cd_traffic, cd_src = _pmc_traffic("profiles/r02_final/compact_device/pmc_summary.json",
+                                      "compact_pipe_kernel<true, true, false, 12, 5>", nblocks == 1024)
     res = {
         "metric": "GiB/s of live payload compacted on the device (re-CRC + repack of live files)",
         "value": world * args.steps * live_payload / el / 2**30, "unit": "GiB/s of live payload", "n_gpus": world,

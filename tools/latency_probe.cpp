@@ -109,6 +109,31 @@ int main(int argc, char** argv) {
              pct(us, 0.5), pct(us, 0.99), bad);
     out += b;
   }
+  // One V1 RPC frame of a 64 KiB write (header: flag, length, type, version, id,
+  // crc; base_packet.h:92-162), sealed, then verified as BasePacket::decode does.
+  {
+    std::vector<char> frame(24 + kFile);
+    const uint32_t flag = TFS_PACKET_FLAG_V1, blen = kFile;
+    const int16_t type = 1, version = 1;
+    const uint64_t id = 7;
+    memcpy(&frame[0], &flag, 4);
+    memcpy(&frame[4], &blen, 4);
+    memcpy(&frame[8], &type, 2);
+    memcpy(&frame[10], &version, 2);
+    memcpy(&frame[12], &id, 8);
+    memcpy(&frame[24], pageable.data(), kFile);
+    tfs_packet_desc pd{0, uint32_t(frame.size()), 0};
+    int32_t pst = 0;
+    uint32_t pcrc = 0, pbad = 0;
+    tfs_packet_seal(ctx, &pd, 1, frame.data(), frame.size(), &pcrc, &pst);
+    run("packet_verify_64k_pageable", [&] {
+      return tfs_packet_verify(ctx, &pd, 1, frame.data(), frame.size(), &pcrc, &pst, &pbad) | pst;
+    });
+    memcpy(pinned, frame.data(), frame.size());
+    run("packet_verify_64k_pinned", [&] {
+      return tfs_packet_verify(ctx, &pd, 1, pinned, frame.size(), &pcrc, &pst, &pbad) | pst;
+    });
+  }
   uint64_t launches = 0, files = 0;
   tfs_crc32_resident_stats(ctx, &launches, &files);
   {
