@@ -232,3 +232,43 @@ def test_ds_packet_codec_roundtrip(gpu_ctx, oracle):
     rc, off3, st3, _, consumed = ds.decode_stream(gpu_ctx, cut)
     assert rc == 0 and consumed == off[30] and st3[-1] == 1 and len(st3) == 31
     enc.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["small_host_parse", "launched"])
+def test_gpu_packet_small_batches_both_paths(monkeypatch, oracle, path):
+    """Batches of <= 256 frames within 8 MiB take the small path (headers walked on
+    the host, bodies through the synchronous small-batch CRC); TFS_CRC_VARIANT=20
+    keeps the launched parse/CRC/finish path.  Both give the oracle's statuses,
+    CRCs and sealed bytes on the every-branch stream and on a seal batch."""
+    import tfs_amd.crc as crc_mod
+    monkeypatch.setenv("TFS_CRC_VARIANT", "20" if path == "launched" else "0")
+    ctx = crc_mod.Context(0)
+    monkeypatch.setenv("TFS_CRC_VARIANT", "0")
+    try:
+        rng = np.random.default_rng(21)
+        buf, frames, kinds = build_stream(rng, n=40)
+        assert len(frames) <= 256
+        crc, st, nbad, rc = ctx.packet_verify(buf, [f[0] for f in frames], [f[1] for f in frames])
+        ocrc_, ost, obad = o_verify(oracle, buf, frames)
+        assert np.array_equal(st, ost) and np.array_equal(crc, ocrc_)
+        assert nbad == obad and rc == (-1010 if obad else 0)
+        parts, fr2, pos = [], [], 0
+        for i in range(100):
+            body = pk.write_data_body(i, i, 0, synth_bytes(300 + i, int(rng.integers(1, 40000))).tobytes())
+            f = pk.frame_v1(body, pid=i, version=int(rng.integers(0, 3)))
+            gap = int(rng.integers(0, 5))
+            parts.append(b"\0" * gap + f)
+            fr2.append((pos + gap, len(f)))
+            pos += gap + len(f)
+        raw = b"".join(parts)
+        ob, ocrc2, ost2 = o_seal(oracle, raw, fr2)
+        b2 = np.frombuffer(raw, np.uint8).copy()
+        c2, s2 = ctx.packet_seal(b2, [f[0] for f in fr2], [f[1] for f in fr2])
+        assert np.array_equal(s2, ost2) and np.array_equal(c2, ocrc2) and np.array_equal(b2, ob)
+        # only V0 / version-0 frames: nothing to check on the GPU
+        v0 = pk.header_v0(40, 9) + b"z" * 40
+        c3, s3, nb3, rc3 = ctx.packet_verify(v0, [0], [len(v0)])
+        assert rc3 == 0 and nb3 == 0 and s3[0] == 0 and c3[0] == 0
+    finally:
+        ctx.close()

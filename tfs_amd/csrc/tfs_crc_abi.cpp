@@ -104,7 +104,12 @@ struct PinBuf {
     size_t want = std::max<size_t>(bytes, 4096);
     want = (want + 0xFFFF) & ~size_t(0xFFFF);
     hipError_t e = hipHostMalloc(&p, want, coherent ? hipHostMallocCoherent : hipHostMallocDefault);
-    if (e == hipSuccess) cap = want;
+    if (e == hipSuccess) {
+      cap = want;
+      // Completion words are compared with sequence numbers: recycled memory
+      // must not hold one (0 is never a sequence number).
+      if (coherent) memset(p, 0, want);
+    }
     return e;
   }
   void release() {
@@ -142,6 +147,11 @@ struct Slot {
     done = nullptr;
   }
 };
+
+// Sequence numbers of zero-copy submissions (completion flags, resident result
+// words): process-wide, so a word in page-locked memory recycled from another
+// context can never carry the value a new submission waits for.
+std::atomic<uint32_t> g_flag_seq{0};
 
 constexpr int kSlots = 4;
 constexpr int kSyncSlots = 8;
@@ -192,7 +202,6 @@ struct tfs_crc_ctx {
   uint32_t* d_sched = nullptr;
   std::mutex sched_mu;
   std::vector<hipStream_t> sched_streams;
-  std::atomic<uint32_t> flag_seq{0};  // completion-flag values of zero-copy launches
   int compact_slots = 8;  // blocks in flight in tfs_blocks_compact (TFS_CRC_COMPACT_SLOTS, 1..8)
   int variant = 0;  // kernel variant (TFS_CRC_VARIANT, measurement knob; 0 = product default)
   std::atomic<uint32_t> inject_skip{0}, inject_count{0};  // tfs_crc32_inject_device_error
@@ -564,8 +573,8 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
         hipHostGetDevicePointer(&zcrc, s.h_crc.p, 0) == hipSuccess &&
         hipHostGetDevicePointer(&zok, s.h_ok.p, 0) == hipSuccess &&
         hipHostGetDevicePointer(&zflag, s.h_flag.p, 0) == hipSuccess) {
-      s.seq = ctx->flag_seq.fetch_add(1) + 1u;
-      if (s.seq == 0) s.seq = ctx->flag_seq.fetch_add(1) + 1u;  // 0 is the flag's initial value
+      s.seq = g_flag_seq.fetch_add(1) + 1u;
+      if (s.seq == 0) s.seq = g_flag_seq.fetch_add(1) + 1u;  // 0 is the words' initial value
       if (job >= 0 && ctx->resident && ctx->variant == 0 && n <= kWgMaxFiles) {
         const int rc = resident_post(ctx, s, mode, static_cast<const uint8_t*>(zb) - lo, static_cast<const Desc*>(d), n);
         if (rc < 0) return rc;
@@ -1246,11 +1255,111 @@ static int packet_device(tfs_crc_ctx* ctx, int mode, const tfs_packet_desc* d_de
                         ctx->packet_scratch.p, d_out_crc, d_out_status, d_n_bad, st);
 }
 
+static uint32_t le32(const uint8_t* p) {
+  return uint32_t(p[0]) | uint32_t(p[1]) << 8 | uint32_t(p[2]) << 16 | uint32_t(p[3]) << 24;
+}
+
+// A frame's header as packet_parse_kernel reads it (getPacketInfo, base_packet_
+// streamer.cpp:43-124, and the version decode() sees, base_packet.cpp:100-141):
+// the body descriptor (seed TFS_PACKET_FLAG_V1; aux = the stored crc for a
+// verify) and the pre-status -- kPacketPending when the body CRC decides.
+static void packet_parse_host(const uint8_t* base, const tfs_packet_desc& f, int mode, Desc* d, int32_t* pre) {
+  *d = Desc{f.offset, 0u, kPacketFlagV1};
+  const uint8_t* p = base + f.offset;
+  if (f.len < uint32_t(kPacketHeaderV0Size)) {
+    *pre = kPacketIncomplete;
+    return;
+  }
+  const uint32_t flag = le32(p);
+  const int32_t length = int32_t(le32(p + 4));
+  const int32_t type = int16_t(uint16_t(p[8] | p[9] << 8)), check = int16_t(uint16_t(p[10] | p[11] << 8));
+  const bool v1 = flag == kPacketFlagV1;
+  if (v1 && f.len < uint32_t(kPacketHeaderV0Size + kPacketHeaderDiffSize)) {
+    *pre = kPacketIncomplete;
+  } else if ((flag != kPacketFlagV0 && !v1) || length <= 0 || length > kPacketMaxDataLen) {
+    *pre = kTfsError;
+  } else {
+    const int64_t data_len = int64_t(length) + (v1 ? kPacketHeaderDiffSize : 0);
+    const uint32_t version = ((type < 0) ? 0xFFFFu : 0u) | (v1 ? uint32_t(uint16_t(check)) : 0u);
+    if (uint64_t(kPacketHeaderV0Size) + uint64_t(data_len) > f.len) {
+      *pre = kPacketIncomplete;
+    } else if (version >= 1u) {
+      if (data_len < kPacketHeaderDiffSize) {
+        *pre = kTfsError;
+      } else {
+        d->offset = f.offset + kPacketHeaderV0Size + kPacketHeaderDiffSize;
+        d->len = uint32_t(data_len - kPacketHeaderDiffSize);
+        d->aux = mode == 1 ? le32(p + kPacketHeaderV0Size + 8) : kPacketFlagV1;
+        *pre = kPacketPending;
+      }
+    } else {
+      *pre = kSuccess;
+    }
+  }
+}
+
+// Small host batches (a connection's read, a send queue's few packets): the
+// headers are walked on the host as the streamer does and the bodies' CRCs go
+// through the synchronous small-batch path (read in place, the resident kernel)
+// -- one GPU round trip instead of parse, CRC and finish launches with their
+// copies.  Same statuses, CRCs and sealed bytes as the launched path.
+static int packet_host_small(tfs_crc_ctx* ctx, int mode, const tfs_packet_desc* d, uint32_t n, void* base,
+                             uint64_t base_len, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad) {
+  std::vector<Desc> body;
+  std::vector<uint32_t> idx;
+  std::vector<int32_t> pre(n);
+  std::vector<uint32_t> stored(n, 0u);
+  body.reserve(n);
+  idx.reserve(n);
+  const uint8_t* b8 = static_cast<const uint8_t*>(base);
+  for (uint32_t i = 0; i < n; ++i) {
+    Desc x;
+    packet_parse_host(b8, d[i], mode, &x, &pre[i]);
+    if (pre[i] != kPacketPending) continue;
+    stored[i] = x.aux;
+    x.aux = kPacketFlagV1;  // computed with the packet seed, compared here
+    idx.push_back(i);
+    body.push_back(x);
+  }
+  std::vector<uint32_t> crc(body.size());
+  if (body.empty()) {
+    if (const int f = injected_fault(ctx)) return f;  // as the launched path (no GPU call to fail here)
+  } else {
+    const int rc = tfs_crc32_batch(ctx, reinterpret_cast<const tfs_crc_desc*>(body.data()), uint32_t(body.size()),
+                                   base, base_len, crc.data());
+    if (rc) return rc;
+  }
+  uint32_t bad = 0;
+  if (out_crc) memset(out_crc, 0, size_t(n) * 4);
+  for (size_t k = 0; k < idx.size(); ++k) {
+    const uint32_t i = idx[k];
+    if (out_crc) out_crc[i] = crc[k];
+    if (mode == 1) {
+      pre[i] = crc[k] == stored[i] ? kSuccess : kExitCheckCrcError;  // decode (base_packet.cpp:142-148)
+    } else {
+      pre[i] = kSuccess;
+      uint8_t* p = static_cast<uint8_t*>(base) + d[i].offset;
+      if (le32(p) == TFS_PACKET_FLAG_V1)  // seal: only V1 headers carry a crc (base_packet_streamer.cpp:166-175)
+        for (int b = 0; b < 4; ++b) p[TFS_PACKET_HEADER_V0_SIZE + 8 + b] = uint8_t(crc[k] >> (8 * b));
+    }
+  }
+  for (uint32_t i = 0; i < n; ++i) bad += pre[i] != kSuccess ? 1u : 0u;
+  if (out_status) memcpy(out_status, pre.data(), size_t(n) * 4);
+  if (n_bad) *n_bad = bad;
+  if (mode == 0) return TFS_SUCCESS;
+  return bad ? TFS_EXIT_CHECK_CRC_ERROR : TFS_SUCCESS;
+}
+
 static int packet_host(tfs_crc_ctx* ctx, int mode, const tfs_packet_desc* d, uint32_t n, void* base,
                        uint64_t base_len, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad) {
   if (!ctx || (n && (!d || !base))) return TFS_EXIT_PARAMETER_ERROR;
   if (n_bad) *n_bad = 0;
   if (n == 0) return TFS_SUCCESS;
+  {
+    uint64_t lo = 0, hi = 0;
+    if (ctx->variant == 0 && n <= kWgMaxFiles && span_of(d, n, base_len, &lo, &hi) && hi - lo <= kZeroCopySpan)
+      return packet_host_small(ctx, mode, d, n, base, base_len, out_crc, out_status, n_bad);
+  }
   std::lock_guard<std::mutex> g(ctx->mu);
   if (const int f = injected_fault(ctx)) return f;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
