@@ -157,3 +157,21 @@ def test_resident_process_exit_right_after_a_call():
     for _ in range(3):
         r = subprocess.run([sys.executable, "-c", code], timeout=120, capture_output=True)
         assert r.returncode == 0, r.stderr[-2000:]
+
+
+def test_resident_contexts_created_and_destroyed_in_turn(oracle):
+    """Contexts made and destroyed one after another (page-locked completion memory
+    recycled between them): every result of every call is this call's own --
+    sequence numbers are process-wide and completion words start zeroed."""
+    import tfs_amd.crc as crc
+    rng = np.random.default_rng(34)
+    for c in range(8):
+        ctx = crc.Context(0)
+        try:
+            for it in range(40):
+                n = int(rng.integers(1, 6))
+                buf, offs, lens = _random_batch(rng, n, maxlen=300000, seed=900 + 40 * c + it)
+                seeds = rng.integers(0, 2**32, n).astype(np.uint32)
+                assert (ctx.batch(buf, offs, lens, seeds) == _oracle_batch(oracle, buf, offs, lens, seeds)).all(), (c, it)
+        finally:
+            ctx.close()
