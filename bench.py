@@ -812,20 +812,25 @@ def bench_compact(args):
     # block, kernel device to device, D2H of the new block) on the same jobs.
     os.environ["TFS_CRC_VARIANT"] = "8"
     ctx_dma = crc.Context(local)
+    os.environ["TFS_CRC_VARIANT"] = "38"  # live records read in place, the new block back by DMA
+    ctx_hyb = crc.Context(local)
     os.environ["TFS_CRC_VARIANT"] = "0"
     nab = min(nblocks, 512)
     ab_jobs = (crc.BlockJob * nab)(*jobs[:nab])
-    ctx_dma.blocks_compact(warm)
-    if not (dests[0].array[:w] == odest[:w]).all():
-        raise SystemExit("compact: DMA form disagrees with oracle")
+    for c in (ctx_dma, ctx_hyb):
+        dests[0].array[:] = 0
+        c.blocks_compact(warm)
+        if not (dests[0].array[:w] == odest[:w]).all():
+            raise SystemExit("compact: DMA / hybrid form disagrees with oracle")
     ab = {}
-    for name, c in (("dma", ctx_dma), ("zero_copy", ctx)):
+    for name, c in (("dma", ctx_dma), ("zero_copy", ctx), ("zc_read_dma_write", ctx_hyb)):
         if dist:
             dist.barrier()
         t0 = time.perf_counter()
         c.blocks_compact(ab_jobs)
         ab[name + "_ms_per_block"] = _max_over_ranks(dist, time.perf_counter() - t0) / nab * 1e3
     ctx_dma.close()
+    ctx_hyb.close()
     for s in [int(x) for x in args.slots.split(",") if x]:  # blocks in flight (measurement knob)
         os.environ["TFS_CRC_COMPACT_SLOTS"] = str(s)
         cs = crc.Context(local)

@@ -177,6 +177,8 @@ constexpr int kCompactSlots = 8;          // slots allocated; ctx->compact_slots
 constexpr uint32_t kSchedSlots = 256;
 constexpr int kVariantUnfusedCompact = 7;  // TFS_CRC_VARIANT=7: two-pass device compaction (A/B baseline)
 constexpr int kVariantDmaCompact = 8;      // TFS_CRC_VARIANT=8: DMA staging for host compaction / block verify / small batches
+constexpr int kVariantZcReadDmaWrite = 38; // TFS_CRC_VARIANT=38: host compaction reads live records in place, the
+                                           // new block goes to device memory and back by a DMA copy
 constexpr uint64_t kZeroCopySpan = 8ull << 20;  // page-locked batches up to this span are read in place
 
 }  // namespace
@@ -1059,12 +1061,19 @@ static int compact_enqueue(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job
   HIP_TRY(ctx, cs.h_status.reserve(fb + 4));
   if (zc) {
     HIP_TRY(ctx, hipMemcpyAsync(da, ha, ob + mb + fb, hipMemcpyHostToDevice, cs.stream));
+    uint8_t* kdst = static_cast<uint8_t*>(zc_dst);
+    const bool dma_write = ctx->variant == kVariantZcReadDmaWrite;
+    if (dma_write) {
+      HIP_TRY(ctx, cs.d_dst.reserve(uint64_t(w) + 16));
+      kdst = static_cast<uint8_t*>(cs.d_dst.p);
+    }
     uint32_t* sched = nullptr;
     HIP_TRY(ctx, sched_slot(ctx, cs.stream, &sched));
     HIP_TRY(ctx, launch_compact_fused(static_cast<const uint8_t*>(zc_src), job->src_len, d_metas, d_flags, d_doff, nl,
-                                      static_cast<uint8_t*>(zc_dst), ctx->d_tables, d_crc, d_status, nullptr, sched,
-                                      cs.stream, ctx->variant));
+                                      kdst, ctx->d_tables, d_crc, d_status, nullptr, sched, cs.stream, ctx->variant));
     HIP_TRY(ctx, hipMemcpyAsync(cs.h_status.p, d_status, fb, hipMemcpyDeviceToHost, cs.stream));
+    if (dma_write && w)
+      HIP_TRY(ctx, hipMemcpyAsync(job->dest_image, cs.d_dst.p, size_t(w), hipMemcpyDeviceToHost, cs.stream));
   } else {
     const int rc = compact_dma(ctx, cs, job, nl, w, da, ha, ob + mb + fb, d_metas, d_flags, d_doff, d_crc, d_status);
     if (rc != TFS_SUCCESS) return rc;
