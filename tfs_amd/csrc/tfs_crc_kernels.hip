@@ -440,11 +440,19 @@ __device__ __forceinline__ void store_bshift(uintptr_t chunk, uintptr_t own, con
 // NTS: non-temporal copy-through stores (product).  NOCRC (measurement only,
 // TFS_CRC_VARIANT=26: wrong CRCs): skip the payload steps, so the record kernel
 // runs its own load/store schedule without the table lookups.
+// XF (cross-file ring): a slot freed past this file's last stripe is refilled
+// with the NEXT file's stripe (`ng`) that the slot holds in that file's ring
+// (slot f always holds stripes congruent to 1 + f mod PF), so the next file's
+// first PF stripes are in flight while this one drains, and on return the ring
+// is the next file's.  Without XF those slots read the L2-resident `junk`
+// region and the caller issues the next file's ring after this one ends.
 template <int RUN, int PF, bool NT, bool S8, bool COPY = false, int G = 1, bool DPPSH = false, int NTS = 1,
-          bool NOCRC = false, bool HEADST = true, bool BSU = false>
+          bool NOCRC = false, bool HEADST = true, bool BSU = false, bool XF = false>
 __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase& lb, const FileGeo<RUN>& g,
                                                const Head<RUN>& h, uint4 (&buf)[PF][RUN / 16], int lane,
-                                               uintptr_t junk, intptr_t delta = 0, bool copy_on = false) {
+                                               uintptr_t junk, intptr_t delta = 0, bool copy_on = false,
+                                               const FileGeo<RUN>* ng = nullptr) {
+  static_assert(!XF || G == 1, "the cross-file ring refills one slot at a time");
   constexpr uint32_t kStripe = 64u * RUN;
   constexpr int kVec = RUN / 16;
   // Stripe 0: mask the bytes before `start` in the dword at A and inject the
@@ -522,17 +530,25 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
         if ((f + 1) % G == 0) {
 #pragma unroll
           for (int q = f + 1 - G; q <= f; ++q) {
-            const uintptr_t sb = stripe_base<RUN>(g, r + q + PF, junk) + uintptr_t(lane) * RUN;
+            const uint32_t t = r + uint32_t(q) + uint32_t(PF);
+            const uintptr_t sb = (XF && t >= g.nstripes ? stripe_base<RUN>(*ng, 1u + uint32_t(q), junk)
+                                                         : stripe_base<RUN>(g, t, junk)) +
+                                 uintptr_t(lane) * RUN;
 #pragma unroll
             for (int v = 0; v < kVec; ++v) buf[q][v] = ld128s<NT>(sb + 16u * v);
           }
         }
       }
     }
-    // Remaining 0..PF-1 stripes are already in buf[0..].
+    // Remaining 0..PF-1 stripes are already in buf[0..].  XF: each slot then
+    // takes the next file's stripe -- after its last use here, or now if the
+    // main loop never ran (a slot past the end still holds `junk`; when the loop
+    // ran, its last pass refilled every slot past the end already).
+    const bool ran = r > 1u;
 #pragma unroll
-    for (int f = 0; f < PF - 1; ++f) {
-      if (r + f < g.nstripes) {
+    for (int f = 0; f < PF; ++f) {
+      const bool use = f < PF - 1 && r + f < g.nstripes;  // at most PF - 1 stripes are left
+      if (use) {
         const uint32_t c_old = c;
         c = shift_stripe<S8>(T, c);
         if (f == 0) c ^= inj;
@@ -541,7 +557,14 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
         c = (r + f == last && !lane_in_last) ? c_old : c;
         if (COPY && copy_on) copy_stripe(r + f, buf[f][0]);
       }
+      if (XF && (use || !ran)) {
+        const uintptr_t sb = stripe_base<RUN>(*ng, 1u + uint32_t(f), junk) + uintptr_t(lane) * RUN;
+#pragma unroll
+        for (int v = 0; v < kVec; ++v) buf[f][v] = ld128s<NT>(sb + 16u * v);
+      }
     }
+  } else if (XF) {  // one stripe: the ring (all junk) becomes the next file's
+    load_ring<RUN, PF, NT>(*ng, lane, buf, junk);
   }
   return c;
 }
@@ -700,7 +723,7 @@ __device__ __forceinline__ void launch_exit(uint32_t* sched, uint32_t units, uin
 // and its first PF stripes are in flight while this file's lane chains are
 // combined, so HBM never waits on a file boundary.
 template <int MODE, int RUN, int PF, bool NT, bool DYN, bool S8, int G = 1, bool HV = false, bool IL = false,
-          int W = 1>
+          int W = 1, bool XF = false>
 __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __restrict__ base,
                                                            const Desc* __restrict__ desc, uint32_t n,
                                                            const Tables* __restrict__ tg, uint32_t* out_crc,
@@ -736,17 +759,23 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
   Desc nxt = fn < n ? desc[fn] : Desc{0, 0, 0};
   uint32_t jv = DYN && fn < n ? tk.issue(lane) : 0u;  // ticket of the file after next, in flight
   for (;;) {
-    const uint32_t c = g.nstripes ? lane_chain<RUN, PF, NT, S8, false, G>(lds_tables, lb, g, h, buf, lane, junk) : 0u;
-    // Start the next file's loads before combining this one.
     const bool more = fn < n;
-    FileGeo<RUN> ng = g;
-    Head<RUN> nh = h;
     const Desc ncur = nxt;
+    // XF: the next file's geometry first -- this file's ring refills run into it.
+    FileGeo<RUN> ng = XF ? make_geo<RUN>(more ? base + ncur.offset : reinterpret_cast<const uint8_t*>(junk),
+                                         more ? ncur.len : 0u, MODE == 0 ? ncur.aux : vseed)
+                         : g;
+    const uint32_t c =
+        g.nstripes ? lane_chain<RUN, PF, NT, S8, false, G, false, 1, false, true, false, XF>(
+                         lds_tables, lb, g, h, buf, lane, junk, 0, false, &ng)
+                   : 0u;
+    // Start the next file's loads before combining this one.
+    Head<RUN> nh = h;
     uint32_t fnn = n;
     if (more) {
-      ng = make_geo<RUN>(base + ncur.offset, ncur.len, MODE == 0 ? ncur.aux : vseed);
+      if (!XF) ng = make_geo<RUN>(base + ncur.offset, ncur.len, MODE == 0 ? ncur.aux : vseed);
       nh = load_head<RUN, HV>(ng, lane);
-      load_ring<RUN, PF, NT>(ng, lane, buf, junk);
+      if (!XF || !g.nstripes) load_ring<RUN, PF, NT>(ng, lane, buf, junk);
       fnn = DYN ? tk.resolve(jv, lane) : fn + stride;
       if (fnn < n) nxt = desc[fnn];
       if (DYN && fnn < n) jv = tk.issue(lane);
@@ -1786,6 +1815,14 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
     case 16:
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, true, 4>), grid, block, 0, stream,
                          base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
+      break;
+    case 17:  // cross-file ring (lane_chain XF): the next file's first stripes refill this file's freed slots
+      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, true>), grid, block, 0,
+                         stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
+      break;
+    case 18:  // cross-file ring, PF 6
+      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, 6, kNT, kDYN, kS8, 1, false, kIL, 1, true>), grid, block, 0,
+                         stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
       break;
     case 14:  // contiguous ticket groups (the product before interleaving)
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, false>), grid, block, 0, stream,
