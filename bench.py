@@ -1924,7 +1924,7 @@ def bench_loopback(args):
     res["roofline"] = {"bound": "pcie", "achieved": reps * pcie_bytes / el / 1e9, "peak": ceil["h2d_GBs"],
                        "unit": "GB/s (per GPU)", "frac": reps * pcie_bytes / el / 1e9 / ceil["h2d_GBs"],
                        "traffic": None, "peak_source": ceil["source"],
-                       "kernel": "crc_wg_kernel<1> (close batches) + block_verify_kernel (zero-copy)",
+                       "kernel": "crc_resident_kernel (close batches, no launch per batch) + compact_pipe_kernel verify form (whole block, zero-copy)",
                        "note": "latency-bound: one GPU round trip per batch of concurrent closes"}
     if rank == 0 and world == 1 and not args.no_cpu:
         # CPU legs (test infrastructure): the restated loop of config 1 with the
