@@ -348,7 +348,7 @@ def _stripe_edge_cases(run, count=24):
     return out[:count]
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 20, 21])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21])
 def test_kernel_variants_parity(oracle, variant, monkeypatch):
     """Every compiled (RUN, PF) variant is bit-exact, including the stripe-0 seed edge."""
     import tfs_amd.crc as crc
@@ -371,7 +371,7 @@ def test_kernel_variants_parity(oracle, variant, monkeypatch):
         ctx.close()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 4, 10, 13, 14, 15, 16, 17, 18, 20])
+@pytest.mark.parametrize("variant", [0, 1, 4, 10, 13, 14, 15, 16, 17, 18, 19, 20])
 def test_cross_file_pipeline_many_files(oracle, variant, monkeypatch):
     """> 4096 files so every wave runs a sequence of files of mixed geometry
     (tiny / single-stripe / multi-stripe, any alignment, any seed): exercises

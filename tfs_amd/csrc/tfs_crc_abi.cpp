@@ -1490,6 +1490,18 @@ int tfs_crc32_dev_malloc(tfs_crc_ctx* ctx, uint64_t bytes, void** d_ptr) {
   if (!ctx || !d_ptr) return TFS_EXIT_PARAMETER_ERROR;
   *d_ptr = nullptr;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
+  // TFS_CRC_DEV_CONTIG=1 (measurement): physically contiguous memory, so the
+  // page tables can map it with the largest fragments (fewer address-translation
+  // misses for a scan over tens of GiB); ordinary memory when that fails.
+  static const bool contig = [] {
+    const char* v = getenv("TFS_CRC_DEV_CONTIG");
+    return v && atoi(v) != 0;
+  }();
+  if (contig && bytes >= (64ull << 20)) {
+    if (hipExtMallocWithFlags(d_ptr, bytes, hipDeviceMallocContiguous) == hipSuccess) return TFS_SUCCESS;
+    (void)hipGetLastError();
+    *d_ptr = nullptr;
+  }
   HIP_TRY(ctx, hipMalloc(d_ptr, bytes ? bytes : 1));
   return TFS_SUCCESS;
 }

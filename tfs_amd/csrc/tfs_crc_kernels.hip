@@ -722,8 +722,12 @@ __device__ __forceinline__ void launch_exit(uint32_t* sched, uint32_t units, uin
 // Files are software-pipelined per wave: the next file's stripe-0/tail words
 // and its first PF stripes are in flight while this file's lane chains are
 // combined, so HBM never waits on a file boundary.
+// BLK (measurement, with DYN = false): wave w takes the contiguous files
+// [w*per, (w+1)*per) instead of w, w+W, ... -- each CU's waves then walk a few
+// long sequential ranges (few address-translation misses) instead of files
+// spread over the whole moving window.
 template <int MODE, int RUN, int PF, bool NT, bool DYN, bool S8, int G = 1, bool HV = false, bool IL = false,
-          int W = 1, bool XF = false>
+          int W = 1, bool XF = false, bool BLK = false>
 __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __restrict__ base,
                                                            const Desc* __restrict__ desc, uint32_t n,
                                                            const Tables* __restrict__ tg, uint32_t* out_crc,
@@ -739,12 +743,20 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
   Tickets<IL, W> tk{sched, n, blockIdx.x & 7u};
   tk.init_static(stride, blockIdx.x * wpb + wave);
   uint32_t bad = 0;
+  const uint32_t blk_per = (n + stride - 1u) / stride;
+  const uint32_t blk_end =
+      BLK ? uint32_t(min(uint64_t(n), (uint64_t(blockIdx.x) * wpb + wave + 1u) * uint64_t(blk_per))) : n;
   do {  // `break` = this wave has no (more) files; every wave reaches launch_exit
   uint32_t f, fn;
   if (DYN) {
     f = tk.resolve(tk.issue(lane), lane);
     if (f >= n) break;
     fn = tk.resolve(tk.issue(lane), lane);
+  } else if (BLK) {
+    const uint64_t f0 = (uint64_t(blockIdx.x) * wpb + wave) * uint64_t(blk_per);
+    if (f0 >= uint64_t(blk_end)) break;
+    f = uint32_t(f0);
+    fn = f + 1u < blk_end ? f + 1u : n;
   } else {
     f = blockIdx.x * wpb + wave;
     if (f >= n) break;
@@ -776,7 +788,7 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
       if (!XF) ng = make_geo<RUN>(base + ncur.offset, ncur.len, MODE == 0 ? ncur.aux : vseed);
       nh = load_head<RUN, HV>(ng, lane);
       if (!XF || !g.nstripes) load_ring<RUN, PF, NT>(ng, lane, buf, junk);
-      fnn = DYN ? tk.resolve(jv, lane) : fn + stride;
+      fnn = DYN ? tk.resolve(jv, lane) : (BLK ? (fn + 1u < blk_end ? fn + 1u : n) : fn + stride);
       if (fnn < n) nxt = desc[fnn];
       if (DYN && fnn < n) jv = tk.issue(lane);
     }
@@ -1815,6 +1827,10 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
     case 16:
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, true, 4>), grid, block, 0, stream,
                          base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
+      break;
+    case 19:  // static contiguous ranges per wave (BLK)
+      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, false, kS8, 1, false, kIL, 1, false, true>), grid, block,
+                         0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
       break;
     case 17:  // cross-file ring (lane_chain XF): the next file's first stripes refill this file's freed slots
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, true>), grid, block, 0,
