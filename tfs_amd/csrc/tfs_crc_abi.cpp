@@ -94,6 +94,7 @@ struct DevBuf {
 // the GPU writes while the host polls them (verdicts, completion flags).
 struct PinBuf {
   void* p = nullptr;
+  void* dev = nullptr;  // its device-visible address (looked up once per allocation)
   size_t cap = 0;
   bool coherent = false;
   hipError_t reserve(size_t bytes) {
@@ -109,12 +110,17 @@ struct PinBuf {
       // Completion words are compared with sequence numbers: recycled memory
       // must not hold one (0 is never a sequence number).
       if (coherent) memset(p, 0, want);
+      if (hipHostGetDevicePointer(&dev, p, 0) != hipSuccess) {
+        dev = nullptr;
+        (void)hipGetLastError();
+      }
     }
     return e;
   }
   void release() {
     if (p) (void)hipHostFree(p);
     p = nullptr;
+    dev = nullptr;
     cap = 0;
   }
 };
@@ -434,8 +440,8 @@ int resident_post(tfs_crc_ctx* ctx, Slot& s, int mode, const uint8_t* zb, const 
   for (const Slot& x : ctx->sync_slots)
     if (&x != &s && x.busy && x.resident && int32_t(P + n - kResUnits - x.res_first) > 0) return 1;
   HIP_TRY(ctx, s.h_res.reserve(size_t(n) * 8));
-  void* zres = nullptr;
-  HIP_TRY(ctx, hipHostGetDevicePointer(&zres, s.h_res.p, 0));
+  void* zres = s.h_res.dev;
+  if (!zres) return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "resident result words are not mapped");
   for (uint32_t i = 0; i < n; ++i) {
     ResUnit& u = H->units[(P + i) % kResUnits];
     u.addr = uint64_t(reinterpret_cast<uintptr_t>(zb + d[i].offset));
@@ -569,12 +575,10 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
     }
     HIP_TRY(ctx, s.h_desc.reserve(size_t(n) * sizeof(Desc)));
     memcpy(s.h_desc.p, d, size_t(n) * sizeof(Desc));
-    void *zb = nullptr, *zd = nullptr, *zcrc = nullptr, *zok = nullptr, *zflag = nullptr;
-    if (hipHostGetDevicePointer(&zb, host_span, 0) == hipSuccess &&
-        hipHostGetDevicePointer(&zd, s.h_desc.p, 0) == hipSuccess &&
-        hipHostGetDevicePointer(&zcrc, s.h_crc.p, 0) == hipSuccess &&
-        hipHostGetDevicePointer(&zok, s.h_ok.p, 0) == hipSuccess &&
-        hipHostGetDevicePointer(&zflag, s.h_flag.p, 0) == hipSuccess) {
+    void *zb = nullptr, *zd = s.h_desc.dev, *zcrc = s.h_crc.dev, *zok = s.h_ok.dev, *zflag = s.h_flag.dev;
+    if (host_span == s.h_data.p) zb = s.h_data.dev;
+    else if (hipHostGetDevicePointer(&zb, host_span, 0) != hipSuccess) zb = nullptr;
+    if (zb && zd && zcrc && zok && zflag) {
       s.seq = g_flag_seq.fetch_add(1) + 1u;
       if (s.seq == 0) s.seq = g_flag_seq.fetch_add(1) + 1u;  // 0 is the words' initial value
       if (job >= 0 && ctx->resident && ctx->variant == 0 && n <= kWgMaxFiles) {
