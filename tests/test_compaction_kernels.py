@@ -13,7 +13,7 @@ from test_gpu_parity import _block_image, _oracle_compact
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[0, 22, 23, 25, 27, 29, 31, 32, 33, 35, 36, 37])
+@pytest.fixture(params=[0, 22, 23, 25, 27, 29, 31, 32, 33, 35, 36, 37, 39, 40, 42, 43, 45])
 def vctx(request, monkeypatch):
     import tfs_amd.crc as crc
     monkeypatch.setenv("TFS_CRC_VARIANT", str(request.param))
@@ -149,7 +149,7 @@ def test_zero_copy_host_images(vctx, oracle):
         dst.free()
 
 
-@pytest.fixture(params=[0, 24])
+@pytest.fixture(params=[0, 24, 50])
 def vfy_ctx(request, monkeypatch):
     """Verify-on-read forms: the pipelined record kernel (product) and round 1's
     grid-stride block_verify_kernel (TFS_CRC_VARIANT=24)."""
@@ -237,3 +237,77 @@ def test_blocks_verify_device_many_blocks(gpu_ctx, oracle):
     gpu_ctx.sync()
     assert (d_s.download(np.int32, n) == want).all()
     assert int(d_b.download(np.uint32, 1)[0]) == int((want != 0).sum())
+
+
+@pytest.fixture(scope="module")
+def many_records(oracle):
+    """420 k short records (1..300-byte payloads) in one image, every third deleted:
+    enough records per wave for the dynamic-ticket path with chunks of up to 4."""
+    import tfs_amd.crc as crc
+    from tfs_amd.synth import synth_bytes
+    rng = np.random.default_rng(350)
+    n = 420_000
+    sizes = rng.integers(1, 301, n)
+    recs = sizes + 36
+    offs = np.concatenate([[0], np.cumsum(recs)[:-1]]).astype(np.int64)
+    img = synth_bytes(351, int(recs.sum()) + 64).copy()
+    d = np.zeros(n, crc.DESC_DTYPE)
+    d["offset"], d["len"] = offs + 36, sizes
+    c = np.zeros(n, np.uint32)
+    oracle.oracle_crc_batch(d.ctypes.data, n, img.ctypes.data, c.ctypes.data)
+    fi = np.zeros(n, crc.FILEINFO_DTYPE)
+    fi["id_"] = 1000 + np.arange(n)
+    fi["offset_"] = offs
+    fi["size_"] = fi["usize_"] = recs
+    fi["crc_"] = c
+    img[offs[:, None] + np.arange(36)[None, :]] = fi.view(np.uint8).reshape(n, 36)
+    metas = np.zeros(n, crc.META_DTYPE)
+    metas["file_id"], metas["offset"], metas["size"] = 1000 + np.arange(n), offs, recs
+    fl = np.zeros(n, np.int32)
+    fl[1::3] = 1
+    return img, metas, fl, c
+
+
+@pytest.fixture(params=[0, 39, 40, 42, 43, 45, 47, 48, 50])
+def chunk_ctx(request, monkeypatch):
+    """The product record kernel and its chunked-ticket forms (TFS_CRC_VARIANT
+    39-45: 2, 4, 4 + single tail, 4 + longer single tail, 3 records per ticket)."""
+    import tfs_amd.crc as crc
+    monkeypatch.setenv("TFS_CRC_VARIANT", str(request.param))
+    ctx = crc.Context(0)
+    monkeypatch.setenv("TFS_CRC_VARIANT", "0")
+    yield ctx
+    ctx.close()
+
+
+def test_dynamic_tickets_many_records(chunk_ctx, oracle, many_records):
+    """Compaction (jobs form) and verify-on-read (jobs form) over 280 k / 420 k
+    records in one launch each: byte-exact against the oracle's real_compact and
+    its CRCs, every status 0."""
+    import tfs_amd.crc as crc
+    img, metas, fl, c = many_records
+    odest, doff, ook = _oracle_compact(oracle, img, metas, fl)
+    live = np.nonzero(fl == 0)[0]
+    j = np.zeros(live.size, crc.COMPACT_JOB_DTYPE)
+    j["src_offset"], j["dest_offset"] = metas["offset"][live], doff[live]
+    j["file_id"], j["size"], j["new_offset"] = metas["file_id"][live], metas["size"][live], doff[live]
+    d_src = crc.DeviceBuffer(chunk_ctx, img.size + 64).upload(img)
+    d_j = crc.DeviceBuffer(chunk_ctx, j.nbytes).upload(j)
+    d_dst = crc.DeviceBuffer(chunk_ctx, odest.size + 64)
+    d_dst.zero()
+    d_st = crc.DeviceBuffer(chunk_ctx, 4 * len(metas))
+    d_c = crc.DeviceBuffer(chunk_ctx, 4 * len(metas))
+    d_bad = crc.DeviceBuffer(chunk_ctx, 4)
+    d_bad.zero()
+    chunk_ctx.compact_jobs_device(d_src, img.size, d_j, live.size, d_dst, None, d_st, d_bad)
+    chunk_ctx.sync()
+    assert int(d_bad.download(np.uint32, 1)[0]) == 0 and (d_st.download(np.int32, live.size) == 0).all()
+    assert (d_dst.download(np.uint8, odest.size) == odest).all()
+    n = len(metas)
+    jv = np.zeros(n, crc.COMPACT_JOB_DTYPE)
+    jv["src_offset"], jv["file_id"], jv["size"] = metas["offset"], metas["file_id"], metas["size"]
+    d_jv = crc.DeviceBuffer(chunk_ctx, jv.nbytes).upload(jv)
+    chunk_ctx.blocks_verify_device(d_src, img.size, d_jv, n, d_c, d_st, d_bad)
+    chunk_ctx.sync()
+    assert int(d_bad.download(np.uint32, 1)[0]) == 0 and (d_st.download(np.int32, n) == 0).all()
+    assert (d_c.download(np.uint32, n) == c).all()

@@ -348,7 +348,8 @@ def _stripe_edge_cases(run, count=24):
     return out[:count]
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21,
+                                     39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 50])
 def test_kernel_variants_parity(oracle, variant, monkeypatch):
     """Every compiled (RUN, PF) variant is bit-exact, including the stripe-0 seed edge."""
     import tfs_amd.crc as crc
@@ -371,7 +372,7 @@ def test_kernel_variants_parity(oracle, variant, monkeypatch):
         ctx.close()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 4, 10, 13, 14, 15, 16, 17, 18, 19, 20])
+@pytest.mark.parametrize("variant", [0, 1, 4, 10, 13, 14, 15, 16, 17, 18, 19, 20, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 50])
 def test_cross_file_pipeline_many_files(oracle, variant, monkeypatch):
     """> 4096 files so every wave runs a sequence of files of mixed geometry
     (tiny / single-stripe / multi-stripe, any alignment, any seed): exercises
@@ -398,6 +399,32 @@ def test_cross_file_pipeline_many_files(oracle, variant, monkeypatch):
         oracle.oracle_crc_batch(d.ctypes.data, n, buf.ctypes.data, exp.ctypes.data)
         bad = np.nonzero(got != exp)[0]
         assert bad.size == 0, [(int(i), int(lens[i]), int(offs[i]) % 16, int(seeds[i])) for i in bad[:10]]
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("variant", [0, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 50])
+def test_dynamic_tickets_million_files(oracle, variant, monkeypatch):
+    """> 16 files (or chunks of CF files, variants 39-41) per wave, so the launch
+    takes the dynamic-ticket path with stealing across the eight groups: 1 M short
+    files of every length class below 300 bytes, any alignment and seed."""
+    import tfs_amd.crc as crc
+    monkeypatch.setenv("TFS_CRC_VARIANT", str(variant))
+    ctx = crc.Context(0)
+    try:
+        rng = np.random.default_rng(4040 + variant)
+        n = (1 << 20) + 777
+        lens = rng.integers(0, 300, n)
+        offs = np.cumsum(rng.integers(0, 8, n) + np.concatenate([[0], lens[:-1]])).astype(np.uint64)
+        buf = synth_bytes(9090 + variant, int(offs[-1] + lens[-1] + 64))
+        seeds = np.where(rng.integers(0, 2, n) == 0, 0, rng.integers(0, 2**32, n)).astype(np.uint32)
+        got = ctx.batch(buf, offs, lens, seeds)
+        d = np.zeros(n, crc.DESC_DTYPE)
+        d["offset"], d["len"], d["aux"] = offs, lens, seeds
+        exp = np.zeros(n, np.uint32)
+        oracle.oracle_crc_batch(d.ctypes.data, n, buf.ctypes.data, exp.ctypes.data)
+        bad = np.nonzero(got != exp)[0]
+        assert bad.size == 0, (variant, bad.size, [(int(i), int(lens[i])) for i in bad[:10]])
     finally:
         ctx.close()
 

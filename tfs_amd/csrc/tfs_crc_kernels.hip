@@ -625,6 +625,11 @@ constexpr bool kPAR = false;
 constexpr bool kDYN = true;
 constexpr bool kS8 = true;
 constexpr bool kIL = true;  // interleaved ticket groups (Tickets<IL>): +3 % Zipf, box-dependent +-3 % verify
+// Chunked tickets (FileCursor): 4 consecutive files per ticket, the last n/8 one
+// by one -- verify -2.8 to -3.8 %, Zipf -2.5 to -3.9 %, device block verify
+// -3.6 % against one file per ticket, in-process A/B on three boxes.
+constexpr int kCF = 4;
+constexpr int kTS = 3;
 
 // Work distribution.  Static: wave w takes files w, w+W, w+2W, ... (W = all
 // waves) -- ideal when every file has the same size.  Dynamic: eight ticket
@@ -696,6 +701,50 @@ struct Tickets {
   }
 };
 
+// A wave's walk over the files of a launch by tickets of CF consecutive files
+// (a wave that stays in one address range for several files reads
+// faster; all waves still take their chunks from one moving window).  Tickets
+// [0, nA) are chunks of CF files from file 0 on; with TS > 0 the last n >> TS
+// files come one per ticket (tickets [nA, nt)), so a chunk of large files
+// cannot become the launch's tail.  The ticket of the wave's next chunk is in
+// flight while it works through this one; every issued ticket is resolved
+// before take() returns n (launch_exit relies on that).
+template <bool IL, int W, int CF, int TS>
+struct FileCursor {
+  Tickets<IL, W> tk;
+  uint32_t n = 0, nA = 0, nt = 0, jv = 0, next = 0, end = 0;
+  bool done = false;
+  __device__ __forceinline__ void init(uint32_t* sched, uint32_t n_, uint32_t group, uint32_t waves_total,
+                                       uint32_t global_wave) {
+    n = n_;
+    nA = CF > 1 ? (TS > 0 ? (n - (n >> TS)) / uint32_t(CF) : (n + uint32_t(CF) - 1u) / uint32_t(CF)) : n;
+    nt = CF > 1 && TS > 0 ? nA + (n - nA * uint32_t(CF)) : nA;
+    tk.ctr = sched;
+    tk.n = nt;
+    tk.group = group;
+    tk.init_static(waves_total, global_wave);
+  }
+  __device__ __forceinline__ void start(int lane) { jv = tk.issue(lane); }
+  __device__ __forceinline__ uint32_t take(int lane) {  // next file of this wave, n = none left
+    if (next < end) return next++;
+    if (done) return n;
+    const uint32_t c = tk.resolve(jv, lane);
+    if (c >= nt) {
+      done = true;
+      return n;
+    }
+    if (c < nA) {
+      next = c * uint32_t(CF);
+      end = min(next + uint32_t(CF), n);
+    } else {
+      next = nA * uint32_t(CF) + (c - nA);
+      end = next + 1u;
+    }
+    jv = tk.issue(lane);
+    return next++;
+  }
+};
+
 // End of a launch (every wave, or every workgroup, calls this once, after its
 // last ticket atomic has returned): count it on the slot's finished line; the
 // last one zeroes the slot for the next launch on the same stream and, for a
@@ -726,8 +775,14 @@ __device__ __forceinline__ void launch_exit(uint32_t* sched, uint32_t units, uin
 // [w*per, (w+1)*per) instead of w, w+W, ... -- each CU's waves then walk a few
 // long sequential ranges (few address-translation misses) instead of files
 // spread over the whole moving window.
+// CF (measurement, with DYN): a ticket hands its wave CF consecutive files, so
+// each wave stays inside one address range for CF files (fewer translation
+// misses per CU) while all waves still read one moving window; the chunk
+// after this one is ticketed as soon as this one is taken.  TS > 0: the last
+// n >> TS files are ticketed one by one (chunks only while much work is left,
+// so a chunk of large files cannot become the launch's tail).
 template <int MODE, int RUN, int PF, bool NT, bool DYN, bool S8, int G = 1, bool HV = false, bool IL = false,
-          int W = 1, bool XF = false, bool BLK = false>
+          int W = 1, bool XF = false, bool BLK = false, int CF = 1, int TS = 0>
 __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __restrict__ base,
                                                            const Desc* __restrict__ desc, uint32_t n,
                                                            const Tables* __restrict__ tg, uint32_t* out_crc,
@@ -740,15 +795,22 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
   const uint32_t wpb = kBlock / kWave;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t stride = gridDim.x * wpb;
-  Tickets<IL, W> tk{sched, n, blockIdx.x & 7u};
-  tk.init_static(stride, blockIdx.x * wpb + wave);
+  FileCursor<IL, W, CF, TS> cur_files;
+  Tickets<IL, W>& tk = cur_files.tk;
+  cur_files.init(sched, n, blockIdx.x & 7u, stride, blockIdx.x * wpb + wave);
+  if (CF > 1 && DYN) cur_files.start(lane);
+  auto take = [&]() -> uint32_t { return cur_files.take(lane); };
   uint32_t bad = 0;
   const uint32_t blk_per = (n + stride - 1u) / stride;
   const uint32_t blk_end =
       BLK ? uint32_t(min(uint64_t(n), (uint64_t(blockIdx.x) * wpb + wave + 1u) * uint64_t(blk_per))) : n;
   do {  // `break` = this wave has no (more) files; every wave reaches launch_exit
   uint32_t f, fn;
-  if (DYN) {
+  if (DYN && CF > 1) {
+    f = take();
+    if (f >= n) break;
+    fn = take();
+  } else if (DYN) {
     f = tk.resolve(tk.issue(lane), lane);
     if (f >= n) break;
     fn = tk.resolve(tk.issue(lane), lane);
@@ -769,7 +831,7 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
   uint4 buf[PF][RUN / 16];
   load_ring<RUN, PF, NT>(g, lane, buf, junk);
   Desc nxt = fn < n ? desc[fn] : Desc{0, 0, 0};
-  uint32_t jv = DYN && fn < n ? tk.issue(lane) : 0u;  // ticket of the file after next, in flight
+  uint32_t jv = DYN && CF == 1 && fn < n ? tk.issue(lane) : 0u;  // ticket of the file after next, in flight
   for (;;) {
     const bool more = fn < n;
     const Desc ncur = nxt;
@@ -788,9 +850,10 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
       if (!XF) ng = make_geo<RUN>(base + ncur.offset, ncur.len, MODE == 0 ? ncur.aux : vseed);
       nh = load_head<RUN, HV>(ng, lane);
       if (!XF || !g.nstripes) load_ring<RUN, PF, NT>(ng, lane, buf, junk);
-      fnn = DYN ? tk.resolve(jv, lane) : (BLK ? (fn + 1u < blk_end ? fn + 1u : n) : fn + stride);
+      fnn = DYN ? (CF > 1 ? take() : tk.resolve(jv, lane))
+                : (BLK ? (fn + 1u < blk_end ? fn + 1u : n) : fn + stride);
       if (fnn < n) nxt = desc[fnn];
-      if (DYN && fnn < n) jv = tk.issue(lane);
+      if (DYN && CF == 1 && fnn < n) jv = tk.issue(lane);
     }
     const uint32_t crc = finish_file<RUN, S8>(lds_tables, lb, g, h, c, lane);
     if (lane == 0) {
@@ -1525,7 +1588,8 @@ __device__ __forceinline__ void copy_unaligned(const uint8_t* s, uint8_t* d, uin
 // of line-aligned alignbyte chunks (DIAG bit 6), 36 = sc1 copy-through stores
 // (DIAG bit 7).  CPF: stripes in flight per wave (variants 33-35, 37: 6, 7, 8, 4).
 constexpr int kCompactDiag = 4 | 8;
-template <bool WIDE, bool DPPSH = true, bool VERIFY = false, int DIAG = kCompactDiag, int CPF = kPF>
+template <bool WIDE, bool DPPSH = true, bool VERIFY = false, int DIAG = kCompactDiag, int CPF = kPF, int CF = 1,
+          int TS = 0>
 __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __restrict__ src, uint64_t src_len,
                                                               const RawMeta* __restrict__ metas,
                                                               const int32_t* __restrict__ flags,
@@ -1543,19 +1607,22 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
   const LaneBase lb = lane_base_of(lane);
   const uint32_t wpb = kBlock / kWave;
   const uintptr_t junk = reinterpret_cast<uintptr_t>(tg->slice);
-  Tickets<kIL> tk{sched, n, blockIdx.x & 7u};
-  tk.init_static(gridDim.x * wpb, blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave));
+  FileCursor<kIL, 1, CF, TS> fc;  // CF > 1: chunks of CF records per ticket (measurement)
+  Tickets<kIL>& tk = fc.tk;
+  fc.init(sched, n, blockIdx.x & 7u, gridDim.x * wpb,
+          blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave));
+  if (CF > 1) fc.start(lane);
   uint32_t bad = 0;
   do {
-    uint32_t f = tk.resolve(tk.issue(lane), lane);
+    uint32_t f = CF > 1 ? fc.take(lane) : tk.resolve(tk.issue(lane), lane);
     if (f >= n) break;
-    uint32_t fn = tk.resolve(tk.issue(lane), lane);
+    uint32_t fn = CF > 1 ? fc.take(lane) : tk.resolve(tk.issue(lane), lane);
     CRec cur = load_crec<WIDE, VERIFY>(f, src_len, metas, flags, dest_off, jobs);
     CState st = issue_crec<DA>(cur, src, src_len, dst, lane, junk);
     uint4 buf[CPF][kRun / 16];
     load_ring<kRun, CPF, LNT>(st.g, lane, buf, junk);
     CRec nxt = fn < n ? load_crec<WIDE, VERIFY>(fn, src_len, metas, flags, dest_off, jobs) : CRec{};
-    uint32_t jv = fn < n ? tk.issue(lane) : 0u;
+    uint32_t jv = CF == 1 && fn < n ? tk.issue(lane) : 0u;
     for (;;) {
       // DIAG bit 5 (variant 31, measurement): byte-shifted records copy after the CRC (copy_unaligned)
       const bool chain_copy = !(DIAG & 32) || (st.delta & 3) == 0;
@@ -1571,10 +1638,10 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
       if (more) {
         ns = issue_crec<DA>(ncur, src, src_len, dst, lane, junk);
         load_ring<kRun, CPF, LNT>(ns.g, lane, buf, junk);
-        fnn = tk.resolve(jv, lane);
+        fnn = CF > 1 ? fc.take(lane) : tk.resolve(jv, lane);
         if (fnn < n) {
           nxt = load_crec<WIDE, VERIFY>(fnn, src_len, metas, flags, dest_off, jobs);
-          jv = tk.issue(lane);
+          if (CF == 1) jv = tk.issue(lane);
         }
       }
       int32_t status = cur.pre;
@@ -1840,6 +1907,29 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, 6, kNT, kDYN, kS8, 1, false, kIL, 1, true>), grid, block, 0,
                          stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
       break;
+    case 39:  // CF: 2 consecutive files per ticket
+      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, 2>), grid,
+                         block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
+      break;
+    case 40:  // CF: 4 consecutive files per ticket
+      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, 4>), grid,
+                         block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
+      break;
+    case 41:  // CF: 16 consecutive files per ticket
+      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, 16>), grid,
+                         block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
+      break;
+#define TFS_LAUNCH_CF(CF, TS)                                                                                         \
+  hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, CF, TS>), grid, \
+                     block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq)
+    case 42: TFS_LAUNCH_CF(4, 3); break;  // chunks of 4, the last n/8 files one by one (= the product)
+    case 47: TFS_LAUNCH_CF(4, 4); break;  // chunks of 4, the last n/16 one by one
+    case 48: TFS_LAUNCH_CF(4, 5); break;  // chunks of 4, the last n/32 one by one
+    case 43: TFS_LAUNCH_CF(4, 2); break;  // chunks of 4, the last n/4 one by one
+    case 44: TFS_LAUNCH_CF(2, 3); break;  // chunks of 2, the last n/8 one by one
+    case 45: TFS_LAUNCH_CF(3, 0); break;  // chunks of 3
+    case 46: TFS_LAUNCH_CF(3, 3); break;  // chunks of 3, the last n/8 one by one
+#undef TFS_LAUNCH_CF
     case 14:  // contiguous ticket groups (the product before interleaving)
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, false>), grid, block, 0, stream,
                          base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
@@ -1847,9 +1937,14 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
 #define TFS_LAUNCH(R, P, N, D, S)                                                                          \
   hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N, D, S>), grid, block, 0, stream, base, desc, n, tg, out_crc, \
                      out_ok, n_bad, sched, vseed, done_flag, seq)
-    default:
+    case 50:  // one file per ticket (the product before chunked tickets)
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL>), grid, block, 0, stream,
                          base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
+      break;
+    default:
+      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, kCF, kTS>),
+                         grid, block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag,
+                         seq);
       break;
   }
 #undef TFS_LAUNCH
@@ -1942,6 +2037,11 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
   else if (variant == 35) TFS_CJ(true, true, false, kCompactDiag, 8);
   else if (variant == 36) TFS_CJ(true, true, false, kCompactDiag | 128);
   else if (variant == 37) TFS_CJ(true, true, false, kCompactDiag, 4);
+  else if (variant == 39) TFS_CJ(true, true, false, kCompactDiag, kPF, 2, 0);  // chunked tickets (as crc_files 39-45)
+  else if (variant == 40) TFS_CJ(true, true, false, kCompactDiag, kPF, 4, 0);
+  else if (variant == 42) TFS_CJ(true, true, false, kCompactDiag, kPF, 4, 3);
+  else if (variant == 43) TFS_CJ(true, true, false, kCompactDiag, kPF, 4, 2);
+  else if (variant == 45) TFS_CJ(true, true, false, kCompactDiag, kPF, 3, 0);
   else TFS_CJ(true);
 #undef TFS_CJ
   return hipGetLastError();
@@ -1954,15 +2054,30 @@ hipError_t launch_block_verify_pipe(const uint8_t* image, uint64_t image_len, co
                                     int32_t* out_status, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
                                     int variant) {
   if (n == 0) return hipSuccess;
-  if (jobs)
-    hipLaunchKernelGGL((compact_pipe_kernel<true, true, true>), dim3(grid_for(n)), dim3(kBlock), 0, stream, image,
-                       image_len, nullptr, nullptr, nullptr, jobs, n, nullptr, tg, out_crc, out_status, n_bad, sched);
+#define TFS_BV(...)                                                                                               \
+  hipLaunchKernelGGL((compact_pipe_kernel<true, true, true, kCompactDiag, kPF, __VA_ARGS__>), dim3(grid_for(n)),       \
+                     dim3(kBlock), 0, stream, image, image_len, nullptr, nullptr, nullptr, jobs, n, nullptr, tg, out_crc, \
+                     out_status, n_bad, sched)
+  if (jobs && variant == 39) TFS_BV(2, 0);  // chunked tickets (as crc_files 39-45)
+  else if (jobs && variant == 40) TFS_BV(4, 0);
+  else if (jobs && variant == 42) TFS_BV(4, 3);
+  else if (jobs && variant == 43) TFS_BV(4, 2);
+  else if (jobs && variant == 45) TFS_BV(3, 0);
+  else if (jobs && variant == 47) TFS_BV(4, 4);
+  else if (jobs && variant == 48) TFS_BV(4, 5);
+  else if (jobs && variant == 50) TFS_BV(1, 0);  // one record per ticket (the product before chunked tickets)
+  else if (jobs) TFS_BV(kCF, kTS);
+#undef TFS_BV
   else if (variant == 24 || !sched)
     hipLaunchKernelGGL(block_verify_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, image, image_len, metas, n, tg,
                        out_crc, out_status, n_bad);
-  else
+  else if (variant == 50)
     hipLaunchKernelGGL((compact_pipe_kernel<false, true, true>), dim3(grid_for(n)), dim3(kBlock), 0, stream, image,
                        image_len, metas, nullptr, nullptr, nullptr, n, nullptr, tg, out_crc, out_status, n_bad, sched);
+  else
+    hipLaunchKernelGGL((compact_pipe_kernel<false, true, true, kCompactDiag, kPF, kCF, kTS>), dim3(grid_for(n)),
+                       dim3(kBlock), 0, stream, image, image_len, metas, nullptr, nullptr, nullptr, n, nullptr, tg,
+                       out_crc, out_status, n_bad, sched);
   return hipGetLastError();
 }
 

@@ -15,7 +15,9 @@ by round, launches of
     shift) and mod 128 (whole destination lines per stripe), and on
     destinations one byte off (every record takes the unaligned copy),
 
-each timed with HIP events on its own context's stream.  The streaming-copy
+each timed with HIP events on its own context's stream.  With chunked-ticket
+variants (39-45) in AB_VARIANTS, verify-on-read of every resident record
+(tfs_blocks_verify_device) is timed for them and the product too.  The streaming-copy
 ceiling of the same bytes (membench pattern 52114) is timed in the same rounds.
 
   python tools/ab_compact.py [ROUNDS] [NBLOCKS]
@@ -89,6 +91,12 @@ def main():
     cases = [(0, "packed")] + [(v, "packed") for v in want if v not in (31, 32)] + [(0, "dst128")]
     if 31 in want or 32 in want:
         cases += [(0, "shift1")] + [(v, "shift1") for v in want if v in (31, 32)]
+    # verify-on-read of every record of the resident blocks (tfs_blocks_verify_device)
+    allj = np.zeros(n, crc.COMPACT_JOB_DTYPE)
+    allj["src_offset"], allj["file_id"], allj["size"] = rec_off, 1 + np.arange(n, dtype=np.uint64), rec
+    d_allj = crc.DeviceBuffer(ctx, allj.nbytes).upload(allj)
+    d_vst = crc.DeviceBuffer(ctx, 4 * n)
+    vcases = [0] + [v for v in want if v in (39, 40, 42, 43, 45, 47, 48, 50)]
     nj = int(k.size)
     live_bytes = float(nj) * rec
     algo = 2 * live_bytes + nj * (40 + 4)
@@ -104,6 +112,13 @@ def main():
             raise SystemExit("ab_compact: variant %d on %s reports bad records" % (v, js))
     times = {"%d_%s" % c: [] for c in cases}
     times["copy_52114"] = []
+    for v in vcases:
+        d_bad.zero()
+        ctxs[v].blocks_verify_device(img, total, d_allj, n, None, d_vst, d_bad)
+        ctxs[v].sync()
+        if int(d_bad.download(np.uint32, 1)[0]) != 0:
+            raise SystemExit("ab_compact: verify variant %d reports bad records" % v)
+        times["verify_%d" % v] = []
     cb = int(live_bytes) // 16 * 16
     for r in range(rounds):
         for v, js in cases:
@@ -116,6 +131,16 @@ def main():
             e1.record()
             c.sync()
             times["%d_%s" % (v, js)].append(e0.elapsed_ms(e1) / 3)
+        for v in vcases:
+            c = ctxs[v]
+            e0, e1 = crc.Event(c), crc.Event(c)
+            c.blocks_verify_device(img, total, d_allj, n, None, d_vst, d_bad)
+            e0.record()
+            for _ in range(3):
+                c.blocks_verify_device(img, total, d_allj, n, None, d_vst, d_bad)
+            e1.record()
+            c.sync()
+            times["verify_%d" % v].append(e0.elapsed_ms(e1) / 3)
         e0, e1 = crc.Event(ctx), crc.Event(ctx)
         ctx.membench_device(52114, img, None, 0, cb, d_dst)
         e0.record()
@@ -129,7 +154,7 @@ def main():
     for name, v in times.items():
         v = sorted(v)
         med = v[len(v) // 2]
-        by = 2.0 * cb if name.startswith("copy") else algo
+        by = 2.0 * cb if name.startswith("copy") else (n * (rec + 40 + 8) if name.startswith("verify") else algo)
         res[name] = {"median_ms": med, "min_ms": v[0], "max_ms": v[-1], "GBs": by / (med / 1e3) / 1e9,
                      "frac_8TBs": by / (med / 1e3) / 1e9 / 8000.0}
     print(json.dumps({"tool": "ab_compact", "rounds": rounds, "nblocks": nblocks, "records": nj,
