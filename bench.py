@@ -72,6 +72,10 @@ def parse():
     return p.parse_args()
 
 
+# The product verify kernel as rocprofv3 names it (profiles/pmc_latest.json is of this kernel).
+HEADLINE_KERNEL = "crc_files_kernel<1, 16, 5, true, true, true, 1, false, true, 1, false, false, 4, 3"
+
+
 def _pmc_traffic(rel, kernel, applies):
     """HBM bytes per launch from a committed rocprofv3 PMC summary of this same
     command at full size (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), or
@@ -308,14 +312,8 @@ def main():
 
     # HBM traffic per launch from the committed rocprofv3 PMC passes of this same
     # command (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; profiles/pmc_latest.json).
-    pmc = {}
-    try:
-        with open(os.path.join(ROOT, "profiles", "pmc_latest.json")) as fh:
-            pmc = json.load(fh)
-        if nfiles != 1048576 or os.environ.get("TFS_CRC_VARIANT", "0") != "0":
-            pmc = {}
-    except (OSError, ValueError):
-        pmc = {}
+    hv_traffic, hv_src = _pmc_traffic("profiles/pmc_latest.json", HEADLINE_KERNEL, nfiles == 1048576)
+    pmc = {"traffic_bytes_per_launch": hv_traffic, "source": hv_src} if hv_traffic else {}
     result = {
         "metric": "GiB/s CRC32 verify, device-resident 64 KiB files; 1/2/4/8 MI355X",
         "value": value,
@@ -1298,8 +1296,8 @@ def bench_block_verify_device(args):
     c24.close()
     algo_per_rec = FILEINFO + FILE_SIZE + 40 + 4 + 4   # header + payload + job read, crc + status written
     achieved = nfiles * algo_per_rec / (kms / 1e3) / 1e9
-    bv_traffic, bv_src = _pmc_traffic("profiles/r02_final/block_verify_device/pmc_summary.json",
-                                      "compact_pipe_kernel<true, true, true, 12, 5>", nblocks == 1024)
+    bv_traffic, bv_src = _pmc_traffic("profiles/r02_s4/block_verify_device/pmc_summary.json",
+                                      "compact_pipe_kernel<true, true, true, 12, 5, 4, 3", nblocks == 1024)
     res = {
         "metric": "GiB/s payload verified on read from device-resident block images (FileInfo checks + re-CRC)",
         "value": world * args.steps * nfiles * FILE_SIZE / el / 2**30, "unit": "GiB/s", "n_gpus": world,

@@ -37,11 +37,11 @@ fi
 if [[ $PART == all || $PART == compact ]]; then
 C=(--workload compact_device --no-cpu --steps 4 --warmup 1)
 run_trace compact "${C[@]}"
-for grp in FETCH_SIZE WRITE_SIZE; do run_pmc compact "$grp" "compact_pipe_kernel<true, true, false, 12, 5>" --workload compact_device --no-cpu --steps 1 --warmup 1; done
+for grp in FETCH_SIZE WRITE_SIZE; do run_pmc compact "$grp" "compact_pipe_kernel<true, true, false, 12, 5, 1, 0" --workload compact_device --no-cpu --steps 1 --warmup 1; done
 fi
 if [[ $PART == all || $PART == bverify ]]; then
 B=(--workload block_verify_device --no-cpu --steps 4 --warmup 1)
 run_trace bverify "${B[@]}"
-for grp in FETCH_SIZE WRITE_SIZE; do run_pmc bverify "$grp" "compact_pipe_kernel<true, true, true, 12, 5>" --workload block_verify_device --no-cpu --steps 1 --warmup 1; done
+for grp in FETCH_SIZE WRITE_SIZE; do run_pmc bverify "$grp" "compact_pipe_kernel<true, true, true, 12, 5, 4, 3" --workload block_verify_device --no-cpu --steps 1 --warmup 1; done
 fi
 echo "profile_r02 done"
