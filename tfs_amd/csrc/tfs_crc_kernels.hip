@@ -708,17 +708,25 @@ struct Tickets {
 // files come one per ticket (tickets [nA, nt)), so a chunk of large files
 // cannot become the launch's tail.  The ticket of the wave's next chunk is in
 // flight while it works through this one; every issued ticket is resolved
-// before take() returns n (launch_exit relies on that).
+// before take() returns n (launch_exit relies on that).  A launch too short
+// for dynamic tickets over chunks (fewer than kDynMinPerWave chunks per wave:
+// a block of 1,024 files, a small batch) takes single files as before, so its
+// files stay spread over all waves.
 template <bool IL, int W, int CF, int TS>
 struct FileCursor {
   Tickets<IL, W> tk;
-  uint32_t n = 0, nA = 0, nt = 0, jv = 0, next = 0, end = 0;
+  uint32_t n = 0, cf = 1, nA = 0, nt = 0, jv = 0, next = 0, end = 0;
   bool done = false;
   __device__ __forceinline__ void init(uint32_t* sched, uint32_t n_, uint32_t group, uint32_t waves_total,
                                        uint32_t global_wave) {
     n = n_;
+    cf = uint32_t(CF);
     nA = CF > 1 ? (TS > 0 ? (n - (n >> TS)) / uint32_t(CF) : (n + uint32_t(CF) - 1u) / uint32_t(CF)) : n;
     nt = CF > 1 && TS > 0 ? nA + (n - nA * uint32_t(CF)) : nA;
+    if (CF > 1 && uint64_t(nt) < uint64_t(kDynMinPerWave) * waves_total) {
+      cf = 1u;
+      nA = nt = n;
+    }
     tk.ctr = sched;
     tk.n = nt;
     tk.group = group;
@@ -734,10 +742,10 @@ struct FileCursor {
       return n;
     }
     if (c < nA) {
-      next = c * uint32_t(CF);
-      end = min(next + uint32_t(CF), n);
+      next = c * cf;
+      end = min(next + cf, n);
     } else {
-      next = nA * uint32_t(CF) + (c - nA);
+      next = nA * cf + (c - nA);
       end = next + 1u;
     }
     jv = tk.issue(lane);
