@@ -1602,6 +1602,30 @@ def bench_ec(args):
         kms = e0.elapsed_ms(e1) / args.steps
         out[name] = {"ms": kms, "GiBs_data": world * args.steps * k * size / el / 2**30,
                      "hbm_GBs": (rd + wr) * size / (kms / 1e3) / 1e9}
+    if args.ab:  # interleaved rounds of kernel forms (TFS_EC_VARIANT ids) in this process (stderr)
+        forms = [int(v) for v in args.ab.split(",") if v != ""]
+        encs = {}
+        for v in forms:
+            os.environ["TFS_EC_VARIANT"] = str(v)
+            encs[v] = ErasureCode(ctx, k, m)
+        os.environ["TFS_EC_VARIANT"] = "0"
+        times = {v: [] for v in forms}
+        for _ in range(args.ab_rounds):
+            for v in forms:
+                encs[v].encode_device(d, size)
+                e0, e1 = crc.Event(ctx), crc.Event(ctx)
+                e0.record()
+                for _ in range(3):
+                    encs[v].encode_device(d, size)
+                e1.record()
+                ctx.sync()
+                times[v].append(e0.elapsed_ms(e1) / 3)
+        ab = {}
+        for v in forms:
+            t = sorted(times[v])
+            ab[v] = {"median_ms": t[len(t) // 2], "min_ms": t[0],
+                     "frac_at_median": (k + m) * size / (t[len(t) // 2] / 1e3) / 1e9 / HBM_PEAK_GBS}
+        print(json.dumps({"ab": ab}), file=sys.stderr)
     res = {
         "metric": "GiB/s of data encoded (ErasureCode k=5 m=3, Cauchy bitmatrix w=8 ps=128), device-resident",
         "value": out["encode"]["GiBs_data"], "unit": "GiB/s", "n_gpus": world, "steps": args.steps,

@@ -174,3 +174,34 @@ def test_gpu_statuses_and_device_form(gpu_ctx, ec_oracle):
     gpu_ctx.sync()
     for i in (0, 2, 6):
         assert (d[i].download(np.uint8, size) == o[i]).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_gpu_kernel_forms_ragged_sizes(gpu_ctx, ec_oracle, variant, monkeypatch):
+    """Every kernel form (TFS_EC_VARIANT 0: grid-stride tiles; 1-3: chunks of 2, 4,
+    8 tiles per wave step with the cross-tile prefetch) on unit counts that leave
+    partial tiles, partial chunks and a grid stride larger than the work:
+    encode and a 3-member decode byte-exact against the oracle."""
+    from tfs_amd.ec import ErasureCode
+    monkeypatch.setenv("TFS_EC_VARIANT", str(variant))
+    k, m = 5, 3
+    for units in (1, 3, 5, 17, 33, 1031, 70001):
+        size = units * 1024
+        ms = members(k, m, size, 500 + units)
+        enc = ErasureCode(gpu_ctx, k, m)
+        assert enc.encode(ms, size) == 0
+        o = [a.copy() for a in ms]
+        for i in range(k, k + m):
+            o[i][:] = 0
+        assert o_encode(ec_oracle, k, m, o, size) == 0
+        for i in range(k, k + m):
+            assert (ms[i] == o[i]).all(), (variant, units, i)
+        er = [0, 1, 0, 0, 1, 0, 0, 1]
+        work = [np.zeros(size, np.uint8) if er[i] else ms[i].copy() for i in range(k + m)]
+        dec = ErasureCode(gpu_ctx, k, m, er)
+        assert dec.rc == 0 and dec.decode(work, size) == 0
+        for i in (1, 4, 7):
+            assert (work[i] == ms[i]).all(), (variant, units, i)
+        enc.free()
+        dec.free()

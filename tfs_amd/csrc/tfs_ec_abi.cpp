@@ -3,6 +3,7 @@
 // fallback: without a device every call fails with the ctx's error.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -35,6 +36,7 @@ struct tfs_ec {
   std::mutex mu;
   std::vector<void*> staging;  // host-form device buffers (dn+pn), grown on demand
   std::vector<uint64_t> staging_cap;
+  int variant = 0;  // kernel form (TFS_EC_VARIANT at creation, measurement knob; 0 = product)
 };
 
 namespace {
@@ -86,7 +88,7 @@ int run_plan(tfs_ec* ec, const Plan& p, void* const* members, int size, hipStrea
     a.masks = p.d_masks + o0 * 8 * size_t(S) * 8;
     a.S = uint32_t(S);
     a.units = units;
-    if (launch_ec_apply(a, og, st) != hipSuccess) return TFS_CRC_EXIT_DEVICE_ERROR;
+    if (launch_ec_apply(a, og, ec->variant, st) != hipSuccess) return TFS_CRC_EXIT_DEVICE_ERROR;
   }
   return TFS_SUCCESS;
 }
@@ -145,6 +147,7 @@ int tfs_ec_config(tfs_crc_ctx* ctx, int dn, int pn, const int* erased, tfs_ec** 
   ec->ctx = ctx;
   ec->dn = dn;
   ec->pn = pn;
+  if (const char* v = getenv("TFS_EC_VARIANT")) ec->variant = atoi(v);
   *out = ec;
   std::vector<int> data(dn), parity(pn);
   for (int j = 0; j < dn; ++j) data[j] = j;

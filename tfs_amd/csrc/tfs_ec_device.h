@@ -16,6 +16,6 @@ struct EcArgs {
   uint64_t units;         // size / 1024
 };
 
-hipError_t launch_ec_apply(const EcArgs& a, int og, hipStream_t stream);
+hipError_t launch_ec_apply(const EcArgs& a, int og, int variant, hipStream_t stream);
 
 }  // namespace tfsec

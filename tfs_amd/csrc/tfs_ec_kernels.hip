@@ -86,9 +86,97 @@ __global__ void __launch_bounds__(256) ec_apply_kernel(EcArgs a, const uint32_t*
   }
 }
 
-hipError_t launch_ec_apply(const EcArgs& a, int og, hipStream_t stream) {
+// Chunked form (K > 1): a wave takes K consecutive tiles (4K KiB of every
+// member) per step of its grid stride, and the next tile's first member is
+// loaded while the current tile's last member is combined, so the loads never
+// stop at a tile boundary inside a chunk.
+template <int OG, int K>
+__global__ void __launch_bounds__(256) ec_apply_chunk_kernel(EcArgs a, const uint32_t* __restrict__ masks) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t u = uint32_t(lane) >> 4;
+  const uint32_t off = 8u * uint32_t(lane & 15);
+  const uint64_t ntiles = (a.units + 3) / 4;
+  const uint64_t nchunks = (ntiles + K - 1) / K;
+  const uint64_t wave = uint64_t(blockIdx.x) * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t nwaves = uint64_t(gridDim.x) * (blockDim.x / 64);
+  for (uint64_t q = wave; q < nchunks; q += nwaves) {
+    const uint64_t t0 = q * K;
+    const uint64_t t1 = t0 + K < ntiles ? t0 + K : ntiles;
+    u32x2 in[8];
+    {
+      const uint64_t unit = t0 * 4 + u;
+      const bool ok = unit < a.units;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) in[c] = ok ? ld64nt(a.src[0] + unit * 1024u + off + 128u * c) : u32x2{0u, 0u};
+    }
+    for (uint64_t t = t0; t < t1; ++t) {
+      const uint64_t unit = t * 4 + u;
+      const bool ok = unit < a.units;
+      const uint64_t base = unit * 1024u + off;
+      const uint64_t nunit = unit + 4u;  // the next tile's unit of this lane
+      const bool nok = t + 1 < t1 && nunit < a.units;
+      u32x2 acc[OG][8];
+#pragma unroll
+      for (int o = 0; o < OG; ++o)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) acc[o][r] = u32x2{0u, 0u};
+      for (uint32_t s = 0; s < a.S; ++s) {
+        u32x2 nx[8];
+        const bool more = s + 1 < a.S;
+        const uint8_t* np = more ? a.src[s + 1] + base : a.src[0] + nunit * 1024u + off;
+        const bool lok = more ? ok : nok;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) nx[c] = lok ? ld64nt(np + 128u * c) : u32x2{0u, 0u};
+#pragma unroll
+        for (int o = 0; o < OG; ++o)
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const uint32_t* m = masks + ((uint32_t(o) * 8u + uint32_t(r)) * a.S + s) * 8u;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+              const uint32_t mk = m[c];
+              acc[o][r].x = xand(acc[o][r].x, in[c].x, mk);
+              acc[o][r].y = xand(acc[o][r].y, in[c].y, mk);
+            }
+          }
+#pragma unroll
+        for (int c = 0; c < 8; ++c) in[c] = nx[c];
+      }
+      if (ok) {
+#pragma unroll
+        for (int o = 0; o < OG; ++o)
+#pragma unroll
+          for (int r = 0; r < 8; ++r) st64nt(a.dst[o] + base + 128u * r, acc[o][r]);
+      }
+    }
+  }
+}
+
+template <int K>
+static void launch_chunk(const EcArgs& a, int og, dim3 g, dim3 b, hipStream_t stream) {
+  switch (og) {
+    case 1: hipLaunchKernelGGL((ec_apply_chunk_kernel<1, K>), g, b, 0, stream, a, a.masks); break;
+    case 2: hipLaunchKernelGGL((ec_apply_chunk_kernel<2, K>), g, b, 0, stream, a, a.masks); break;
+    case 3: hipLaunchKernelGGL((ec_apply_chunk_kernel<3, K>), g, b, 0, stream, a, a.masks); break;
+    default: hipLaunchKernelGGL((ec_apply_chunk_kernel<4, K>), g, b, 0, stream, a, a.masks); break;
+  }
+}
+
+// variant (TFS_EC_VARIANT, measurement): 0 the grid-stride tile kernel; 1, 2, 3
+// the chunked form with K = 2, 4, 8 tiles per wave step.
+hipError_t launch_ec_apply(const EcArgs& a, int og, int variant, hipStream_t stream) {
   if (a.units == 0) return hipSuccess;
   const uint64_t ntiles = (a.units + 3) / 4;
+  if (variant >= 1 && variant <= 3) {
+    const int K = 1 << variant;
+    uint64_t blocks = ((ntiles + K - 1) / K + 3) / 4;
+    if (blocks > 2048) blocks = 2048;
+    const dim3 g(static_cast<unsigned>(blocks)), b(256);
+    if (K == 2) launch_chunk<2>(a, og, g, b, stream);
+    else if (K == 4) launch_chunk<4>(a, og, g, b, stream);
+    else launch_chunk<8>(a, og, g, b, stream);
+    return hipGetLastError();
+  }
   uint64_t blocks = (ntiles + 3) / 4;
   if (blocks > 2048) blocks = 2048;
   const dim3 g(static_cast<unsigned>(blocks)), b(256);
