@@ -1945,6 +1945,15 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
 #define TFS_LAUNCH(R, P, N, D, S)                                                                          \
   hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N, D, S>), grid, block, 0, stream, base, desc, n, tg, out_crc, \
                      out_ok, n_bad, sched, vseed, done_flag, seq)
+#define TFS_LAUNCH_CX(P, IL_, CF, TS)                                                                                \
+  hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, P, kNT, kDYN, kS8, 1, false, IL_, 1, false, false, CF, TS>), grid,   \
+                     block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq)
+    case 51: TFS_LAUNCH_CX(kPF, false, kCF, kTS); break;  // chunked tickets over contiguous eighths
+    case 52: TFS_LAUNCH_CX(kPF, kIL, 8, kTS); break;      // chunks of 8
+    case 53: TFS_LAUNCH_CX(6, kIL, kCF, kTS); break;      // PF 6
+    case 54: TFS_LAUNCH_CX(4, kIL, kCF, kTS); break;      // PF 4
+    case 55: TFS_LAUNCH_CX(kPF, kIL, 6, kTS); break;      // chunks of 6
+#undef TFS_LAUNCH_CX
     case 50:  // one file per ticket (the product before chunked tickets)
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL>), grid, block, 0, stream,
                          base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
