@@ -2114,8 +2114,50 @@ hipError_t launch_synth_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, uint
   return hipGetLastError();
 }
 
+// Calibration: copy by wave-contiguous chunks of CH bytes (the record kernel's
+// shape: one wave streams one range), chunk c to wave c mod W; each wave moves
+// PF 1 KiB stripes per step (16 B per lane, nt loads, store kind SK).
+template <int PF, int SK>
+__global__ void __launch_bounds__(kBlock) membench_copy_chunk_kernel(const uint8_t* __restrict__ src,
+                                                                     uint8_t* __restrict__ dst, uint64_t nbytes,
+                                                                     uint64_t ch) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint64_t wave = uint64_t(blockIdx.x) * (kBlock / kWave) + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t nw = uint64_t(gridDim.x) * (kBlock / kWave);
+  const uint64_t nch = nbytes / ch;
+  const uintptr_t s = reinterpret_cast<uintptr_t>(src), d = reinterpret_cast<uintptr_t>(dst);
+  for (uint64_t c = wave; c < nch; c += nw) {
+    const uint64_t b = c * ch + 16u * uint64_t(lane);
+    for (uint64_t o = 0; o < ch; o += 1024u * PF) {
+      uint4 v[PF];
+#pragma unroll
+      for (int k = 0; k < PF; ++k) v[k] = ld128s<true>(s + b + o + 1024u * k);
+#pragma unroll
+      for (int k = 0; k < PF; ++k) {
+        const u32x4 w = {v[k].x, v[k].y, v[k].z, v[k].w};
+        gu128wp a = reinterpret_cast<gu128wp>(d + b + o + 1024u * k);
+        if (SK == 1) __builtin_nontemporal_store(w, a);
+        else *a = w;
+      }
+    }
+  }
+}
+
 hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, uint32_t n, uint64_t nbytes,
                            uint32_t* out, unsigned grid, hipStream_t stream) {
+  if (pattern >= 53000 && pattern < 54000) {
+    // 53SCC: chunked copy, S = store kind (0 plain, 1 nt), CC = chunk in 16 KiB units; PF 8, 256 workgroups
+    const int S = (pattern / 100) % 10, CC = pattern % 100;
+    const uint64_t ch = uint64_t(CC ? CC : 4) * 16384u;
+    const uint64_t nb = nbytes / ch * ch;
+    const dim3 g(grid ? grid : kMaxGrid);
+    uint8_t* d = reinterpret_cast<uint8_t*>(out);
+    if (S == 1)
+      hipLaunchKernelGGL((membench_copy_chunk_kernel<8, 1>), g, dim3(kBlock), 0, stream, base, d, nb, ch);
+    else
+      hipLaunchKernelGGL((membench_copy_chunk_kernel<8, 0>), g, dim3(kBlock), 0, stream, base, d, nb, ch);
+    return hipGetLastError();
+  }
   // pattern: 0 = coalesced, 16 = stripe pattern (run 16); +1000 = non-temporal loads;
   // +10000 = stripes anchored at 128-byte boundaries (else 16);
   // 50000 / 51000 = streaming copy of nbytes into `out` (default / non-temporal)

@@ -112,6 +112,9 @@ def main():
             raise SystemExit("ab_compact: variant %d on %s reports bad records" % (v, js))
     times = {"%d_%s" % c: [] for c in cases}
     times["copy_52114"] = []
+    copies = [53104, 53116, 53004, 53016]  # wave-contiguous chunks: nt / plain stores, 64 / 256 KiB
+    for pat in copies:
+        times["copy_%d" % pat] = []
     for v in vcases:
         d_bad.zero()
         ctxs[v].blocks_verify_device(img, total, d_allj, n, None, d_vst, d_bad)
@@ -149,6 +152,15 @@ def main():
         e1.record()
         ctx.sync()
         times["copy_52114"].append(e0.elapsed_ms(e1) / 3)
+        for pat in copies:
+            e0, e1 = crc.Event(ctx), crc.Event(ctx)
+            ctx.membench_device(pat, img, None, 0, cb, d_dst)
+            e0.record()
+            for _ in range(3):
+                ctx.membench_device(pat, img, None, 0, cb, d_dst)
+            e1.record()
+            ctx.sync()
+            times["copy_%d" % pat].append(e0.elapsed_ms(e1) / 3)
         print("round %d done" % r, file=sys.stderr, flush=True)
     res = {}
     for name, v in times.items():
