@@ -297,7 +297,8 @@ def main():
     extra = {}
     if args.membench:
         out = crc.DeviceBuffer(ctx, 16)
-        for pat, grid in ((1000, 0), (1000, 1024), (16, 0), (1016, 0), (10016, 0), (11016, 0)):
+        for pat, grid in ((1000, 0), (1000, 1024), (16, 0), (1016, 0), (10016, 0), (11016, 0), (54004, 0),
+                          (54016, 0), (54064, 0)):
             e0, e1 = crc.Event(ctx), crc.Event(ctx)
             ctx.membench_device(pat, img, d_vdesc, nfiles, total, out, grid=grid)
             e0.record()
@@ -306,7 +307,11 @@ def main():
             e1.record()
             ms = e0.elapsed_ms(e1) / 5
             run = pat % 1000
-            nb = total if run == 0 else nfiles * ((FILE_SIZE - 127) // (64 * run)) * 64 * run
+            if pat >= 54000:  # wave-contiguous chunks of (pat % 100) x 16 KiB over the whole image
+                ch = (pat % 100) * 16384
+                nb = total // ch * ch
+            else:
+                nb = total if run == 0 else nfiles * ((FILE_SIZE - 127) // (64 * run)) * 64 * run
             extra["membench_p%d_g%d_GBs" % (pat, grid)] = nb / (ms / 1e3) / 1e9
         print(json.dumps({"membench": extra}), file=sys.stderr)
 
