@@ -394,11 +394,20 @@ int resident_setup(tfs_crc_ctx* ctx) {
     return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "resident ring: hipHostGetDevicePointer failed");
   }
   void* st = nullptr;
-  if (hipMalloc(&st, kResStateBytes) != hipSuccess || hipMemset(st, 0, kResStateBytes) != hipSuccess ||
+  // The device state (done counts, exit line) is zeroed on the kernel's own stream
+  // and waited for: a recycled allocation may hold a previous context's counts,
+  // and a plain hipMemset on the null stream is not ordered before a kernel on a
+  // non-blocking stream (a stale done count makes a workgroup wait for a unit
+  // that is never posted while the host relaunches the kernel for its batch).
+  if (hipMalloc(&st, kResStateBytes) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->res_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMemsetAsync(st, 0, kResStateBytes, ctx->res_stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->res_stream) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->res_event, hipEventDisableTiming) != hipSuccess) {
     (void)hipHostFree(h);
     if (st) (void)hipFree(st);
+    if (ctx->res_stream) (void)hipStreamDestroy(ctx->res_stream);
+    ctx->res_stream = nullptr;
     return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "resident ring: device state allocation failed");
   }
   ctx->res_host = static_cast<ResHost*>(h);
@@ -713,11 +722,16 @@ int tfs_crc32_ctx_create(int device, tfs_crc_ctx** out) {
     build_tables(host.data());
     e = hipMalloc(reinterpret_cast<void**>(&ctx->d_tables), sizeof(Tables));
     if (e != hipSuccess) { rc = set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "hipMalloc(tables): %s", hipGetErrorString(e)); break; }
-    e = hipMemcpy(ctx->d_tables, host.data(), sizeof(Tables), hipMemcpyHostToDevice);
+    // The tables and the zeroed scheduler slots are written on the context's
+    // stream and waited for: the kernels run on non-blocking streams, which do
+    // not wait for work on the null stream, and a recycled allocation may still
+    // hold another context's counters.
+    e = hipMemcpyAsync(ctx->d_tables, host.data(), sizeof(Tables), hipMemcpyHostToDevice, ctx->stream);
     if (e != hipSuccess) { rc = set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "hipMemcpy(tables): %s", hipGetErrorString(e)); break; }
     e = hipMalloc(reinterpret_cast<void**>(&ctx->d_sched), size_t(kSchedSlots) * kSchedSlotBytes);
     if (e != hipSuccess) { rc = set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "hipMalloc(sched): %s", hipGetErrorString(e)); break; }
-    e = hipMemset(ctx->d_sched, 0, size_t(kSchedSlots) * kSchedSlotBytes);  // then kept zero by the kernels
+    e = hipMemsetAsync(ctx->d_sched, 0, size_t(kSchedSlots) * kSchedSlotBytes, ctx->stream);  // then kept zero by the kernels
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) { rc = set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "hipMemset(sched): %s", hipGetErrorString(e)); break; }
     ctx->sched_streams.push_back(ctx->stream);
   } while (0);
