@@ -477,12 +477,22 @@ int resident_post(tfs_crc_ctx* ctx, Slot& s, int mode, const uint8_t* zb, const 
 // relaunch it (under mu) when it left with this batch outstanding (idle or
 // lifetime exit racing the post).  Then the CRCs and verdicts go where
 // finish_slot reads them (the expected CRCs are in s.h_desc).
+// A workgroup takes its units in ring order, so units of other threads' batches
+// ahead of ours (at most kResUnits / grid per workgroup) may take a relaunch each.
+constexpr uint32_t kResMaxIdleRelaunches = 4u * kResUnits;
+
 int wait_resident(tfs_crc_ctx* ctx, Slot& s, int mode, uint32_t n) {
   const volatile uint64_t* res = static_cast<const volatile uint64_t*>(s.h_res.p);
+  // Every launch finishes at least one pending unit of each workgroup that has
+  // one before it can leave, so relaunches without a new result of this batch
+  // are bounded by the units queued ahead of it; past kResMaxIdleRelaunches in a
+  // row the wait ends with a device error.
   uint32_t i = 0, relaunches = 0;
   for (uint32_t spins = 1;; ++spins) {
+    const uint32_t i0 = i;
     while (i < n && uint32_t(res[i] >> 32) == s.seq) ++i;
     if (i == n) break;
+    if (i != i0) relaunches = 0;
     __builtin_ia32_pause();
     if ((spins & 255u) == 0) {
       const hipError_t e = hipEventQuery(ctx->res_event);
@@ -493,7 +503,7 @@ int wait_resident(tfs_crc_ctx* ctx, Slot& s, int mode, uint32_t n) {
         ctx->resident = false;  // as in resident_post
         return rc;
       }
-      if (ctx->res_launches != before && ++relaunches > 100000u) {
+      if (ctx->res_launches != before && ++relaunches > kResMaxIdleRelaunches) {
         ctx->resident = false;
         return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "resident kernel makes no progress (seq %u)", s.seq);
       }
