@@ -74,6 +74,8 @@ def parse():
 
 # The product verify kernel as rocprofv3 names it (profiles/pmc_latest.json is of this kernel).
 HEADLINE_KERNEL = "crc_files_kernel<1, 16, 5, true, true, true, 1, false, true, 1, false, false, 4, 3"
+PACKET_PIPELINE = ("packet pipeline: packet_parse_kernel + crc_files_kernel<1, ..., 4, 3> + "
+                   "packet_finish_kernel")
 
 
 def _pmc_traffic(rel, kernel, applies):
@@ -599,6 +601,8 @@ def bench_zipf(args):
     kms = float(np.mean([a.elapsed_ms(b) for a, b in ev]))
     payload = float(lens.astype(np.float64).sum())
     algo = payload + 21.0 * n
+    z_traffic, z_src = _pmc_traffic("profiles/r02_s4/zipf/pmc_summary.json", HEADLINE_KERNEL.replace("<1,", "<0,", 1),
+                                    nblocks == 1024 and not align)
     res = {
         "metric": "GiB/s CRC32 compute-on-write, device-resident Zipf 4 KiB-1 MiB files",
         "value": world * args.steps * payload / el / 2**30, "unit": "GiB/s", "n_gpus": world,
@@ -608,7 +612,8 @@ def bench_zipf(args):
         "config": {"workload": "BASELINE configs[2]: %d blocks x 64 MiB, %d files, mean %.1f KiB" % (
             nblocks, n, payload / n / 1024), "files_per_gpu": n},
         "roofline": {"bound": "hbm", "achieved": algo / (kms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": algo / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                     "frac": algo / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": z_traffic,
+                     "traffic_source": z_src, "algorithmic_bytes_per_launch": algo,
                      "kernel": "crc_files_kernel<0> (compute)", "kernel_ms_avg": kms},
     }
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -707,6 +712,7 @@ def bench_packet(args):
     # the CRC kernel reads the body and its descriptor and writes crc + ok; finish
     # reads pre-status/ok and writes status (and crc).
     algo = n * (float(frame) + 16 + 16 + 4 + 16 + 4 + 1 + 4 + 4 + 1 + 4)
+    p_traffic, p_src = _pmc_traffic("profiles/r02_s4/packet/pmc_summary.json", PACKET_PIPELINE, n == 1048576)
     res = {
         "metric": "GiB/s packet bytes CRC-verified (BasePacket::decode), device-resident V1 frames",
         "value": world * args.steps * n * frame / el / 2**30, "unit": "GiB/s", "n_gpus": world,
@@ -716,7 +722,8 @@ def bench_packet(args):
         "config": {"workload": "SURVEY §8 f1: %d V1 frames x %d B (64 KiB write + message fields)" % (n, frame),
                    "frames_per_gpu": n},
         "roofline": {"bound": "hbm", "achieved": algo / (kms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": algo / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                     "frac": algo / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": p_traffic,
+                     "traffic_source": p_src, "algorithmic_bytes_per_launch": algo,
                      "kernel": "packet_parse + crc_files_kernel<1> + packet_finish", "kernel_ms_avg": kms},
     }
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -1631,6 +1638,7 @@ def bench_ec(args):
             ab[v] = {"median_ms": t[len(t) // 2], "min_ms": t[0],
                      "frac_at_median": (k + m) * size / (t[len(t) // 2] / 1e3) / 1e9 / HBM_PEAK_GBS}
         print(json.dumps({"ab": ab}), file=sys.stderr)
+    e_traffic, e_src = _pmc_traffic("profiles/r02_s4/ec/pmc_summary.json", "ec_apply_kernel<3>", args.ec_mib == 1536)
     res = {
         "metric": "GiB/s of data encoded (ErasureCode k=5 m=3, Cauchy bitmatrix w=8 ps=128), device-resident",
         "value": out["encode"]["GiBs_data"], "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
@@ -1638,7 +1646,8 @@ def bench_ec(args):
         "vs_baseline": None, "dtype": "u8", "data": "synthetic (splitmix64) members",
         "config": {"workload": "SURVEY §8 f4: k=5 + m=3 members of %d MiB" % args.ec_mib},
         "roofline": {"bound": "hbm", "achieved": out["encode"]["hbm_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": out["encode"]["hbm_GBs"] / HBM_PEAK_GBS, "traffic": None,
+                     "frac": out["encode"]["hbm_GBs"] / HBM_PEAK_GBS, "traffic": e_traffic, "traffic_source": e_src,
+                     "algorithmic_bytes_per_launch": float(k + m) * size,
                      "kernel": "ec_apply_kernel<3>", "kernel_ms_avg": out["encode"]["ms"]},
         "decode": out["decode"],
     }

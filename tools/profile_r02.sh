@@ -4,7 +4,7 @@
 # PMC group in its own pass (FETCH_SIZE and WRITE_SIZE cannot share one; counters
 # never combined with other trace domains).  Outputs under gpurun_out/prof_r02/;
 # tools/pmc_summary.py folds them into profiles/r02/.
-# Usage: tools/profile_r02.sh [all|compact|verify|bverify] [outdir]
+# Usage: tools/profile_r02.sh [all|compact|verify|bverify|zipf|packet|ec] [outdir]
 set -euo pipefail
 PART=${1:-all}
 OUT=${2:-gpurun_out/prof_r02}
@@ -43,5 +43,21 @@ if [[ $PART == all || $PART == bverify ]]; then
 B=(--workload block_verify_device --no-cpu --steps 4 --warmup 1)
 run_trace bverify "${B[@]}"
 for grp in FETCH_SIZE WRITE_SIZE; do run_pmc bverify "$grp" "compact_pipe_kernel<true, true, true, 12, 5, 4, 3" --workload block_verify_device --no-cpu --steps 1 --warmup 1; done
+fi
+mkdir -p "$OUT/zipf" "$OUT/packet" "$OUT/ec"
+if [[ $PART == all || $PART == zipf ]]; then
+Z=(--workload zipf --no-cpu --steps 4 --warmup 1)
+run_trace zipf "${Z[@]}"
+for grp in FETCH_SIZE WRITE_SIZE; do run_pmc zipf "$grp" "crc_files_kernel<0" --workload zipf --no-cpu --steps 1 --warmup 1; done
+fi
+if [[ $PART == all || $PART == packet ]]; then
+P=(--workload packet --no-cpu --steps 4 --warmup 1)
+run_trace packet "${P[@]}"
+for grp in FETCH_SIZE WRITE_SIZE; do run_pmc packet "$grp" "packet_parse_kernel|crc_files_kernel<1|packet_finish_kernel" --workload packet --no-cpu --steps 1 --warmup 1; done
+fi
+if [[ $PART == all || $PART == ec ]]; then
+E=(--workload ec --no-cpu --steps 4 --warmup 1)
+run_trace ec "${E[@]}"
+for grp in FETCH_SIZE WRITE_SIZE; do run_pmc ec "$grp" "ec_apply_kernel<3>" --workload ec --no-cpu --steps 1 --warmup 1; done
 fi
 echo "profile_r02 done"
