@@ -41,10 +41,22 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--latest", action="store_true")
     ap.add_argument("--work", default="1,048,576 files x 64 KiB payload (block images, FileInfo|payload)")
+    ap.add_argument("--trace", help="kernel_trace.csv of the same command: also report the timed dispatches")
+    ap.add_argument("--skip", type=int, default=0, help="dispatches before the timed ones (warm-up)")
+    ap.add_argument("--count", type=int, default=0, help="timed dispatches")
     ap.add_argument("csvs", nargs="+", help="counter_collection.csv of each --pmc pass")
     a = ap.parse_args()
     c = counters(a.csvs, a.kernel)
     ks = kernel_stats(a.stats, a.kernel)
+    if a.trace and a.count:
+        # The --stats average includes the cold first dispatches; the bench line's
+        # HIP events time only the steps after its warm-up.
+        with open(a.trace) as fh:
+            d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) for r in csv.DictReader(fh)
+                 if a.kernel in r["Kernel_Name"]]
+        timed = d[a.skip:a.skip + a.count]
+        ks["timed_dispatches"] = {"skip": a.skip, "count": len(timed), "avg_ns": sum(timed) / len(timed),
+                                  "all_ns": d}
     read = c["FETCH_SIZE"] * 1024.0 * 2.0
     write = c.get("WRITE_SIZE", 0.0) * 1024.0
     res = {
@@ -57,6 +69,8 @@ def main():
         "algorithmic_bytes_per_launch": a.algo_bytes,
         "traffic_over_algorithmic": (read + write) / a.algo_bytes,
         "achieved_GBs_algorithmic_at_rocprof_avg": a.algo_bytes / (ks["avg_ns"] * 1e-9) / 1e9,
+        "achieved_GBs_algorithmic_at_rocprof_timed_avg": (a.algo_bytes / (ks["timed_dispatches"]["avg_ns"] * 1e-9) / 1e9
+                                                          if "timed_dispatches" in ks else None),
         "correction": "gfx950 FETCH_SIZE reports half the bytes of a wide coalesced stream "
                       "(MI355X_MICROARCH.md §HBM): x2; cross-checked by TCC_EA0_RDREQ x 128 B",
         "source": os.path.relpath(a.out, os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
