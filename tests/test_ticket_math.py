@@ -1,0 +1,51 @@
+"""Host restatement of the kernels' work split (tfs_crc_kernels.hip: Tickets<IL>
+and FileCursor<IL, W, CF, TS>): every ticket of the eight interleaved groups is
+handed out once, and the chunk/single mapping of chunked tickets covers every
+file of a launch exactly once -- for the long-launch (chunked) and the
+short-launch (one file per ticket) forms."""
+import numpy as np
+import pytest
+
+K_DYN_MIN_PER_WAVE = 16  # tfs_crc_device.h kDynMinPerWave
+
+
+def gcount(n, g):  # Tickets<true>::gcount
+    return (n - g + 7) >> 3 if n > g else 0
+
+
+def file_of(g, j):  # Tickets<true>::file_of
+    return j * 8 + g
+
+
+def cursor_geometry(n, cf, ts, waves):  # FileCursor::init
+    if cf > 1:
+        nA = (n - (n >> ts)) // cf if ts > 0 else (n + cf - 1) // cf
+        nt = nA + (n - nA * cf) if ts > 0 else nA
+        if nt < K_DYN_MIN_PER_WAVE * waves:
+            return 1, n, n
+        return cf, nA, nt
+    return 1, n, n
+
+
+def files_of_tickets(t, n, cf, nA):  # FileCursor::take, vectorised over tickets t
+    chunk = t[t < nA]
+    first = np.repeat(chunk * cf, cf) + np.tile(np.arange(cf), chunk.size)
+    first = first[first < n]
+    single = nA * cf + (t[t >= nA] - nA)
+    return np.concatenate([first, single])
+
+
+@pytest.mark.parametrize("cf,ts", [(1, 0), (2, 0), (3, 0), (4, 0), (16, 0), (4, 3), (4, 2), (2, 3), (3, 3), (4, 5)])
+def test_every_file_exactly_once(cf, ts):
+    rng = np.random.default_rng(cf * 31 + ts)
+    waves = 4096
+    ns = [1, 7, 8, 9, 1023, 65535, 65536 * 4 + 3, 1 << 20, (1 << 20) + 777] + [int(x) for x in rng.integers(1, 3 << 20, 6)]
+    for n in ns:
+        c, nA, nt = cursor_geometry(n, cf, ts, waves)
+        tickets = np.concatenate([file_of(g, np.arange(gcount(nt, g), dtype=np.int64)) for g in range(8)])
+        assert np.array_equal(np.sort(tickets), np.arange(nt))
+        files = files_of_tickets(tickets, n, c, nA)
+        seen = np.bincount(files, minlength=n)
+        assert seen.size == n and (seen == 1).all(), (n, cf, ts)
+        if c > 1 and ts > 0:  # long launches take chunks; the last n >> ts files come one per ticket
+            assert nt - nA == n - nA * cf >= n >> ts
