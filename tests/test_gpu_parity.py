@@ -349,7 +349,7 @@ def _stripe_edge_cases(run, count=24):
 
 
 @pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21,
-                                     39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 50, 51, 52, 53, 54, 55])
+                                     39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 50, 51, 52, 53, 54, 55, 56, 57, 58])
 def test_kernel_variants_parity(oracle, variant, monkeypatch):
     """Every compiled (RUN, PF) variant is bit-exact, including the stripe-0 seed edge."""
     import tfs_amd.crc as crc
@@ -403,7 +403,7 @@ def test_cross_file_pipeline_many_files(oracle, variant, monkeypatch):
         ctx.close()
 
 
-@pytest.mark.parametrize("variant", [0, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 50, 51, 52, 53, 54, 55])
+@pytest.mark.parametrize("variant", [0, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 50, 51, 52, 53, 54, 55, 56, 57, 58])
 def test_dynamic_tickets_million_files(oracle, variant, monkeypatch):
     """> 16 files (or chunks of CF files, variants 39-41) per wave, so the launch
     takes the dynamic-ticket path with stealing across the eight groups: 1 M short

@@ -49,3 +49,21 @@ def test_every_file_exactly_once(cf, ts):
         assert seen.size == n and (seen == 1).all(), (n, cf, ts)
         if c > 1 and ts > 0:  # long launches take chunks; the last n >> ts files come one per ticket
             assert nt - nA == n - nA * cf >= n >> ts
+
+
+def gcount_w(n, g, w):  # Tickets<true, W>::gcount
+    rem, lo = n % (8 * w), g * w
+    return (n // (8 * w)) * w + ((min(rem - lo, w)) if rem > lo else 0)
+
+
+def file_of_w(g, j, w):  # Tickets<true, W>::file_of
+    return (j // w) * (8 * w) + g * w + j % w
+
+
+@pytest.mark.parametrize("w", [2, 4, 8])
+def test_interleaved_slots_of_w_tickets(w):
+    """W consecutive tickets per group slot (variants 15/16 on files, 56-58 on
+    chunks): the eight groups still hand out every ticket exactly once."""
+    for n in [1, 5, 8 * w - 1, 8 * w, 8 * w + 1, 65536 + 13, 1 << 18, (1 << 18) + 8 * w * 3 + 5]:
+        t = np.concatenate([file_of_w(g, np.arange(gcount_w(n, g, w), dtype=np.int64), w) for g in range(8)])
+        assert np.array_equal(np.sort(t), np.arange(n)), (w, n)

@@ -1954,6 +1954,13 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
     case 54: TFS_LAUNCH_CX(4, kIL, kCF, kTS); break;      // PF 4
     case 55: TFS_LAUNCH_CX(kPF, kIL, 6, kTS); break;      // chunks of 6
 #undef TFS_LAUNCH_CX
+#define TFS_LAUNCH_CW(WW)                                                                                           \
+  hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, WW, false, false, kCF, kTS>), \
+                     grid, block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq)
+    case 56: TFS_LAUNCH_CW(2); break;  // chunked tickets, WW consecutive chunks per group slot (one XCD)
+    case 57: TFS_LAUNCH_CW(8); break;
+    case 58: TFS_LAUNCH_CW(4); break;
+#undef TFS_LAUNCH_CW
     case 50:  // one file per ticket (the product before chunked tickets)
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL>), grid, block, 0, stream,
                          base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
