@@ -997,24 +997,43 @@ def bench_compact_files(args):
             launches += cnt["launches"]
             dest_total += cnt["dest_size"]
         el = _max_over_ranks(dist, time.perf_counter() - t0)
-        # ---- the same bytes moved by the host alone: the source files read and the
-        # new block's bytes written, single thread, page cache (the I/O floor)
+        # ---- the same bytes moved by the host alone: the source files read by one
+        # thread while a second writes the new block's bytes, page cache (the I/O
+        # floor of the compactor's reader + writer threads)
+        import threading
         buf = np.empty(8 << 20, np.uint8)
+        wbuf = np.empty(8 << 20, np.uint8)
         names = sorted(os.listdir(src))
-        t1 = time.perf_counter()
-        for f in [os.path.join(src, x) for x in names if x.isdigit()] + [os.path.join(src, "extend", x) for x in
-                                                                         os.listdir(os.path.join(src, "extend"))]:
-            with open(f, "rb", buffering=0) as fh:
-                while fh.readinto(buf):
-                    pass
         scratch = os.path.join(root, "io_floor.dat")
-        fd = os.open(scratch, os.O_CREAT | os.O_WRONLY, 0o644)
-        left = dest_total
-        while left > 0:
-            left -= os.write(fd, buf[:min(left, buf.size)])
-        os.close(fd)
-        io_s = time.perf_counter() - t1
+
+        def read_all():
+            for f in [os.path.join(src, x) for x in names if x.isdigit()] + [
+                    os.path.join(src, "extend", x) for x in os.listdir(os.path.join(src, "extend"))]:
+                with open(f, "rb", buffering=0) as fh:
+                    while fh.readinto(buf):
+                        pass
+
+        def write_all():
+            fd = os.open(scratch, os.O_CREAT | os.O_WRONLY, 0o644)
+            left = dest_total
+            while left > 0:
+                left -= os.write(fd, wbuf[:min(left, wbuf.size)])
+            os.close(fd)
+
+        t1 = time.perf_counter()
+        read_all()
+        write_all()
+        io_serial = time.perf_counter() - t1
         os.unlink(scratch)
+        t1 = time.perf_counter()
+        wt = threading.Thread(target=write_all)
+        wt.start()
+        read_all()
+        wt.join()
+        io_conc = time.perf_counter() - t1
+        os.unlink(scratch)
+        writer_thread = os.environ.get("TFS_DS_COMPACT_WRITER", "0") not in ("", "0")
+        io_s = io_conc if writer_thread else io_serial
         live_total = float(world) * nb * live * L
         res = {
             "metric": "GiB/s of live payload compacted from block files (FileIterator 8 MiB windows, re-CRC, repack, "
@@ -1026,15 +1045,19 @@ def bench_compact_files(args):
             "data": "synthetic 64 KiB files, 1024 per block (main 64 MiB block + extension block), evens + every "
                     "3rd of the rest deleted (%d live), written in TFS's block-file format" % live,
             "config": {"workload": "compaction from block files: %d blocks on disk per GPU, one BlockFileCompactor "
-                                   "(4 windows per launch, zero-copy)" % nb,
+                                   "(4 windows per launch, zero-copy%s)" % (
+                                       nb, "; new bytes written by a writer thread" if os.environ.get(
+                                           "TFS_DS_COMPACT_WRITER", "0") not in ("", "0") else ""),
                        "storage": "page cache (source just written; new files not fsynced)",
                        "windows": windows, "launches": launches},
             "roofline": {"bound": "host-io", "achieved": (src_bytes + dest_total) / el / 1e9,
                          "peak": (src_bytes + dest_total) / io_s / 1e9, "unit": "GB/s (source read + new block written)",
                          "frac": io_s / el,
-                         "peak_source": "measured this run: the same source files read and as many bytes written "
-                                        "through the page cache by one thread with no CRC or repack (%.1f ms)" %
-                                        (io_s * 1e3),
+                         "peak_source": "measured this run: the same source files read and as many bytes "
+                                        "written through the page cache, no CRC or repack, %s (%.1f ms; %s: %.1f ms)" % (
+                                            "by two threads at once" if writer_thread else "by one thread in turn",
+                                            io_s * 1e3, "in turn" if writer_thread else "two threads at once",
+                                            (io_serial if writer_thread else io_conc) * 1e3),
                          "traffic": "whole source block files read from the page cache, live records over PCIe "
                                     "(zero-copy), new block files written"},
             "parity": "block 1: new block files byte-identical to oracle real_compact of the stitched source",

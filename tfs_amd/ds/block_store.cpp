@@ -7,8 +7,13 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <functional>
+#include <mutex>
+#include <thread>
 
 namespace tfs {
 namespace dataserver {
@@ -426,6 +431,74 @@ struct WindowGroup {
   bool inflight = false;
 };
 
+// The new block's bytes go to the destination files on a writer thread, in the
+// order they were queued, while the compaction thread reads the next windows
+// (the reference's task thread does both in turn: task.cpp:753-836).  A group's
+// write buffer is refilled by its next launch only after wait_idle().
+class AsyncWriter {
+ public:
+  // threaded = false: post() runs the write at once on the caller's thread.
+  explicit AsyncWriter(bool threaded) : threaded_(threaded) {
+    if (threaded_) th_ = std::thread([this] { run(); });
+  }
+  ~AsyncWriter() {
+    if (!threaded_) return;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  void post(std::function<int()> f) {
+    if (!threaded_) {
+      if (!rc_) rc_ = f();
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      q_.push_back(std::move(f));
+    }
+    cv_.notify_all();
+  }
+  // Every queued write done; the first failure, if any.
+  int wait_idle() {
+    if (!threaded_) return rc_;
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return q_.empty() && !busy_; });
+    return rc_;
+  }
+
+ private:
+  void run() {
+    for (;;) {
+      std::function<int()> f;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;
+        f = std::move(q_.front());
+        q_.pop_front();
+        busy_ = true;
+      }
+      const int r = rc_ ? rc_ : f();  // after a failure the rest is not written
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        busy_ = false;
+        if (r && !rc_) rc_ = r;
+      }
+      cv_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<int()>> q_;
+  const bool threaded_;
+  bool busy_ = false, stop_ = false;
+  int rc_ = TFS_SUCCESS;
+  std::thread th_;
+};
+
 }  // namespace
 
 struct BlockFileCompactor::Impl {
@@ -504,9 +577,16 @@ int BlockFileCompactor::Impl::compact(const BlockStore& src, uint32_t src_main_i
   ChainWriter w(dst, dst_main_id, first_ext_id, logic_id);
   int64_t dest_off = 0;
   int cur = 0;
+  // TFS_DS_COMPACT_WRITER=1 (measurement): the new bytes go out on a writer
+  // thread while the next windows are read; default: written in turn by this
+  // thread, as the reference's task thread does.
+  static const bool kAsyncWrites = getenv("TFS_DS_COMPACT_WRITER") && atoi(getenv("TFS_DS_COMPACT_WRITER")) != 0;
+  AsyncWriter writer(kAsyncWrites);  // declared after w: joined (every queued write done) before w goes
 
   auto submit = [&](WindowGroup& g) -> int {
     if (g.inflight || g.wins.empty()) return TFS_SUCCESS;
+    // The launch rewrites g.dst: the writes queued from it must be done.
+    if (const int r = writer.wait_idle()) return r;
     g.inflight = true;
     if (g.njobs == 0) return TFS_SUCCESS;
     ++out->launches;
@@ -524,8 +604,13 @@ int BlockFileCompactor::Impl::compact(const BlockStore& src, uint32_t src_main_i
     if (!g.inflight) return TFS_SUCCESS;
     int r = tfs_crc32_stream_sync(ctx, g.stream);
     if (r) return r;
-    for (const WindowGroup::Win& win : g.wins)
-      if (win.dst_len && (r = w.write(g.dst.p + win.dst_slot, win.dst_len, win.dst_off))) return r;
+    writer.post([&w, wins = g.wins, dp = g.dst.p]() -> int {
+      for (const WindowGroup::Win& win : wins)
+        if (win.dst_len)
+          if (const int wr = w.write(dp + win.dst_slot, win.dst_len, win.dst_off)) return wr;
+      return TFS_SUCCESS;
+    });
+    if (!kAsyncWrites && (r = writer.wait_idle())) return r;  // written in turn: its failure now
     const int32_t* st = reinterpret_cast<const int32_t*>(g.status.p);
     for (uint32_t j = 0; j < g.njobs; ++j) {
       out->status[g.file_idx[j]] = st[j];
@@ -593,6 +678,7 @@ int BlockFileCompactor::Impl::compact(const BlockStore& src, uint32_t src_main_i
     int r;
     for (WindowGroup& g : groups)
       if ((r = submit(g)) || (r = drain(g))) return r;
+    if ((r = writer.wait_idle())) return r;  // the big file's pieces follow every queued write
     tfs_raw_meta m = metas[i];
     const int32_t raw = m.size;
     m.size = raw & kFileSizeMask;
@@ -662,6 +748,8 @@ int BlockFileCompactor::Impl::compact(const BlockStore& src, uint32_t src_main_i
     const int r2 = drain(g);
     if (!rc) rc = r ? r : r2;
   }
+  const int rw = writer.wait_idle();
+  if (!rc) rc = rw;
   if (rc) return rc;
   out->dest_size = dest_off;
   out->ext_ids.assign(w.chain().begin() + 1, w.chain().end());
