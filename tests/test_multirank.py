@@ -1,4 +1,4 @@
-"""World-size-2 CPU (gloo) rehearsal of bench.py's multi-GPU plumbing: the
+"""World-size-2 and -8 CPU (gloo) rehearsals of bench.py's multi-GPU plumbing: the
 batch partitions by block id with no data-path collective; ranks only meet at
 the barrier and the max-over-ranks of the timing."""
 import os
@@ -6,6 +6,7 @@ import subprocess
 import sys
 
 import numpy as np
+import pytest
 
 from conftest import ROOT
 
@@ -15,11 +16,11 @@ sys.path.insert(0, os.environ["TFS_ROOT"])
 import numpy as np
 import bench
 world, rank, local, dist = bench._dist_init()
-assert world == 2 and dist is not None
+assert world == int(os.environ["TFS_EXPECT_WORLD"]) and dist is not None
 mine = bench.rank_blocks(1024 * world, world, rank)
 assert len(mine) == 1024 and (mine % world == rank).all()
 t = bench._max_over_ranks(dist, 1.0 + rank)
-assert t == 2.0, t
+assert t == float(world), t
 import torch
 allb = [None] * world
 dist.all_gather_object(allb, mine.tolist())
@@ -32,12 +33,14 @@ dist.destroy_process_group()
 '''
 
 
-def test_gloo_world2_partition_and_timing(tmp_path):
-    script = tmp_path / "w2.py"
+@pytest.mark.parametrize("world", [2, 8])
+def test_gloo_partition_and_timing(tmp_path, world):
+    """world 8 rehearses the driver's 8-GPU node (configs[4]) with CPU ranks."""
+    script = tmp_path / "w.py"
     script.write_text(SCRIPT)
-    env = dict(os.environ, TFS_ROOT=ROOT, MASTER_ADDR="127.0.0.1")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-                        "--master-addr", "127.0.0.1", "--master-port", "29517", str(script)],
+    env = dict(os.environ, TFS_ROOT=ROOT, MASTER_ADDR="127.0.0.1", TFS_EXPECT_WORLD=str(world), OMP_NUM_THREADS="1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % world,
+                        "--master-addr", "127.0.0.1", "--master-port", str(29517 + world), str(script)],
                        capture_output=True, text=True, env=env, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "PARTITION_OK" in r.stdout
