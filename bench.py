@@ -400,7 +400,7 @@ def main():
 def ab_compare(args, crc, img, d_vdesc, nfiles, d_ok, d_bad, mode=1, algo_bytes=None, d_out=None):
     """Rule: perf deltas come from interleaved rounds in one process on one device."""
     algo_bytes = algo_bytes if algo_bytes is not None else nfiles * ALGO_BYTES_PER_FILE
-    variants = [int(v) for v in args.ab.split(",") if v != ""]
+    variants = list(dict.fromkeys(int(v) for v in args.ab.split(",") if v != ""))  # each id once, in order
     ctxs = {}
     for v in variants:
         os.environ["TFS_CRC_VARIANT"] = str(v)
@@ -1638,7 +1638,7 @@ def bench_ec(args):
         out[name] = {"ms": kms, "GiBs_data": world * args.steps * k * size / el / 2**30,
                      "hbm_GBs": (rd + wr) * size / (kms / 1e3) / 1e9}
     if args.ab:  # interleaved rounds of kernel forms (TFS_EC_VARIANT ids) in this process (stderr)
-        forms = [int(v) for v in args.ab.split(",") if v != ""]
+        forms = list(dict.fromkeys(int(v) for v in args.ab.split(",") if v != ""))
         encs = {}
         for v in forms:
             os.environ["TFS_EC_VARIANT"] = str(v)
