@@ -1976,6 +1976,10 @@ def bench_loopback(args):
         lat["close_%d_leases" % nl] = {"p50_us": float(np.percentile(cl, 50)), "p99_us": float(np.percentile(cl, 99)),
                                        "closes": int(cl.size)}
     res["latency"] = lat
+    # resident kernel over this whole line: launches (first + relaunches after
+    # idle or lifetime exits) against the files it took
+    launches, rfiles = ctx.resident_stats()
+    res["resident_kernel"] = {"launches": int(launches), "files": int(rfiles)}
     # PCIe bytes of one loopback: every payload crosses once for the close check
     # (zero-copy reads of the lease buffers) and once for the whole-block verify.
     pcie_bytes = 2.0 * n * L
