@@ -667,3 +667,42 @@ def test_device_resident_max_len_and_64bit_offsets(gpu_ctx, oracle):
         assert int(nb.download(np.uint32)[0]) == 1 and okd.download().tolist() == [0, 1, 1]
     finally:
         img.free()
+
+
+@pytest.mark.parametrize("variant", [0, 50, 40])
+def test_dynamic_tickets_verify_counts_each_file_once(oracle, variant, monkeypatch):
+    """Verify over 1 M device-resident files on the dynamic (chunked) path with
+    1,000 wrong expectations: n_bad is exactly 1,000 and the verdicts are 0 at
+    exactly those files -- a file taken twice (or never) would show here."""
+    import tfs_amd.crc as crc
+    monkeypatch.setenv("TFS_CRC_VARIANT", str(variant))
+    ctx = crc.Context(0)
+    try:
+        rng = np.random.default_rng(5050 + variant)
+        n = (1 << 20) + 333
+        lens = rng.integers(0, 200, n)
+        offs = np.cumsum(rng.integers(0, 8, n) + np.concatenate([[0], lens[:-1]])).astype(np.uint64)
+        total = int(offs[-1] + lens[-1] + 64)
+        buf = synth_bytes(6060 + variant, total)
+        d = np.zeros(n, crc.DESC_DTYPE)
+        d["offset"], d["len"] = offs, lens
+        exp = np.zeros(n, np.uint32)
+        oracle.oracle_crc_batch(d.ctypes.data, n, buf.ctypes.data, exp.ctypes.data)
+        bad = rng.choice(n, 1000, replace=False)
+        d["aux"] = exp
+        d["aux"][bad] ^= 0x80000000
+        img = crc.DeviceBuffer(ctx, (total + 4095) // 4096 * 4096).upload(buf)
+        dd = crc.DeviceBuffer(ctx, d.nbytes).upload(d)
+        okd = crc.DeviceBuffer(ctx, n)
+        nb = crc.DeviceBuffer(ctx, 4)
+        outc = crc.DeviceBuffer(ctx, 4 * n)
+        okd.zero()
+        nb.zero()
+        ctx.verify_device(dd, n, img, outc, okd, nb)
+        ctx.sync()
+        assert int(nb.download(np.uint32)[0]) == 1000
+        ok = okd.download(np.uint8, n)
+        assert np.array_equal(np.sort(np.nonzero(ok == 0)[0]), np.sort(bad)) and (ok <= 1).all()
+        assert np.array_equal(outc.download(np.uint32, n), exp)
+    finally:
+        ctx.close()
