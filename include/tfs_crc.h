@@ -110,11 +110,32 @@ int tfs_crc32_device_numa_node(int device);
 
 /* Replaces `static uint32_t Func::crc(uint32_t crc, const char* data,
  * const int32_t len)` (src/common/func.h:90, func.cpp:426-435).  Host buffer,
- * result by value, len <= 0 returns crc.  Runs on the process-wide default
- * context (device 0).  On device failure returns `crc` and sets *err (when
- * err != NULL) -- use the batch API when errors must be observed. */
+ * result by value, len <= 0 returns crc.  Runs on the scalar context: the
+ * calling thread's binding (tfs_crc32_bind_thread), else the process default
+ * (tfs_crc32_set_default_ctx), else a context on device 0 made on first use.
+ *
+ * Failure mode: Func::crc has no error channel, so on a device failure
+ * tfs_crc32 returns `crc` (the seed) -- a value the caller will usually take
+ * for a CRC mismatch.  Every such failure is counted (tfs_crc32_error_count,
+ * process-wide, never reset), and the first is reported on stderr.  Call sites
+ * that can act on an error -- the packet decode check (base_packet.cpp:141) and
+ * the mirror / repair re-CRC (sync_backup.cpp:383,412, file_repair.cpp:142) --
+ * use tfs_crc32_e, whose *err (TFS_CRC_EXIT_DEVICE_ERROR / _NO_DEVICE, or
+ * TFS_SUCCESS) tells a device fault from a mismatch. */
 uint32_t tfs_crc32(uint32_t crc, const char* data, int32_t len);
 uint32_t tfs_crc32_e(uint32_t crc, const char* data, int32_t len, int* err);
+/* Scalar drop-in failures so far in this process (both forms). */
+uint64_t tfs_crc32_error_count(void);
+/* Choose the scalar context: for the whole process (NULL = back to device 0's
+ * default), or for the calling thread only (a packet worker serving one GPU's
+ * blocks binds that group member's context; NULL unbinds).  The caller keeps the
+ * context alive while it is selected; destroying it clears the process default
+ * and the destroying thread's binding. */
+int tfs_crc32_set_default_ctx(tfs_crc_ctx* ctx);
+int tfs_crc32_bind_thread(tfs_crc_ctx* ctx);
+/* The context the scalar calls of this thread use (created on first use), or
+ * NULL when none can be made. */
+tfs_crc_ctx* tfs_crc32_default_ctx(void);
 
 /* Replaces DataFile::get_crc() (src/dataserver/data_file.cpp:168-194):
  * Func::crc(0, data, length).  The reference re-reads payloads > 2 MiB in
@@ -383,7 +404,9 @@ int tfs_crc32_write_packet_headers_device(tfs_crc_ctx* ctx, void* d_base, const 
                                           uint64_t first_id, void* stream);
 /* Calibration: stream the bytes without CRC arithmetic.  pattern 0 = coalesced
  * grid-stride over [d_base, d_base+nbytes); pattern 1 = the CRC kernel's
- * per-file lane-segment access pattern over d_desc (len multiple of 1 KiB). */
+ * per-file lane-segment access pattern over d_desc (len multiple of 1 KiB).
+ * Measurement build only (libtfs_crc_measure.so); the product library returns
+ * TFS_EXIT_PARAMETER_ERROR. */
 int tfs_crc32_membench_device(tfs_crc_ctx* ctx, int pattern, const void* d_base, const tfs_crc_desc* d_desc,
                               uint32_t n, uint64_t nbytes, uint32_t* d_out, unsigned grid, void* stream);
 /* Device / pinned memory and event plumbing for callers that hold no HIP
@@ -412,9 +435,22 @@ int tfs_crc32_sync(tfs_crc_ctx* ctx);
  * block verify / block compaction / packet calls) the next `count` ones fail with
  * TFS_CRC_EXIT_DEVICE_ERROR before any GPU work.  count = 0 disarms. */
 int tfs_crc32_inject_device_error(tfs_crc_ctx* ctx, uint32_t skip, uint32_t count);
-/* Extra non-blocking streams on ctx's device for the *_device calls (each stream
- * gets its own scheduler slot; at most 255 besides the ctx stream), a
- * synchronize on one, and its release. */
+/* Test hooks for the scheduler and resident-ring state (tests/test_resident.py):
+ * the device addresses and sizes of ctx's scheduler slots and resident-kernel
+ * state (NULL before the first resident batch), and a poisoned resident state --
+ * every workgroup's count of units done set to `done`, as a stale recycled
+ * allocation would hold -- to check that such a batch ends in
+ * TFS_CRC_EXIT_DEVICE_ERROR in bounded time instead of hanging. */
+int tfs_crc32_debug_state(tfs_crc_ctx* ctx, void** d_sched, uint64_t* sched_bytes, void** d_res_state,
+                          uint64_t* res_state_bytes);
+int tfs_crc32_debug_poison_resident(tfs_crc_ctx* ctx, uint32_t done);
+/* Extra non-blocking streams on ctx's device for the *_device calls (each
+ * stream gets its own self-resetting scheduler slot; at most 192 live per ctx
+ * incl. its own and the compaction streams), a synchronize on one, and its
+ * release.  The *_device calls also take any other hipStream_t of the caller's
+ * (each launch then leases a pooled slot and zeroes it on that stream first: one
+ * memset more per launch); hipStreamPerThread is refused
+ * (TFS_EXIT_PARAMETER_ERROR): it names a different queue on every thread. */
 int tfs_crc32_stream_create(tfs_crc_ctx* ctx, void** stream);
 int tfs_crc32_stream_sync(tfs_crc_ctx* ctx, void* stream);
 int tfs_crc32_stream_destroy(tfs_crc_ctx* ctx, void* stream);
@@ -428,6 +464,19 @@ int tfs_crc32_stream_destroy(tfs_crc_ctx* ctx, void* stream);
  * Stats: kernel launches made and files taken through the ring so far. */
 int tfs_crc32_set_resident(tfs_crc_ctx* ctx, int on);
 int tfs_crc32_resident_stats(tfs_crc_ctx* ctx, uint64_t* launches, uint64_t* files);
+/* Throughput launches (the *_device calls and large host batches: one
+ * persistent workgroup per CU) leave the CUs of every resident kernel of their
+ * device free while it lives or has had a batch in the last 50 ms, so a close
+ * batch never waits for a 10 ms verify or compaction launch and such a launch
+ * never waits for the resident kernel's lifetime.  on = 0 uses
+ * every CU regardless.  tfs_crc32_throughput_grid: workgroups the next
+ * throughput launch of ctx would use. */
+int tfs_crc32_set_cu_reserve(tfs_crc_ctx* ctx, int on);
+int tfs_crc32_throughput_grid(tfs_crc_ctx* ctx);
+/* Scheduler slots: ctx-owned streams bound (the ctx stream, compaction streams,
+ * tfs_crc32_stream_create), and launches so far on streams the ctx does not own
+ * (each of those takes a pooled slot zeroed on its stream before the kernel). */
+int tfs_crc32_sched_stats(tfs_crc_ctx* ctx, uint32_t* owned_streams, uint64_t* foreign_launches);
 
 #ifdef __cplusplus
 }

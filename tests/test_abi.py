@@ -63,10 +63,18 @@ def test_no_device_fails_loudly():
     with pytest.raises(crc.TfsCrcError) as e:
         crc.Context(0)
     assert e.value.code == crc.TFS_CRC_EXIT_NO_DEVICE
-    with pytest.raises(crc.TfsCrcError):
+    before = crc.lib().tfs_crc32_error_count()
+    with pytest.raises(crc.TfsCrcError) as e2:
         crc.func_crc(0, b"123456789")
+    assert e2.value.code == crc.TFS_CRC_EXIT_NO_DEVICE
+    # the plain Func::crc drop-in returns its seed (no error channel) but the
+    # failure is counted, never silent (include/tfs_crc.h, tfs_crc32_error_count)
+    assert crc.lib().tfs_crc32(7, b"123456789", 9) == 7
+    assert crc.lib().tfs_crc32_error_count() == before + 2
+    assert crc.lib().tfs_crc32_default_ctx() is None
     # len <= 0 never touches the device (func.cpp:429 loop does not run)
     assert crc.func_crc(0x1234, b"", 0) == 0x1234
+    assert crc.lib().tfs_crc32_error_count() == before + 2
 
 
 def test_product_path_does_not_reference_oracle():
@@ -75,3 +83,46 @@ def test_product_path_does_not_reference_oracle():
             if f.endswith((".py", ".cpp", ".hip", ".h")):
                 txt = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in txt.lower(), os.path.join(dirpath, f)
+
+
+def _kernel_symbols(so):
+    out = subprocess.run(["nm", "-C", so], capture_output=True, text=True, check=True).stdout
+    return set(re.findall(r"(\w+_kernel(?:<[^>]*>)?)\(", out))
+
+
+def test_product_library_holds_one_form_of_each_kernel():
+    """The A/B kernel forms and calibration kernels live only in the measurement
+    build (libtfs_crc_measure.so, -DTFS_CRC_MEASURE): the product library holds
+    one crc_files_kernel per mode, no round-1 baselines, no membench, and never
+    names TFS_CRC_VARIANT / TFS_EC_VARIANT, so no environment variable can swap
+    a dataserver's kernel."""
+    prod = os.path.join(ROOT, "tfs_amd", "libtfs_crc.so")
+    meas = os.path.join(ROOT, "tfs_amd", "libtfs_crc_measure.so")
+    blob = open(prod, "rb").read()
+    assert b"TFS_CRC_VARIANT" not in blob and b"TFS_EC_VARIANT" not in blob
+    assert b"TFS_CRC_VARIANT" in open(meas, "rb").read()
+    kp, km = _kernel_symbols(prod), _kernel_symbols(meas)
+    files_p = {k for k in kp if k.startswith("crc_files_kernel<")}
+    assert len(files_p) == 2, files_p  # verify and compute
+    assert len({k for k in km if k.startswith("crc_files_kernel<")}) > 20
+    for name in ("membench", "block_verify_kernel", "compact_fused_kernel", "compact_copy_kernel",
+                 "ec_apply_chunk_kernel"):
+        assert not any(name in k for k in kp), name
+        assert any(name in k for k in km), name
+    # the product's kernels are all in the measurement build too (same sources)
+    assert files_p <= km
+
+
+def test_measurement_library_only_on_request(monkeypatch):
+    """Contexts load the product library unless a variant is asked for."""
+    import tfs_amd.crc as crc
+    monkeypatch.delenv("TFS_CRC_VARIANT", raising=False)
+    monkeypatch.delenv("TFS_EC_VARIANT", raising=False)
+    assert not crc.measuring()
+    monkeypatch.setenv("TFS_CRC_VARIANT", "0")
+    assert not crc.measuring()
+    monkeypatch.setenv("TFS_CRC_VARIANT", "42")
+    assert crc.measuring()
+    assert crc.lib(True) is not crc.lib(False)
+    for n in crc.EXPORTED:
+        assert hasattr(crc.lib(True), n), n

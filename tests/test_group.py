@@ -177,3 +177,25 @@ def test_bench_two_ranks_partitioned_by_block(tmp_path):
     assert part["disjoint"] and part["covers"] and part["blocks_per_rank"] == [32, 32]
     assert res["parity"]["files_checked"] >= 4 * 1024 and res["parity"]["mismatches"] == 0
     assert res["parity"]["verdicts_all_ok"]
+
+
+def test_bench_gpus_2_self_launched(tmp_path):
+    """Plain `python3 bench.py --gpus 2` -- no launcher around it, as a driver may
+    run it: bench.py starts the two ranks itself (both on the one GPU here,
+    TFS_BENCH_SHARE_DEVICE=1) and relays rank 0's line: n_gpus 2, the ranks'
+    blocks disjoint and covering, every pass clean, parity checked."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(TFS_BENCH_SHARE_DEVICE="1", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--blocks", "32", "--steps", "2",
+           "--warmup", "1", "--no-cpu", "--e2e-blocks", "4", "--parity-every", "8"]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["value"] > 0 and res["end_to_end"]["value"] > 0
+    part = res["config"]["partition_check"]
+    assert part["disjoint"] and part["covers"] and part["blocks_per_rank"] == [32, 32]
+    assert res["parity"]["files_checked"] >= 4 * 1024 and res["parity"]["mismatches"] == 0
+    assert res["parity"]["verdicts_all_ok"]
+    assert "starting 2 ranks" in r.stderr

@@ -1,6 +1,7 @@
 """World-size-2 and -8 CPU (gloo) rehearsals of bench.py's multi-GPU plumbing: the
 batch partitions by block id with no data-path collective; ranks only meet at
 the barrier and the max-over-ranks of the timing."""
+import json
 import os
 import subprocess
 import sys
@@ -55,3 +56,33 @@ def test_zipf_sizes_match_config():
         assert int((L + 36).sum()) <= bench.BLOCK_DATA
     allL = np.concatenate(blocks)
     assert (allL // 4096 == 1).mean() > 0.1   # heavy head of the Zipf law
+
+
+def test_bench_gpus_n_starts_its_own_ranks():
+    """Plain `python3 bench.py --gpus N` (no launcher around it) starts N ranks
+    itself through torch.distributed.run; --launch-check stops each rank after
+    the rendezvous, so this runs on the CPU (the -m gpu twin runs the real line)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--launch-check"],
+                       capture_output=True, text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    chk = json.loads(lines[0])["launch_check"]
+    assert chk["world"] == 3 and chk["gpus"] == 3
+    assert sorted(x[0] for x in chk["ranks"]) == [0, 1, 2]
+    assert sorted(x[1] for x in chk["ranks"]) == [0, 1, 2]
+    assert len({x[2] for x in chk["ranks"]}) == 3 and os.getpid() not in {x[2] for x in chk["ranks"]}
+
+
+@pytest.mark.parametrize("world,gpus", [(2, 1), (8, 4), (1, 2)])
+def test_bench_refuses_world_size_mismatch(world, gpus):
+    """A launcher that started another number of ranks than --gpus asks for is
+    refused before any GPU work (the line would report the wrong N)."""
+    env = dict(os.environ, WORLD_SIZE=str(world), RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus)],
+                       capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode != 0
+    assert "WORLD_SIZE=%d but --gpus %d" % (world, gpus) in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

@@ -175,3 +175,112 @@ def test_resident_contexts_created_and_destroyed_in_turn(oracle):
                 assert (ctx.batch(buf, offs, lens, seeds) == _oracle_batch(oracle, buf, offs, lens, seeds)).all(), (c, it)
         finally:
             ctx.close()
+
+
+def _poisoned_free(ctx, nbytes, word=0x01010101):
+    """Allocate nbytes of device memory, fill every 32-bit word with `word` (a
+    stale done count / ticket value) and free it, so the next allocation of that
+    size is likely to get the same, poisoned, memory back."""
+    import tfs_amd.crc as crc
+    b = crc.DeviceBuffer(ctx, nbytes)
+    b.upload(np.full(nbytes // 4, word, np.uint32))
+    ctx.sync()
+    p = b.ptr
+    b.free()
+    return p
+
+
+def test_resident_state_recycled_from_a_destroyed_context(monkeypatch, oracle):
+    """gputests.log:67 of round 2 (a stale done count in a recycled allocation
+    made the resident kernel wait for a unit never posted), made deterministic:
+    a context runs resident batches (its workgroups' done counts become nonzero)
+    and is destroyed; a block of the resident state's size is allocated, filled
+    with garbage and freed; a new context's first batch must complete through
+    exactly one resident launch -- whether or not it got that memory back."""
+    import tfs_amd.crc as crc
+    rng = np.random.default_rng(35)
+    a = _ctx(monkeypatch, TFS_CRC_RESIDENT=1)
+    try:
+        for it in range(20):
+            buf, offs, lens = _random_batch(rng, 7, seed=1200 + it)
+            seeds = rng.integers(0, 2**32, 7).astype(np.uint32)
+            assert (a.batch(buf, offs, lens, seeds) == _oracle_batch(oracle, buf, offs, lens, seeds)).all()
+        st = a.debug_state()
+        assert st["res_state"] and st["res_state_bytes"] > 0
+        nbytes = st["res_state_bytes"]
+    finally:
+        a.close()
+    for trial in range(3):
+        tmp = crc.Context(0)
+        garbage = _poisoned_free(tmp, nbytes)
+        tmp.close()
+        b = _ctx(monkeypatch, TFS_CRC_RESIDENT=1)
+        try:
+            buf, offs, lens = _random_batch(rng, 5, seed=1300 + trial)
+            seeds = rng.integers(0, 2**32, 5).astype(np.uint32)
+            t0 = time.perf_counter()
+            got = b.batch(buf, offs, lens, seeds)
+            dt = time.perf_counter() - t0
+            assert (got == _oracle_batch(oracle, buf, offs, lens, seeds)).all(), trial
+            launches, files = b.resident_stats()
+            assert (launches, files) == (1, 5), (trial, launches, files)
+            assert dt < 1.0, dt
+            print("trial %d: recycled poisoned block %s" % (trial, b.debug_state()["res_state"] == garbage))
+        finally:
+            b.close()
+
+
+def test_resident_poisoned_state_fails_in_bounded_time(monkeypatch, oracle):
+    """A batch that can never complete (every workgroup's done count poisoned
+    past the ring's published units) returns TFS_CRC_EXIT_DEVICE_ERROR within a
+    bounded time instead of hanging, and the context keeps working (it stops
+    using the ring and launches)."""
+    import tfs_amd.crc as crc
+    ctx = _ctx(monkeypatch, TFS_CRC_RESIDENT=1, TFS_CRC_RESIDENT_IDLE_US=20)
+    try:
+        rng = np.random.default_rng(36)
+        buf, offs, lens = _random_batch(rng, 3, seed=1400)
+        seeds = rng.integers(0, 2**32, 3).astype(np.uint32)
+        exp = _oracle_batch(oracle, buf, offs, lens, seeds)
+        assert (ctx.batch(buf, offs, lens, seeds) == exp).all()
+        time.sleep(0.01)  # past the idle exit: the kernel is gone, its lines are the host's to write
+        ctx.debug_poison_resident(1 << 20)
+        t0 = time.perf_counter()
+        with pytest.raises(crc.TfsCrcError) as e:
+            ctx.batch(buf, offs, lens, seeds)
+        dt = time.perf_counter() - t0
+        assert e.value.code == crc.TFS_CRC_EXIT_DEVICE_ERROR
+        assert "no progress" in str(e.value)
+        assert dt < 60, dt
+        print("poisoned batch failed after %.2f s" % dt)
+        assert (ctx.batch(buf, offs, lens, seeds) == exp).all()  # launched from now on
+    finally:
+        ctx.close()
+
+
+def test_sched_slots_recycled_from_a_destroyed_context(oracle):
+    """The scheduler slots of a new context come zeroed whatever the recycled
+    memory held: a garbage-filled block of their size is freed just before the
+    context is made, then a dynamic-ticket launch (>= 16 files per wave) and a
+    latency-form launch must both be oracle-exact."""
+    import tfs_amd.crc as crc
+    probe = crc.Context(0)
+    nbytes = probe.debug_state()["sched_bytes"]
+    probe.close()
+    rng = np.random.default_rng(37)
+    n = 70000
+    lens = rng.integers(0, 200, n).astype(np.uint32)
+    offs = np.cumsum(np.concatenate([[0], lens[:-1]]).astype(np.uint64))
+    buf = synth_bytes(1500, int(offs[-1] + lens[-1]) + 64)
+    seeds = rng.integers(0, 2**32, n).astype(np.uint32)
+    exp = _oracle_batch(oracle, buf, offs, lens, seeds)
+    for trial in range(3):
+        tmp = crc.Context(0)
+        _poisoned_free(tmp, nbytes, word=0x00FFFFFF)
+        tmp.close()
+        ctx = crc.Context(0)
+        try:
+            assert (ctx.batch(buf, offs, lens, seeds) == exp).all(), trial
+            assert (ctx.batch(buf, offs[:9], lens[:9], seeds[:9]) == exp[:9]).all(), trial
+        finally:
+            ctx.close()

@@ -18,8 +18,13 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# TFS_CRC_LIB (measurement only): time another build of the library (an old commit) in an A/B.
-LIB_PATH = os.environ.get("TFS_CRC_LIB") or os.path.join(HERE, "libtfs_crc.so")
+LIB_PATH = os.path.join(HERE, "libtfs_crc.so")  # the product: one form of each kernel
+# The measurement build (-DTFS_CRC_MEASURE): the A/B kernel forms selected by
+# TFS_CRC_VARIANT / TFS_EC_VARIANT and the calibration kernels.  Loaded only
+# for a Context(measure=True) or when TFS_CRC_VARIANT / TFS_EC_VARIANT is set
+# (A/B tools, variant parity tests); TFS_CRC_LIB points it at another build
+# (an old commit) for an A/B.  The product library never reads those variables.
+MEASURE_LIB_PATH = os.environ.get("TFS_CRC_LIB") or os.path.join(HERE, "libtfs_crc_measure.so")
 
 TFS_SUCCESS = 0
 TFS_EXIT_CHECK_CRC_ERROR = -1010
@@ -64,7 +69,9 @@ EXPORTED = [
     "tfs_crc32_event_elapsed_ms", "tfs_crc32_event_destroy",
     "tfs_crc32_stream", "tfs_crc32_sync", "tfs_crc32_stream_create", "tfs_crc32_stream_sync",
     "tfs_crc32_stream_destroy", "tfs_crc32_inject_device_error", "tfs_crc32_set_resident",
-    "tfs_crc32_resident_stats",
+    "tfs_crc32_resident_stats", "tfs_crc32_error_count", "tfs_crc32_set_default_ctx", "tfs_crc32_bind_thread",
+    "tfs_crc32_default_ctx", "tfs_crc32_set_cu_reserve", "tfs_crc32_throughput_grid", "tfs_crc32_sched_stats",
+    "tfs_crc32_debug_state", "tfs_crc32_debug_poison_resident",
     "tfs_crc_group_create", "tfs_crc_group_destroy", "tfs_crc_group_last_error", "tfs_crc_group_size",
     "tfs_crc_group_ctx", "tfs_crc_group_member_of", "tfs_crc_group_ctx_for_block", "tfs_crc_group_numa_node",
     "tfs_crc_group_member_bound", "tfs_crc_group_host_malloc", "tfs_crc_group_host_free",
@@ -88,16 +95,23 @@ class TfsCrcError(RuntimeError):
         self.code = code
 
 
-_LIB = None
+_LIBS = {}
 
 
-def lib():
-    """Load libtfs_crc.so; raise loudly when it is missing (no fallback)."""
-    global _LIB
-    if _LIB is None:
-        if not os.path.exists(LIB_PATH):
-            raise ImportError("tfs_amd native library not built: %s (run __graft_entry__.build())" % LIB_PATH)
-        L = ctypes.CDLL(LIB_PATH)
+def measuring():
+    """True when this process asked for a measurement kernel form."""
+    return os.environ.get("TFS_CRC_VARIANT", "0") not in ("", "0") or \
+        os.environ.get("TFS_EC_VARIANT", "0") not in ("", "0")
+
+
+def lib(measure=False):
+    """Load libtfs_crc.so (or the measurement build); raise loudly when it is
+    missing (no fallback)."""
+    path = MEASURE_LIB_PATH if measure else LIB_PATH
+    if path not in _LIBS:
+        if not os.path.exists(path):
+            raise ImportError("tfs_amd native library not built: %s (run __graft_entry__.build())" % path)
+        L = ctypes.CDLL(path)
         vp, u32, i32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64
         sig = {
             "tfs_crc32_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(vp)]),
@@ -144,6 +158,17 @@ def lib():
             "tfs_crc32_set_resident": (ctypes.c_int, [vp, ctypes.c_int]),
             "tfs_crc32_resident_stats": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64),
                                                         ctypes.POINTER(ctypes.c_uint64)]),
+            "tfs_crc32_error_count": (ctypes.c_uint64, []),
+            "tfs_crc32_set_default_ctx": (ctypes.c_int, [vp]),
+            "tfs_crc32_bind_thread": (ctypes.c_int, [vp]),
+            "tfs_crc32_default_ctx": (vp, []),
+            "tfs_crc32_set_cu_reserve": (ctypes.c_int, [vp, ctypes.c_int]),
+            "tfs_crc32_throughput_grid": (ctypes.c_int, [vp]),
+            "tfs_crc32_sched_stats": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint32),
+                                                     ctypes.POINTER(ctypes.c_uint64)]),
+            "tfs_crc32_debug_state": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_uint64),
+                                                     ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_uint64)]),
+            "tfs_crc32_debug_poison_resident": (ctypes.c_int, [vp, u32]),
             "tfs_crc_group_create": (ctypes.c_int, [vp, u32, ctypes.POINTER(vp)]),
             "tfs_crc_group_destroy": (ctypes.c_int, [vp]),
             "tfs_crc_group_last_error": (ctypes.c_char_p, [vp]),
@@ -167,13 +192,13 @@ def lib():
             try:
                 f = getattr(L, name)
             except AttributeError:
-                if os.environ.get("TFS_CRC_LIB"):  # an older build under A/B lacks newer entry points
+                if measure and os.environ.get("TFS_CRC_LIB"):  # an older build under A/B lacks newer entry points
                     continue
                 raise
             f.restype = res
             f.argtypes = args
-        _LIB = L
-    return _LIB
+        _LIBS[path] = L
+    return _LIBS[path]
 
 
 def device_count():
@@ -204,27 +229,31 @@ class Context:
     """One per GPU: wraps tfs_crc_ctx (device tables, stream, staging pools)."""
 
     @classmethod
-    def wrap(cls, handle, device):
+    def wrap(cls, handle, device, L=None):
         """A non-owning view of a context owned elsewhere (a Group member)."""
         c = cls.__new__(cls)
         c.handle, c.device, c._owned = ctypes.c_void_p(handle), device, False
+        c.L = L or lib()
         return c
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, measure=None):
+        """measure: use the measurement build (A/B kernel forms); None = when
+        TFS_CRC_VARIANT / TFS_EC_VARIANT asks for one."""
         self._owned = True
+        self.L = lib(measuring() if measure is None else measure)
         h = ctypes.c_void_p()
-        rc = lib().tfs_crc32_ctx_create(device, ctypes.byref(h))
+        rc = self.L.tfs_crc32_ctx_create(device, ctypes.byref(h))
         if rc != TFS_SUCCESS:
-            msg = lib().tfs_crc32_last_error(h).decode() if h.value else "ctx_create failed"
+            msg = self.L.tfs_crc32_last_error(h).decode() if h.value else "ctx_create failed"
             if h.value:
-                lib().tfs_crc32_ctx_destroy(h)
+                self.L.tfs_crc32_ctx_destroy(h)
             raise TfsCrcError(rc, "tfs_crc32_ctx_create(%d): %s" % (device, msg))
         self.handle = h
         self.device = device
 
     def close(self):
         if getattr(self, "_owned", True) and self.handle is not None and self.handle.value:
-            lib().tfs_crc32_ctx_destroy(self.handle)
+            self.L.tfs_crc32_ctx_destroy(self.handle)
         self.handle = None
 
     def __del__(self):
@@ -241,40 +270,69 @@ class Context:
 
     def _check(self, rc, what, ok=(TFS_SUCCESS,)):
         if rc not in ok:
-            raise TfsCrcError(rc, "%s: %s" % (what, lib().tfs_crc32_last_error(self.handle).decode()))
+            raise TfsCrcError(rc, "%s: %s" % (what, self.L.tfs_crc32_last_error(self.handle).decode()))
         return rc
 
     @property
     def stream(self):
-        return lib().tfs_crc32_stream(self.handle)
+        return self.L.tfs_crc32_stream(self.handle)
 
     def sync(self):
-        self._check(lib().tfs_crc32_sync(self.handle), "sync")
+        self._check(self.L.tfs_crc32_sync(self.handle), "sync")
 
     def inject_device_error(self, skip=0, count=1):
         """Fault injection: the next `count` host submissions after `skip` fail with -20001."""
-        self._check(lib().tfs_crc32_inject_device_error(self.handle, skip, count), "inject_device_error")
+        self._check(self.L.tfs_crc32_inject_device_error(self.handle, skip, count), "inject_device_error")
 
     def set_resident(self, on):
         """Small synchronous batches through the resident kernel (on) or a launch each (off)."""
-        self._check(lib().tfs_crc32_set_resident(self.handle, 1 if on else 0), "set_resident")
+        self._check(self.L.tfs_crc32_set_resident(self.handle, 1 if on else 0), "set_resident")
 
     def resident_stats(self):
         """(launches of the resident kernel, files taken through its ring) so far."""
         a, b = ctypes.c_uint64(), ctypes.c_uint64()
-        self._check(lib().tfs_crc32_resident_stats(self.handle, ctypes.byref(a), ctypes.byref(b)), "resident_stats")
+        self._check(self.L.tfs_crc32_resident_stats(self.handle, ctypes.byref(a), ctypes.byref(b)), "resident_stats")
         return a.value, b.value
+
+    def set_cu_reserve(self, on):
+        """Leave live resident kernels' CUs out of throughput launches (on, the default) or not."""
+        self._check(self.L.tfs_crc32_set_cu_reserve(self.handle, 1 if on else 0), "set_cu_reserve")
+
+    def throughput_grid(self):
+        """Workgroups the next throughput launch of this context would use."""
+        g = self.L.tfs_crc32_throughput_grid(self.handle)
+        if g < 0:
+            self._check(g, "throughput_grid")
+        return g
+
+    def sched_stats(self):
+        """(ctx-owned streams bound, launches so far on streams the ctx does not own)."""
+        a, b = ctypes.c_uint32(), ctypes.c_uint64()
+        self._check(self.L.tfs_crc32_sched_stats(self.handle, ctypes.byref(a), ctypes.byref(b)), "sched_stats")
+        return a.value, b.value
+
+    def debug_state(self):
+        """{sched, sched_bytes, res_state, res_state_bytes}: device addresses of the scheduler slots and
+        resident-kernel state (test hook)."""
+        a, b, c, d = ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_void_p(), ctypes.c_uint64()
+        self._check(self.L.tfs_crc32_debug_state(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c),
+                                                 ctypes.byref(d)), "debug_state")
+        return {"sched": a.value, "sched_bytes": b.value, "res_state": c.value, "res_state_bytes": d.value}
+
+    def debug_poison_resident(self, done):
+        """Test hook: set every resident workgroup's count of units done to `done`."""
+        self._check(self.L.tfs_crc32_debug_poison_resident(self.handle, done), "debug_poison_resident")
 
     def stream_create(self):
         p = ctypes.c_void_p()
-        self._check(lib().tfs_crc32_stream_create(self.handle, ctypes.byref(p)), "stream_create")
+        self._check(self.L.tfs_crc32_stream_create(self.handle, ctypes.byref(p)), "stream_create")
         return p.value
 
     def stream_sync(self, stream):
-        self._check(lib().tfs_crc32_stream_sync(self.handle, stream), "stream_sync")
+        self._check(self.L.tfs_crc32_stream_sync(self.handle, stream), "stream_sync")
 
     def stream_destroy(self, stream):
-        self._check(lib().tfs_crc32_stream_destroy(self.handle, stream), "stream_destroy")
+        self._check(self.L.tfs_crc32_stream_destroy(self.handle, stream), "stream_destroy")
 
     # ---- host-memory batches -------------------------------------------------
     def batch(self, base, offsets, lens, seeds=0):
@@ -286,7 +344,7 @@ class Context:
         d["len"] = lens
         d["aux"] = seeds
         out = np.zeros(n, np.uint32)
-        self._check(lib().tfs_crc32_batch(self.handle, _ptr(d), n, _ptr(buf), buf.size, _ptr(out)), "batch")
+        self._check(self.L.tfs_crc32_batch(self.handle, _ptr(d), n, _ptr(buf), buf.size, _ptr(out)), "batch")
         return out
 
     def verify(self, base, offsets, lens, expected):
@@ -300,7 +358,7 @@ class Context:
         crc = np.zeros(n, np.uint32)
         ok = np.zeros(n, np.uint8)
         nbad = np.zeros(1, np.uint32)
-        rc = lib().tfs_crc32_verify(self.handle, _ptr(d), n, _ptr(buf), buf.size, _ptr(crc), _ptr(ok), _ptr(nbad))
+        rc = self.L.tfs_crc32_verify(self.handle, _ptr(d), n, _ptr(buf), buf.size, _ptr(crc), _ptr(ok), _ptr(nbad))
         self._check(rc, "verify", ok=(TFS_SUCCESS, TFS_EXIT_CHECK_CRC_ERROR))
         return crc, ok, int(nbad[0]), rc
 
@@ -316,69 +374,69 @@ class Context:
         ok = np.zeros(n, np.uint8)
         nbad = np.zeros(1, np.uint32)
         t = ctypes.c_uint64()
-        rc = lib().tfs_crc32_submit_verify(self.handle, _ptr(d), n, _ptr(buf), buf.size, _ptr(crc), _ptr(ok),
+        rc = self.L.tfs_crc32_submit_verify(self.handle, _ptr(d), n, _ptr(buf), buf.size, _ptr(crc), _ptr(ok),
                                            _ptr(nbad), ctypes.byref(t))
         self._check(rc, "submit_verify")
         return {"ticket": t.value, "keep": (buf, d), "crc": crc, "ok": ok, "nbad": nbad}
 
     def wait(self, h):
-        rc = lib().tfs_crc32_wait(self.handle, h["ticket"])
+        rc = self.L.tfs_crc32_wait(self.handle, h["ticket"])
         self._check(rc, "wait", ok=(TFS_SUCCESS, TFS_EXIT_CHECK_CRC_ERROR))
         return h["crc"], h["ok"], int(h["nbad"][0]), rc
 
     def datafile_get_crc(self, data):
         b = bytes(data)
         out = ctypes.c_uint32()
-        self._check(lib().tfs_datafile_get_crc(self.handle, b, len(b), ctypes.byref(out)), "datafile_get_crc")
+        self._check(self.L.tfs_datafile_get_crc(self.handle, b, len(b), ctypes.byref(out)), "datafile_get_crc")
         return out.value
 
     # ---- device-resident (pointers are device addresses: DeviceBuffer or int) ---
     def batch_device(self, d_desc, n, d_base, d_out, stream=None):
-        self._check(lib().tfs_crc32_batch_device(self.handle, _ptr(d_desc), n, _ptr(d_base), _ptr(d_out), stream),
+        self._check(self.L.tfs_crc32_batch_device(self.handle, _ptr(d_desc), n, _ptr(d_base), _ptr(d_out), stream),
                     "batch_device")
 
     def verify_device(self, d_desc, n, d_base, d_crc=None, d_ok=None, d_nbad=None, stream=None):
-        self._check(lib().tfs_crc32_verify_device(self.handle, _ptr(d_desc), n, _ptr(d_base), _ptr(d_crc),
+        self._check(self.L.tfs_crc32_verify_device(self.handle, _ptr(d_desc), n, _ptr(d_base), _ptr(d_crc),
                                                   _ptr(d_ok), _ptr(d_nbad), stream), "verify_device")
 
     def synth_fill_device(self, d_dst, nbytes, seed, first_word=0, stream=None):
-        self._check(lib().tfs_crc32_synth_fill_device(self.handle, _ptr(d_dst), nbytes, seed, first_word, stream),
+        self._check(self.L.tfs_crc32_synth_fill_device(self.handle, _ptr(d_dst), nbytes, seed, first_word, stream),
                     "synth_fill_device")
 
     def write_headers_device(self, d_image, d_rec_off, d_len, d_crc, first_id, n, stream=None):
-        self._check(lib().tfs_crc32_write_headers_device(self.handle, _ptr(d_image), _ptr(d_rec_off), _ptr(d_len),
+        self._check(self.L.tfs_crc32_write_headers_device(self.handle, _ptr(d_image), _ptr(d_rec_off), _ptr(d_len),
                                                          _ptr(d_crc), first_id, n, stream), "write_headers_device")
 
     def membench_device(self, pattern, d_base, d_desc, n, nbytes, d_out, grid=0, stream=None):
-        self._check(lib().tfs_crc32_membench_device(self.handle, pattern, _ptr(d_base), _ptr(d_desc), n, nbytes,
+        self._check(self.L.tfs_crc32_membench_device(self.handle, pattern, _ptr(d_base), _ptr(d_desc), n, nbytes,
                                                     _ptr(d_out), grid, stream), "membench_device")
 
     def block_verify_device(self, d_image, image_len, d_metas, n, d_crc=None, d_status=None, d_nbad=None,
                             stream=None):
-        self._check(lib().tfs_block_verify_device(self.handle, _ptr(d_image), image_len, _ptr(d_metas), n,
+        self._check(self.L.tfs_block_verify_device(self.handle, _ptr(d_image), image_len, _ptr(d_metas), n,
                                                   _ptr(d_crc), _ptr(d_status), _ptr(d_nbad), stream),
                     "block_verify_device")
 
     def block_compact_device(self, d_src, src_len, d_live_metas, d_flags, d_dest_off, n, d_dest, d_crc=None,
                              d_status=None, d_nbad=None, stream=None):
-        self._check(lib().tfs_block_compact_device(self.handle, _ptr(d_src), src_len, _ptr(d_live_metas),
+        self._check(self.L.tfs_block_compact_device(self.handle, _ptr(d_src), src_len, _ptr(d_live_metas),
                                                    _ptr(d_flags), _ptr(d_dest_off), n, _ptr(d_dest), _ptr(d_crc),
                                                    _ptr(d_status), _ptr(d_nbad), stream), "block_compact_device")
 
     def compact_jobs_device(self, d_src, src_len, d_jobs, n, d_dest, d_crc=None, d_status=None, d_nbad=None,
                             stream=None):
-        self._check(lib().tfs_compact_jobs_device(self.handle, _ptr(d_src), src_len, _ptr(d_jobs), n, _ptr(d_dest),
+        self._check(self.L.tfs_compact_jobs_device(self.handle, _ptr(d_src), src_len, _ptr(d_jobs), n, _ptr(d_dest),
                                                   _ptr(d_crc), _ptr(d_status), _ptr(d_nbad), stream),
                     "compact_jobs_device")
 
     def blocks_verify_device(self, d_src, src_len, d_jobs, n, d_crc=None, d_status=None, d_nbad=None, stream=None):
         """Verify-on-read of records of many device-resident blocks (tfs_compact_job layout)."""
-        self._check(lib().tfs_blocks_verify_device(self.handle, _ptr(d_src), src_len, _ptr(d_jobs), n, _ptr(d_crc),
+        self._check(self.L.tfs_blocks_verify_device(self.handle, _ptr(d_src), src_len, _ptr(d_jobs), n, _ptr(d_crc),
                                                    _ptr(d_status), _ptr(d_nbad), stream), "blocks_verify_device")
 
     def blocks_compact(self, jobs):
         """Pipelined compaction of many blocks; `jobs` is a ctypes array of BlockJob."""
-        rc = lib().tfs_blocks_compact(self.handle, ctypes.cast(jobs, ctypes.c_void_p), len(jobs))
+        rc = self.L.tfs_blocks_compact(self.handle, ctypes.cast(jobs, ctypes.c_void_p), len(jobs))
         self._check(rc, "blocks_compact", ok=(TFS_SUCCESS, TFS_EXIT_CHECK_CRC_ERROR))
         return rc
 
@@ -398,7 +456,7 @@ class Context:
         crc = np.zeros(n, np.uint32)
         st = np.zeros(n, np.int32)
         nbad = np.zeros(1, np.uint32)
-        rc = lib().tfs_packet_verify(self.handle, _ptr(d), n, _ptr(buf), buf.size, _ptr(crc), _ptr(st), _ptr(nbad))
+        rc = self.L.tfs_packet_verify(self.handle, _ptr(d), n, _ptr(buf), buf.size, _ptr(crc), _ptr(st), _ptr(nbad))
         self._check(rc, "packet_verify", ok=(TFS_SUCCESS, TFS_EXIT_CHECK_CRC_ERROR))
         return crc, st, int(nbad[0]), rc
 
@@ -409,22 +467,22 @@ class Context:
         n = len(d)
         crc = np.zeros(n, np.uint32)
         st = np.zeros(n, np.int32)
-        self._check(lib().tfs_packet_seal(self.handle, _ptr(d), n, _ptr(buf), buf.size, _ptr(crc), _ptr(st)),
+        self._check(self.L.tfs_packet_seal(self.handle, _ptr(d), n, _ptr(buf), buf.size, _ptr(crc), _ptr(st)),
                     "packet_seal")
         return crc, st
 
     def write_packet_headers_device(self, d_base, d_frame_off, d_body_len, n, pcode=9, version=2, first_id=1,
                                     stream=None):
-        self._check(lib().tfs_crc32_write_packet_headers_device(self.handle, _ptr(d_base), _ptr(d_frame_off),
+        self._check(self.L.tfs_crc32_write_packet_headers_device(self.handle, _ptr(d_base), _ptr(d_frame_off),
                                                                 _ptr(d_body_len), n, pcode, version, first_id,
                                                                 stream), "write_packet_headers_device")
 
     def packet_verify_device(self, d_desc, n, d_base, d_crc, d_status, d_nbad=None, stream=None):
-        self._check(lib().tfs_packet_verify_device(self.handle, _ptr(d_desc), n, _ptr(d_base), _ptr(d_crc),
+        self._check(self.L.tfs_packet_verify_device(self.handle, _ptr(d_desc), n, _ptr(d_base), _ptr(d_crc),
                                                    _ptr(d_status), _ptr(d_nbad), stream), "packet_verify_device")
 
     def packet_seal_device(self, d_desc, n, d_base, d_crc, d_status, stream=None):
-        self._check(lib().tfs_packet_seal_device(self.handle, _ptr(d_desc), n, _ptr(d_base), _ptr(d_crc),
+        self._check(self.L.tfs_packet_seal_device(self.handle, _ptr(d_desc), n, _ptr(d_base), _ptr(d_crc),
                                                  _ptr(d_status), stream), "packet_seal_device")
 
     # ---- block images (host) -------------------------------------------------
@@ -435,7 +493,7 @@ class Context:
         crc = np.zeros(n, np.uint32)
         st = np.zeros(n, np.int32)
         nbad = np.zeros(1, np.uint32)
-        rc = lib().tfs_block_verify(self.handle, _ptr(img), img.size, _ptr(m), n, _ptr(crc), _ptr(st), _ptr(nbad))
+        rc = self.L.tfs_block_verify(self.handle, _ptr(img), img.size, _ptr(m), n, _ptr(crc), _ptr(st), _ptr(nbad))
         self._check(rc, "block_verify", ok=(TFS_SUCCESS, TFS_EXIT_CHECK_CRC_ERROR))
         return crc, st, int(nbad[0]), rc
 
@@ -450,7 +508,7 @@ class Context:
         ok = np.zeros(n, np.uint8)
         dlen = ctypes.c_uint64()
         nlive = ctypes.c_uint32()
-        rc = lib().tfs_block_compact(self.handle, _ptr(img), img.size, _ptr(m), _ptr(fl), n, _ptr(dest), cap,
+        rc = self.L.tfs_block_compact(self.handle, _ptr(img), img.size, _ptr(m), _ptr(fl), n, _ptr(dest), cap,
                                      _ptr(dmetas), _ptr(ok), ctypes.byref(dlen), ctypes.byref(nlive))
         self._check(rc, "block_compact", ok=(TFS_SUCCESS, TFS_EXIT_CHECK_CRC_ERROR))
         return dest[:dlen.value], dmetas[:nlive.value], ok, rc
@@ -535,12 +593,12 @@ class DeviceBuffer:
 
     def __init__(self, ctx, nbytes):
         p = ctypes.c_void_p()
-        ctx._check(lib().tfs_crc32_dev_malloc(ctx.handle, nbytes, ctypes.byref(p)), "dev_malloc(%d)" % nbytes)
+        ctx._check(ctx.L.tfs_crc32_dev_malloc(ctx.handle, nbytes, ctypes.byref(p)), "dev_malloc(%d)" % nbytes)
         self.ctx, self.ptr, self.nbytes = ctx, p.value, nbytes
 
     def free(self):
         if self.ptr:
-            lib().tfs_crc32_dev_free(self.ctx.handle, self.ptr)
+            self.ctx.L.tfs_crc32_dev_free(self.ctx.handle, self.ptr)
             self.ptr = None
 
     def __del__(self):
@@ -551,7 +609,7 @@ class DeviceBuffer:
 
     def upload(self, arr, offset=0):
         a = np.ascontiguousarray(arr)
-        self.ctx._check(lib().tfs_crc32_memcpy(self.ctx.handle, self.ptr + offset, a.ctypes.data, a.nbytes, None),
+        self.ctx._check(self.ctx.L.tfs_crc32_memcpy(self.ctx.handle, self.ptr + offset, a.ctypes.data, a.nbytes, None),
                         "memcpy h2d")
         return self
 
@@ -560,12 +618,12 @@ class DeviceBuffer:
         if count is None:
             count = (self.nbytes - offset) // dt.itemsize
         out = np.empty(count, dt)
-        self.ctx._check(lib().tfs_crc32_memcpy(self.ctx.handle, out.ctypes.data, self.ptr + offset, out.nbytes,
+        self.ctx._check(self.ctx.L.tfs_crc32_memcpy(self.ctx.handle, out.ctypes.data, self.ptr + offset, out.nbytes,
                                                None), "memcpy d2h")
         return out
 
     def zero(self, stream=None):
-        self.ctx._check(lib().tfs_crc32_memset_device(self.ctx.handle, self.ptr, 0, self.nbytes, stream), "memset")
+        self.ctx._check(self.ctx.L.tfs_crc32_memset_device(self.ctx.handle, self.ptr, 0, self.nbytes, stream), "memset")
 
 
 class PinnedBuffer:
@@ -573,10 +631,10 @@ class PinnedBuffer:
 
     def __init__(self, ctx, nbytes):
         p = ctypes.c_void_p()
-        ctx._check(lib().tfs_crc32_host_malloc_pinned(ctx.handle, nbytes, ctypes.byref(p)), "host_malloc_pinned")
+        ctx._check(ctx.L.tfs_crc32_host_malloc_pinned(ctx.handle, nbytes, ctypes.byref(p)), "host_malloc_pinned")
         self.ctx, self.ptr, self.nbytes = ctx, p.value, nbytes
         self.array = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p.value))
-        self._free = lambda ptr: lib().tfs_crc32_host_free_pinned(self.ctx.handle, ptr)
+        self._free = lambda ptr: self.ctx.L.tfs_crc32_host_free_pinned(self.ctx.handle, ptr)
 
     @classmethod
     def adopt(cls, ctx, ptr, nbytes, free_fn):
@@ -595,21 +653,21 @@ class PinnedBuffer:
 class Event:
     def __init__(self, ctx):
         p = ctypes.c_void_p()
-        ctx._check(lib().tfs_crc32_event_create(ctx.handle, ctypes.byref(p)), "event_create")
+        ctx._check(ctx.L.tfs_crc32_event_create(ctx.handle, ctypes.byref(p)), "event_create")
         self.ctx, self.ptr = ctx, p.value
 
     def record(self, stream=None):
-        self.ctx._check(lib().tfs_crc32_event_record(self.ctx.handle, self.ptr, stream), "event_record")
+        self.ctx._check(self.ctx.L.tfs_crc32_event_record(self.ctx.handle, self.ptr, stream), "event_record")
 
     def elapsed_ms(self, end):
         ms = ctypes.c_float()
-        self.ctx._check(lib().tfs_crc32_event_elapsed_ms(self.ctx.handle, self.ptr, end.ptr, ctypes.byref(ms)),
+        self.ctx._check(self.ctx.L.tfs_crc32_event_elapsed_ms(self.ctx.handle, self.ptr, end.ptr, ctypes.byref(ms)),
                         "event_elapsed")
         return ms.value
 
     def __del__(self):
         try:
-            lib().tfs_crc32_event_destroy(self.ctx.handle, self.ptr)
+            self.ctx.L.tfs_crc32_event_destroy(self.ctx.handle, self.ptr)
         except Exception:
             pass
 

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
@@ -25,35 +26,39 @@
 namespace tfscrc {
 hipError_t launch_crc_files(int mode, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
                             uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
-                            int variant, uint32_t vseed, uint32_t* done_flag, uint32_t seq);
+                            int variant, uint32_t vseed, uint32_t* done_flag, uint32_t seq, unsigned cap);
 hipError_t launch_packet_parse(const uint8_t* base, const PacketDesc* pd, uint32_t n, int mode, Desc* desc,
                                int32_t* pre, hipStream_t stream);
 hipError_t launch_packet_finish(uint8_t* base, const PacketDesc* pd, const Desc* desc, uint32_t n, int mode,
                                 const int32_t* pre, const uint8_t* ok, uint32_t* crc, int32_t* status,
                                 uint32_t* n_bad, hipStream_t stream);
-hipError_t launch_block_verify(const uint8_t* image, uint64_t image_len, const RawMeta* metas, uint32_t n,
-                               const Tables* tg, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
-                               hipStream_t stream);
 hipError_t launch_block_verify_pipe(const uint8_t* image, uint64_t image_len, const RawMeta* metas,
                                     const CompactJob* jobs, uint32_t n, const Tables* tg, uint32_t* out_crc,
                                     int32_t* out_status, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
-                                    int variant);
-hipError_t launch_compact_copy(const uint8_t* src, const RawMeta* metas, const int32_t* flags, const int64_t* dest_off,
-                               uint32_t n, uint8_t* dst, hipStream_t stream);
+                                    int variant, unsigned cap);
 hipError_t launch_compact_fused(const uint8_t* src, uint64_t src_len, const RawMeta* metas, const int32_t* flags,
                                 const int64_t* dest_off, uint32_t n, uint8_t* dst, const Tables* tg, uint32_t* out_crc,
                                 int32_t* out_status, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
-                                int variant);
+                                int variant, unsigned cap);
 hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const CompactJob* jobs, uint32_t n, uint8_t* dst,
                                const Tables* tg, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
-                               uint32_t* sched, hipStream_t stream, int variant);
+                               uint32_t* sched, hipStream_t stream, int variant, unsigned cap);
+#ifdef TFS_CRC_MEASURE
+hipError_t launch_block_verify(const uint8_t* image, uint64_t image_len, const RawMeta* metas, uint32_t n,
+                               const Tables* tg, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
+                               hipStream_t stream);
+hipError_t launch_compact_copy(const uint8_t* src, const RawMeta* metas, const int32_t* flags, const int64_t* dest_off,
+                               uint32_t n, uint8_t* dst, hipStream_t stream);
+#endif
 hipError_t launch_synth_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, uint64_t first_word, hipStream_t stream);
 hipError_t launch_write_headers(uint8_t* image, const uint64_t* rec_off, const uint32_t* len, const uint32_t* crc,
                                 uint64_t first_id, uint32_t n, hipStream_t stream);
 hipError_t launch_write_packet_headers(uint8_t* base, const uint64_t* rec_off, const uint32_t* len, uint32_t n,
                                        int32_t pcode, int32_t version, uint64_t first_id, hipStream_t stream);
+#ifdef TFS_CRC_MEASURE
 hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, uint32_t n, uint64_t nbytes,
                            uint32_t* out, unsigned grid, hipStream_t stream);
+#endif
 hipError_t launch_resident(const Tables* tg, const ResHost* hs, uint32_t* dstate, unsigned grid, uint32_t idle_ticks,
                            uint32_t life_ticks, uint32_t gen, hipStream_t stream);
 }  // namespace tfscrc
@@ -181,10 +186,19 @@ struct CompactSlot {
 };
 constexpr int kCompactSlots = 8;          // slots allocated; ctx->compact_slots of them are used
 constexpr uint32_t kSchedSlots = 256;
-constexpr int kVariantUnfusedCompact = 7;  // TFS_CRC_VARIANT=7: two-pass device compaction (A/B baseline)
-constexpr int kVariantDmaCompact = 8;      // TFS_CRC_VARIANT=8: DMA staging for host compaction / block verify / small batches
-constexpr int kVariantZcReadDmaWrite = 38; // TFS_CRC_VARIANT=38: host compaction reads live records in place, the
-                                           // new block goes to device memory and back by a DMA copy
+constexpr uint32_t kForeignSlots = 64;    // the last 64 scheduler slots: launches on streams the ctx does not own
+constexpr uint32_t kOwnedSlots = kSchedSlots - kForeignSlots;
+// Measurement build only (TFS_CRC_VARIANT; the product's ctx->variant is a constant 0):
+constexpr int kVariantDmaCompact = 8;      // DMA staging for host compaction / block verify / small batches
+constexpr int kVariantZcReadDmaWrite = 38; // host compaction reads live records in place, the new block goes to
+                                           // device memory and back by a DMA copy
+#ifdef TFS_CRC_MEASURE
+constexpr int kVariantUnfusedCompact = 7;  // two-pass device compaction (A/B baseline)
+#endif
+// A context that posted a close batch this recently keeps the resident kernel's
+// CUs out of its device's throughput launches even while the kernel is between
+// lifetimes.
+constexpr int64_t kResRecentNs = 50'000'000;
 constexpr uint64_t kZeroCopySpan = 8ull << 20;  // page-locked batches up to this span are read in place
 
 }  // namespace
@@ -204,14 +218,26 @@ struct tfs_crc_ctx {
   CompactSlot cslots[kCompactSlots];
   uint64_t next_ticket = 1;
   // Work-distribution counters: kSchedSlots slots of 8 ticket counters and a
-  // finished-waves counter (one 256-byte line each).  A slot belongs to one
-  // stream (slot 0 = ctx->stream), so the launches sharing it are ordered; each
-  // launch leaves it zeroed (launch_exit in the kernels).
+  // finished-waves counter (one 256-byte line each).  The first kOwnedSlots
+  // belong to streams this ctx owns (slot 0 = ctx->stream, the compaction
+  // streams, tfs_crc32_stream_create), so the launches sharing one are ordered
+  // and each leaves it zeroed (launch_exit in the kernels).  Launches on any
+  // other stream take a slot of the foreign pool per launch (sched_acquire).
   uint32_t* d_sched = nullptr;
   std::mutex sched_mu;
-  std::vector<hipStream_t> sched_streams;
+  std::vector<hipStream_t> sched_streams;  // owned stream of slot k (nullptr = free)
+  hipEvent_t foreign_done[kForeignSlots] = {};  // behind the last launch on foreign slot k
+  bool foreign_busy[kForeignSlots] = {};
+  uint32_t foreign_next = 0;
+  uint64_t foreign_launches = 0;
   int compact_slots = 8;  // blocks in flight in tfs_blocks_compact (TFS_CRC_COMPACT_SLOTS, 1..8)
-  int variant = 0;  // kernel variant (TFS_CRC_VARIANT, measurement knob; 0 = product default)
+#ifdef TFS_CRC_MEASURE
+  int variant = 0;  // kernel variant (TFS_CRC_VARIANT; measurement build only)
+#else
+  static constexpr int variant = 0;  // the product library holds one form of each kernel
+#endif
+  unsigned cus = kMaxGrid;  // compute units of the device: throughput grids are at most this
+  bool cu_reserve = true;   // leave a live resident kernel's CUs out of throughput launches
   std::atomic<uint32_t> inject_skip{0}, inject_count{0};  // tfs_crc32_inject_device_error
   DevBuf packet_scratch;  // device-resident packet calls (parse descriptors, verdicts)
   hipStream_t packet_scratch_stream = nullptr;
@@ -230,6 +256,10 @@ struct tfs_crc_ctx {
   uint32_t res_published = 0;
   uint32_t res_idle_ticks = 0, res_life_ticks = 0;
   uint64_t res_launches = 0, res_files = 0;
+  // Read without ctx->mu by other contexts' throughput launches (throughput_cap):
+  std::atomic<uint32_t> res_gen{0};           // generation of the latest resident launch
+  std::atomic<int64_t> res_last_post_ns{0};   // steady-clock time of the latest post
+  std::atomic<bool> res_ring{false};          // ring set up (res_host valid)
 };
 
 namespace {
@@ -316,22 +346,116 @@ int stage_span(tfs_crc_ctx* ctx, Slot& s, const void* base, uint64_t lo, uint64_
   return TFS_SUCCESS;
 }
 
-// The scheduler slot of stream `st` (see tfs_crc_ctx::d_sched).  Launches on
-// one stream are ordered and each leaves its slot zeroed, so no memset launch is
-// needed; two streams never share a slot.
-hipError_t sched_slot(tfs_crc_ctx* ctx, hipStream_t st, uint32_t** out) {
-  std::lock_guard<std::mutex> g(ctx->sched_mu);
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// (Caller holds sched_mu.)  Give stream `st` its own self-resetting slot.
+hipError_t bind_owned_stream_locked(tfs_crc_ctx* ctx, hipStream_t st) {
   size_t k = 0;
-  while (k < ctx->sched_streams.size() && ctx->sched_streams[k] != st) ++k;
-  if (k == ctx->sched_streams.size()) {
-    k = 0;  // a slot released by tfs_crc32_stream_destroy, else a new one
-    while (k < ctx->sched_streams.size() && ctx->sched_streams[k] != nullptr) ++k;
-    if (k == kSchedSlots) return hipErrorOutOfMemory;  // more than 256 live streams on one context
-    if (k == ctx->sched_streams.size()) ctx->sched_streams.push_back(st);
-    else ctx->sched_streams[k] = st;
+  while (k < ctx->sched_streams.size() && ctx->sched_streams[k] != st && ctx->sched_streams[k] != nullptr) ++k;
+  if (k < ctx->sched_streams.size()) {
+    ctx->sched_streams[k] = st;
+    return hipSuccess;
   }
-  *out = ctx->d_sched + (kSchedSlotBytes / 4u) * k;
+  if (k >= kOwnedSlots) return hipErrorOutOfMemory;  // more than 192 live ctx-owned streams
+  ctx->sched_streams.push_back(st);
   return hipSuccess;
+}
+
+hipError_t bind_owned_stream(tfs_crc_ctx* ctx, hipStream_t st) {
+  std::lock_guard<std::mutex> g(ctx->sched_mu);
+  return bind_owned_stream_locked(ctx, st);
+}
+
+// The scheduler slot one launch on stream `st` uses (see tfs_crc_ctx::d_sched).
+// A ctx-owned stream has its own slot: launches on one stream are ordered and
+// each leaves its slot zeroed, so no memset launch is needed.  Any other stream
+// (a caller's hipStream_t) takes the next slot of the foreign pool: the launch
+// that used it last is waited for, and the slot is zeroed on `st` before the
+// kernel -- so a caller's stream never depends on another launch having left a
+// slot clean, and two unordered streams never share counters.  hipStreamPerThread
+// is refused: it is one handle for a different queue on every thread.
+struct SchedLease {
+  uint32_t* slot = nullptr;
+  int foreign = -1;
+};
+
+int sched_acquire(tfs_crc_ctx* ctx, hipStream_t st, SchedLease* L) {
+  if (st == hipStreamPerThread)
+    return set_err(ctx, TFS_EXIT_PARAMETER_ERROR,
+                   "hipStreamPerThread is not accepted (a different queue per thread behind one handle); pass NULL, a "
+                   "tfs_crc32_stream_create stream or a stream of your own");
+  std::unique_lock<std::mutex> lk(ctx->sched_mu);
+  for (size_t k = 0; k < ctx->sched_streams.size(); ++k)
+    if (ctx->sched_streams[k] == st) {
+      L->slot = ctx->d_sched + (kSchedSlotBytes / 4u) * k;
+      L->foreign = -1;
+      return TFS_SUCCESS;
+    }
+  int k = -1;
+  for (uint32_t i = 0; i < kForeignSlots && k < 0; ++i) {
+    const uint32_t c = (ctx->foreign_next + i) % kForeignSlots;
+    if (!ctx->foreign_busy[c]) k = int(c);
+  }
+  if (k < 0) return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "all %u foreign-stream slots in use", kForeignSlots);
+  ctx->foreign_next = uint32_t(k + 1) % kForeignSlots;
+  ctx->foreign_busy[k] = true;
+  ++ctx->foreign_launches;
+  hipEvent_t prev = ctx->foreign_done[k];
+  lk.unlock();
+  uint32_t* slot = ctx->d_sched + (kSchedSlotBytes / 4u) * (kOwnedSlots + uint32_t(k));
+  hipError_t e = hipSuccess;
+  if (prev) e = hipEventSynchronize(prev);  // the slot's previous launch (normally long finished)
+  if (e == hipSuccess) e = hipMemsetAsync(slot, 0, kSchedSlotBytes, st);
+  if (e != hipSuccess) {
+    std::lock_guard<std::mutex> g(ctx->sched_mu);
+    ctx->foreign_busy[k] = false;
+    return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "foreign-stream slot: %s", hipGetErrorString(e));
+  }
+  L->slot = slot;
+  L->foreign = k;
+  return TFS_SUCCESS;
+}
+
+// After the launch that used lease L on `st` (launch_rc its result).  A launch
+// that failed leaves an owned slot zeroed again on its stream (launch_exit never
+// ran); a foreign slot gets the event its next user waits for.
+int sched_release(tfs_crc_ctx* ctx, hipStream_t st, const SchedLease& L, hipError_t launch_rc, const char* what) {
+  hipError_t e = hipSuccess;
+  if (launch_rc != hipSuccess) (void)hipMemsetAsync(L.slot, 0, kSchedSlotBytes, st);
+  if (L.foreign >= 0) {
+    std::lock_guard<std::mutex> g(ctx->sched_mu);
+    hipEvent_t& ev = ctx->foreign_done[L.foreign];
+    if (!ev) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(ev, st);
+    if (e != hipSuccess && ev) {
+      (void)hipEventDestroy(ev);  // no stale event: the next user of the slot synchronises the stream instead
+      ev = nullptr;
+      (void)hipStreamSynchronize(st);
+    }
+    ctx->foreign_busy[L.foreign] = false;
+  }
+  if (launch_rc != hipSuccess)
+    return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "%s launch failed: %s", what, hipGetErrorString(launch_rc));
+  if (e != hipSuccess) return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "%s: %s", what, hipGetErrorString(e));
+  return TFS_SUCCESS;
+}
+
+// Workgroups of a throughput launch (crc_files_kernel, compact_pipe_kernel: one
+// persistent workgroup per CU).  A resident kernel (§3.7 of DESIGN.md) holds
+// res_grid CUs of its device while it lives; a throughput launch that asked
+// for every CU would then wait with res_grid workgroups until it leaves (up to
+// its lifetime, 10 ms), and a resident kernel launched behind a full-grid launch
+// waits for CUs until that launch ends.  So while any context on this device
+// has a resident kernel alive or posted a batch within kResRecentNs, throughput
+// launches leave its CUs free.
+bool resident_live(const tfs_crc_ctx* c, int64_t now) {
+  if (!c->res_ring.load(std::memory_order_acquire)) return false;
+  const uint32_t gen = c->res_gen.load(std::memory_order_acquire);
+  const bool alive = gen != 0 && __atomic_load_n(&c->res_host->left, __ATOMIC_ACQUIRE) != gen;
+  return alive || now - c->res_last_post_ns.load(std::memory_order_relaxed) < kResRecentNs;
 }
 
 // Host side of a zero-copy launch's completion: spin on the page-locked flag
@@ -416,8 +540,42 @@ int resident_setup(tfs_crc_ctx* ctx) {
   ctx->res_published = 0;
   std::lock_guard<std::mutex> g(g_res_mu);
   g_res_ctxs.push_back(ctx);
+  ctx->res_ring.store(true, std::memory_order_release);
   return TFS_SUCCESS;
 }
+
+// Workgroups for a throughput launch of ctx: its device's CUs minus those of
+// the live resident kernels on that device (resident_live), in multiples of 8
+// (one per XCD).
+unsigned throughput_cap(const tfs_crc_ctx* ctx) {
+  const unsigned cap = ctx->cus < kMaxGrid ? ctx->cus : kMaxGrid;
+  if (!ctx->cu_reserve) return cap;
+  const int64_t now = now_ns();
+  unsigned held = 0;
+  {
+    std::lock_guard<std::mutex> g(g_res_mu);
+    for (const tfs_crc_ctx* c : g_res_ctxs)
+      if (c->device == ctx->device && resident_live(c, now)) held += c->res_grid;
+  }
+  if (held == 0) return cap;
+  const unsigned left = held + 8u < cap ? cap - held : 8u;
+  return left & ~7u ? left & ~7u : 8u;
+}
+
+// Grid cap for a crc_files launch of n files (batches of at most kWgMaxFiles
+// take the latency form, one workgroup per file: no cap to compute).
+unsigned cap_for(const tfs_crc_ctx* ctx, uint32_t n) { return n <= kWgMaxFiles ? kMaxGrid : throughput_cap(ctx); }
+
+// One launch on stream `st` with a scheduler slot leased for it (`sched` in
+// LAUNCH); returns from the caller on failure.
+#define SCHED_LAUNCH(ctx, st, what, LAUNCH)                                       \
+  do {                                                                           \
+    SchedLease lease_;                                                           \
+    if (const int r_ = sched_acquire((ctx), (st), &lease_)) return r_;          \
+    uint32_t* sched = lease_.slot;                                               \
+    const hipError_t le_ = (LAUNCH);                                             \
+    if (const int r2_ = sched_release((ctx), (st), lease_, le_, (what))) return r2_; \
+  } while (0)
 
 // (Caller holds ctx->mu.)  Launch the resident kernel unless one is running.
 // Only one is ever in flight: a new one is launched only after the event behind
@@ -429,11 +587,13 @@ int resident_ensure_running(tfs_crc_ctx* ctx) {
     if (e != hipSuccess) return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "resident kernel failed: %s", hipGetErrorString(e));
     ctx->res_running = false;
   }
+  const uint32_t gen = uint32_t(ctx->res_launches + 1u);
   HIP_TRY(ctx, launch_resident(ctx->d_tables, ctx->res_host_d, ctx->res_state, ctx->res_grid, ctx->res_idle_ticks,
-                               ctx->res_life_ticks, uint32_t(ctx->res_launches + 1u), ctx->res_stream));
+                               ctx->res_life_ticks, gen, ctx->res_stream));
   HIP_TRY(ctx, hipEventRecord(ctx->res_event, ctx->res_stream));
   ctx->res_running = true;
   ++ctx->res_launches;
+  ctx->res_gen.store(gen, std::memory_order_release);
   return TFS_SUCCESS;
 }
 
@@ -463,6 +623,7 @@ int resident_post(tfs_crc_ctx* ctx, Slot& s, int mode, const uint8_t* zb, const 
   s.res_first = P;
   ctx->res_published = P + n;
   ctx->res_files += n;
+  ctx->res_last_post_ns.store(now_ns(), std::memory_order_relaxed);
   __atomic_store_n(&H->published, uint64_t(ctx->res_published), __ATOMIC_RELEASE);
   const int rc = resident_ensure_running(ctx);
   // A launch that fails leaves units published that no kernel may ever take (or
@@ -525,6 +686,7 @@ void resident_teardown(tfs_crc_ctx* ctx) {
   {
     std::lock_guard<std::mutex> g(g_res_mu);
     g_res_ctxs.erase(std::remove(g_res_ctxs.begin(), g_res_ctxs.end(), ctx), g_res_ctxs.end());
+    ctx->res_ring.store(false, std::memory_order_release);
   }
   __atomic_store_n(&ctx->res_host->published, uint64_t(ctx->res_published) | (uint64_t(1) << 32), __ATOMIC_RELEASE);
   if (ctx->res_stream) (void)hipStreamSynchronize(ctx->res_stream);
@@ -611,12 +773,12 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
         }
         // no room in the ring: launch this batch
       }
-      uint32_t* sched = nullptr;
-      HIP_TRY(ctx, sched_slot(ctx, ctx->stream, &sched));
       // n_bad is counted from the verdicts on the host (no atomics on host memory)
-      HIP_TRY(ctx, launch_crc_files(mode, static_cast<const uint8_t*>(zb) - lo, static_cast<const Desc*>(zd), n,
+      SCHED_LAUNCH(ctx, ctx->stream, "crc_files",
+                   launch_crc_files(mode, static_cast<const uint8_t*>(zb) - lo, static_cast<const Desc*>(zd), n,
                                     ctx->d_tables, static_cast<uint32_t*>(zcrc), static_cast<uint8_t*>(zok), nullptr,
-                                    sched, ctx->stream, ctx->variant, 0u, static_cast<uint32_t*>(zflag), s.seq));
+                                    sched, ctx->stream, ctx->variant, 0u, static_cast<uint32_t*>(zflag), s.seq,
+                                    cap_for(ctx, n)));
       HIP_TRY(ctx, hipEventRecord(s.done, ctx->stream));
       s.count_bad = true;
       s.spin = true;
@@ -634,11 +796,9 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
   HIP_TRY(ctx, s.d_bad.reserve(4));
   HIP_TRY(ctx, hipMemcpyAsync(s.d_desc.p, d, size_t(n) * sizeof(Desc), hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(ctx, hipMemsetAsync(s.d_bad.p, 0, 4, ctx->stream));
-  uint32_t* sched = nullptr;
-  HIP_TRY(ctx, sched_slot(ctx, ctx->stream, &sched));
-  HIP_TRY(ctx, launch_crc_files(mode, d_base, static_cast<const Desc*>(s.d_desc.p), n, ctx->d_tables,
+  SCHED_LAUNCH(ctx, ctx->stream, "crc_files", launch_crc_files(mode, d_base, static_cast<const Desc*>(s.d_desc.p), n, ctx->d_tables,
                                 static_cast<uint32_t*>(s.d_crc.p), static_cast<uint8_t*>(s.d_ok.p),
-                                static_cast<uint32_t*>(s.d_bad.p), sched, ctx->stream, ctx->variant, 0u, nullptr, 0u));
+                                static_cast<uint32_t*>(s.d_bad.p), sched, ctx->stream, ctx->variant, 0u, nullptr, 0u, cap_for(ctx, n)));
   HIP_TRY(ctx, hipMemcpyAsync(s.h_crc.p, s.d_crc.p, size_t(n) * 4, hipMemcpyDeviceToHost, ctx->stream));
   if (mode == 1) {
     HIP_TRY(ctx, hipMemcpyAsync(s.h_ok.p, s.d_ok.p, n, hipMemcpyDeviceToHost, ctx->stream));
@@ -688,6 +848,34 @@ tfs_crc_ctx* default_ctx(int* rc) {
   return g_default;
 }
 
+// The scalar drop-in's context: the calling thread's binding
+// (tfs_crc32_bind_thread), else the process default the caller chose
+// (tfs_crc32_set_default_ctx), else a context on device 0 created on first use.
+thread_local tfs_crc_ctx* t_scalar_ctx = nullptr;
+std::atomic<tfs_crc_ctx*> g_scalar_ctx{nullptr};
+
+tfs_crc_ctx* scalar_ctx(int* rc) {
+  if (rc) *rc = TFS_SUCCESS;
+  if (t_scalar_ctx) return t_scalar_ctx;
+  if (tfs_crc_ctx* c = g_scalar_ctx.load(std::memory_order_acquire)) return c;
+  return default_ctx(rc);
+}
+
+// Failures of the scalar drop-in (Func::crc has no error channel): counted for
+// the whole process and reported on stderr once, so a device fault never passes
+// as a plain CRC mismatch unseen (tfs_crc32_error_count).
+std::atomic<uint64_t> g_scalar_errors{0};
+std::atomic<bool> g_scalar_logged{false};
+
+void scalar_failed(tfs_crc_ctx* ctx, int rc) {
+  g_scalar_errors.fetch_add(1, std::memory_order_relaxed);
+  if (!g_scalar_logged.exchange(true))
+    fprintf(stderr,
+            "tfs_crc32: the scalar Func::crc drop-in failed (%d: %s) and returned its seed; callers that can act on "
+            "an error use tfs_crc32_e (tfs_crc32_error_count counts every such failure; reported once)\n",
+            rc, ctx ? ctx->last_error : g_default_err.c_str());
+}
+
 }  // namespace
 
 extern "C" {
@@ -709,7 +897,9 @@ int tfs_crc32_ctx_create(int device, tfs_crc_ctx** out) {
   if (device < 0 || device >= ndev) return TFS_EXIT_PARAMETER_ERROR;
   auto* ctx = new tfs_crc_ctx();
   ctx->device = device;
+#ifdef TFS_CRC_MEASURE
   if (const char* v = getenv("TFS_CRC_VARIANT")) ctx->variant = atoi(v);
+#endif
   if (const char* v = getenv("TFS_CRC_COMPACT_SLOTS")) ctx->compact_slots = std::min(std::max(atoi(v), 1), kCompactSlots);
   if (const char* v = getenv("TFS_CRC_RESIDENT")) ctx->resident = atoi(v) != 0;
   if (const char* v = getenv("TFS_CRC_RESIDENT_WGS")) ctx->res_grid = unsigned(std::min(std::max(atoi(v), 1), 256));
@@ -726,6 +916,7 @@ int tfs_crc32_ctx_create(int device, tfs_crc_ctx** out) {
       rc = set_err(ctx, TFS_CRC_EXIT_NO_DEVICE, "device %d is %s; kernels are built for gfx950 only", device, prop.gcnArchName);
       break;
     }
+    if (prop.multiProcessorCount > 0) ctx->cus = unsigned(prop.multiProcessorCount);
     e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e != hipSuccess) { rc = set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "hipStreamCreate: %s", hipGetErrorString(e)); break; }
     std::vector<Tables> host(1);
@@ -751,6 +942,11 @@ int tfs_crc32_ctx_create(int device, tfs_crc_ctx** out) {
 
 int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx) {
   if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
+  {
+    tfs_crc_ctx* expect = ctx;  // no longer the scalar default (a thread binding is the caller's to clear)
+    g_scalar_ctx.compare_exchange_strong(expect, nullptr);
+    if (t_scalar_ctx == ctx) t_scalar_ctx = nullptr;
+  }
   if (ctx->device >= 0) (void)hipSetDevice(ctx->device);
   resident_teardown(ctx);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
@@ -759,6 +955,11 @@ int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx) {
   for (auto& cs : ctx->cslots) {
     if (cs.stream) (void)hipStreamSynchronize(cs.stream);
     cs.release();
+  }
+  for (hipEvent_t& ev : ctx->foreign_done) {
+    if (ev) (void)hipEventSynchronize(ev);
+    if (ev) (void)hipEventDestroy(ev);
+    ev = nullptr;
   }
   ctx->packet_scratch.release();
   if (ctx->d_tables) (void)hipFree(ctx->d_tables);
@@ -770,11 +971,27 @@ int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx) {
 
 const char* tfs_crc32_last_error(const tfs_crc_ctx* ctx) {
   if (!ctx) {
+    if (t_scalar_ctx) return t_scalar_ctx->last_error;
+    if (const tfs_crc_ctx* c = g_scalar_ctx.load()) return c->last_error;
     if (g_default) return g_default->last_error;
     return g_default_err.c_str();
   }
   return ctx->last_error;
 }
+
+uint64_t tfs_crc32_error_count(void) { return g_scalar_errors.load(); }
+
+int tfs_crc32_set_default_ctx(tfs_crc_ctx* ctx) {
+  g_scalar_ctx.store(ctx, std::memory_order_release);
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_bind_thread(tfs_crc_ctx* ctx) {
+  t_scalar_ctx = ctx;
+  return TFS_SUCCESS;
+}
+
+tfs_crc_ctx* tfs_crc32_default_ctx(void) { return scalar_ctx(nullptr); }
 
 namespace {
 
@@ -878,10 +1095,8 @@ int tfs_crc32_batch_device(tfs_crc_ctx* ctx, const tfs_crc_desc* d_desc, uint32_
   if (!ctx || (n && (!d_desc || !d_base || !d_out_crc))) return TFS_EXIT_PARAMETER_ERROR;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  uint32_t* sched = nullptr;
-  HIP_TRY(ctx, sched_slot(ctx, st, &sched));
-  HIP_TRY(ctx, launch_crc_files(0, static_cast<const uint8_t*>(d_base), reinterpret_cast<const Desc*>(d_desc), n,
-                                ctx->d_tables, d_out_crc, nullptr, nullptr, sched, st, ctx->variant, 0u, nullptr, 0u));
+  SCHED_LAUNCH(ctx, st, "crc_files", launch_crc_files(0, static_cast<const uint8_t*>(d_base), reinterpret_cast<const Desc*>(d_desc), n,
+                                ctx->d_tables, d_out_crc, nullptr, nullptr, sched, st, ctx->variant, 0u, nullptr, 0u, cap_for(ctx, n)));
   return TFS_SUCCESS;
 }
 
@@ -890,10 +1105,8 @@ int tfs_crc32_verify_device(tfs_crc_ctx* ctx, const tfs_crc_vdesc* d_desc, uint3
   if (!ctx || (n && (!d_desc || !d_base))) return TFS_EXIT_PARAMETER_ERROR;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  uint32_t* sched = nullptr;
-  HIP_TRY(ctx, sched_slot(ctx, st, &sched));
-  HIP_TRY(ctx, launch_crc_files(1, static_cast<const uint8_t*>(d_base), reinterpret_cast<const Desc*>(d_desc), n,
-                                ctx->d_tables, d_out_crc, d_out_ok, d_n_bad, sched, st, ctx->variant, 0u, nullptr, 0u));
+  SCHED_LAUNCH(ctx, st, "crc_files", launch_crc_files(1, static_cast<const uint8_t*>(d_base), reinterpret_cast<const Desc*>(d_desc), n,
+                                ctx->d_tables, d_out_crc, d_out_ok, d_n_bad, sched, st, ctx->variant, 0u, nullptr, 0u, cap_for(ctx, n)));
   return TFS_SUCCESS;
 }
 
@@ -905,8 +1118,9 @@ uint32_t tfs_crc32_e(uint32_t crc, const char* data, int32_t len, int* err) {
     return crc;
   }
   int rc = 0;
-  tfs_crc_ctx* ctx = default_ctx(&rc);
+  tfs_crc_ctx* ctx = scalar_ctx(&rc);
   if (!ctx) {
+    scalar_failed(nullptr, rc);
     if (err) *err = rc;
     return crc;
   }
@@ -914,6 +1128,7 @@ uint32_t tfs_crc32_e(uint32_t crc, const char* data, int32_t len, int* err) {
   uint32_t out = crc;
   rc = tfs_crc32_batch(ctx, &d, 1, data, uint64_t(len), &out);
   if (rc) {
+    scalar_failed(ctx, rc);
     if (err) *err = rc;
     return crc;
   }
@@ -930,7 +1145,7 @@ int tfs_datafile_get_crc(tfs_crc_ctx* ctx, const char* data, int32_t length, uin
   }
   if (!ctx) {
     int rc = 0;
-    ctx = default_ctx(&rc);
+    ctx = scalar_ctx(&rc);
     if (!ctx) return rc;
   }
   tfs_crc_desc d{0, uint32_t(length), 0u};
@@ -942,11 +1157,9 @@ int tfs_block_verify_device(tfs_crc_ctx* ctx, const void* d_image, uint64_t imag
   if (!ctx || (n && (!d_image || !d_metas))) return TFS_EXIT_PARAMETER_ERROR;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  uint32_t* sched = nullptr;
-  HIP_TRY(ctx, sched_slot(ctx, st, &sched));
-  HIP_TRY(ctx, launch_block_verify_pipe(static_cast<const uint8_t*>(d_image), image_len,
+  SCHED_LAUNCH(ctx, st, "block_verify_pipe", launch_block_verify_pipe(static_cast<const uint8_t*>(d_image), image_len,
                                         reinterpret_cast<const RawMeta*>(d_metas), nullptr, n, ctx->d_tables, d_out_crc,
-                                        d_out_status, d_n_bad, sched, st, ctx->variant));
+                                        d_out_status, d_n_bad, sched, st, ctx->variant, throughput_cap(ctx)));
   return TFS_SUCCESS;
 }
 
@@ -955,11 +1168,9 @@ int tfs_blocks_verify_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_l
   if (!ctx || (n && (!d_src || !d_jobs))) return TFS_EXIT_PARAMETER_ERROR;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  uint32_t* sched = nullptr;
-  HIP_TRY(ctx, sched_slot(ctx, st, &sched));
-  HIP_TRY(ctx, launch_block_verify_pipe(static_cast<const uint8_t*>(d_src), src_len, nullptr,
+  SCHED_LAUNCH(ctx, st, "block_verify_pipe", launch_block_verify_pipe(static_cast<const uint8_t*>(d_src), src_len, nullptr,
                                         reinterpret_cast<const CompactJob*>(d_jobs), n, ctx->d_tables, d_out_crc,
-                                        d_out_status, d_n_bad, sched, st, ctx->variant));
+                                        d_out_status, d_n_bad, sched, st, ctx->variant, throughput_cap(ctx)));
   return TFS_SUCCESS;
 }
 
@@ -997,12 +1208,10 @@ int tfs_block_verify(tfs_crc_ctx* ctx, const void* image, uint64_t image_len, co
   HIP_TRY(ctx, s->h_bad.reserve(4));
   HIP_TRY(ctx, hipMemcpyAsync(s->d_desc.p, metas, size_t(n) * sizeof(RawMeta), hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(ctx, hipMemsetAsync(s->d_bad.p, 0, 4, ctx->stream));
-  uint32_t* sched = nullptr;
-  HIP_TRY(ctx, sched_slot(ctx, ctx->stream, &sched));
-  HIP_TRY(ctx, launch_block_verify_pipe(d_base, image_len, static_cast<const RawMeta*>(s->d_desc.p), nullptr, n,
+  SCHED_LAUNCH(ctx, ctx->stream, "block_verify_pipe", launch_block_verify_pipe(d_base, image_len, static_cast<const RawMeta*>(s->d_desc.p), nullptr, n,
                                         ctx->d_tables, static_cast<uint32_t*>(s->d_crc.p),
                                         static_cast<int32_t*>(s->d_ok.p), static_cast<uint32_t*>(s->d_bad.p), sched,
-                                        ctx->stream, ctx->variant));
+                                        ctx->stream, ctx->variant, throughput_cap(ctx)));
   HIP_TRY(ctx, hipMemcpyAsync(s->h_crc.p, s->d_crc.p, size_t(n) * 4, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipMemcpyAsync(s->h_ok.p, s->d_ok.p, size_t(n) * 4, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipMemcpyAsync(s->h_bad.p, s->d_bad.p, 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -1095,10 +1304,8 @@ static int compact_enqueue(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job
       HIP_TRY(ctx, cs.d_dst.reserve(uint64_t(w) + 16));
       kdst = static_cast<uint8_t*>(cs.d_dst.p);
     }
-    uint32_t* sched = nullptr;
-    HIP_TRY(ctx, sched_slot(ctx, cs.stream, &sched));
-    HIP_TRY(ctx, launch_compact_fused(static_cast<const uint8_t*>(zc_src), job->src_len, d_metas, d_flags, d_doff, nl,
-                                      kdst, ctx->d_tables, d_crc, d_status, nullptr, sched, cs.stream, ctx->variant));
+    SCHED_LAUNCH(ctx, cs.stream, "compact_fused", launch_compact_fused(static_cast<const uint8_t*>(zc_src), job->src_len, d_metas, d_flags, d_doff, nl,
+                                      kdst, ctx->d_tables, d_crc, d_status, nullptr, sched, cs.stream, ctx->variant, throughput_cap(ctx)));
     HIP_TRY(ctx, hipMemcpyAsync(cs.h_status.p, d_status, fb, hipMemcpyDeviceToHost, cs.stream));
     if (dma_write && w)
       HIP_TRY(ctx, hipMemcpyAsync(job->dest_image, cs.d_dst.p, size_t(w), hipMemcpyDeviceToHost, cs.stream));
@@ -1137,11 +1344,9 @@ static int compact_dma(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job, ui
     const uint8_t* d_src = static_cast<const uint8_t*>(cs.d_src.p);
     // One read of every live record: re-CRC (the verify the reference's
     // real_compact does not do) and repack from the same registers.
-    uint32_t* sched = nullptr;
-    HIP_TRY(ctx, sched_slot(ctx, cs.stream, &sched));
-    HIP_TRY(ctx, launch_compact_fused(d_src, job->src_len, d_metas, d_flags, d_doff, nl,
+    SCHED_LAUNCH(ctx, cs.stream, "compact_fused", launch_compact_fused(d_src, job->src_len, d_metas, d_flags, d_doff, nl,
                                       static_cast<uint8_t*>(cs.d_dst.p), ctx->d_tables, d_crc, d_status, nullptr, sched,
-                                      cs.stream, ctx->variant));
+                                      cs.stream, ctx->variant, throughput_cap(ctx)));
     HIP_TRY(ctx, hipMemcpyAsync(cs.h_status.p, d_status, fb, hipMemcpyDeviceToHost, cs.stream));
     if (w) HIP_TRY(ctx, hipMemcpyAsync(job->dest_image, cs.d_dst.p, size_t(w), hipMemcpyDeviceToHost, cs.stream));
   }
@@ -1171,7 +1376,10 @@ int tfs_blocks_compact(tfs_crc_ctx* ctx, tfs_block_job* jobs, uint32_t njobs) {
   std::lock_guard<std::mutex> g(ctx->mu);
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   for (auto& cs : ctx->cslots)
-    if (!cs.stream) HIP_TRY(ctx, hipStreamCreateWithFlags(&cs.stream, hipStreamNonBlocking));
+    if (!cs.stream) {
+      HIP_TRY(ctx, hipStreamCreateWithFlags(&cs.stream, hipStreamNonBlocking));
+      HIP_TRY(ctx, bind_owned_stream(ctx, cs.stream));
+    }
   int worst = TFS_SUCCESS;
   auto note = [&](int rc) {
     if (rc != TFS_SUCCESS && (worst == TFS_SUCCESS || worst == TFS_EXIT_CHECK_CRC_ERROR)) worst = rc;
@@ -1196,7 +1404,8 @@ int tfs_block_compact_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_l
   if (!ctx || (n && (!d_src || !d_live_metas || !d_flags || !d_dest_off || !d_dest))) return TFS_EXIT_PARAMETER_ERROR;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  if (ctx->variant == kVariantUnfusedCompact) {  // measurement knob: verify, then a separate copy pass
+#ifdef TFS_CRC_MEASURE
+  if (ctx->variant == kVariantUnfusedCompact) {  // measurement build: verify, then a separate copy pass
     HIP_TRY(ctx, launch_block_verify(static_cast<const uint8_t*>(d_src), src_len,
                                      reinterpret_cast<const RawMeta*>(d_live_metas), n, ctx->d_tables, d_out_crc,
                                      d_out_status, d_n_bad, st));
@@ -1204,12 +1413,11 @@ int tfs_block_compact_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_l
                                      d_flags, d_dest_off, n, static_cast<uint8_t*>(d_dest), st));
     return TFS_SUCCESS;
   }
-  uint32_t* sched = nullptr;
-  HIP_TRY(ctx, sched_slot(ctx, st, &sched));
-  HIP_TRY(ctx, launch_compact_fused(static_cast<const uint8_t*>(d_src), src_len,
+#endif
+  SCHED_LAUNCH(ctx, st, "compact_fused", launch_compact_fused(static_cast<const uint8_t*>(d_src), src_len,
                                     reinterpret_cast<const RawMeta*>(d_live_metas), d_flags, d_dest_off, n,
                                     static_cast<uint8_t*>(d_dest), ctx->d_tables, d_out_crc, d_out_status, d_n_bad,
-                                    sched, st, ctx->variant));
+                                    sched, st, ctx->variant, throughput_cap(ctx)));
   return TFS_SUCCESS;
 }
 
@@ -1219,11 +1427,9 @@ int tfs_compact_jobs_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_le
   if (!ctx || (n && (!d_src || !d_jobs || !d_dest))) return TFS_EXIT_PARAMETER_ERROR;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  uint32_t* sched = nullptr;
-  HIP_TRY(ctx, sched_slot(ctx, st, &sched));
-  HIP_TRY(ctx, launch_compact_jobs(static_cast<const uint8_t*>(d_src), src_len,
+  SCHED_LAUNCH(ctx, st, "compact_jobs", launch_compact_jobs(static_cast<const uint8_t*>(d_src), src_len,
                                    reinterpret_cast<const CompactJob*>(d_jobs), n, static_cast<uint8_t*>(d_dest),
-                                   ctx->d_tables, d_out_crc, d_out_status, d_n_bad, sched, st, ctx->variant));
+                                   ctx->d_tables, d_out_crc, d_out_status, d_n_bad, sched, st, ctx->variant, throughput_cap(ctx)));
   return TFS_SUCCESS;
 }
 
@@ -1264,10 +1470,8 @@ static int packet_enqueue(tfs_crc_ctx* ctx, int mode, const PacketDesc* d_pd, ui
   uint8_t* d_ok = sp + size_t(n) * (sizeof(Desc) + 8);
   uint32_t* crc = d_crc ? d_crc : d_tmp_crc;
   HIP_TRY(ctx, launch_packet_parse(d_base, d_pd, n, mode, d_desc, d_pre, st));
-  uint32_t* sched = nullptr;
-  HIP_TRY(ctx, sched_slot(ctx, st, &sched));
-  HIP_TRY(ctx, launch_crc_files(mode, d_base, d_desc, n, ctx->d_tables, crc, mode == 1 ? d_ok : nullptr, nullptr,
-                                sched, st, ctx->variant, kPacketFlagV1, nullptr, 0u));
+  SCHED_LAUNCH(ctx, st, "crc_files", launch_crc_files(mode, d_base, d_desc, n, ctx->d_tables, crc, mode == 1 ? d_ok : nullptr, nullptr,
+                                sched, st, ctx->variant, kPacketFlagV1, nullptr, 0u, cap_for(ctx, n)));
   HIP_TRY(ctx, launch_packet_finish(d_base, d_pd, d_desc, n, mode, d_pre, d_ok, crc, d_status, d_n_bad, st));
   return TFS_SUCCESS;
 }
@@ -1507,11 +1711,17 @@ int tfs_crc32_write_packet_headers_device(tfs_crc_ctx* ctx, void* d_base, const 
 int tfs_crc32_membench_device(tfs_crc_ctx* ctx, int pattern, const void* d_base, const tfs_crc_desc* d_desc,
                               uint32_t n, uint64_t nbytes, uint32_t* d_out, unsigned grid, void* stream) {
   if (!ctx || !d_base || !d_out) return TFS_EXIT_PARAMETER_ERROR;
+#ifdef TFS_CRC_MEASURE
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   HIP_TRY(ctx, launch_membench(pattern, static_cast<const uint8_t*>(d_base), reinterpret_cast<const Desc*>(d_desc), n,
                                nbytes, d_out, grid, st));
   return TFS_SUCCESS;
+#else
+  (void)pattern, (void)d_desc, (void)n, (void)nbytes, (void)grid, (void)stream;
+  return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "calibration kernels are in the measurement build only "
+                 "(tfs_amd/libtfs_crc_measure.so)");
+#endif
 }
 
 int tfs_crc32_dev_malloc(tfs_crc_ctx* ctx, uint64_t bytes, void** d_ptr) {
@@ -1635,6 +1845,55 @@ int tfs_crc32_set_resident(tfs_crc_ctx* ctx, int on) {
   return TFS_SUCCESS;
 }
 
+int tfs_crc32_debug_state(tfs_crc_ctx* ctx, void** d_sched, uint64_t* sched_bytes, void** d_res_state,
+                          uint64_t* res_state_bytes) {
+  if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (d_sched) *d_sched = ctx->d_sched;
+  if (sched_bytes) *sched_bytes = uint64_t(kSchedSlots) * kSchedSlotBytes;
+  if (d_res_state) *d_res_state = ctx->res_state;
+  if (res_state_bytes) *res_state_bytes = kResStateBytes;
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_debug_poison_resident(tfs_crc_ctx* ctx, uint32_t done) {
+  if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  if (const int rc = resident_setup(ctx)) return rc;
+  if (ctx->res_running) {  // only between lifetimes: a live kernel owns its lines
+    const hipError_t e = hipEventQuery(ctx->res_event);
+    if (e == hipErrorNotReady) return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "resident kernel is running");
+  }
+  std::vector<uint32_t> lines(size_t(kResMaxGrid) * kSchedStride, 0u);
+  for (uint32_t w = 0; w < kResMaxGrid; ++w) lines[size_t(w) * kSchedStride] = done;
+  HIP_TRY(ctx, hipMemcpyAsync(ctx->res_state, lines.data(), lines.size() * 4, hipMemcpyHostToDevice, ctx->res_stream));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->res_stream));
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_set_cu_reserve(tfs_crc_ctx* ctx, int on) {
+  if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  ctx->cu_reserve = on != 0;
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_throughput_grid(tfs_crc_ctx* ctx) {
+  if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
+  return int(throughput_cap(ctx));
+}
+
+int tfs_crc32_sched_stats(tfs_crc_ctx* ctx, uint32_t* owned_streams, uint64_t* foreign_launches) {
+  if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
+  std::lock_guard<std::mutex> g(ctx->sched_mu);
+  uint32_t k = 0;
+  for (hipStream_t st : ctx->sched_streams) k += st ? 1u : 0u;
+  if (owned_streams) *owned_streams = k;
+  if (foreign_launches) *foreign_launches = ctx->foreign_launches;
+  return TFS_SUCCESS;
+}
+
 int tfs_crc32_resident_stats(tfs_crc_ctx* ctx, uint64_t* launches, uint64_t* files) {
   if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
   std::lock_guard<std::mutex> g(ctx->mu);
@@ -1649,6 +1908,10 @@ int tfs_crc32_stream_create(tfs_crc_ctx* ctx, void** stream) {
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   hipStream_t st = nullptr;
   HIP_TRY(ctx, hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  if (bind_owned_stream(ctx, st) != hipSuccess) {
+    (void)hipStreamDestroy(st);
+    return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "more than %u live streams on one context", kOwnedSlots);
+  }
   *stream = st;
   return TFS_SUCCESS;
 }
@@ -1665,7 +1928,8 @@ int tfs_crc32_stream_destroy(tfs_crc_ctx* ctx, void* stream) {
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   HIP_TRY(ctx, hipStreamSynchronize(static_cast<hipStream_t>(stream)));
   {
-    // Its scheduler slot is zero (every launch leaves it so) and may be rebound.
+    // Its scheduler slot is zero (every launch leaves it so, a failed one is
+    // zeroed again) and may be rebound.
     std::lock_guard<std::mutex> g(ctx->sched_mu);
     for (auto& s : ctx->sched_streams)
       if (s == static_cast<hipStream_t>(stream)) s = nullptr;

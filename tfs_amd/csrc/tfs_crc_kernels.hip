@@ -1177,6 +1177,12 @@ __device__ __forceinline__ HdrFields read_hdr(const uint8_t* rec) {
   return h;
 }
 
+#ifdef TFS_CRC_MEASURE
+// ---------------------------------------------------------------------------
+// Measurement build only (libtfs_crc_measure.so, -DTFS_CRC_MEASURE): earlier
+// kernel forms kept as A/B baselines (TFS_CRC_VARIANT 7, 22, 24).  The product
+// library does not contain them and ignores TFS_CRC_VARIANT.
+// ---------------------------------------------------------------------------
 // Verify files stored in a block image (FileInfo header + payload per RawMeta):
 // the checks of sync_backup.cpp:345-435 / block_console.cpp:543-577.
 __global__ void __launch_bounds__(kBlock) block_verify_kernel(const uint8_t* __restrict__ image, uint64_t image_len,
@@ -1214,6 +1220,7 @@ __global__ void __launch_bounds__(kBlock) block_verify_kernel(const uint8_t* __r
   }
   if (lane == 0 && bad && n_bad) atomicAdd(n_bad, bad);
 }
+#endif  // TFS_CRC_MEASURE
 
 // ---------------------------------------------------------------------------
 // Packet CRC (BasePacket, src/common/base_packet.cpp).  A wire frame is the
@@ -1314,8 +1321,10 @@ __global__ void packet_finish_kernel(uint8_t* __restrict__ base, const PacketDes
   (void)desc;
 }
 
+#ifdef TFS_CRC_MEASURE
 // Compaction repack (task.cpp:753-798): copy each live record (FileInfo|payload)
 // to its new offset and rewrite offset_/size_/usize_/flag_.  One wave per record.
+// (Measurement build: the unfused A/B baseline, TFS_CRC_VARIANT=7.)
 __global__ void __launch_bounds__(kBlock) compact_copy_kernel(const uint8_t* __restrict__ src,
                                                               const RawMeta* __restrict__ metas,
                                                               const int32_t* __restrict__ flags,
@@ -1457,6 +1466,7 @@ __global__ void __launch_bounds__(kBlock) compact_fused_kernel(const uint8_t* __
   }
   if (lane == 0 && bad && n_bad) atomicAdd(n_bad, bad);
 }
+#endif  // TFS_CRC_MEASURE
 
 // ---------------------------------------------------------------------------
 // Pipelined compaction (task.cpp:713-836): the crc_files_kernel
@@ -1750,6 +1760,7 @@ __global__ void write_packet_headers_kernel(uint8_t* __restrict__ base, const ui
   for (int i = 0; i < 24; ++i) p[i] = uint8_t(w[i >> 2] >> (8 * (i & 3)));
 }
 
+#ifdef TFS_CRC_MEASURE
 // Calibration kernel (not on the product path): stream the same bytes without
 // the CRC arithmetic.  run == 0: fully coalesced grid-stride, 16 B/lane.
 // run > 0: the CRC kernel's pattern -- one wave per file, each lane reading
@@ -1840,38 +1851,38 @@ __global__ void __launch_bounds__(kBlock) membench_copy2_kernel(const uint8_t* _
     *reinterpret_cast<gu128wp>(d + 16 * i) = w;
   }
 }
+#endif  // TFS_CRC_MEASURE
 
 }  // namespace tfscrc
 
 // ---------------------------------------------------------------------------
 // Launch wrappers (called from tfs_crc_abi.cpp; no HIP types leak past this TU
-// except through that file).
+// except through that file).  `cap` is the workgroup count of a throughput
+// launch: kMaxGrid, or fewer when CUs are left free for a resident kernel on
+// the same device (tfs_crc_abi.cpp, throughput_cap).
+//
+// The product library (libtfs_crc.so) holds exactly one form of each kernel.
+// The measurement build (-DTFS_CRC_MEASURE, libtfs_crc_measure.so) adds the A/B
+// forms selected by TFS_CRC_VARIANT; the product never reads it.
 // ---------------------------------------------------------------------------
 namespace tfscrc {
 
-static unsigned grid_for(uint32_t nwork) {
+static unsigned grid_for(uint32_t nwork, unsigned cap = kMaxGrid) {
   const uint32_t wpb = kBlock / kWave;
   uint64_t g = (uint64_t(nwork) + wpb - 1) / wpb;
-  if (g > kMaxGrid) g = kMaxGrid;
+  if (g > cap) g = cap;
   if (g == 0) g = 1;
   return unsigned(g);
 }
 
-// Kernel variants (RUN bytes per lane per stripe, PF stripes in flight).  The
-// product default is kRun/kPF; TFS_CRC_VARIANT selects another for measurement.
+#ifdef TFS_CRC_MEASURE
+// Kernel variants (RUN bytes per lane per stripe, PF stripes in flight, ticket
+// forms).  Returns false for an id that is not a crc_files_kernel variant.
 template <int MODE>
-static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
-                                 uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched,
-                                 hipStream_t stream, uint32_t vseed, uint32_t* done_flag, uint32_t seq) {
-  // Latency form for small batches of the product configuration (TFS_CRC_VARIANT
-  // 20 forces it for any n; 21 and the measurement variants 1-16 never use it).
-  if (variant == 20 || (variant == 0 && n <= kWgMaxFiles)) {
-    const unsigned wg = n < kMaxGrid ? n : kMaxGrid;
-    hipLaunchKernelGGL((crc_wg_kernel<MODE>), dim3(wg), dim3(kBlock), 0, stream, base, desc, n, tg, out_crc, out_ok,
-                       n_bad, sched, vseed, done_flag, seq);
-    return hipGetLastError();
-  }
-  const dim3 grid(grid_for(n)), block(kBlock);
+static bool launch_measure_variant(int variant, dim3 grid, dim3 block, const uint8_t* base, const Desc* desc,
+                                   uint32_t n, const Tables* tg, uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad,
+                                   uint32_t* sched, hipStream_t stream, uint32_t vseed, uint32_t* done_flag,
+                                   uint32_t seq) {
 #define TFS_LAUNCH(R, P, N, D, S)                                                                          \
   hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N, D, S>), grid, block, 0, stream, base, desc, n, tg, out_crc, \
                      out_ok, n_bad, sched, vseed, done_flag, seq)
@@ -1966,22 +1977,48 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
                          base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
       break;
     default:
-      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, kCF, kTS>),
-                         grid, block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag,
-                         seq);
-      break;
+      return false;
   }
 #undef TFS_LAUNCH
+  return true;
+}
+#endif  // TFS_CRC_MEASURE
+
+template <int MODE>
+static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
+                                 uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched,
+                                 hipStream_t stream, uint32_t vseed, uint32_t* done_flag, uint32_t seq, unsigned cap) {
+  // Latency form for small batches (TFS_CRC_VARIANT 20 forces it for any n in
+  // the measurement build; the other measurement variants never use it).
+  if (variant == 20 || (variant == 0 && n <= kWgMaxFiles)) {
+    const unsigned wg = n < kMaxGrid ? n : kMaxGrid;
+    hipLaunchKernelGGL((crc_wg_kernel<MODE>), dim3(wg), dim3(kBlock), 0, stream, base, desc, n, tg, out_crc, out_ok,
+                       n_bad, sched, vseed, done_flag, seq);
+    return hipGetLastError();
+  }
+  if (!sched) return hipErrorInvalidValue;
+  const dim3 grid(grid_for(n, cap)), block(kBlock);
+#ifdef TFS_CRC_MEASURE
+  if (variant != 0 && launch_measure_variant<MODE>(variant, grid, block, base, desc, n, tg, out_crc, out_ok, n_bad,
+                                                   sched, stream, vseed, done_flag, seq))
+    return hipGetLastError();
+#endif
+  // The product: chunked interleaved tickets (kCF files per ticket, the last
+  // n >> kTS one by one), PF stripes in flight.
+  hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, kCF, kTS>),
+                     grid, block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
   return hipGetLastError();
 }
 
 hipError_t launch_crc_files(int mode, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
                             uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
-                            int variant, uint32_t vseed, uint32_t* done_flag, uint32_t seq) {
+                            int variant, uint32_t vseed, uint32_t* done_flag, uint32_t seq, unsigned cap) {
   if (n == 0) return hipSuccess;
   if (mode == 0)
-    return launch_variant<0>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, sched, stream, vseed, done_flag, seq);
-  return launch_variant<1>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, sched, stream, vseed, done_flag, seq);
+    return launch_variant<0>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, sched, stream, vseed, done_flag, seq,
+                             cap);
+  return launch_variant<1>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, sched, stream, vseed, done_flag, seq,
+                           cap);
 }
 
 hipError_t launch_resident(const Tables* tg, const ResHost* hs, uint32_t* dstate, unsigned grid, uint32_t idle_ticks,
@@ -2007,6 +2044,7 @@ hipError_t launch_packet_finish(uint8_t* base, const PacketDesc* pd, const Desc*
   return hipGetLastError();
 }
 
+#ifdef TFS_CRC_MEASURE
 hipError_t launch_block_verify(const uint8_t* image, uint64_t image_len, const RawMeta* metas, uint32_t n,
                                const Tables* tg, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
                                hipStream_t stream) {
@@ -2016,38 +2054,58 @@ hipError_t launch_block_verify(const uint8_t* image, uint64_t image_len, const R
   return hipGetLastError();
 }
 
-// Product: compact_pipe_kernel (dynamic tickets on the stream's slot, next-record
-// prefetch).  variant 22 (measurement): the unpipelined compact_fused_kernel.
+hipError_t launch_compact_copy(const uint8_t* src, const RawMeta* metas, const int32_t* flags, const int64_t* dest_off,
+                               uint32_t n, uint8_t* dst, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(compact_copy_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, src, metas, flags, dest_off, n,
+                     dst);
+  return hipGetLastError();
+}
+#endif  // TFS_CRC_MEASURE
+
+// Compaction of one block (RawMeta + flags + dest offsets): compact_pipe_kernel
+// (dynamic tickets on the stream's slot, next-record prefetch).  Measurement
+// build: 22 the unpipelined compact_fused_kernel, 23 ds_bpermute lane shifts,
+// 27 the source-anchored grid.
 hipError_t launch_compact_fused(const uint8_t* src, uint64_t src_len, const RawMeta* metas, const int32_t* flags,
                                 const int64_t* dest_off, uint32_t n, uint8_t* dst, const Tables* tg, uint32_t* out_crc,
                                 int32_t* out_status, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
-                                int variant) {
+                                int variant, unsigned cap) {
   if (n == 0) return hipSuccess;
-  if (variant == 22 || !sched)
-    hipLaunchKernelGGL(compact_fused_kernel<false>, dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len, metas,
-                       flags, dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad);
+  if (!sched) return hipErrorInvalidValue;
+  const dim3 grid(grid_for(n, cap));
+#ifdef TFS_CRC_MEASURE
+  if (variant == 22)
+    hipLaunchKernelGGL(compact_fused_kernel<false>, grid, dim3(kBlock), 0, stream, src, src_len, metas, flags,
+                       dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad);
   else if (variant == 23)
-    hipLaunchKernelGGL((compact_pipe_kernel<false, false>), dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len,
-                       metas, flags, dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched);
+    hipLaunchKernelGGL((compact_pipe_kernel<false, false>), grid, dim3(kBlock), 0, stream, src, src_len, metas, flags,
+                       dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched);
   else if (variant == 27)
-    hipLaunchKernelGGL((compact_pipe_kernel<false, true, false, 0>), dim3(grid_for(n)), dim3(kBlock), 0, stream, src,
-                       src_len, metas, flags, dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched);
+    hipLaunchKernelGGL((compact_pipe_kernel<false, true, false, 0>), grid, dim3(kBlock), 0, stream, src, src_len,
+                       metas, flags, dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched);
   else
-    hipLaunchKernelGGL(compact_pipe_kernel<false>, dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len, metas,
-                       flags, dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched);
+#endif
+    hipLaunchKernelGGL(compact_pipe_kernel<false>, grid, dim3(kBlock), 0, stream, src, src_len, metas, flags,
+                       dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched);
+  (void)variant;
   return hipGetLastError();
 }
 
+// Compaction of many blocks (CompactJob, 64-bit offsets) in one launch.
 hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const CompactJob* jobs, uint32_t n, uint8_t* dst,
                                const Tables* tg, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
-                               uint32_t* sched, hipStream_t stream, int variant) {
+                               uint32_t* sched, hipStream_t stream, int variant, unsigned cap) {
   if (n == 0) return hipSuccess;
-#define TFS_CJ(...)                                                                                                \
-  hipLaunchKernelGGL((compact_pipe_kernel<__VA_ARGS__>), dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len, \
-                     nullptr, nullptr, nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad, sched)
-  if (variant == 22 || !sched)
-    hipLaunchKernelGGL(compact_fused_kernel<true>, dim3(grid_for(n)), dim3(kBlock), 0, stream, src, src_len, nullptr,
-                       nullptr, nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad);
+  if (!sched) return hipErrorInvalidValue;
+  const dim3 grid(grid_for(n, cap));
+#define TFS_CJ(...)                                                                                                  \
+  hipLaunchKernelGGL((compact_pipe_kernel<__VA_ARGS__>), grid, dim3(kBlock), 0, stream, src, src_len, nullptr, nullptr, \
+                     nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad, sched)
+#ifdef TFS_CRC_MEASURE
+  if (variant == 22)
+    hipLaunchKernelGGL(compact_fused_kernel<true>, grid, dim3(kBlock), 0, stream, src, src_len, nullptr, nullptr,
+                       nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad);
   else if (variant == 23) TFS_CJ(true, false);
   else if (variant == 25) TFS_CJ(true, true, false, kCompactDiag | 1);
   else if (variant == 26) TFS_CJ(true, true, false, kCompactDiag | 2);
@@ -2066,23 +2124,30 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
   else if (variant == 42) TFS_CJ(true, true, false, kCompactDiag, kPF, 4, 3);
   else if (variant == 43) TFS_CJ(true, true, false, kCompactDiag, kPF, 4, 2);
   else if (variant == 45) TFS_CJ(true, true, false, kCompactDiag, kPF, 3, 0);
-  else TFS_CJ(true);
+  else
+#endif
+    TFS_CJ(true);
 #undef TFS_CJ
+  (void)variant;
   return hipGetLastError();
 }
 
-// Verify-on-read of block records: the pipelined form (product) or the
-// static grid-stride block_verify_kernel (TFS_CRC_VARIANT=24, round 1's).
+// Verify-on-read of block records: the verify form of the record kernel
+// (chunked tickets like the file kernel).  Measurement build: round 1's static
+// grid-stride block_verify_kernel (24), other ticket forms (39-50).
 hipError_t launch_block_verify_pipe(const uint8_t* image, uint64_t image_len, const RawMeta* metas,
                                     const CompactJob* jobs, uint32_t n, const Tables* tg, uint32_t* out_crc,
                                     int32_t* out_status, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
-                                    int variant) {
+                                    int variant, unsigned cap) {
   if (n == 0) return hipSuccess;
-#define TFS_BV(...)                                                                                               \
-  hipLaunchKernelGGL((compact_pipe_kernel<true, true, true, kCompactDiag, kPF, __VA_ARGS__>), dim3(grid_for(n)),       \
-                     dim3(kBlock), 0, stream, image, image_len, nullptr, nullptr, nullptr, jobs, n, nullptr, tg, out_crc, \
-                     out_status, n_bad, sched)
-  if (jobs && variant == 39) TFS_BV(2, 0);  // chunked tickets (as crc_files 39-45)
+  if (!sched) return hipErrorInvalidValue;
+  const dim3 grid(grid_for(n, cap));
+#define TFS_BV(...)                                                                                                  \
+  hipLaunchKernelGGL((compact_pipe_kernel<true, true, true, kCompactDiag, kPF, __VA_ARGS__>), grid, dim3(kBlock), 0, \
+                     stream, image, image_len, nullptr, nullptr, nullptr, jobs, n, nullptr, tg, out_crc, out_status,   \
+                     n_bad, sched)
+#ifdef TFS_CRC_MEASURE
+  if (jobs && variant == 39) TFS_BV(2, 0);
   else if (jobs && variant == 40) TFS_BV(4, 0);
   else if (jobs && variant == 42) TFS_BV(4, 3);
   else if (jobs && variant == 43) TFS_BV(4, 2);
@@ -2090,26 +2155,22 @@ hipError_t launch_block_verify_pipe(const uint8_t* image, uint64_t image_len, co
   else if (jobs && variant == 47) TFS_BV(4, 4);
   else if (jobs && variant == 48) TFS_BV(4, 5);
   else if (jobs && variant == 50) TFS_BV(1, 0);  // one record per ticket (the product before chunked tickets)
-  else if (jobs) TFS_BV(kCF, kTS);
-#undef TFS_BV
-  else if (variant == 24 || !sched)
-    hipLaunchKernelGGL(block_verify_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, image, image_len, metas, n, tg,
-                       out_crc, out_status, n_bad);
-  else if (variant == 50)
-    hipLaunchKernelGGL((compact_pipe_kernel<false, true, true>), dim3(grid_for(n)), dim3(kBlock), 0, stream, image,
-                       image_len, metas, nullptr, nullptr, nullptr, n, nullptr, tg, out_crc, out_status, n_bad, sched);
+  else if (!jobs && variant == 24)
+    hipLaunchKernelGGL(block_verify_kernel, grid, dim3(kBlock), 0, stream, image, image_len, metas, n, tg, out_crc,
+                       out_status, n_bad);
+  else if (!jobs && variant == 50)
+    hipLaunchKernelGGL((compact_pipe_kernel<false, true, true>), grid, dim3(kBlock), 0, stream, image, image_len, metas,
+                       nullptr, nullptr, nullptr, n, nullptr, tg, out_crc, out_status, n_bad, sched);
   else
-    hipLaunchKernelGGL((compact_pipe_kernel<false, true, true, kCompactDiag, kPF, kCF, kTS>), dim3(grid_for(n)),
-                       dim3(kBlock), 0, stream, image, image_len, metas, nullptr, nullptr, nullptr, n, nullptr, tg,
-                       out_crc, out_status, n_bad, sched);
-  return hipGetLastError();
-}
-
-hipError_t launch_compact_copy(const uint8_t* src, const RawMeta* metas, const int32_t* flags, const int64_t* dest_off,
-                               uint32_t n, uint8_t* dst, hipStream_t stream) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(compact_copy_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, src, metas, flags, dest_off, n,
-                     dst);
+#endif
+  if (jobs)
+    TFS_BV(kCF, kTS);
+  else
+    hipLaunchKernelGGL((compact_pipe_kernel<false, true, true, kCompactDiag, kPF, kCF, kTS>), grid, dim3(kBlock), 0,
+                       stream, image, image_len, metas, nullptr, nullptr, nullptr, n, nullptr, tg, out_crc, out_status,
+                       n_bad, sched);
+#undef TFS_BV
+  (void)variant;
   return hipGetLastError();
 }
 
@@ -2121,6 +2182,7 @@ hipError_t launch_synth_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, uint
   return hipGetLastError();
 }
 
+#ifdef TFS_CRC_MEASURE
 // Calibration: copy by wave-contiguous chunks of CH bytes (the record kernel's
 // shape: one wave streams one range), chunk c to wave c mod W; each wave moves
 // PF 1 KiB stripes per step (16 B per lane, nt loads, store kind SK).
@@ -2233,6 +2295,8 @@ hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, u
     hipLaunchKernelGGL(membench_kernel<false>, g, dim3(kBlock), 0, stream, base, desc, n, nbytes, run, out, align);
   return hipGetLastError();
 }
+
+#endif  // TFS_CRC_MEASURE
 
 hipError_t launch_write_packet_headers(uint8_t* base, const uint64_t* rec_off, const uint32_t* len, uint32_t n,
                                        int32_t pcode, int32_t version, uint64_t first_id, hipStream_t stream) {

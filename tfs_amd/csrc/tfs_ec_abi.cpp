@@ -147,7 +147,9 @@ int tfs_ec_config(tfs_crc_ctx* ctx, int dn, int pn, const int* erased, tfs_ec** 
   ec->ctx = ctx;
   ec->dn = dn;
   ec->pn = pn;
+#ifdef TFS_CRC_MEASURE
   if (const char* v = getenv("TFS_EC_VARIANT")) ec->variant = atoi(v);
+#endif
   *out = ec;
   std::vector<int> data(dn), parity(pn);
   for (int j = 0; j < dn; ++j) data[j] = j;

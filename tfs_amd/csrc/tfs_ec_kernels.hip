@@ -152,6 +152,7 @@ __global__ void __launch_bounds__(256) ec_apply_chunk_kernel(EcArgs a, const uin
   }
 }
 
+#ifdef TFS_CRC_MEASURE
 template <int K>
 static void launch_chunk(const EcArgs& a, int og, dim3 g, dim3 b, hipStream_t stream) {
   switch (og) {
@@ -162,11 +163,14 @@ static void launch_chunk(const EcArgs& a, int og, dim3 g, dim3 b, hipStream_t st
   }
 }
 
-// variant (TFS_EC_VARIANT, measurement): 0 the grid-stride tile kernel; 1, 2, 3
-// the chunked form with K = 2, 4, 8 tiles per wave step.
+#endif  // TFS_CRC_MEASURE
+
+// The product: the grid-stride tile kernel.  Measurement build (TFS_EC_VARIANT
+// 1, 2, 3): the chunked form with K = 2, 4, 8 tiles per wave step.
 hipError_t launch_ec_apply(const EcArgs& a, int og, int variant, hipStream_t stream) {
   if (a.units == 0) return hipSuccess;
   const uint64_t ntiles = (a.units + 3) / 4;
+#ifdef TFS_CRC_MEASURE
   if (variant >= 1 && variant <= 3) {
     const int K = 1 << variant;
     uint64_t blocks = ((ntiles + K - 1) / K + 3) / 4;
@@ -177,6 +181,9 @@ hipError_t launch_ec_apply(const EcArgs& a, int og, int variant, hipStream_t str
     else launch_chunk<8>(a, og, g, b, stream);
     return hipGetLastError();
   }
+#else
+  (void)variant;
+#endif
   uint64_t blocks = (ntiles + 3) / 4;
   if (blocks > 2048) blocks = 2048;
   const dim3 g(static_cast<unsigned>(blocks)), b(256);

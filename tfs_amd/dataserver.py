@@ -19,6 +19,15 @@ LIB_PATH = os.path.join(HERE, "ds", "libtfs_ds.so")
 _LIB = None
 
 
+def _ctx(ctx):
+    """The tfs_crc_ctx handle of a product-library context: libtfs_ds.so links
+    libtfs_crc.so, so a measurement-build context (another struct layout) is
+    refused here."""
+    if getattr(ctx, "L", None) is not _crc.lib():
+        raise ValueError("the dataserver harness takes contexts of the product library (libtfs_crc.so)")
+    return ctx.handle
+
+
 def lib():
     global _LIB
     if _LIB is None:
@@ -37,6 +46,7 @@ def lib():
             "tfs_ds_pool_new": (vp, [vp, u32, u64]),
             "tfs_ds_pool_free": (None, [vp]),
             "tfs_ds_pool_size": (u32, [vp]),
+            "tfs_ds_pool_in_use": (u32, [vp]),
             "tfs_ds_block_new_in": (vp, [vp, u32, i64]),
             "tfs_ds_block_free": (None, [vp]),
             "tfs_ds_block_size": (i64, [vp]),
@@ -89,6 +99,7 @@ def lib():
                                              ctypes.POINTER(i64)]),
             "tfs_ds_close_latency": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, i32, vp]),
             "tfs_ds_scalar_latency": (ctypes.c_int, [ctypes.c_int, i32, vp]),
+            "tfs_ds_close_stream": (ctypes.c_int, [vp, ctypes.c_int, i32, vp, vp, u64, ctypes.POINTER(u64)]),
             "tfs_ds_service_new": (vp, [vp, u32, ctypes.c_int]),
             "tfs_ds_service_free": (None, [vp]),
             "tfs_ds_service_ctx_for_block": (vp, [vp, u32]),
@@ -108,7 +119,7 @@ class DataFile:
     """DataFile (src/dataserver/data_file.h:33-96)."""
 
     def __init__(self, ctx, fn, tmp_dir="/tmp"):
-        self.h = lib().tfs_ds_datafile_new(ctx.handle, fn, tmp_dir.encode())
+        self.h = lib().tfs_ds_datafile_new(_ctx(ctx), fn, tmp_dir.encode())
 
     def set_data(self, data, offset):
         b = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8))
@@ -141,13 +152,21 @@ class BlockImagePool:
     preallocated blocks); a page-locked image is verified in place (zero-copy)."""
 
     def __init__(self, ctx, count, nbytes):
-        self.h = lib().tfs_ds_pool_new(ctx.handle, count, nbytes)
+        self.h = lib().tfs_ds_pool_new(_ctx(ctx), count, nbytes)
 
     def size(self):
         return lib().tfs_ds_pool_size(self.h)
 
+    def in_use(self):
+        """Arenas lent to live LogicBlocks."""
+        return lib().tfs_ds_pool_in_use(self.h)
+
     def free(self):
+        """Free the page-locked arenas; refused while a LogicBlock still uses one."""
         if self.h:
+            if self.in_use():
+                raise RuntimeError("BlockImagePool.free: %d arenas still lent to live blocks (free them first)"
+                                   % self.in_use())
             lib().tfs_ds_pool_free(self.h)
             self.h = None
 
@@ -157,6 +176,7 @@ class LogicBlock:
 
     def __init__(self, block_id, capacity=1 << 40, pool=None):
         self.block_id = block_id
+        self.pool = pool  # kept alive while this block may hold one of its arenas
         self.h = lib().tfs_ds_block_new_in(pool.h, block_id, capacity) if pool else \
             lib().tfs_ds_block_new(block_id, capacity)
 
@@ -187,7 +207,7 @@ class LogicBlock:
         """read_data + GPU verify-on-read against FileInfo.crc_: returns (rc, FileInfo|payload)."""
         buf = np.zeros(cap, np.uint8)
         n = ctypes.c_int32(0)
-        rc = lib().tfs_ds_read_file_verified(ctx.handle, self.h, file_id, buf.ctypes.data, cap, ctypes.byref(n),
+        rc = lib().tfs_ds_read_file_verified(_ctx(ctx), self.h, file_id, buf.ctypes.data, cap, ctypes.byref(n),
                                              checker.h if checker else None)
         return rc, buf[:min(max(n.value, 0), cap)].tobytes()
 
@@ -220,7 +240,7 @@ class CloseBatcher:
     """Batches close_write_file CRC checks from many threads into one GPU verify."""
 
     def __init__(self, ctx, max_batch=64, max_wait_us=200):
-        self.h = lib().tfs_ds_batcher_new(ctx.handle, max_batch, max_wait_us)
+        self.h = lib().tfs_ds_batcher_new(_ctx(ctx), max_batch, max_wait_us)
 
     def close(self, block, file_id, client_crc, df):
         return lib().tfs_ds_batcher_close(self.h, block.h, file_id, client_crc, df.h)
@@ -296,7 +316,7 @@ class PacketEncoder:
     """Send-side packet batch (packet_codec.h): V1 frames sealed on the GPU."""
 
     def __init__(self, ctx):
-        self.h = lib().tfs_ds_encoder_new(ctx.handle)
+        self.h = lib().tfs_ds_encoder_new(_ctx(ctx))
 
     def add(self, pcode, version, pid, body):
         b = bytes(body)
@@ -331,7 +351,7 @@ def decode_stream(ctx, data, cap=1 << 16):
     crc = np.zeros(cap, np.uint32)
     nfr = ctypes.c_uint32()
     consumed = ctypes.c_int64()
-    rc = lib().tfs_ds_decode(ctx.handle, b.ctypes.data, b.size, off.ctypes.data, st.ctypes.data, crc.ctypes.data,
+    rc = lib().tfs_ds_decode(_ctx(ctx), b.ctypes.data, b.size, off.ctypes.data, st.ctypes.data, crc.ctypes.data,
                              cap, ctypes.byref(nfr), ctypes.byref(consumed))
     k = min(nfr.value, cap)
     return rc, off[:k], st[:k], crc[:k], consumed.value
@@ -361,7 +381,7 @@ class LoadedBlock:
     """A block read back from disk (chain, index, flags, data in pinned memory)."""
 
     def __init__(self, ctx, mount, main_id, main_size=MAIN_BLOCK_SIZE, ext_size=EXT_BLOCK_SIZE):
-        self.h = lib().tfs_ds_loaded_new(ctx.handle if ctx is not None else None)
+        self.h = lib().tfs_ds_loaded_new(_ctx(ctx) if ctx is not None else None)
         self.rc = lib().tfs_ds_loaded_load(self.h, mount.encode(), main_size, ext_size, main_id)
         if self.rc != 0:
             return
@@ -398,7 +418,7 @@ def verify_block_files(ctx, mount, main_id, checker=None, main_size=MAIN_BLOCK_S
     """Verify-on-read from block files on disk: returns (nbad or <0, live statuses)."""
     st = np.zeros(1 << 16, np.int32)
     nl = ctypes.c_uint32()
-    rc = lib().tfs_ds_verify_block_files(ctx.handle, mount.encode(), main_size, ext_size, main_id, st.ctypes.data,
+    rc = lib().tfs_ds_verify_block_files(_ctx(ctx), mount.encode(), main_size, ext_size, main_id, st.ctypes.data,
                                          st.size, ctypes.byref(nl), checker.h if checker else None)
     return rc, st[:nl.value]
 
@@ -407,18 +427,18 @@ def compact_block_files(ctx, src_mount, src_main_id, dst_mount, dst_main_id, fir
                         windows_per_launch=4, main_size=MAIN_BLOCK_SIZE, ext_size=EXT_BLOCK_SIZE, cap=1 << 20):
     """real_compact from block files on disk through 8 MiB windows (block_store.h
     compact_block_files).  Returns (rc, dest metas, statuses, ext ids, counters)
-    with counters {n_live, dest_size, windows, launches, big_files, n_bad}."""
+    with counters {n_live, dest_size, windows, launches, big_files, n_bad, n_dropped}."""
     metas = np.zeros(cap, _crc.META_DTYPE)
     st = np.zeros(cap, np.int32)
     ext = np.zeros(64, np.uint32)
     next_ = ctypes.c_uint32()
-    cnt = np.zeros(6, np.int64)
-    rc = lib().tfs_ds_compact_block_files(ctx.handle, src_mount.encode(), dst_mount.encode(), main_size, ext_size,
+    cnt = np.zeros(7, np.int64)
+    rc = lib().tfs_ds_compact_block_files(_ctx(ctx), src_mount.encode(), dst_mount.encode(), main_size, ext_size,
                                           src_main_id, dst_main_id, first_ext_id, bucket_size, windows_per_launch,
                                           metas.ctypes.data, st.ctypes.data, cap, ext.ctypes.data, 64,
                                           ctypes.byref(next_), cnt.ctypes.data)
     n = int(cnt[0])
-    keys = ("n_live", "dest_size", "windows", "launches", "big_files", "n_bad")
+    keys = ("n_live", "dest_size", "windows", "launches", "big_files", "n_bad", "n_dropped")
     return rc, metas[:n], st[:n], ext[:next_.value].tolist(), dict(zip(keys, (int(x) for x in cnt)))
 
 
@@ -427,13 +447,13 @@ class BlockFileCompactor:
     (block_store.h BlockFileCompactor: a compaction thread's state)."""
 
     def __init__(self, ctx, windows_per_launch=4):
-        self.h = lib().tfs_ds_compactor_new(ctx.handle, windows_per_launch)
+        self.h = lib().tfs_ds_compactor_new(_ctx(ctx), windows_per_launch)
         if not self.h:
             raise _crc.TfsCrcError(-1016, "tfs_ds_compactor_new")
         self.metas = np.zeros(1 << 16, _crc.META_DTYPE)
         self.status = np.zeros(1 << 16, np.int32)
         self.ext = np.zeros(64, np.uint32)
-        self.cnt = np.zeros(6, np.int64)
+        self.cnt = np.zeros(7, np.int64)
 
     def compact(self, src_mount, src_main_id, dst_mount, dst_main_id, first_ext_id, bucket_size=0,
                 main_size=MAIN_BLOCK_SIZE, ext_size=EXT_BLOCK_SIZE):
@@ -446,7 +466,7 @@ class BlockFileCompactor:
                                             self.ext.ctypes.data, self.ext.size, ctypes.byref(next_),
                                             self.cnt.ctypes.data)
         n = int(self.cnt[0])
-        keys = ("n_live", "dest_size", "windows", "launches", "big_files", "n_bad")
+        keys = ("n_live", "dest_size", "windows", "launches", "big_files", "n_bad", "n_dropped")
         return (rc, self.metas[:n], self.status[:n], self.ext[:next_.value].tolist(),
                 dict(zip(keys, (int(x) for x in self.cnt))))
 
@@ -465,7 +485,7 @@ class BlockFileCompactor:
 def verify_block(ctx, block, checker=None):
     m, f = block.metas()
     st = np.zeros(max(len(m), 1), np.int32)
-    nbad = lib().tfs_ds_verify_block(ctx.handle, block.h, st.ctypes.data, st.size, checker.h if checker else None)
+    nbad = lib().tfs_ds_verify_block(_ctx(ctx), block.h, st.ctypes.data, st.size, checker.h if checker else None)
     live = (f & (_crc.FI_DELETED | _crc.FI_INVALID)) == 0
     return nbad, st[:int(live.sum())]
 
@@ -473,7 +493,7 @@ def verify_block(ctx, block, checker=None):
 def compact_block(ctx, src, dest):
     m, _ = src.metas()
     ok = np.zeros(max(len(m), 1), np.uint8)
-    rc = lib().tfs_ds_compact_block(ctx.handle, src.h, dest.h, ok.ctypes.data, ok.size)
+    rc = lib().tfs_ds_compact_block(_ctx(ctx), src.h, dest.h, ok.ctypes.data, ok.size)
     return rc, ok[:len(m)]
 
 
@@ -486,17 +506,45 @@ def loopback_block(ctx, payloads, n, length, client_crc, nthreads, block, batche
     c = np.ascontiguousarray(client_crc, dtype=np.uint32)
     if p.size < n * length or c.size < n:
         raise ValueError("payloads/client_crc too small")
-    return lib().tfs_ds_loopback_block_with(ctx.handle, batcher.h if batcher else None, p.ctypes.data, n, length,
+    return lib().tfs_ds_loopback_block_with(_ctx(ctx), batcher.h if batcher else None, p.ctypes.data, n, length,
                                             c.ctypes.data, nthreads, block.h)
 
 
 def close_latency(ctx, nleases, iters, length=65536):
     """Microseconds per CloseBatcher close with `nleases` leases closing concurrently."""
     out = np.zeros(nleases * iters, np.float64)
-    rc = lib().tfs_ds_close_latency(ctx.handle, nleases, iters, length, out.ctypes.data)
+    rc = lib().tfs_ds_close_latency(_ctx(ctx), nleases, iters, length, out.ctypes.data)
     if rc != 0:
         raise _crc.TfsCrcError(rc, "close_latency")
     return out
+
+
+class CloseStream:
+    """Closes from `nleases` worker threads through one CloseBatcher, in a
+    background thread, until stop(): the close traffic a throughput launch
+    shares its GPU with (tfs_ds_close_stream)."""
+
+    def __init__(self, ctx, nleases=8, length=65536, cap=1 << 20):
+        import threading
+        self._stop = ctypes.c_int(0)
+        self.lat = np.zeros(cap, np.float64)
+        self.count = ctypes.c_uint64(0)
+        self.rc = None
+        h = _ctx(ctx)
+
+        def run():
+            self.rc = lib().tfs_ds_close_stream(h, nleases, length, ctypes.byref(self._stop), self.lat.ctypes.data,
+                                                cap, ctypes.byref(self.count))
+        self._t = threading.Thread(target=run)
+        self._t.start()
+
+    def stop(self):
+        """Stop, join; returns (rc, closes done, latencies in us)."""
+        self._stop.value = 1
+        self._t.join()
+        n = min(int(self.count.value), self.lat.size)
+        lat = self.lat[:n]
+        return self.rc, int(self.count.value), lat[lat > 0]
 
 
 def scalar_latency(iters, length=65536):
@@ -511,5 +559,5 @@ def scalar_latency(iters, length=65536):
 def recombine_block(ctx, src, dest):
     """TranBlock::recombine_data over the GPU: returns (rc, files skipped for their CRC)."""
     k = ctypes.c_int(0)
-    rc = lib().tfs_ds_recombine_block(ctx.handle, src.h, dest.h, ctypes.byref(k))
+    rc = lib().tfs_ds_recombine_block(_ctx(ctx), src.h, dest.h, ctypes.byref(k))
     return rc, k.value

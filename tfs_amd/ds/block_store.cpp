@@ -13,7 +13,9 @@
 #include <deque>
 #include <functional>
 #include <mutex>
+#include <set>
 #include <thread>
+#include <utility>
 
 namespace tfs {
 namespace dataserver {
@@ -294,9 +296,19 @@ int read_range(const BlockStore& st, const std::vector<uint32_t>& chain, char* d
   return len == 0 ? TFS_SUCCESS : TFS_ERROR;  // EXIT_PHYSIC_BLOCK_OFFSET_ERROR
 }
 
+// LogicBlock::get_real_flag (logic_block.cpp:996-1009): the index entry's unlink
+// bits when its use-index bit is set, the FileInfo's flag_ otherwise.
+int32_t index_flag(int32_t raw_size, const tfs_file_info& fi) {
+  return (raw_size & kUseIndexFlag) ? (raw_size & kUnlinkMask) >> kUnlinkShift : fi.flag_;
+}
+
+// A file's flag as FileIterator::next sees it for a file read from its window
+// (logic_block.cpp:1250-1273): FI_INVALID when the FileInfo disagrees with the
+// index entry, else index_flag.  (A big file takes index_flag with no such
+// check, :1221-1240.)
 int32_t real_flag(const tfs_raw_meta& m, int32_t raw_size, const tfs_file_info& fi) {
   if (fi.id_ != m.file_id || fi.size_ != m.size) return TFS_FI_INVALID;
-  return (raw_size & kUseIndexFlag) ? (raw_size & kUnlinkMask) >> kUnlinkShift : fi.flag_;
+  return index_flag(raw_size, fi);
 }
 
 // Pinned when a ctx is given (direct DMA); plain heap memory otherwise
@@ -568,6 +580,27 @@ int BlockFileCompactor::Impl::compact(const BlockStore& src, uint32_t src_main_i
   uint32_t logic_id = 0;
   int rc = load_chain(src, src_main_id, &chain, &logic_id);
   if (rc) return rc;
+  // The reference always compacts into another logic block.  ChainWriter opens
+  // the destination files with O_TRUNC before any source window is read, so a
+  // destination file that IS a source file (same inode: the same mount and id,
+  // an overlapping extension id, a symlinked or hard-linked path) would destroy
+  // the block: refuse that before anything is opened for writing.
+  {
+    std::set<std::pair<dev_t, ino_t>> src_files;
+    auto add = [&](const std::string& p) {
+      struct stat sb;
+      if (stat(p.c_str(), &sb) == 0) src_files.insert({sb.st_dev, sb.st_ino});
+    };
+    for (size_t k = 0; k < chain.size(); ++k) add(k == 0 ? main_path(src, chain[k]) : ext_path(src, chain[k]));
+    add(index_path(src, src_main_id));
+    auto clash = [&](const std::string& p) {
+      struct stat sb;
+      return stat(p.c_str(), &sb) == 0 && src_files.count({sb.st_dev, sb.st_ino}) != 0;
+    };
+    bool bad = clash(main_path(dst, dst_main_id)) || clash(index_path(dst, dst_main_id));
+    for (int k = 0; k + 1 < kMaxChain && !bad; ++k) bad = clash(ext_path(dst, first_ext_id + uint32_t(k)));
+    if (bad) return TFS_EXIT_PARAMETER_ERROR;
+  }
   IndexHeader h;
   std::vector<tfs_raw_meta> metas;  // sorted by offset, sizes with their flag bits
   rc = load_index(src, src_main_id, &h, &metas);
@@ -642,9 +675,13 @@ int BlockFileCompactor::Impl::compact(const BlockStore& src, uint32_t src_main_i
       const int32_t raw = m.size;
       m.size = raw & kFileSizeMask;  // RawMeta::get_size
       // A record shorter than its FileInfo, or running past the block's data,
-      // cannot be read whole: FI_INVALID, skipped (FileIterator reports it so
-      // or fails the read).
-      if (m.size < TFS_FILEINFO_SIZE || int64_t(m.offset) + m.size > w1) continue;
+      // cannot be read whole.  FileIterator would hand it on with whatever
+      // bytes follow the data area (parity unpinned: no fixture covers it);
+      // here it is not copied, and reported (out->dropped) so the caller sees it.
+      if (m.size < TFS_FILEINFO_SIZE || int64_t(m.offset) + m.size > w1) {
+        out->dropped.push_back(m.file_id);
+        continue;
+      }
       tfs_file_info fi;
       memcpy(&fi, buf + (m.offset - w0), sizeof fi);
       const int32_t flag = real_flag(m, raw, fi);
@@ -684,7 +721,10 @@ int BlockFileCompactor::Impl::compact(const BlockStore& src, uint32_t src_main_i
     m.size = raw & kFileSizeMask;
     tfs_file_info fi;
     if ((r = read_range(src, chain, reinterpret_cast<char*>(&fi), m.offset, sizeof fi))) return r;
-    const int32_t flag = real_flag(m, raw, fi);
+    // FileIterator's big-file branch (logic_block.cpp:1221-1240) takes the flag
+    // with no id/size check against the index, and write_big_file copies the
+    // file whatever its header says (task.cpp:838-880).
+    const int32_t flag = index_flag(raw, fi);
     if (flag & (TFS_FI_DELETED | TFS_FI_INVALID)) return TFS_SUCCESS;
     tfs_file_info dfi = fi;
     dfi.offset_ = int32_t(dest_off);

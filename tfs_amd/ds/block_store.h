@@ -170,13 +170,17 @@ int verify_block_files(tfs_crc_ctx* ctx, const BlockStore& st, uint32_t main_id,
 // live files, del_* 0, version_ + 1 (VERSION_INC_STEP_DEFAULT), the rest
 // copied} (batch_write_meta, logic_block.cpp:817-857).  Returns TFS_SUCCESS,
 // TFS_EXIT_CHECK_CRC_ERROR when some file failed its CRC, or an error
-// (EXIT_META_OFFSET_ERROR -8027 for a meta past the data, as FileIterator::next).
+// (EXIT_META_OFFSET_ERROR -8027 for a meta past the data, as FileIterator::next;
+// TFS_EXIT_PARAMETER_ERROR, before anything is written, when a destination file
+// would be one of the source chain's files).  A record shorter than its FileInfo
+// or running past the data area is not copied and its id is listed in `dropped`.
 struct CompactFilesResult {
   std::vector<tfs_raw_meta> dest_metas;
   std::vector<int32_t> status;
   std::vector<uint32_t> ext_ids;
   int64_t dest_size = 0;
   uint32_t windows = 0, launches = 0, big_files = 0, n_bad = 0;
+  std::vector<uint64_t> dropped;  // ids of records that cannot be read whole (shorter than FileInfo / past the data)
 };
 constexpr int32_t kMaxCompactReadSize = 8388608;  // MAX_COMPACT_READ_SIZE, dataserver_define.h:41
 constexpr int kExitMetaOffsetError = -8027;       // EXIT_META_OFFSET_ERROR, error_msg.h:163

@@ -10,6 +10,8 @@
 #include <memory>
 #include <cstring>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "ds_harness.h"
 
@@ -38,6 +40,7 @@ void* tfs_ds_pool_new(tfs_crc_ctx* ctx, uint32_t count, uint64_t bytes) {
   return new BlockImagePool(ctx, count, size_t(bytes));
 }
 void tfs_ds_pool_free(void* pool) { delete static_cast<BlockImagePool*>(pool); }
+uint32_t tfs_ds_pool_in_use(void* pool) { return uint32_t(static_cast<BlockImagePool*>(pool)->in_use()); }
 uint32_t tfs_ds_pool_size(void* pool) { return uint32_t(static_cast<BlockImagePool*>(pool)->size()); }
 void* tfs_ds_block_new_in(void* pool, uint32_t block_id, int64_t capacity) {
   return new LogicBlockImage(block_id, capacity, pool ? static_cast<BlockImagePool*>(pool)->take() : nullptr);
@@ -247,6 +250,61 @@ int tfs_ds_close_latency(tfs_crc_ctx* ctx, int nleases, int iters, int32_t len, 
   return err.load();
 }
 
+// A stream of closes (DataManagement::close_write_file, data_management.cpp:
+// 173-236) from `nleases` worker threads through one CloseBatcher, running until
+// *stop is set: the dataserver's packet workers closing 64 KiB writes while a
+// throughput launch (a compaction on the task thread, dataservice.cpp:2915-2918,
+// or a block verify) runs on the same GPU.  Each thread appends to a block of its
+// own, replaced when full.  Latencies of up to `cap` closes (in completion order
+// per thread, threads interleaved by slot) go to out_us; *count = closes done.
+int tfs_ds_close_stream(tfs_crc_ctx* ctx, int nleases, int32_t len, const volatile int* stop, double* out_us,
+                        uint64_t cap, uint64_t* count) {
+  if (!ctx || nleases < 1 || len < 0 || !stop || !count) return TFS_EXIT_PARAMETER_ERROR;
+  std::vector<char> payload(size_t(len) + 1);
+  for (int32_t i = 0; i < len; ++i) payload[size_t(i)] = char((i * 2654435761u) >> 13);
+  uint32_t client = 0;
+  int rc = tfs_datafile_get_crc(ctx, payload.data(), len, &client);
+  if (rc != TFS_SUCCESS) return rc;
+  constexpr int64_t kBlockBytes = 64ll << 20;
+  const int64_t per_block = std::max<int64_t>(1, kBlockBytes / (int64_t(len) + TFS_FILEINFO_SIZE));
+  std::atomic<int> err{0};
+  std::atomic<uint64_t> done{0};
+  {
+    CloseBatcher batcher(ctx, size_t(nleases), 100);
+    std::vector<std::thread> workers;
+    for (int t = 0; t < nleases; ++t)
+      workers.emplace_back([&, t] {
+        std::unique_ptr<LogicBlockImage> blk;
+        int64_t in_blk = per_block;
+        for (uint64_t k = 0; !*stop && err.load() == TFS_SUCCESS; ++k) {
+          if (in_blk == per_block) {
+            blk.reset(new LogicBlockImage(uint32_t(t + 1), kBlockBytes));
+            blk->reserve(kBlockBytes);
+            in_blk = 0;
+          }
+          ++in_blk;
+          const uint64_t fid = k + 1;
+          DataFile df(fid, "/tmp", ctx);
+          df.set_data(payload.data(), len, 0);
+          CloseFileInfo info;
+          info.block_id_ = uint32_t(t + 1);
+          info.file_id_ = fid;
+          info.crc_ = client;
+          const auto t0 = std::chrono::steady_clock::now();
+          const int r = batcher.close(info, df, *blk);
+          const auto t1 = std::chrono::steady_clock::now();
+          const uint64_t slot = k * uint64_t(nleases) + uint64_t(t);
+          if (out_us && slot < cap) out_us[slot] = std::chrono::duration<double, std::micro>(t1 - t0).count();
+          if (r != TFS_SUCCESS) err = r;
+          done.fetch_add(1);
+        }
+      });
+    for (auto& w : workers) w.join();
+  }
+  *count = done.load();
+  return err.load();
+}
+
 // The scalar drop-in: tfs_crc32(0, data, len) on a pageable buffer, timed per call.
 int tfs_ds_scalar_latency(int iters, int32_t len, double* out_us) {
   if (iters < 1 || len < 0 || !out_us) return TFS_EXIT_PARAMETER_ERROR;
@@ -437,13 +495,14 @@ int export_compact_result(int rc, const tfs::dataserver::CompactFilesResult& r, 
     counters[3] = r.launches;
     counters[4] = r.big_files;
     counters[5] = r.n_bad;
+    counters[6] = int64_t(r.dropped.size());
   }
   return rc;
 }
 }  // namespace
 
 // compact_block_files: the new block's metas / statuses (cap entries), ext ids
-// (ext_cap), and counters[6] = {n_live, dest_size, windows, launches, big_files, n_bad}.
+// (ext_cap), and counters[7] = {n_live, dest_size, windows, launches, big_files, n_bad, n_dropped}.
 int tfs_ds_compact_block_files(tfs_crc_ctx* ctx, const char* src_mount, const char* dst_mount, int32_t main_size,
                                int32_t ext_size, uint32_t src_main_id, uint32_t dst_main_id, uint32_t first_ext_id,
                                int32_t bucket_size, int windows_per_launch, tfs_raw_meta* dest_metas,

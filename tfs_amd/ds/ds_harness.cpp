@@ -125,7 +125,15 @@ uint32_t DataFile::get_crc() {
 // ---------------- LogicBlockImage (logic_block.cpp) ----------------
 
 LogicBlockImage::LogicBlockImage(uint32_t block_id, int64_t capacity, ImageArena* arena)
-    : block_id_(block_id), capacity_(capacity), data_(ImageAlloc<char>(arena)) {}
+    : block_id_(block_id), capacity_(capacity), data_(ImageAlloc<char>(arena)) {
+  // A pooled image takes its whole arena now and never grows past it: a growth
+  // would move the image to pageable memory and give the arena back, and the
+  // in-place verify of a page-locked image would silently stop applying.
+  if (arena && arena->cap) {
+    capacity_ = std::min<int64_t>(capacity_, int64_t(arena->cap));
+    data_.reserve(arena->cap);
+  }
+}
 
 BlockImagePool::BlockImagePool(tfs_crc_ctx* ctx, size_t count, size_t bytes) : ctx_(ctx) {
   for (size_t i = 0; i < count; ++i) {
@@ -138,7 +146,17 @@ BlockImagePool::BlockImagePool(tfs_crc_ctx* ctx, size_t count, size_t bytes) : c
 }
 
 BlockImagePool::~BlockImagePool() {
-  for (auto& a : arenas_) tfs_crc32_host_free_pinned(ctx_, a->p);
+  // An arena still lent to a live image is not freed under it (that image would
+  // write to freed page-locked memory); the caller frees the pool after its
+  // blocks (tfs_amd/dataserver.py refuses otherwise).
+  for (auto& a : arenas_)
+    if (!a->in_use.load()) tfs_crc32_host_free_pinned(ctx_, a->p);
+}
+
+size_t BlockImagePool::in_use() const {
+  size_t k = 0;
+  for (const auto& a : arenas_) k += a->in_use.load() ? 1u : 0u;
+  return k;
 }
 
 ImageArena* BlockImagePool::take() {

@@ -133,6 +133,7 @@ class BlockImagePool {
   ~BlockImagePool();
   ImageArena* take();  // a free arena, or nullptr (the image then lives in pageable memory)
   size_t size() const { return arenas_.size(); }
+  size_t in_use() const;  // arenas lent to live images
 
  private:
   tfs_crc_ctx* ctx_;

@@ -18,13 +18,14 @@ TFS_EXIT_NO_ENOUGH_DATA = -16004
 UNIT = 1024  # ws_ * ps_ (erasure_code.cpp:33-34)
 EXPORTED = ["tfs_ec_config", "tfs_ec_free", "tfs_ec_encode_device", "tfs_ec_encode", "tfs_ec_decode_device",
             "tfs_ec_decode"]
-_SIG = False
+_SIG = set()
 
 
-def lib():
-    global _SIG
-    L = _crc.lib()
-    if not _SIG:
+def lib(L=None):
+    """The library of a context (ctx.L: the product, or the measurement build
+    for the TFS_EC_VARIANT forms), with the tfs_ec_* signatures set."""
+    L = L or _crc.lib()
+    if id(L) not in _SIG:
         vp, i32 = ctypes.c_void_p, ctypes.c_int
         for name, res, args in [
                 ("tfs_ec_config", i32, [vp, i32, i32, vp, ctypes.POINTER(vp)]),
@@ -35,7 +36,7 @@ def lib():
                 ("tfs_ec_decode", i32, [vp, vp, vp, i32])]:
             f = getattr(L, name)
             f.restype, f.argtypes = res, args
-        _SIG = True
+        _SIG.add(id(L))
     return L
 
 
@@ -46,7 +47,8 @@ class ErasureCode:
         self.ctx, self.dn, self.pn = ctx, dn, pn
         h = ctypes.c_void_p()
         e = None if erased is None else (ctypes.c_int * (dn + pn))(*erased)
-        self.rc = lib().tfs_ec_config(ctx.handle, dn, pn, e, ctypes.byref(h))
+        self.L = lib(ctx.L)
+        self.rc = self.L.tfs_ec_config(ctx.handle, dn, pn, e, ctypes.byref(h))
         self.h = h
 
     @staticmethod
@@ -66,23 +68,23 @@ class ErasureCode:
 
     def encode(self, members, size, sizes=None):
         """Host members (numpy uint8 arrays, written in place for parity)."""
-        return lib().tfs_ec_encode(self.h, self._ptrs(members), self._sizes(sizes, len(members)), self._size(size))
+        return self.L.tfs_ec_encode(self.h, self._ptrs(members), self._sizes(sizes, len(members)), self._size(size))
 
     def decode(self, members, size, sizes=None):
-        return lib().tfs_ec_decode(self.h, self._ptrs(members), self._sizes(sizes, len(members)), self._size(size))
+        return self.L.tfs_ec_decode(self.h, self._ptrs(members), self._sizes(sizes, len(members)), self._size(size))
 
     def encode_device(self, d_members, size, sizes=None, stream=None):
         p = (ctypes.c_void_p * len(d_members))(*[d if isinstance(d, int) or d is None else d.ptr for d in d_members])
-        return lib().tfs_ec_encode_device(self.h, p, self._sizes(sizes, len(d_members)), self._size(size), stream)
+        return self.L.tfs_ec_encode_device(self.h, p, self._sizes(sizes, len(d_members)), self._size(size), stream)
 
     def decode_device(self, d_members, size, sizes=None, stream=None):
         p = (ctypes.c_void_p * len(d_members))(*[d if isinstance(d, int) or d is None else d.ptr for d in d_members])
-        return lib().tfs_ec_decode_device(self.h, p, self._sizes(sizes, len(d_members)), self._size(size), stream)
+        return self.L.tfs_ec_decode_device(self.h, p, self._sizes(sizes, len(d_members)), self._size(size), stream)
 
     def free(self):
         # after the context is closed its device memory is gone with it: only drop the handle
         if self.h is not None and self.h.value and self.ctx.handle is not None and self.ctx.handle.value:
-            lib().tfs_ec_free(self.h)
+            self.L.tfs_ec_free(self.h)
         self.h = None
 
     def __del__(self):
