@@ -115,6 +115,9 @@ def launch_check(args):
         print(json.dumps({"launch_check": {"world": world, "gpus": args.gpus, "ranks": got}}), flush=True)
 
 
+TRAFFIC_NOTE = ("quoted: HBM bytes per launch from the committed rocprofv3 PMC passes of this same command at "
+                "full size (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE, tools/pmc_summary.py), not counted in this "
+                "run; null when this run is not the profiled configuration")
 # The product verify kernel as rocprofv3 names it (profiles/pmc_latest.json is of this kernel).
 HEADLINE_KERNEL = "crc_files_kernel<1, 16, 5, true, true, true, 1, false, true, 1, false, false, 4, 3"
 PACKET_PIPELINE = ("packet pipeline: packet_parse_kernel + crc_files_kernel<1, ..., 4, 3> + "
@@ -410,7 +413,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": pmc.get("traffic_bytes_per_launch"),
-            "traffic_source": pmc.get("source"),
+            "traffic_source": pmc.get("source"), "traffic_measured_in_this_run": False, "traffic_note": TRAFFIC_NOTE,
             "kernel": "crc_files_kernel<1> (verify)",
             "kernel_ms_avg": avg_kern_s * 1e3,
             "algorithmic_bytes_per_launch": nfiles * ALGO_BYTES_PER_FILE,
@@ -666,7 +669,7 @@ def bench_zipf(args):
             nblocks, n, payload / n / 1024), "files_per_gpu": n},
         "roofline": {"bound": "hbm", "achieved": algo / (kms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": algo / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": z_traffic,
-                     "traffic_source": z_src, "algorithmic_bytes_per_launch": algo,
+                     "traffic_source": z_src, "traffic_measured_in_this_run": False, "traffic_note": TRAFFIC_NOTE, "algorithmic_bytes_per_launch": algo,
                      "kernel": "crc_files_kernel<0> (compute)", "kernel_ms_avg": kms},
     }
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -776,7 +779,7 @@ def bench_packet(args):
                    "frames_per_gpu": n},
         "roofline": {"bound": "hbm", "achieved": algo / (kms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": algo / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": p_traffic,
-                     "traffic_source": p_src, "algorithmic_bytes_per_launch": algo,
+                     "traffic_source": p_src, "traffic_measured_in_this_run": False, "traffic_note": TRAFFIC_NOTE, "algorithmic_bytes_per_launch": algo,
                      "kernel": "packet_parse + crc_files_kernel<1> + packet_finish", "kernel_ms_avg": kms},
     }
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -1396,7 +1399,7 @@ def bench_block_verify_device(args):
             nblocks, FILES_PER_BLOCK, nfiles * FILE_SIZE / 2**30), "files_per_gpu": nfiles,
             "algorithmic_bytes_per_record": algo_per_rec},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": bv_traffic, "traffic_source": bv_src,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": bv_traffic, "traffic_source": bv_src, "traffic_measured_in_this_run": False, "traffic_note": TRAFFIC_NOTE,
                      "kernel": "compact_pipe_kernel<true,true,true> (verify form)", "kernel_ms_avg": kms,
                      "algorithmic_bytes_per_launch": nfiles * algo_per_rec},
         "parity": {"statuses_all_ok": True, "crcs_equal_write_pass": nfiles, "oracle_checked": checked},
@@ -1508,13 +1511,18 @@ def bench_mixed(args):
     if not (d_dst.download(np.uint8, int(wlen)) == odest[:wlen]).all():
         raise SystemExit("mixed: GPU compaction disagrees with the oracle")
     modes = ("idle", "closes", "closes_all_cus")
+    ctx_full_grid = ctx.throughput_grid()
     res = {m: {"verify_ms": [], "compact_ms": [], "grid": [], "closes": 0, "close_s": 0.0, "lat": []} for m in modes}
     K = max(1, args.steps // 2)
     for rnd in range(max(1, args.ab_rounds)):
         for m in modes:
             ctx.set_cu_reserve(m != "closes_all_cus")
             cs = None
-            if m != "idle":
+            if m == "idle":  # no resident kernel alive or recently used: the full grid
+                t_w = time.perf_counter()
+                while ctx.throughput_grid() != ctx_full_grid and time.perf_counter() - t_w < 1.0:
+                    time.sleep(0.01)
+            else:
                 cs = ds.CloseStream(ctx, nleases=8)
                 time.sleep(0.05)  # the close stream in steady state (resident kernel up)
             d_ok.zero()
@@ -1552,7 +1560,9 @@ def bench_mixed(args):
         if r["lat"]:
             lat = np.concatenate(r["lat"])
             o.update(close_p50_us=float(np.percentile(lat, 50)), close_p99_us=float(np.percentile(lat, 99)),
-                     close_max_us=float(lat.max()), closes=r["closes"], closes_per_s=r["closes"] / r["close_s"])
+                     close_p999_us=float(np.percentile(lat, 99.9)), close_max_us=float(lat.max()),
+                     closes_over_1ms=int((lat > 1000).sum()), closes=r["closes"],
+                     closes_per_s=r["closes"] / r["close_s"])
         out[m] = o
     line = {
         "metric": "GiB/s CRC32 verify, device-resident 64 KiB files, with 64 KiB closes flowing on the same GPU",
@@ -1748,7 +1758,7 @@ def bench_compact_device(args):
         "config": {"workload": "SURVEY §8 f3: %d resident blocks, %d live files (%.1f GiB live)" % (
             nblocks, nlive, live_bytes / 2**30)},
         "roofline": {"bound": "hbm", "achieved": algo / (kms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": algo / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": cd_traffic, "traffic_source": cd_src,
+                     "frac": algo / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": cd_traffic, "traffic_source": cd_src, "traffic_measured_in_this_run": False, "traffic_note": TRAFFIC_NOTE,
                      "kernel": "compact_pipe_kernel<WIDE> (one launch)", "kernel_ms_avg": kms,
                      "algorithmic_bytes_per_launch": algo},
         "membench": extra,
@@ -1883,7 +1893,7 @@ def bench_ec(args):
         "vs_baseline": None, "dtype": "u8", "data": "synthetic (splitmix64) members",
         "config": {"workload": "SURVEY §8 f4: k=5 + m=3 members of %d MiB" % args.ec_mib},
         "roofline": {"bound": "hbm", "achieved": out["encode"]["hbm_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": out["encode"]["hbm_GBs"] / HBM_PEAK_GBS, "traffic": e_traffic, "traffic_source": e_src,
+                     "frac": out["encode"]["hbm_GBs"] / HBM_PEAK_GBS, "traffic": e_traffic, "traffic_source": e_src, "traffic_measured_in_this_run": False, "traffic_note": TRAFFIC_NOTE,
                      "algorithmic_bytes_per_launch": float(k + m) * size,
                      "kernel": "ec_apply_kernel<3>", "kernel_ms_avg": out["encode"]["ms"]},
         "decode": out["decode"],

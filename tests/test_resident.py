@@ -284,3 +284,83 @@ def test_sched_slots_recycled_from_a_destroyed_context(oracle):
             assert (ctx.batch(buf, offs[:9], lens[:9], seeds[:9]) == exp[:9]).all(), trial
         finally:
             ctx.close()
+
+
+def test_closes_beside_throughput_launches(oracle):
+    """The dataserver's mix on one GPU (data_management.cpp:173-236 beside
+    dataservice.cpp:2915-2918 -> task.cpp:713-836): 8 threads closing 64 KiB
+    writes through CloseBatcher and the resident kernel, while the same context
+    runs verify and compaction launches of 65,536 records (the chunked-ticket
+    path).  Both sides' results are checked: every close succeeds, every verdict
+    is 1, block 0's compaction equals the oracle's real_compact.  While closes
+    flow, throughput launches leave the resident kernel's CUs free (grid 256 - 16);
+    with the reserve off, or once the closes have stopped, they take every CU."""
+    import tfs_amd.crc as crc
+    import tfs_amd.dataserver as ds
+    from test_gpu_parity import _oracle_compact
+    ctx = crc.Context(0)
+    try:
+        nblocks, per, rec = 64, 1024, 65536 + 36
+        n = nblocks * per
+        total = n * rec
+        img = crc.DeviceBuffer(ctx, total + 4096)
+        ctx.synth_fill_device(img, (total + 7) // 8 * 8, 0xBEEF, 0)
+        roff = np.arange(n, dtype=np.uint64) * rec
+        desc = np.zeros(n, crc.DESC_DTYPE)
+        desc["offset"], desc["len"] = roff + 36, 65536
+        d_desc = crc.DeviceBuffer(ctx, desc.nbytes).upload(desc)
+        d_crc = crc.DeviceBuffer(ctx, 4 * n)
+        ctx.batch_device(d_desc, n, img, d_crc)
+        d_roff = crc.DeviceBuffer(ctx, roff.nbytes).upload(roff)
+        d_len = crc.DeviceBuffer(ctx, 4 * n).upload(np.full(n, 65536, np.uint32))
+        ctx.write_headers_device(img, d_roff, d_len, d_crc, 1, n)
+        ctx.sync()
+        desc["aux"] = d_crc.download(np.uint32)
+        d_v = crc.DeviceBuffer(ctx, desc.nbytes).upload(desc)
+        live = np.arange(0, per, 3)
+        nl = live.size
+        jobs = np.zeros(nblocks * nl, crc.COMPACT_JOB_DTYPE)
+        bidx = np.repeat(np.arange(nblocks, dtype=np.uint64), nl)
+        loc = np.tile(np.arange(nl, dtype=np.uint64) * rec, nblocks)
+        jobs["src_offset"] = bidx * (per * rec) + np.tile(live.astype(np.uint64) * rec, nblocks)
+        jobs["dest_offset"] = bidx * (nl * rec) + loc
+        jobs["file_id"] = 1 + bidx * per + np.tile(live.astype(np.uint64), nblocks)
+        jobs["size"] = rec
+        jobs["new_offset"] = loc.astype(np.int32)
+        d_j = crc.DeviceBuffer(ctx, jobs.nbytes).upload(jobs)
+        d_dst = crc.DeviceBuffer(ctx, jobs.size * rec + 64)
+        d_st = crc.DeviceBuffer(ctx, 4 * jobs.size)
+        d_ok = crc.DeviceBuffer(ctx, n)
+        d_nb = crc.DeviceBuffer(ctx, 4)
+        assert ctx.throughput_grid() == 256
+        for reserve in (True, False):
+            ctx.set_cu_reserve(reserve)
+            cs = ds.CloseStream(ctx, nleases=8)
+            time.sleep(0.05)
+            grid = ctx.throughput_grid()
+            assert grid == (240 if reserve else 256), (reserve, grid)
+            d_nb.zero()
+            for _ in range(4):
+                d_ok.zero()
+                ctx.verify_device(d_v, n, img, None, d_ok, d_nb)
+                ctx.compact_jobs_device(img, total, d_j, int(jobs.size), d_dst, None, d_st, d_nb)
+            ctx.sync()
+            rc, count, lat = cs.stop()
+            assert rc == 0 and count > 0, (rc, count)
+            assert int(d_nb.download(np.uint32)[0]) == 0
+            assert (d_ok.download(np.uint8, n) == 1).all() and (d_st.download(np.int32, jobs.size) == 0).all()
+            print("reserve %s: %d closes, p50 %.1f us, p99 %.1f us" % (reserve, count, np.percentile(lat, 50),
+                                                                      np.percentile(lat, 99)))
+        ctx.set_cu_reserve(True)
+        host = img.download(np.uint8, per * rec)
+        m = np.zeros(per, crc.META_DTYPE)
+        m["file_id"], m["offset"], m["size"] = 1 + np.arange(per), np.arange(per) * rec, rec
+        fl = np.where(np.arange(per) % 3 == 0, 0, 1).astype(np.int32)
+        odest, _, _ = _oracle_compact(oracle, host, m, fl)
+        assert (d_dst.download(np.uint8, odest.size) == odest).all()
+        time.sleep(0.1)  # the resident kernel idles out and the last post is > 50 ms old
+        assert ctx.throughput_grid() == 256
+        for b in (img, d_desc, d_crc, d_roff, d_len, d_v, d_j, d_dst, d_st, d_ok, d_nb):
+            b.free()
+    finally:
+        ctx.close()

@@ -206,6 +206,11 @@ constexpr uint64_t kZeroCopySpan = 8ull << 20;  // page-locked batches up to thi
 struct tfs_crc_ctx {
   int device = -1;
   hipStream_t stream = nullptr;
+  // The latency path's streams (zero-copy small batches; the resident kernel's
+  // res_stream) have the device's greatest priority: they never queue behind
+  // a throughput launch on `stream`, and their workgroups are dispatched first.
+  hipStream_t lat_stream = nullptr;
+  int lat_prio = 0;
   Tables* d_tables = nullptr;
   std::mutex mu;
   std::mutex err_mu;
@@ -524,7 +529,7 @@ int resident_setup(tfs_crc_ctx* ctx) {
   // non-blocking stream (a stale done count makes a workgroup wait for a unit
   // that is never posted while the host relaunches the kernel for its batch).
   if (hipMalloc(&st, kResStateBytes) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->res_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithPriority(&ctx->res_stream, hipStreamNonBlocking, ctx->lat_prio) != hipSuccess ||
       hipMemsetAsync(st, 0, kResStateBytes, ctx->res_stream) != hipSuccess ||
       hipStreamSynchronize(ctx->res_stream) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->res_event, hipEventDisableTiming) != hipSuccess) {
@@ -774,12 +779,12 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
         // no room in the ring: launch this batch
       }
       // n_bad is counted from the verdicts on the host (no atomics on host memory)
-      SCHED_LAUNCH(ctx, ctx->stream, "crc_files",
+      SCHED_LAUNCH(ctx, ctx->lat_stream, "crc_files",
                    launch_crc_files(mode, static_cast<const uint8_t*>(zb) - lo, static_cast<const Desc*>(zd), n,
                                     ctx->d_tables, static_cast<uint32_t*>(zcrc), static_cast<uint8_t*>(zok), nullptr,
-                                    sched, ctx->stream, ctx->variant, 0u, static_cast<uint32_t*>(zflag), s.seq,
+                                    sched, ctx->lat_stream, ctx->variant, 0u, static_cast<uint32_t*>(zflag), s.seq,
                                     cap_for(ctx, n)));
-      HIP_TRY(ctx, hipEventRecord(s.done, ctx->stream));
+      HIP_TRY(ctx, hipEventRecord(s.done, ctx->lat_stream));
       s.count_bad = true;
       s.spin = true;
       return TFS_SUCCESS;
@@ -919,6 +924,11 @@ int tfs_crc32_ctx_create(int device, tfs_crc_ctx** out) {
     if (prop.multiProcessorCount > 0) ctx->cus = unsigned(prop.multiProcessorCount);
     e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e != hipSuccess) { rc = set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "hipStreamCreate: %s", hipGetErrorString(e)); break; }
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess) ctx->lat_prio = greatest;
+    else (void)hipGetLastError();
+    e = hipStreamCreateWithPriority(&ctx->lat_stream, hipStreamNonBlocking, ctx->lat_prio);
+    if (e != hipSuccess) { rc = set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "hipStreamCreateWithPriority: %s", hipGetErrorString(e)); break; }
     std::vector<Tables> host(1);
     build_tables(host.data());
     e = hipMalloc(reinterpret_cast<void**>(&ctx->d_tables), sizeof(Tables));
@@ -935,6 +945,7 @@ int tfs_crc32_ctx_create(int device, tfs_crc_ctx** out) {
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) { rc = set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "hipMemset(sched): %s", hipGetErrorString(e)); break; }
     ctx->sched_streams.push_back(ctx->stream);
+    ctx->sched_streams.push_back(ctx->lat_stream);
   } while (0);
   *out = ctx;  // returned even on failure so the caller can read last_error; destroy it
   return rc;
@@ -950,6 +961,7 @@ int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx) {
   if (ctx->device >= 0) (void)hipSetDevice(ctx->device);
   resident_teardown(ctx);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->lat_stream) (void)hipStreamSynchronize(ctx->lat_stream);
   for (auto& s : ctx->slots) s.release();
   for (auto& s : ctx->sync_slots) s.release();
   for (auto& cs : ctx->cslots) {
@@ -965,6 +977,7 @@ int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx) {
   if (ctx->d_tables) (void)hipFree(ctx->d_tables);
   if (ctx->d_sched) (void)hipFree(ctx->d_sched);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->lat_stream) (void)hipStreamDestroy(ctx->lat_stream);
   delete ctx;
   return TFS_SUCCESS;
 }
@@ -1924,7 +1937,7 @@ int tfs_crc32_stream_sync(tfs_crc_ctx* ctx, void* stream) {
 }
 
 int tfs_crc32_stream_destroy(tfs_crc_ctx* ctx, void* stream) {
-  if (!ctx || !stream || stream == ctx->stream) return TFS_EXIT_PARAMETER_ERROR;
+  if (!ctx || !stream || stream == ctx->stream || stream == ctx->lat_stream) return TFS_EXIT_PARAMETER_ERROR;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   HIP_TRY(ctx, hipStreamSynchronize(static_cast<hipStream_t>(stream)));
   {
