@@ -657,7 +657,7 @@ def bench_zipf(args):
     kms = float(np.mean([a.elapsed_ms(b) for a, b in ev]))
     payload = float(lens.astype(np.float64).sum())
     algo = payload + 21.0 * n
-    z_traffic, z_src = _pmc_traffic("profiles/r02_s4/zipf/pmc_summary.json", HEADLINE_KERNEL.replace("<1,", "<0,", 1),
+    z_traffic, z_src = _pmc_traffic("profiles/r03/zipf/pmc_summary.json", HEADLINE_KERNEL.replace("<1,", "<0,", 1),
                                     nblocks == 1024 and not align)
     res = {
         "metric": "GiB/s CRC32 compute-on-write, device-resident Zipf 4 KiB-1 MiB files",
@@ -1387,7 +1387,7 @@ def bench_block_verify_device(args):
     c24.close()
     algo_per_rec = FILEINFO + FILE_SIZE + 40 + 4 + 4   # header + payload + job read, crc + status written
     achieved = nfiles * algo_per_rec / (kms / 1e3) / 1e9
-    bv_traffic, bv_src = _pmc_traffic("profiles/r02_s4/block_verify_device/pmc_summary.json",
+    bv_traffic, bv_src = _pmc_traffic("profiles/r03/block_verify_device/pmc_summary.json",
                                       "compact_pipe_kernel<true, true, true, 12, 5, 4, 3", nblocks == 1024)
     res = {
         "metric": "GiB/s payload verified on read from device-resident block images (FileInfo checks + re-CRC)",
@@ -1746,7 +1746,7 @@ def bench_compact_device(args):
     live_bytes = float(nlive) * rec
     algo = 2 * live_bytes + nlive * (40 + 4)  # read + write live records, 40 B CompactJob + 4 B status
     live_payload = float(nlive) * FILE_SIZE
-    cd_traffic, cd_src = _pmc_traffic("profiles/r02_s4/compact_device/pmc_summary.json",
+    cd_traffic, cd_src = _pmc_traffic("profiles/r03/compact_device/pmc_summary.json",
                                       "compact_pipe_kernel<true, true, false, 12, 5, 1, 0", nblocks == 1024)
     res = {
         "metric": "GiB/s of live payload compacted on the device (re-CRC + repack of live files)",

@@ -1,10 +1,10 @@
 #!/usr/bin/env bash
-# tools/profile_r02.sh -- rocprofv3 passes for the round-2 profiles (run on the
+# tools/profile_lines.sh -- rocprofv3 passes for a round's profiles (run on the
 # GPU box through gpurun): kernel trace + stats of each bench command, then each
 # PMC group in its own pass (FETCH_SIZE and WRITE_SIZE cannot share one; counters
-# never combined with other trace domains).  Outputs under gpurun_out/prof_r02/;
-# tools/pmc_summary.py folds them into profiles/r02/.
-# Usage: tools/profile_r02.sh [all|compact|verify|bverify|zipf|packet|ec] [outdir]
+# never combined with other trace domains).  Outputs under OUTDIR;
+# tools/pmc_summary.py folds them into profiles/rNN/.
+# Usage: tools/profile_lines.sh [all|compact|verify|bverify|zipf|packet|ec] OUTDIR
 set -euo pipefail
 PART=${1:-all}
 OUT=${2:-gpurun_out/prof_r02}
@@ -60,4 +60,4 @@ E=(--workload ec --no-cpu --steps 4 --warmup 1)
 run_trace ec "${E[@]}"
 for grp in FETCH_SIZE WRITE_SIZE; do run_pmc ec "$grp" "ec_apply_kernel<3>" --workload ec --no-cpu --steps 1 --warmup 1; done
 fi
-echo "profile_r02 done"
+echo "profile_lines done"
