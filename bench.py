@@ -353,24 +353,29 @@ def main():
         ab_compare(args, crc, img, d_vdesc, nfiles, d_ok, d_bad)
 
     extra = {}
-    if args.membench:
+    if args.membench:  # calibration kernels: measurement build (libtfs_crc_measure.so)
         out = crc.DeviceBuffer(ctx, 16)
-        for pat, grid in ((1000, 0), (1000, 1024), (16, 0), (1016, 0), (10016, 0), (11016, 0), (54004, 0),
-                          (54016, 0), (54064, 0)):
-            e0, e1 = crc.Event(ctx), crc.Event(ctx)
-            ctx.membench_device(pat, img, d_vdesc, nfiles, total, out, grid=grid)
+        mctx = crc.Context(local, measure=True)
+        mb = [(1000, 0), (1000, 1024), (16, 0), (1016, 0), (10016, 0), (11016, 0), (54004, 0), (54016, 0),
+              (54064, 0), (55404, 0), (55804, 0), (55416, 0), (55404, 512), (55804, 512), (55816, 512), (55264, 0)]
+        if os.environ.get("TFS_BENCH_MEMBENCH"):  # "pattern:grid,..." (measurement)
+            mb = [tuple(int(x) for x in p.split(":")) for p in os.environ["TFS_BENCH_MEMBENCH"].split(",")]
+        for pat, grid in mb:
+            e0, e1 = crc.Event(mctx), crc.Event(mctx)
+            mctx.membench_device(pat, img, d_vdesc, nfiles, total, out, grid=grid)
             e0.record()
             for _ in range(5):
-                ctx.membench_device(pat, img, d_vdesc, nfiles, total, out, grid=grid)
+                mctx.membench_device(pat, img, d_vdesc, nfiles, total, out, grid=grid)
             e1.record()
             ms = e0.elapsed_ms(e1) / 5
             run = pat % 1000
-            if pat >= 54000:  # wave-contiguous chunks of (pat % 100) x 16 KiB over the whole image
+            if pat >= 54000:  # wave- / workgroup-contiguous chunks of (pat % 100) x 16 KiB over the whole image
                 ch = (pat % 100) * 16384
                 nb = total // ch * ch
             else:
                 nb = total if run == 0 else nfiles * ((FILE_SIZE - 127) // (64 * run)) * 64 * run
             extra["membench_p%d_g%d_GBs" % (pat, grid)] = nb / (ms / 1e3) / 1e9
+        mctx.close()
         print(json.dumps({"membench": extra}), file=sys.stderr)
 
     # HBM traffic per launch from the committed rocprofv3 PMC passes of this same
@@ -687,16 +692,18 @@ def bench_zipf(args):
         # (whole 1 KiB stripes of every file, 128-byte anchored, nt), and a plain
         # grid-stride stream of the same image: the ceilings the Zipf kernel is held to.
         mb = crc.DeviceBuffer(ctx, 16)
+        mctx = crc.Context(local, measure=True)  # calibration kernels: measurement build
         stripes = np.maximum(lens.astype(np.int64) - 127, 0) // 1024
         for pat, nb in ((11016, float(stripes.sum()) * 1024.0), (1000, float(total))):
-            ctx.membench_device(pat, img, d_desc, n, total, mb)
-            e0, e1 = crc.Event(ctx), crc.Event(ctx)
+            mctx.membench_device(pat, img, d_desc, n, total, mb)
+            e0, e1 = crc.Event(mctx), crc.Event(mctx)
             e0.record()
             for _ in range(5):
-                ctx.membench_device(pat, img, d_desc, n, total, mb)
+                mctx.membench_device(pat, img, d_desc, n, total, mb)
             e1.record()
-            ctx.sync()
+            mctx.sync()
             res.setdefault("membench_GBs", {})["p%d" % pat] = nb / (e0.elapsed_ms(e1) / 5 / 1e3) / 1e9
+        mctx.close()
         mb.free()
     if rank == 0:
         print(json.dumps(res), flush=True)
@@ -1715,15 +1722,17 @@ def bench_compact_device(args):
     if args.membench:  # streaming-copy ceiling for the same number of live bytes
         nb = int(live_bytes_total(windows, rec)) // 16 * 16
         cdst = crc.DeviceBuffer(ctx, nb + 64)
+        mctx = crc.Context(local, measure=True)  # calibration kernels: measurement build
         for pat in (50000, 51000, 52001, 52004, 52008, 52104, 52114, 52014, 52118, 52108):
-            e0, e1 = crc.Event(ctx), crc.Event(ctx)
-            ctx.membench_device(pat, img, None, 0, nb, cdst)
+            e0, e1 = crc.Event(mctx), crc.Event(mctx)
+            mctx.membench_device(pat, img, None, 0, nb, cdst)
             e0.record()
             for _ in range(3):
-                ctx.membench_device(pat, img, None, 0, nb, cdst)
+                mctx.membench_device(pat, img, None, 0, nb, cdst)
             e1.record()
-            ctx.sync()
+            mctx.sync()
             extra["copy_p%d_GBs_rw" % pat] = 2 * nb / (e0.elapsed_ms(e1) / 3 / 1e3) / 1e9
+        mctx.close()
         cdst.free()
     el_w, kms_w = timed(ctx)
     el2, kms2 = timed(ctx2)

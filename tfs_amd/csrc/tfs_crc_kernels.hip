@@ -2236,8 +2236,48 @@ __global__ void __launch_bounds__(kBlock) membench_read_chunk_kernel(const uint8
   if (acc == 0x9E3779B9u) out[0] = acc;  // keep the loads alive
 }
 
+// Calibration: workgroup-contiguous chunks -- chunk c (ch bytes) to workgroup
+// c mod G, and inside a chunk wave w reads 1 KiB stripes w, w+16, ... (the
+// latency form's access shape, crc_wg_kernel): at any moment a CU's 16 waves read
+// one contiguous run of 16 stripes.  PF stripes per wave in flight.
+template <int PF>
+__global__ void __launch_bounds__(kBlock) membench_wg_chunk_kernel(const uint8_t* __restrict__ src, uint64_t nbytes,
+                                                                   uint64_t ch, uint32_t* out) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t nch = nbytes / ch;
+  const uint64_t nst = ch / 1024u;
+  const uintptr_t s = reinterpret_cast<uintptr_t>(src);
+  uint32_t acc = 0;
+  for (uint64_t c = blockIdx.x; c < nch; c += gridDim.x) {
+    const uint64_t b = c * ch + 16u * uint64_t(lane);
+    for (uint64_t st = wave; st < nst; st += 16u * PF) {
+      uint4 v[PF];
+#pragma unroll
+      for (int k = 0; k < PF; ++k) {
+        const uint64_t sk = st + 16u * uint64_t(k);
+        v[k] = ld128s<true>(s + b + 1024u * (sk < nst ? sk : st));
+      }
+#pragma unroll
+      for (int k = 0; k < PF; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    }
+  }
+  if (acc == 0x9E3779B9u) out[0] = acc;  // keep the loads alive
+}
+
 hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, uint32_t n, uint64_t nbytes,
                            uint32_t* out, unsigned grid, hipStream_t stream) {
+  if (pattern >= 55000 && pattern < 56000) {
+    // 55PCC: workgroup-contiguous chunks, CC = chunk in 16 KiB units, P = stripes in flight per wave (1-8)
+    const int P = (pattern / 100) % 10, CC = pattern % 100;
+    const uint64_t ch = uint64_t(CC ? CC : 4) * 16384u;
+    const dim3 g(grid ? grid : kMaxGrid);
+    const uint64_t nb = nbytes / ch * ch;
+    if (P <= 2) hipLaunchKernelGGL(membench_wg_chunk_kernel<2>, g, dim3(kBlock), 0, stream, base, nb, ch, out);
+    else if (P <= 4) hipLaunchKernelGGL(membench_wg_chunk_kernel<4>, g, dim3(kBlock), 0, stream, base, nb, ch, out);
+    else hipLaunchKernelGGL(membench_wg_chunk_kernel<8>, g, dim3(kBlock), 0, stream, base, nb, ch, out);
+    return hipGetLastError();
+  }
   if (pattern >= 54000 && pattern < 55000) {
     // 540CC: chunked read, CC = chunk in 16 KiB units; PF 8, 256 workgroups
     const int CC = pattern % 100;

@@ -37,7 +37,7 @@ import tfs_amd.crc as crc  # noqa: E402
 
 def ctx_for(variant):
     os.environ["TFS_CRC_VARIANT"] = str(variant)
-    c = crc.Context(0)
+    c = crc.Context(0, measure=True)  # variants: measurement build
     os.environ["TFS_CRC_VARIANT"] = "0"
     return c
 
@@ -45,7 +45,7 @@ def ctx_for(variant):
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
     nblocks = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
-    ctx = crc.Context(0)
+    ctx = crc.Context(0, measure=True)  # calibration kernels: measurement build
     nfiles, rec = bench.FILES_PER_BLOCK, bench.FILEINFO + bench.FILE_SIZE
     blk = nfiles * rec
     total = nblocks * blk

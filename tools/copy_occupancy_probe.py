@@ -19,7 +19,7 @@ import tfs_amd.crc as crc  # noqa: E402
 
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 6
-    ctx = crc.Context(0)
+    ctx = crc.Context(0, measure=True)  # calibration kernels: measurement build
     nbytes = 349184 * 65572 // 16 * 16
     src = crc.DeviceBuffer(ctx, nbytes + 4096)
     dst = crc.DeviceBuffer(ctx, nbytes + 4096)

@@ -19,7 +19,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import tfs_amd.crc as crc  # noqa: E402
 
-ctx = crc.Context(0)
+ctx = crc.Context(0, measure=True)  # calibration kernels: measurement build
 TOTAL = 64 << 30
 img = crc.DeviceBuffer(ctx, TOTAL + 4096)
 ctx.synth_fill_device(img, TOTAL, 7, 0)

@@ -10,7 +10,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import tfs_amd.crc as crc  # noqa: E402
 
-ctx = crc.Context(0)
+ctx = crc.Context(0, measure=True)  # calibration kernels: measurement build
 N = 1 << 30
 h = crc.PinnedBuffer(ctx, N)
 h2 = crc.PinnedBuffer(ctx, N)
