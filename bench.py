@@ -351,6 +351,9 @@ def main():
 
     if args.ab:
         ab_compare(args, crc, img, d_vdesc, nfiles, d_ok, d_bad)
+    if os.environ.get("TFS_BENCH_SPLIT_AB"):
+        split_ab(ctx, crc, local, args, lambda c: c.verify_device(d_vdesc, nfiles, img, None, d_ok, d_bad),
+                 nfiles * ALGO_BYTES_PER_FILE)
 
     extra = {}
     if args.membench:  # calibration kernels: measurement build (libtfs_crc_measure.so)
@@ -491,6 +494,28 @@ def ab_compare(args, crc, img, d_vdesc, nfiles, d_ok, d_bad, mode=1, algo_bytes=
                   "frac_at_median": algo_bytes / (ms[len(ms) // 2] / 1e3) / 1e9 / HBM_PEAK_GBS}
         ctxs[v].close()
     print(json.dumps({"ab": out}), file=sys.stderr)
+
+
+def split_ab(ctx, crc, device, args, run, algo_bytes):
+    """Measurement: the product with split files (tfs_crc32_set_split on, the
+    default) against the same library with every file on one wave, interleaved
+    rounds in one process (stderr)."""
+    c2 = crc.Context(device)
+    c2.set_split(False)
+    times = {"split": [], "whole": []}
+    for _ in range(max(1, args.ab_rounds)):
+        for key, c in (("split", ctx), ("whole", c2)):
+            run(c)
+            e0, e1 = crc.Event(c), crc.Event(c)
+            e0.record()
+            for _ in range(3):
+                run(c)
+            e1.record()
+            times[key].append(e0.elapsed_ms(e1) / 3)
+    c2.close()
+    out = {k: {"median_ms": sorted(v)[len(v) // 2], "min_ms": min(v),
+               "frac_at_median": algo_bytes / (sorted(v)[len(v) // 2] / 1e3) / 1e9 / HBM_PEAK_GBS} for k, v in times.items()}
+    print(json.dumps({"split_ab": out}), file=sys.stderr)
 
 
 def e2e_rate(ctx):
@@ -687,6 +712,54 @@ def bench_zipf(args):
             sample[so[j]:so[j] + sl[j]] = img.download(np.uint8, int(lens[i]), int(offs[i]))
         res["cpu_baseline"] = cpu_baseline(sample, so, sl, got[idx], args.cpu_seconds,
                                            "Zipf-sized payloads (evenly spaced files of the batch)")
+    if os.environ.get("TFS_BENCH_SPLIT_AB"):
+        split_ab(ctx, crc, local, args, lambda c: c.batch_device(d_desc, n, img, d_out),
+                 float(lens.astype(np.float64).sum()) + 21.0 * n)
+    if os.environ.get("TFS_BENCH_SPLIT_PROBE"):
+        # Measurement: would splitting large files into fixed segments (several
+        # waves per file, their CRCs folded afterwards) read faster?  The same
+        # payload bytes as descriptor lists where every file longer than T is cut
+        # into a ragged first piece and S-byte segments; timed interleaved with
+        # the unsplit list in this process (the fold is not timed: it is per file).
+        def split_list(T, S):
+            so, sl = [], []
+            big = lens > T
+            so.append(offs[~big]); sl.append(lens[~big])
+            for o, L in zip(offs[big], lens[big]):
+                L = int(L)
+                first = L - (L - 1) // S * S
+                so.append(np.array([int(o)] + [int(o) + first + S * j for j in range((L - first) // S)], np.uint64))
+                sl.append(np.array([first] + [S] * ((L - first) // S), np.uint32))
+            so, sl = np.concatenate(so), np.concatenate(sl)
+            order = np.argsort(so, kind="stable")
+            d = np.zeros(len(so), crc.DESC_DTYPE)
+            d["offset"], d["len"] = so[order], sl[order]
+            return d
+        lists = {"unsplit": (d_desc, n)}
+        spec = [tuple(int(x) for x in v.split(":")) for v in os.environ["TFS_BENCH_SPLIT_PROBE"].split(",")]
+        bufs = []
+        for T, S in spec:
+            d = split_list(T, S)
+            assert int(d["len"].astype(np.int64).sum()) == int(lens.astype(np.int64).sum())
+            dd = crc.DeviceBuffer(ctx, d.nbytes).upload(d)
+            bufs.append(dd)
+            lists["T%d_S%d" % (T, S)] = (dd, len(d))
+        dout = crc.DeviceBuffer(ctx, 4 * max(v[1] for v in lists.values()))
+        times = {k: [] for k in lists}
+        for _ in range(max(1, args.ab_rounds)):
+            for k, (dd, nn) in lists.items():
+                ctx.batch_device(dd, nn, img, dout)
+                e0, e1 = crc.Event(ctx), crc.Event(ctx)
+                e0.record()
+                for _ in range(3):
+                    ctx.batch_device(dd, nn, img, dout)
+                e1.record()
+                times[k].append(e0.elapsed_ms(e1) / 3)
+        print(json.dumps({"split_probe": {k: {"units": lists[k][1], "median_ms": sorted(v)[len(v) // 2],
+                                              "min_ms": min(v), "frac_at_median": algo / (sorted(v)[len(v) // 2] / 1e3)
+                                              / 1e9 / HBM_PEAK_GBS} for k, v in times.items()}}), file=sys.stderr)
+        for b in bufs + [dout]:
+            b.free()
     if args.membench:
         # The kernel's access pattern over this geometry without the CRC arithmetic
         # (whole 1 KiB stripes of every file, 128-byte anchored, nt), and a plain

@@ -472,6 +472,12 @@ int tfs_crc32_resident_stats(tfs_crc_ctx* ctx, uint64_t* launches, uint64_t* fil
  * every CU regardless.  tfs_crc32_throughput_grid: workgroups the next
  * throughput launch of ctx would use. */
 int tfs_crc32_set_cu_reserve(tfs_crc_ctx* ctx, int on);
+/* Throughput launches of the file kernel (batches of more than 256 files) cut
+ * every file longer than 128 KiB into a ragged head and 128 KiB segments that
+ * separate waves checksum, then fold the segment CRCs into the file's CRC on the
+ * GPU: one wave never streams a long file alone.  Results are
+ * identical either way; on = 0 keeps every file on one wave (A/B). */
+int tfs_crc32_set_split(tfs_crc_ctx* ctx, int on);
 int tfs_crc32_throughput_grid(tfs_crc_ctx* ctx);
 /* Scheduler slots: ctx-owned streams bound (the ctx stream, compaction streams,
  * tfs_crc32_stream_create), and launches so far on streams the ctx does not own

@@ -26,7 +26,8 @@
 namespace tfscrc {
 hipError_t launch_crc_files(int mode, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
                             uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
-                            int variant, uint32_t vseed, uint32_t* done_flag, uint32_t seq, unsigned cap);
+                            int variant, uint32_t vseed, uint32_t* done_flag, uint32_t seq, unsigned cap,
+                            const SplitArgs* split);
 hipError_t launch_packet_parse(const uint8_t* base, const PacketDesc* pd, uint32_t n, int mode, Desc* desc,
                                int32_t* pre, hipStream_t stream);
 hipError_t launch_packet_finish(uint8_t* base, const PacketDesc* pd, const Desc* desc, uint32_t n, int mode,
@@ -242,7 +243,15 @@ struct tfs_crc_ctx {
   static constexpr int variant = 0;  // the product library holds one form of each kernel
 #endif
   unsigned cus = kMaxGrid;  // compute units of the device: throughput grids are at most this
+  // Split files (tfs_crc_device.h SplitArgs): one scratch per context, used by one
+  // throughput launch at a time: split_mu is held from the plan's setup to the
+  // event recorded after the fold, and a launch on another stream waits for it.
+  std::mutex split_mu;
+  DevBuf split_base, split_ext, split_crc, split_used;
+  hipEvent_t split_done = nullptr;
+  bool split_pending = false;
   bool cu_reserve = true;   // leave a live resident kernel's CUs out of throughput launches
+  bool split_files = true;  // throughput launches split files > kSplitMin (tfs_crc32_set_split)
   std::atomic<uint32_t> inject_skip{0}, inject_count{0};  // tfs_crc32_inject_device_error
   DevBuf packet_scratch;  // device-resident packet calls (parse descriptors, verdicts)
   hipStream_t packet_scratch_stream = nullptr;
@@ -302,6 +311,7 @@ void build_tables(Tables* t) {
     for (int j = 0; j < kLevels; ++j) make_shift_table(t->level8[ri][j], run << j);
   }
   make_shift_table5(t->wg_jump, 16ull * (64ull * kWgWaves - 1ull));
+  make_shift_table5(t->seg_shift, kSegBytes);
   for (int j = 0; j < kWgLevels; ++j) make_shift_table5(t->wg_level[j], 16ull << j);
 }
 
@@ -582,6 +592,55 @@ unsigned cap_for(const tfs_crc_ctx* ctx, uint32_t n) { return n <= kWgMaxFiles ?
     if (const int r2_ = sched_release((ctx), (st), lease_, le_, (what))) return r2_; \
   } while (0)
 
+// (Caller holds split_mu.)  The split scratch for a throughput crc_files launch
+// of n files on st: per-file unit bases, up to cap ext units and their CRCs.
+int split_prepare(tfs_crc_ctx* ctx, hipStream_t st, uint32_t n, SplitArgs* sa) {
+  const uint64_t want = std::min<uint64_t>(std::max<uint64_t>(2ull * n, 65536ull), kSplitMaxUnits);
+  const bool grow = ctx->split_base.cap < 4ull * n || ctx->split_ext.cap < want * sizeof(Desc) ||
+                    ctx->split_crc.cap < want * 4u || ctx->split_used.cap < 8u;
+  if (ctx->split_pending) {
+    // The previous split launch (maybe on another stream) still owns the scratch:
+    // growing frees it, so wait for that launch; otherwise order after it.
+    if (grow) HIP_TRY(ctx, hipEventSynchronize(ctx->split_done));
+    else HIP_TRY(ctx, hipStreamWaitEvent(st, ctx->split_done, 0));
+  }
+  HIP_TRY(ctx, ctx->split_base.reserve(4ull * n));
+  HIP_TRY(ctx, ctx->split_ext.reserve(want * sizeof(Desc)));
+  HIP_TRY(ctx, ctx->split_crc.reserve(want * 4u));
+  HIP_TRY(ctx, ctx->split_used.reserve(8u));
+  if (!ctx->split_done) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->split_done, hipEventDisableTiming));
+  HIP_TRY(ctx, hipMemsetAsync(ctx->split_used.p, 0, 8u, st));
+  const uint64_t cap = std::min<uint64_t>(std::min<uint64_t>(ctx->split_ext.cap / sizeof(Desc), ctx->split_crc.cap / 4u),
+                                          kSplitMaxUnits);
+  *sa = SplitArgs{static_cast<uint32_t*>(ctx->split_base.p), static_cast<Desc*>(ctx->split_ext.p),
+                  static_cast<uint32_t*>(ctx->split_crc.p), static_cast<unsigned long long*>(ctx->split_used.p),
+                  uint32_t(cap)};
+  return TFS_SUCCESS;
+}
+
+// A crc_files launch of n files on st (no completion flag): throughput launches
+// (n > kWgMaxFiles) get their split plan, a scheduler slot and the CU cap of
+// their device; batches of at most kWgMaxFiles files take the latency form.
+int files_launch(tfs_crc_ctx* ctx, hipStream_t st, int mode, const uint8_t* base, const Desc* desc, uint32_t n,
+                 uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t vseed) {
+  std::unique_lock<std::mutex> lk(ctx->split_mu, std::defer_lock);
+  SplitArgs sa{nullptr, nullptr, nullptr, nullptr, 0u};
+  const SplitArgs* split = nullptr;
+  if (n > kWgMaxFiles && ctx->split_files) {
+    lk.lock();
+    if (const int rc = split_prepare(ctx, st, n, &sa)) return rc;
+    split = &sa;
+  }
+  SCHED_LAUNCH(ctx, st, "crc_files",
+               launch_crc_files(mode, base, desc, n, ctx->d_tables, out_crc, out_ok, n_bad, sched, st, ctx->variant,
+                                vseed, nullptr, 0u, cap_for(ctx, n), split));
+  if (split) {
+    HIP_TRY(ctx, hipEventRecord(ctx->split_done, st));
+    ctx->split_pending = true;
+  }
+  return TFS_SUCCESS;
+}
+
 // (Caller holds ctx->mu.)  Launch the resident kernel unless one is running.
 // Only one is ever in flight: a new one is launched only after the event behind
 // the previous one has completed, i.e. every workgroup of it has left.
@@ -783,7 +842,7 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
                    launch_crc_files(mode, static_cast<const uint8_t*>(zb) - lo, static_cast<const Desc*>(zd), n,
                                     ctx->d_tables, static_cast<uint32_t*>(zcrc), static_cast<uint8_t*>(zok), nullptr,
                                     sched, ctx->lat_stream, ctx->variant, 0u, static_cast<uint32_t*>(zflag), s.seq,
-                                    cap_for(ctx, n)));
+                                    cap_for(ctx, n), nullptr));
       HIP_TRY(ctx, hipEventRecord(s.done, ctx->lat_stream));
       s.count_bad = true;
       s.spin = true;
@@ -801,9 +860,10 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
   HIP_TRY(ctx, s.d_bad.reserve(4));
   HIP_TRY(ctx, hipMemcpyAsync(s.d_desc.p, d, size_t(n) * sizeof(Desc), hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(ctx, hipMemsetAsync(s.d_bad.p, 0, 4, ctx->stream));
-  SCHED_LAUNCH(ctx, ctx->stream, "crc_files", launch_crc_files(mode, d_base, static_cast<const Desc*>(s.d_desc.p), n, ctx->d_tables,
-                                static_cast<uint32_t*>(s.d_crc.p), static_cast<uint8_t*>(s.d_ok.p),
-                                static_cast<uint32_t*>(s.d_bad.p), sched, ctx->stream, ctx->variant, 0u, nullptr, 0u, cap_for(ctx, n)));
+  if (const int rc2 = files_launch(ctx, ctx->stream, mode, d_base, static_cast<const Desc*>(s.d_desc.p), n,
+                                   static_cast<uint32_t*>(s.d_crc.p), static_cast<uint8_t*>(s.d_ok.p),
+                                   static_cast<uint32_t*>(s.d_bad.p), 0u))
+    return rc2;
   HIP_TRY(ctx, hipMemcpyAsync(s.h_crc.p, s.d_crc.p, size_t(n) * 4, hipMemcpyDeviceToHost, ctx->stream));
   if (mode == 1) {
     HIP_TRY(ctx, hipMemcpyAsync(s.h_ok.p, s.d_ok.p, n, hipMemcpyDeviceToHost, ctx->stream));
@@ -974,6 +1034,12 @@ int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx) {
     ev = nullptr;
   }
   ctx->packet_scratch.release();
+  if (ctx->split_done) (void)hipEventSynchronize(ctx->split_done);
+  ctx->split_base.release();
+  ctx->split_ext.release();
+  ctx->split_crc.release();
+  ctx->split_used.release();
+  if (ctx->split_done) (void)hipEventDestroy(ctx->split_done);
   if (ctx->d_tables) (void)hipFree(ctx->d_tables);
   if (ctx->d_sched) (void)hipFree(ctx->d_sched);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -1108,9 +1174,8 @@ int tfs_crc32_batch_device(tfs_crc_ctx* ctx, const tfs_crc_desc* d_desc, uint32_
   if (!ctx || (n && (!d_desc || !d_base || !d_out_crc))) return TFS_EXIT_PARAMETER_ERROR;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  SCHED_LAUNCH(ctx, st, "crc_files", launch_crc_files(0, static_cast<const uint8_t*>(d_base), reinterpret_cast<const Desc*>(d_desc), n,
-                                ctx->d_tables, d_out_crc, nullptr, nullptr, sched, st, ctx->variant, 0u, nullptr, 0u, cap_for(ctx, n)));
-  return TFS_SUCCESS;
+  return files_launch(ctx, st, 0, static_cast<const uint8_t*>(d_base), reinterpret_cast<const Desc*>(d_desc), n,
+                      d_out_crc, nullptr, nullptr, 0u);
 }
 
 int tfs_crc32_verify_device(tfs_crc_ctx* ctx, const tfs_crc_vdesc* d_desc, uint32_t n, const void* d_base,
@@ -1118,9 +1183,8 @@ int tfs_crc32_verify_device(tfs_crc_ctx* ctx, const tfs_crc_vdesc* d_desc, uint3
   if (!ctx || (n && (!d_desc || !d_base))) return TFS_EXIT_PARAMETER_ERROR;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  SCHED_LAUNCH(ctx, st, "crc_files", launch_crc_files(1, static_cast<const uint8_t*>(d_base), reinterpret_cast<const Desc*>(d_desc), n,
-                                ctx->d_tables, d_out_crc, d_out_ok, d_n_bad, sched, st, ctx->variant, 0u, nullptr, 0u, cap_for(ctx, n)));
-  return TFS_SUCCESS;
+  return files_launch(ctx, st, 1, static_cast<const uint8_t*>(d_base), reinterpret_cast<const Desc*>(d_desc), n,
+                      d_out_crc, d_out_ok, d_n_bad, 0u);
 }
 
 uint32_t tfs_crc32_e(uint32_t crc, const char* data, int32_t len, int* err) {
@@ -1483,8 +1547,9 @@ static int packet_enqueue(tfs_crc_ctx* ctx, int mode, const PacketDesc* d_pd, ui
   uint8_t* d_ok = sp + size_t(n) * (sizeof(Desc) + 8);
   uint32_t* crc = d_crc ? d_crc : d_tmp_crc;
   HIP_TRY(ctx, launch_packet_parse(d_base, d_pd, n, mode, d_desc, d_pre, st));
-  SCHED_LAUNCH(ctx, st, "crc_files", launch_crc_files(mode, d_base, d_desc, n, ctx->d_tables, crc, mode == 1 ? d_ok : nullptr, nullptr,
-                                sched, st, ctx->variant, kPacketFlagV1, nullptr, 0u, cap_for(ctx, n)));
+  if (const int rc = files_launch(ctx, st, mode, d_base, d_desc, n, crc, mode == 1 ? d_ok : nullptr, nullptr,
+                                  kPacketFlagV1))
+    return rc;
   HIP_TRY(ctx, launch_packet_finish(d_base, d_pd, d_desc, n, mode, d_pre, d_ok, crc, d_status, d_n_bad, st));
   return TFS_SUCCESS;
 }
@@ -1889,6 +1954,13 @@ int tfs_crc32_set_cu_reserve(tfs_crc_ctx* ctx, int on) {
   if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
   std::lock_guard<std::mutex> g(ctx->mu);
   ctx->cu_reserve = on != 0;
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_set_split(tfs_crc_ctx* ctx, int on) {
+  if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
+  std::lock_guard<std::mutex> g(ctx->split_mu);
+  ctx->split_files = on != 0;
   return TFS_SUCCESS;
 }
 

@@ -154,6 +154,27 @@ struct FileInfoHdr {  // FileInfo, internal.h:432-446
 #pragma pack(pop)
 static_assert(sizeof(FileInfoHdr) == kFileInfoSize, "FileInfo must be 36 bytes");
 
+// Split files.  A throughput launch of crc_files_kernel
+// cuts every file longer than kSplitMin into a ragged head and kSegBytes
+// segments ("ext units"), appended to the launch's work after its files, so no
+// wave streams more than kSegBytes of one file alone (a wave that walks a 1 MiB
+// file alone reads slower than the moving window of the rest: Zipf +4-5 %).
+// The plan (split_plan_kernel) gives every file its first ext unit or kNoSplit;
+// the main kernel skips split files and computes the ext units; the fold
+// (split_fold_kernel) joins each split file's unit CRCs:
+// crc = shift(crc_head, S) ^ crc_1 ... with shift by S bytes from one table.
+constexpr uint32_t kSegBytes = 128u << 10;
+constexpr uint32_t kSplitMin = 128u << 10;
+constexpr uint32_t kNoSplit = 0xffffffffu;
+constexpr uint32_t kSplitMaxUnits = 4u << 20;  // ext units per launch at most (files past it stay whole)
+struct SplitArgs {
+  uint32_t* base;         // per file: its first ext unit, or kNoSplit (nullptr: no split plan)
+  Desc* ext;              // ext units (a split file's head first, then its segments)
+  uint32_t* ext_crc;      // their CRCs
+  unsigned long long* used;  // ext units the plan reserved (zeroed before it; may pass cap)
+  uint32_t cap;
+};
+
 // Device-resident constant tables (built on the host by crc_math.h).
 struct Tables {
   uint32_t slice[4][256];                          // slice-by-4 (slice k: byte then k zero bytes)
@@ -165,6 +186,7 @@ struct Tables {
   uint32_t level8[kNumRuns][kLevels][4][256];
   uint32_t wg_jump[kShiftChunks][32];              // latency form: shift(c, 16 * (64 * kWgWaves - 1))
   uint32_t wg_level[kWgLevels][kShiftChunks][32];  // latency form: shift(c, 16 * 2^j)
+  uint32_t seg_shift[kShiftChunks][32];            // split files: shift(c, kSegBytes)
 };
 
 constexpr int run_index(int run) { return run == 16 ? 0 : run == 32 ? 1 : run == 64 ? 2 : 3; }

@@ -795,9 +795,33 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
                                                            const Desc* __restrict__ desc, uint32_t n,
                                                            const Tables* __restrict__ tg, uint32_t* out_crc,
                                                            uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched,
-                                                           uint32_t vseed, uint32_t* done_flag, uint32_t seq) {
+                                                           uint32_t vseed, uint32_t* done_flag, uint32_t seq,
+                                                           SplitArgs sa) {
   __shared__ uint32_t lds_tables[LdsLayout<S8>::bytes / 4];
   load_tables<RUN, false, S8>(lds_tables, tg);
+  // Work units: the launch's files [0, nfiles), then the ext units of the split
+  // files (tfs_crc_device.h SplitArgs); a split file itself is skipped here.
+  const uint32_t nfiles = n;
+  if (sa.base) {
+    const unsigned long long used = *sa.used;
+    n = nfiles + uint32_t(used < sa.cap ? used : sa.cap);
+  }
+  // kind: 0 a file, 1 an ext unit, 2 a split file (nothing to do: len 0, no output)
+  auto unit = [&](uint32_t u, uint32_t& kind) -> Desc {
+    if (u >= nfiles) {
+      kind = 1u;
+      return sa.ext[u - nfiles];
+    }
+    Desc d = desc[u];
+    kind = 0u;
+    if (sa.base && sa.base[u] != kNoSplit) {
+      kind = 2u;
+      d.len = 0u;
+    }
+    return d;
+  };
+  // ext units carry their own seed (a split file's seed on its head, 0 after)
+  auto seed_of = [&](const Desc& d, uint32_t kind) -> uint32_t { return (MODE == 0 || kind == 1u) ? d.aux : vseed; };
   const int lane = threadIdx.x & (kWave - 1);
   const LaneBase lb = lane_base_of(lane);
   const uint32_t wpb = kBlock / kWave;
@@ -832,20 +856,22 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
     if (f >= n) break;
     fn = f + stride;
   }
-  Desc cur = desc[f];
-  FileGeo<RUN> g = make_geo<RUN>(base + cur.offset, cur.len, MODE == 0 ? cur.aux : vseed);
+  uint32_t kcur = 0, knxt = 0;
+  Desc cur = unit(f, kcur);
+  FileGeo<RUN> g = make_geo<RUN>(base + cur.offset, cur.len, seed_of(cur, kcur));
   Head<RUN> h = load_head<RUN, HV>(g, lane);
   const uintptr_t junk = reinterpret_cast<uintptr_t>(tg->slice);
   uint4 buf[PF][RUN / 16];
   load_ring<RUN, PF, NT>(g, lane, buf, junk);
-  Desc nxt = fn < n ? desc[fn] : Desc{0, 0, 0};
+  Desc nxt = fn < n ? unit(fn, knxt) : Desc{0, 0, 0};
   uint32_t jv = DYN && CF == 1 && fn < n ? tk.issue(lane) : 0u;  // ticket of the file after next, in flight
   for (;;) {
     const bool more = fn < n;
     const Desc ncur = nxt;
+    const uint32_t kn = knxt;
     // XF: the next file's geometry first -- this file's ring refills run into it.
     FileGeo<RUN> ng = XF ? make_geo<RUN>(more ? base + ncur.offset : reinterpret_cast<const uint8_t*>(junk),
-                                         more ? ncur.len : 0u, MODE == 0 ? ncur.aux : vseed)
+                                         more ? ncur.len : 0u, seed_of(ncur, kn))
                          : g;
     const uint32_t c =
         g.nstripes ? lane_chain<RUN, PF, NT, S8, false, G, false, 1, false, true, false, XF>(
@@ -855,33 +881,118 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
     Head<RUN> nh = h;
     uint32_t fnn = n;
     if (more) {
-      if (!XF) ng = make_geo<RUN>(base + ncur.offset, ncur.len, MODE == 0 ? ncur.aux : vseed);
+      if (!XF) ng = make_geo<RUN>(base + ncur.offset, ncur.len, seed_of(ncur, kn));
       nh = load_head<RUN, HV>(ng, lane);
       if (!XF || !g.nstripes) load_ring<RUN, PF, NT>(ng, lane, buf, junk);
       fnn = DYN ? (CF > 1 ? take() : tk.resolve(jv, lane))
                 : (BLK ? (fn + 1u < blk_end ? fn + 1u : n) : fn + stride);
-      if (fnn < n) nxt = desc[fnn];
+      if (fnn < n) nxt = unit(fnn, knxt);
       if (DYN && CF == 1 && fnn < n) jv = tk.issue(lane);
     }
     const uint32_t crc = finish_file<RUN, S8>(lds_tables, lb, g, h, c, lane);
     if (lane == 0) {
-      if (out_crc) out_crc[f] = crc;
-      if (MODE == 1) {
-        const bool ok = crc == cur.aux;
-        if (out_ok) out_ok[f] = ok ? 1 : 0;
-        bad += ok ? 0u : 1u;
+      if (kcur == 1u) {
+        sa.ext_crc[f - nfiles] = crc;
+      } else if (kcur == 0u) {
+        if (out_crc) out_crc[f] = crc;
+        if (MODE == 1) {
+          const bool ok = crc == cur.aux;
+          if (out_ok) out_ok[f] = ok ? 1 : 0;
+          bad += ok ? 0u : 1u;
+        }
       }
     }
     if (!more) break;
     f = fn;
     fn = fnn;
     cur = ncur;
+    kcur = kn;
     g = ng;
     h = nh;
   }
   } while (false);
   if (MODE == 1 && lane == 0 && bad && n_bad) atomicAdd(n_bad, bad);
   if (lane == 0) launch_exit(sched, gridDim.x * wpb, done_flag, seq);
+}
+
+// Split plan (tfs_crc_device.h SplitArgs): one thread per file.  A file longer
+// than kSplitMin becomes K = ceil(len / kSegBytes) ext units -- a ragged head of
+// len - (K-1)*kSegBytes bytes carrying the file's seed, then K-1 whole segments
+// -- reserved as one range per workgroup (one atomic per 256 files).  A
+// workgroup whose range would pass `cap` leaves its files whole (and writes
+// empty units into the part of its range below cap, so every unit the main
+// kernel takes is valid).
+template <int MODE>
+__global__ void __launch_bounds__(256) split_plan_kernel(const Desc* __restrict__ desc, uint32_t n, uint32_t vseed,
+                                                         SplitArgs sa) {
+  __shared__ uint32_t wsum[4];
+  __shared__ unsigned long long blk_base;
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint32_t w = threadIdx.x / kWave;
+  Desc d{0, 0, 0};
+  if (i < n) d = desc[i];
+  const uint32_t K = (i < n && d.len > kSplitMin) ? (d.len - 1u) / kSegBytes + 1u : 0u;
+  uint32_t x = K;  // inclusive scan over the wave
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, kWave);
+    if (lane >= o) x += y;
+  }
+  if (lane == kWave - 1) wsum[w] = x;
+  __syncthreads();
+  uint32_t before = 0, total = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    before += k < w ? wsum[k] : 0u;
+    total += wsum[k];
+  }
+  if (threadIdx.x == 0) blk_base = total ? atomicAdd(sa.used, (unsigned long long)total) : 0ull;
+  __syncthreads();
+  const unsigned long long b0 = blk_base;
+  const bool fits = b0 + total <= sa.cap;
+  const unsigned long long my = b0 + before + (x - K);
+  if (i < n) sa.base[i] = (K && fits) ? uint32_t(my) : kNoSplit;
+  if (!K) return;
+  if (fits) {
+    const uint32_t head = d.len - (K - 1u) * kSegBytes;
+    sa.ext[my] = Desc{d.offset, head, MODE == 0 ? d.aux : vseed};
+    for (uint32_t j = 1; j < K; ++j) sa.ext[my + j] = Desc{d.offset + head + uint64_t(j - 1u) * kSegBytes, kSegBytes, 0u};
+  } else {
+    for (unsigned long long u = my; u < my + K && u < sa.cap; ++u) sa.ext[u] = Desc{0, 0, 0};
+  }
+}
+
+// Split fold: each split file's CRC from its units' CRCs (seed-0 linearity,
+// crc(A||B) = shift(crc(A), |B|) ^ crc(B); the head carries the seed), then its
+// output and verdict as the main kernel writes them for whole files.
+template <int MODE>
+__global__ void __launch_bounds__(256) split_fold_kernel(const Desc* __restrict__ desc, uint32_t n,
+                                                         const Tables* __restrict__ tg, SplitArgs sa,
+                                                         uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad) {
+  __shared__ uint32_t T[uint32_t(kShiftChunks) * 32u];
+  for (uint32_t k = threadIdx.x; k < uint32_t(kShiftChunks) * 32u; k += blockDim.x) T[k] = (&tg->seg_shift[0][0])[k];
+  __syncthreads();
+  uint32_t bad = 0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t b = sa.base[i];
+    if (b == kNoSplit) continue;
+    const Desc d = desc[i];
+    const uint32_t K = (d.len - 1u) / kSegBytes + 1u;
+    uint32_t c = sa.ext_crc[b];
+    for (uint32_t j = 1; j < K; ++j) c = shift5(T, 0u, c) ^ sa.ext_crc[b + j];
+    if (out_crc) out_crc[i] = c;
+    if (MODE == 1) {
+      const bool ok = c == d.aux;
+      if (out_ok) out_ok[i] = ok ? 1 : 0;
+      bad += ok ? 0u : 1u;
+    }
+  }
+  if (MODE == 1 && n_bad) {  // one atomic per wave
+#pragma unroll
+    for (int m = kWave / 2; m >= 1; m >>= 1) bad += __shfl_xor(bad, m, kWave);
+    if ((threadIdx.x & (kWave - 1)) == 0 && bad) atomicAdd(n_bad, bad);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1882,10 +1993,10 @@ template <int MODE>
 static bool launch_measure_variant(int variant, dim3 grid, dim3 block, const uint8_t* base, const Desc* desc,
                                    uint32_t n, const Tables* tg, uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad,
                                    uint32_t* sched, hipStream_t stream, uint32_t vseed, uint32_t* done_flag,
-                                   uint32_t seq) {
+                                   uint32_t seq, const SplitArgs& sa) {
 #define TFS_LAUNCH(R, P, N, D, S)                                                                          \
   hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N, D, S>), grid, block, 0, stream, base, desc, n, tg, out_crc, \
-                     out_ok, n_bad, sched, vseed, done_flag, seq)
+                     out_ok, n_bad, sched, vseed, done_flag, seq, sa)
   switch (variant) {
     case 1: TFS_LAUNCH(16, 5, true, false, true); break;
     case 2: TFS_LAUNCH(16, 4, true, true, true); break;
@@ -1896,7 +2007,7 @@ static bool launch_measure_variant(int variant, dim3 grid, dim3 block, const uin
 #undef TFS_LAUNCH
 #define TFS_LAUNCH_G(R, P, N, D, S, G)                                                                        \
   hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N, D, S, G>), grid, block, 0, stream, base, desc, n, tg, out_crc, \
-                     out_ok, n_bad, sched, vseed, done_flag, seq)
+                     out_ok, n_bad, sched, vseed, done_flag, seq, sa)
     case 9: TFS_LAUNCH_G(16, 6, true, true, true, 2); break;
     case 10: TFS_LAUNCH_G(16, 6, true, true, true, 3); break;
     case 11: TFS_LAUNCH_G(16, 8, true, true, true, 4); break;
@@ -1904,43 +2015,43 @@ static bool launch_measure_variant(int variant, dim3 grid, dim3 block, const uin
 #undef TFS_LAUNCH_G
     case 13:
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, true>), grid, block, 0, stream, base,
-                         desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
+                         desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
       break;
     case 15:
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, true, 2>), grid, block, 0, stream,
-                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
+                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
       break;
     case 16:
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, true, 4>), grid, block, 0, stream,
-                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
+                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
       break;
     case 19:  // static contiguous ranges per wave (BLK)
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, false, kS8, 1, false, kIL, 1, false, true>), grid, block,
-                         0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
+                         0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
       break;
     case 17:  // cross-file ring (lane_chain XF): the next file's first stripes refill this file's freed slots
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, true>), grid, block, 0,
-                         stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
+                         stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
       break;
     case 18:  // cross-file ring, PF 6
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, 6, kNT, kDYN, kS8, 1, false, kIL, 1, true>), grid, block, 0,
-                         stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
+                         stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
       break;
     case 39:  // CF: 2 consecutive files per ticket
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, 2>), grid,
-                         block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
+                         block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
       break;
     case 40:  // CF: 4 consecutive files per ticket
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, 4>), grid,
-                         block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
+                         block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
       break;
     case 41:  // CF: 16 consecutive files per ticket
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, 16>), grid,
-                         block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
+                         block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
       break;
 #define TFS_LAUNCH_CF(CF, TS)                                                                                         \
   hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, CF, TS>), grid, \
-                     block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq)
+                     block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa)
     case 42: TFS_LAUNCH_CF(4, 3); break;  // chunks of 4, the last n/8 files one by one (= the product)
     case 47: TFS_LAUNCH_CF(4, 4); break;  // chunks of 4, the last n/16 one by one
     case 48: TFS_LAUNCH_CF(4, 5); break;  // chunks of 4, the last n/32 one by one
@@ -1951,14 +2062,14 @@ static bool launch_measure_variant(int variant, dim3 grid, dim3 block, const uin
 #undef TFS_LAUNCH_CF
     case 14:  // contiguous ticket groups (the product before interleaving)
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, false>), grid, block, 0, stream,
-                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
+                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
       break;
 #define TFS_LAUNCH(R, P, N, D, S)                                                                          \
   hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N, D, S>), grid, block, 0, stream, base, desc, n, tg, out_crc, \
-                     out_ok, n_bad, sched, vseed, done_flag, seq)
+                     out_ok, n_bad, sched, vseed, done_flag, seq, sa)
 #define TFS_LAUNCH_CX(P, IL_, CF, TS)                                                                                \
   hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, P, kNT, kDYN, kS8, 1, false, IL_, 1, false, false, CF, TS>), grid,   \
-                     block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq)
+                     block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa)
     case 51: TFS_LAUNCH_CX(kPF, false, kCF, kTS); break;  // chunked tickets over contiguous eighths
     case 52: TFS_LAUNCH_CX(kPF, kIL, 8, kTS); break;      // chunks of 8
     case 53: TFS_LAUNCH_CX(6, kIL, kCF, kTS); break;      // PF 6
@@ -1967,14 +2078,14 @@ static bool launch_measure_variant(int variant, dim3 grid, dim3 block, const uin
 #undef TFS_LAUNCH_CX
 #define TFS_LAUNCH_CW(WW)                                                                                           \
   hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, WW, false, false, kCF, kTS>), \
-                     grid, block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq)
+                     grid, block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa)
     case 56: TFS_LAUNCH_CW(2); break;  // chunked tickets, WW consecutive chunks per group slot (one XCD)
     case 57: TFS_LAUNCH_CW(8); break;
     case 58: TFS_LAUNCH_CW(4); break;
 #undef TFS_LAUNCH_CW
     case 50:  // one file per ticket (the product before chunked tickets)
       hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL>), grid, block, 0, stream,
-                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
+                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
       break;
     default:
       return false;
@@ -1987,7 +2098,8 @@ static bool launch_measure_variant(int variant, dim3 grid, dim3 block, const uin
 template <int MODE>
 static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
                                  uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched,
-                                 hipStream_t stream, uint32_t vseed, uint32_t* done_flag, uint32_t seq, unsigned cap) {
+                                 hipStream_t stream, uint32_t vseed, uint32_t* done_flag, uint32_t seq, unsigned cap,
+                                 const SplitArgs* split) {
   // Latency form for small batches (TFS_CRC_VARIANT 20 forces it for any n in
   // the measurement build; the other measurement variants never use it).
   if (variant == 20 || (variant == 0 && n <= kWgMaxFiles)) {
@@ -1998,27 +2110,43 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
   }
   if (!sched) return hipErrorInvalidValue;
   const dim3 grid(grid_for(n, cap)), block(kBlock);
+  // Split files (tfs_crc_device.h): the plan before the main kernel, the fold
+  // after it, all on `stream`; the completion-flag form (done_flag) never splits.
+  const SplitArgs sa = split && !done_flag ? *split : SplitArgs{nullptr, nullptr, nullptr, nullptr, 0u};
+  if (sa.base) {
+    hipLaunchKernelGGL((split_plan_kernel<MODE>), dim3((n + 255u) / 256u), dim3(256), 0, stream, desc, n, vseed, sa);
+    if (const hipError_t e = hipGetLastError()) return e;
+  }
+  bool launched = false;
 #ifdef TFS_CRC_MEASURE
-  if (variant != 0 && launch_measure_variant<MODE>(variant, grid, block, base, desc, n, tg, out_crc, out_ok, n_bad,
-                                                   sched, stream, vseed, done_flag, seq))
-    return hipGetLastError();
+  launched = variant != 0 && launch_measure_variant<MODE>(variant, grid, block, base, desc, n, tg, out_crc, out_ok,
+                                                          n_bad, sched, stream, vseed, done_flag, seq, sa);
 #endif
   // The product: chunked interleaved tickets (kCF files per ticket, the last
   // n >> kTS one by one), PF stripes in flight.
-  hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, kCF, kTS>),
-                     grid, block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq);
+  if (!launched)
+    hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, kCF, kTS>),
+                       grid, block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq,
+                       sa);
+  if (const hipError_t e = hipGetLastError()) return e;
+  if (sa.base) {
+    const uint32_t fg = (n + 255u) / 256u;
+    hipLaunchKernelGGL((split_fold_kernel<MODE>), dim3(fg < 1024u ? fg : 1024u), dim3(256), 0, stream, desc, n, tg, sa,
+                       out_crc, out_ok, n_bad);
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_crc_files(int mode, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
                             uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
-                            int variant, uint32_t vseed, uint32_t* done_flag, uint32_t seq, unsigned cap) {
+                            int variant, uint32_t vseed, uint32_t* done_flag, uint32_t seq, unsigned cap,
+                            const SplitArgs* split) {
   if (n == 0) return hipSuccess;
   if (mode == 0)
     return launch_variant<0>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, sched, stream, vseed, done_flag, seq,
-                             cap);
+                             cap, split);
   return launch_variant<1>(variant, base, desc, n, tg, out_crc, out_ok, n_bad, sched, stream, vseed, done_flag, seq,
-                           cap);
+                           cap, split);
 }
 
 hipError_t launch_resident(const Tables* tg, const ResHost* hs, uint32_t* dstate, unsigned grid, uint32_t idle_ticks,
