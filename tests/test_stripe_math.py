@@ -154,3 +154,54 @@ def test_shift_identity(oracle):
         a, b = d[:cut], d[cut:]
         assert shift(ocrc(oracle, 0, a), len(b)) ^ ocrc(oracle, 0, b) == ocrc(oracle, 0, d)
     assert ocrc(oracle, 0, bytes(100) + d) == ocrc(oracle, 0, d)
+
+
+KSEG = 128 * 1024
+KSPLIT = 128 * 1024
+
+
+def split_units(L, seed):
+    """split_plan_kernel's cut of a file of L bytes (tfs_crc_kernels.hip): a
+    ragged head with the seed, then whole KSEG segments with seed 0."""
+    if L <= KSPLIT:
+        return None
+    K = (L - 1) // KSEG + 1
+    head = L - (K - 1) * KSEG
+    return [(0, head, seed)] + [(head + (j - 1) * KSEG, KSEG, 0) for j in range(1, K)]
+
+
+def shift5_table(nbytes):
+    """make_shift_table5: 7 chunks of 5 bits (the fold's seg_shift table)."""
+    k = x2n(nbytes, 3)
+    return [[0 if (j == 6 and e >= 4) else mult(k, e << (5 * j)) for e in range(32)] for j in range(7)]
+
+
+def shift5(t, c):
+    r = 0
+    for j in range(7):
+        r ^= t[j][(c >> (5 * j)) & 31]
+    return r
+
+
+@pytest.mark.parametrize("L", [KSPLIT + 1, 2 * KSEG, 2 * KSEG + 1, 3 * KSEG - 1, 5 * KSEG + 4097, 9 * (1 << 20) + 3])
+def test_split_fold_equals_whole_file(oracle, L):
+    """The split plan + fold (DESIGN.md §3.1) restated: every unit's Func::crc
+    from the oracle, folded by the 5-bit seg_shift table, equals the whole
+    file's Func::crc with its seed."""
+    rnd = random.Random(L)
+    data = synth_bytes(L, L).tobytes()
+    t = shift5_table(KSEG)
+    for seed in (0, 0x4E534654, rnd.getrandbits(32)):
+        units = split_units(L, seed)
+        assert units and sum(u[1] for u in units) == L and units[0][1] >= 1 and units[0][1] <= KSEG
+        c = ocrc(oracle, units[0][2], data[:units[0][1]])
+        for off, ln, sd in units[1:]:
+            assert sd == 0 and ln == KSEG
+            c = shift5(t, c) ^ ocrc(oracle, 0, data[off:off + ln])
+        assert c == ocrc(oracle, seed, data), (L, hex(seed))
+
+
+def test_split_threshold():
+    assert split_units(KSPLIT, 5) is None and split_units(KSPLIT - 1, 5) is None
+    assert len(split_units(KSPLIT + 1, 5)) == 2 and split_units(KSPLIT + 1, 5)[0][1] == 1
+    assert len(split_units(3 * KSEG, 5)) == 3 and split_units(3 * KSEG, 5)[0][1] == KSEG

@@ -247,7 +247,7 @@ struct tfs_crc_ctx {
   // throughput launch at a time: split_mu is held from the plan's setup to the
   // event recorded after the fold, and a launch on another stream waits for it.
   std::mutex split_mu;
-  DevBuf split_base, split_ext, split_crc, split_used;
+  DevBuf split_plan;
   hipEvent_t split_done = nullptr;
   bool split_pending = false;
   bool cu_reserve = true;   // leave a live resident kernel's CUs out of throughput launches
@@ -592,29 +592,21 @@ unsigned cap_for(const tfs_crc_ctx* ctx, uint32_t n) { return n <= kWgMaxFiles ?
     if (const int r2_ = sched_release((ctx), (st), lease_, le_, (what))) return r2_; \
   } while (0)
 
-// (Caller holds split_mu.)  The split scratch for a throughput crc_files launch
-// of n files on st: per-file unit bases, up to cap ext units and their CRCs.
+// (Caller holds split_mu.)  The split plan for a throughput crc_files launch of
+// n files on st (tfs_crc_device.h: one allocation, up to cap ext units).
 int split_prepare(tfs_crc_ctx* ctx, hipStream_t st, uint32_t n, SplitArgs* sa) {
-  const uint64_t want = std::min<uint64_t>(std::max<uint64_t>(2ull * n, 65536ull), kSplitMaxUnits);
-  const bool grow = ctx->split_base.cap < 4ull * n || ctx->split_ext.cap < want * sizeof(Desc) ||
-                    ctx->split_crc.cap < want * 4u || ctx->split_used.cap < 8u;
+  const uint32_t cap = uint32_t(std::min<uint64_t>(std::max<uint64_t>(2ull * n, 65536ull), kSplitMaxUnits));
+  const uint64_t bytes = split_bytes(n, cap);
   if (ctx->split_pending) {
-    // The previous split launch (maybe on another stream) still owns the scratch:
+    // The previous split launch (maybe on another stream) still owns the plan:
     // growing frees it, so wait for that launch; otherwise order after it.
-    if (grow) HIP_TRY(ctx, hipEventSynchronize(ctx->split_done));
+    if (bytes > ctx->split_plan.cap) HIP_TRY(ctx, hipEventSynchronize(ctx->split_done));
     else HIP_TRY(ctx, hipStreamWaitEvent(st, ctx->split_done, 0));
   }
-  HIP_TRY(ctx, ctx->split_base.reserve(4ull * n));
-  HIP_TRY(ctx, ctx->split_ext.reserve(want * sizeof(Desc)));
-  HIP_TRY(ctx, ctx->split_crc.reserve(want * 4u));
-  HIP_TRY(ctx, ctx->split_used.reserve(8u));
+  HIP_TRY(ctx, ctx->split_plan.reserve(bytes));
   if (!ctx->split_done) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->split_done, hipEventDisableTiming));
-  HIP_TRY(ctx, hipMemsetAsync(ctx->split_used.p, 0, 8u, st));
-  const uint64_t cap = std::min<uint64_t>(std::min<uint64_t>(ctx->split_ext.cap / sizeof(Desc), ctx->split_crc.cap / 4u),
-                                          kSplitMaxUnits);
-  *sa = SplitArgs{static_cast<uint32_t*>(ctx->split_base.p), static_cast<Desc*>(ctx->split_ext.p),
-                  static_cast<uint32_t*>(ctx->split_crc.p), static_cast<unsigned long long*>(ctx->split_used.p),
-                  uint32_t(cap)};
+  HIP_TRY(ctx, hipMemsetAsync(ctx->split_plan.p, 0, 8u, st));  // `used`
+  *sa = SplitArgs{static_cast<uint8_t*>(ctx->split_plan.p), cap};
   return TFS_SUCCESS;
 }
 
@@ -624,7 +616,7 @@ int split_prepare(tfs_crc_ctx* ctx, hipStream_t st, uint32_t n, SplitArgs* sa) {
 int files_launch(tfs_crc_ctx* ctx, hipStream_t st, int mode, const uint8_t* base, const Desc* desc, uint32_t n,
                  uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t vseed) {
   std::unique_lock<std::mutex> lk(ctx->split_mu, std::defer_lock);
-  SplitArgs sa{nullptr, nullptr, nullptr, nullptr, 0u};
+  SplitArgs sa{nullptr, 0u};
   const SplitArgs* split = nullptr;
   if (n > kWgMaxFiles && ctx->split_files) {
     lk.lock();
@@ -1035,10 +1027,7 @@ int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx) {
   }
   ctx->packet_scratch.release();
   if (ctx->split_done) (void)hipEventSynchronize(ctx->split_done);
-  ctx->split_base.release();
-  ctx->split_ext.release();
-  ctx->split_crc.release();
-  ctx->split_used.release();
+  ctx->split_plan.release();
   if (ctx->split_done) (void)hipEventDestroy(ctx->split_done);
   if (ctx->d_tables) (void)hipFree(ctx->d_tables);
   if (ctx->d_sched) (void)hipFree(ctx->d_sched);

@@ -160,20 +160,30 @@ static_assert(sizeof(FileInfoHdr) == kFileInfoSize, "FileInfo must be 36 bytes")
 // wave streams more than kSegBytes of one file alone (a wave that walks a 1 MiB
 // file alone reads slower than the moving window of the rest: Zipf +4-5 %).
 // The plan (split_plan_kernel) gives every file its first ext unit or kNoSplit;
-// the main kernel skips split files and computes the ext units; the fold
-// (split_fold_kernel) joins each split file's unit CRCs:
-// crc = shift(crc_head, S) ^ crc_1 ... with shift by S bytes from one table.
+// the main kernel checksums a split file's ragged head in the file's own place
+// (with the file's seed, into head_crc) and its K-1 whole segments as ext units
+// (seed 0, into ext_crc); the fold (split_fold_kernel) joins them:
+// crc = shift(...shift(crc_head, S) ^ crc_1 ..., S) ^ crc_{K-1}, shift by S
+// bytes from one table.
 constexpr uint32_t kSegBytes = 128u << 10;
 constexpr uint32_t kSplitMin = 128u << 10;
 constexpr uint32_t kNoSplit = 0xffffffffu;
 constexpr uint32_t kSplitMaxUnits = 4u << 20;  // ext units per launch at most (files past it stay whole)
+// One allocation per plan (3 SGPRs in the kernels' arguments instead of a
+// pointer per array): [used u64 | pad][base u32 x n][head_crc u32 x n]
+// [ext_crc u32 x cap][pad to 16][ext Desc x cap].  base: per file its first ext
+// unit, or kNoSplit; head_crc: a split file's head CRC; ext: the split files'
+// whole segments; used: ext units the plan reserved (zeroed before it; may pass
+// cap, the files past it stay whole).
 struct SplitArgs {
-  uint32_t* base;         // per file: its first ext unit, or kNoSplit (nullptr: no split plan)
-  Desc* ext;              // ext units (a split file's head first, then its segments)
-  uint32_t* ext_crc;      // their CRCs
-  unsigned long long* used;  // ext units the plan reserved (zeroed before it; may pass cap)
+  uint8_t* plan;  // nullptr: no split plan
   uint32_t cap;
 };
+constexpr uint64_t split_off_base() { return 16u; }
+constexpr uint64_t split_off_head(uint32_t n) { return 16u + 4ull * n; }
+constexpr uint64_t split_off_ext_crc(uint32_t n) { return 16u + 8ull * n; }
+constexpr uint64_t split_off_ext(uint32_t n, uint32_t cap) { return (16u + 8ull * n + 4ull * cap + 15u) & ~15ull; }
+constexpr uint64_t split_bytes(uint32_t n, uint32_t cap) { return split_off_ext(n, cap) + 16ull * cap; }
 
 // Device-resident constant tables (built on the host by crc_math.h).
 struct Tables {

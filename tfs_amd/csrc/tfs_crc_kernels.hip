@@ -802,21 +802,23 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
   // Work units: the launch's files [0, nfiles), then the ext units of the split
   // files (tfs_crc_device.h SplitArgs); a split file itself is skipped here.
   const uint32_t nfiles = n;
-  if (sa.base) {
-    const unsigned long long used = *sa.used;
+  uint8_t* plan = nullptr;  // stays null when the plan split nothing: no per-file lookup
+  if (sa.plan) {
+    const unsigned long long used = *reinterpret_cast<const unsigned long long*>(sa.plan);
     n = nfiles + uint32_t(used < sa.cap ? used : sa.cap);
+    if (used) plan = sa.plan;
   }
-  // kind: 0 a file, 1 an ext unit, 2 a split file (nothing to do: len 0, no output)
+  // kind: 0 a file, 1 an ext unit (a whole segment), 2 a split file's ragged head
   auto unit = [&](uint32_t u, uint32_t& kind) -> Desc {
     if (u >= nfiles) {
       kind = 1u;
-      return sa.ext[u - nfiles];
+      return reinterpret_cast<const Desc*>(plan + split_off_ext(nfiles, sa.cap))[u - nfiles];
     }
     Desc d = desc[u];
     kind = 0u;
-    if (sa.base && sa.base[u] != kNoSplit) {
+    if (plan && reinterpret_cast<const uint32_t*>(plan + split_off_base())[u] != kNoSplit) {
       kind = 2u;
-      d.len = 0u;
+      d.len -= ((d.len - 1u) / kSegBytes) * kSegBytes;
     }
     return d;
   };
@@ -892,8 +894,10 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
     const uint32_t crc = finish_file<RUN, S8>(lds_tables, lb, g, h, c, lane);
     if (lane == 0) {
       if (kcur == 1u) {
-        sa.ext_crc[f - nfiles] = crc;
-      } else if (kcur == 0u) {
+        reinterpret_cast<uint32_t*>(plan + split_off_ext_crc(nfiles))[f - nfiles] = crc;
+      } else if (kcur == 2u) {
+        reinterpret_cast<uint32_t*>(plan + split_off_head(nfiles))[f] = crc;
+      } else {
         if (out_crc) out_crc[f] = crc;
         if (MODE == 1) {
           const bool ok = crc == cur.aux;
@@ -916,15 +920,16 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
 }
 
 // Split plan (tfs_crc_device.h SplitArgs): one thread per file.  A file longer
-// than kSplitMin becomes K = ceil(len / kSegBytes) ext units -- a ragged head of
-// len - (K-1)*kSegBytes bytes carrying the file's seed, then K-1 whole segments
-// -- reserved as one range per workgroup (one atomic per 256 files).  A
+// than kSplitMin keeps its ragged head (len - K*kSegBytes bytes, K = (len-1) /
+// kSegBytes, with its seed) as its own unit and gets K ext units for its whole
+// segments, reserved as one range per workgroup (one atomic per 256 files).  A
 // workgroup whose range would pass `cap` leaves its files whole (and writes
 // empty units into the part of its range below cap, so every unit the main
 // kernel takes is valid).
 template <int MODE>
 __global__ void __launch_bounds__(256) split_plan_kernel(const Desc* __restrict__ desc, uint32_t n, uint32_t vseed,
                                                          SplitArgs sa) {
+  (void)vseed;  // the head keeps the file's seed: the main kernel checksums it in place
   __shared__ uint32_t wsum[4];
   __shared__ unsigned long long blk_base;
   const uint32_t i = blockIdx.x * 256u + threadIdx.x;
@@ -932,7 +937,7 @@ __global__ void __launch_bounds__(256) split_plan_kernel(const Desc* __restrict_
   const uint32_t w = threadIdx.x / kWave;
   Desc d{0, 0, 0};
   if (i < n) d = desc[i];
-  const uint32_t K = (i < n && d.len > kSplitMin) ? (d.len - 1u) / kSegBytes + 1u : 0u;
+  const uint32_t K = (i < n && d.len > kSplitMin) ? (d.len - 1u) / kSegBytes : 0u;  // whole segments after the head
   uint32_t x = K;  // inclusive scan over the wave
 #pragma unroll
   for (int o = 1; o < kWave; o <<= 1) {
@@ -947,19 +952,20 @@ __global__ void __launch_bounds__(256) split_plan_kernel(const Desc* __restrict_
     before += k < w ? wsum[k] : 0u;
     total += wsum[k];
   }
-  if (threadIdx.x == 0) blk_base = total ? atomicAdd(sa.used, (unsigned long long)total) : 0ull;
+  if (threadIdx.x == 0)
+    blk_base = total ? atomicAdd(reinterpret_cast<unsigned long long*>(sa.plan), (unsigned long long)total) : 0ull;
   __syncthreads();
   const unsigned long long b0 = blk_base;
   const bool fits = b0 + total <= sa.cap;
   const unsigned long long my = b0 + before + (x - K);
-  if (i < n) sa.base[i] = (K && fits) ? uint32_t(my) : kNoSplit;
+  if (i < n) reinterpret_cast<uint32_t*>(sa.plan + split_off_base())[i] = (K && fits) ? uint32_t(my) : kNoSplit;
   if (!K) return;
+  Desc* ext = reinterpret_cast<Desc*>(sa.plan + split_off_ext(n, sa.cap));
   if (fits) {
-    const uint32_t head = d.len - (K - 1u) * kSegBytes;
-    sa.ext[my] = Desc{d.offset, head, MODE == 0 ? d.aux : vseed};
-    for (uint32_t j = 1; j < K; ++j) sa.ext[my + j] = Desc{d.offset + head + uint64_t(j - 1u) * kSegBytes, kSegBytes, 0u};
+    const uint32_t head = d.len - K * kSegBytes;  // checksummed in the file's own place by the main kernel
+    for (uint32_t j = 0; j < K; ++j) ext[my + j] = Desc{d.offset + head + uint64_t(j) * kSegBytes, kSegBytes, 0u};
   } else {
-    for (unsigned long long u = my; u < my + K && u < sa.cap; ++u) sa.ext[u] = Desc{0, 0, 0};
+    for (unsigned long long u = my; u < my + K && u < sa.cap; ++u) ext[u] = Desc{0, 0, 0};
   }
 }
 
@@ -971,16 +977,20 @@ __global__ void __launch_bounds__(256) split_fold_kernel(const Desc* __restrict_
                                                          const Tables* __restrict__ tg, SplitArgs sa,
                                                          uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad) {
   __shared__ uint32_t T[uint32_t(kShiftChunks) * 32u];
+  if (*reinterpret_cast<const unsigned long long*>(sa.plan) == 0ull) return;  // nothing was split
+  const uint32_t* base = reinterpret_cast<const uint32_t*>(sa.plan + split_off_base());
+  const uint32_t* head_crc = reinterpret_cast<const uint32_t*>(sa.plan + split_off_head(n));
+  const uint32_t* ext_crc = reinterpret_cast<const uint32_t*>(sa.plan + split_off_ext_crc(n));
   for (uint32_t k = threadIdx.x; k < uint32_t(kShiftChunks) * 32u; k += blockDim.x) T[k] = (&tg->seg_shift[0][0])[k];
   __syncthreads();
   uint32_t bad = 0;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint32_t b = sa.base[i];
+    const uint32_t b = base[i];
     if (b == kNoSplit) continue;
     const Desc d = desc[i];
-    const uint32_t K = (d.len - 1u) / kSegBytes + 1u;
-    uint32_t c = sa.ext_crc[b];
-    for (uint32_t j = 1; j < K; ++j) c = shift5(T, 0u, c) ^ sa.ext_crc[b + j];
+    const uint32_t K = (d.len - 1u) / kSegBytes;
+    uint32_t c = head_crc[i];
+    for (uint32_t j = 0; j < K; ++j) c = shift5(T, 0u, c) ^ ext_crc[b + j];
     if (out_crc) out_crc[i] = c;
     if (MODE == 1) {
       const bool ok = c == d.aux;
@@ -2112,8 +2122,8 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
   const dim3 grid(grid_for(n, cap)), block(kBlock);
   // Split files (tfs_crc_device.h): the plan before the main kernel, the fold
   // after it, all on `stream`; the completion-flag form (done_flag) never splits.
-  const SplitArgs sa = split && !done_flag ? *split : SplitArgs{nullptr, nullptr, nullptr, nullptr, 0u};
-  if (sa.base) {
+  const SplitArgs sa = split && !done_flag ? *split : SplitArgs{nullptr, 0u};
+  if (sa.plan) {
     hipLaunchKernelGGL((split_plan_kernel<MODE>), dim3((n + 255u) / 256u), dim3(256), 0, stream, desc, n, vseed, sa);
     if (const hipError_t e = hipGetLastError()) return e;
   }
@@ -2129,7 +2139,7 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
                        grid, block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq,
                        sa);
   if (const hipError_t e = hipGetLastError()) return e;
-  if (sa.base) {
+  if (sa.plan) {
     const uint32_t fg = (n + 255u) / 256u;
     hipLaunchKernelGGL((split_fold_kernel<MODE>), dim3(fg < 1024u ? fg : 1024u), dim3(256), 0, stream, desc, n, tg, sa,
                        out_crc, out_ok, n_bad);

@@ -7,7 +7,12 @@ interleaved round by round, each timed with its own HIP events on its own
 context's stream.  Process-to-process placement noise (+-3 % on this pool)
 drops out.
 
-  python tools/ab_inproc.py OTHER_SO [ROUNDS] [mode]   mode: verify (default) | zipf
+  python tools/ab_inproc.py OTHER_SO[,OTHER_SO...] [ROUNDS] [mode]   mode: verify (default) | zipf
+
+A second entry, "product_nosplit", is the product library's SAME context with
+file splitting switched off (tfs_crc32_set_split) for its rounds, so split on
+vs off shares one stream and one scratch set: the per-context placement noise
+(up to +-2 % between two contexts of one library) drops out of that pair.
 """
 import ctypes
 import json
@@ -43,7 +48,11 @@ def main():
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     mode = sys.argv[3] if len(sys.argv) > 3 else "verify"
     ctx = crc.Context(0)
-    libs = {"product": bind(crc.LIB_PATH), "other": bind(os.path.abspath(other))}
+    prod = bind(crc.LIB_PATH)
+    prod[0].tfs_crc32_set_split.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    libs = {"product": prod, "product_nosplit": prod}
+    for i, o in enumerate(other.split(",")):
+        libs["other%d" % i] = bind(os.path.abspath(o))
     if mode == "zipf":
         blocks = bench.zipf_sizes(42, 1024)
         offs, lens = [], []
@@ -80,6 +89,8 @@ def main():
     times = {k: [] for k in libs}
     for r in range(rounds):
         for name, (L, h) in libs.items():
+            if name.startswith("product"):
+                assert L.tfs_crc32_set_split(h, int(name == "product")) == 0
             e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
             L.tfs_crc32_event_create(h, ctypes.byref(e0))
             L.tfs_crc32_event_create(h, ctypes.byref(e1))
