@@ -636,7 +636,14 @@ int files_launch(tfs_crc_ctx* ctx, hipStream_t st, int mode, const uint8_t* base
 // (Caller holds ctx->mu.)  Launch the resident kernel unless one is running.
 // Only one is ever in flight: a new one is launched only after the event behind
 // the previous one has completed, i.e. every workgroup of it has left.
-int resident_ensure_running(tfs_crc_ctx* ctx) {
+// `post`: called right after a post -- while the running launch's last
+// workgroup has not signed out through ResHost::left it is taken as running with
+// no HIP call (the host reads its own memory); a launch that ended in a fault is
+// still found by wait_resident's periodic event query.
+int resident_ensure_running(tfs_crc_ctx* ctx, bool post = false) {
+  if (ctx->res_running && post &&
+      __atomic_load_n(&ctx->res_host->left, __ATOMIC_ACQUIRE) != ctx->res_gen.load(std::memory_order_relaxed))
+    return TFS_SUCCESS;
   if (ctx->res_running) {
     const hipError_t e = hipEventQuery(ctx->res_event);
     if (e == hipErrorNotReady) return TFS_SUCCESS;
@@ -681,7 +688,7 @@ int resident_post(tfs_crc_ctx* ctx, Slot& s, int mode, const uint8_t* zb, const 
   ctx->res_files += n;
   ctx->res_last_post_ns.store(now_ns(), std::memory_order_relaxed);
   __atomic_store_n(&H->published, uint64_t(ctx->res_published), __ATOMIC_RELEASE);
-  const int rc = resident_ensure_running(ctx);
+  const int rc = resident_ensure_running(ctx, true);
   // A launch that fails leaves units published that no kernel may ever take (or
   // one taking them late, into result words since reused): the context stops
   // using the ring and launches from then on.

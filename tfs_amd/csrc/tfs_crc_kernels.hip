@@ -1226,12 +1226,14 @@ __global__ void __launch_bounds__(kBlock) crc_resident_kernel(const Tables* __re
       const uint32_t want = blockIdx.x + done * gridDim.x;  // this workgroup's next unit
       uint32_t go = 0;
       for (uint32_t it = 0;; ++it) {
+        // Both loads in flight together: one PCIe round trip per poll.
         const uint64_t ps = ld_sys64(&hs->published);  // published | stop << 32
+        const uint32_t ex = __hip_atomic_load(&dstate[kResExitLine], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (int32_t(uint32_t(ps) - want) > 0) {
           go = 1;
           break;
         }
-        if (__hip_atomic_load(&dstate[kResExitLine], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) break;
+        if (ex == gen) break;
         const uint64_t now = wall_clock64();
         if (uint32_t(ps) != seen) {  // units posted (to any workgroup): not idle
           seen = uint32_t(ps);
@@ -1244,11 +1246,14 @@ __global__ void __launch_bounds__(kBlock) crc_resident_kernel(const Tables* __re
         __builtin_amdgcn_s_sleep(1);
       }
       if (go) {
+        // The unit's four words are read in one PCIe round trip (all four loads
+        // issued before the first is used), not four.
         const uint64_t* u = reinterpret_cast<const uint64_t*>(&hs->units[want % kResUnits]);
-        claim[1] = ld_sys64(u);
-        claim[2] = ld_sys64(u + 1);
-        claim[3] = ld_sys64(u + 2);
-        seq = uint32_t(ld_sys64(u + 3));
+        const uint64_t w0 = ld_sys64(u), w1 = ld_sys64(u + 1), w2 = ld_sys64(u + 2), w3 = ld_sys64(u + 3);
+        claim[1] = w0;
+        claim[2] = w1;
+        claim[3] = w2;
+        seq = uint32_t(w3);
         ++done;
       }
       claim[0] = go;
