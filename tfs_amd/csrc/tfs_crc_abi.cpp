@@ -15,12 +15,15 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <vector>
 
 #include "../../include/tfs_crc.h"
 #include "crc_math.h"
+#include "pin_registry.h"
 #include "tfs_crc_device.h"
 
 namespace tfscrc {
@@ -64,6 +67,43 @@ hipError_t launch_resident(const Tables* tg, const ResHost* hs, uint32_t* dstate
                            uint32_t life_ticks, uint32_t gen, hipStream_t stream);
 }  // namespace tfscrc
 
+namespace tfscrc {
+
+namespace {
+struct PinRange {
+  uintptr_t end;
+  uintptr_t dev;
+};
+std::shared_mutex g_pin_mu;
+std::map<uintptr_t, PinRange> g_pins;  // keyed by the allocation's first byte
+}  // namespace
+
+void pin_register(void* host, size_t bytes, void* dev) {
+  if (!host || !dev) return;
+  const uintptr_t h = reinterpret_cast<uintptr_t>(host);
+  std::unique_lock<std::shared_mutex> g(g_pin_mu);
+  g_pins[h] = PinRange{h + (bytes ? bytes : 1), reinterpret_cast<uintptr_t>(dev)};
+}
+
+void pin_unregister(void* host) {
+  if (!host) return;
+  std::unique_lock<std::shared_mutex> g(g_pin_mu);
+  g_pins.erase(reinterpret_cast<uintptr_t>(host));
+}
+
+bool pin_lookup(const void* p, void** dev) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  std::shared_lock<std::shared_mutex> g(g_pin_mu);
+  auto it = g_pins.upper_bound(a);
+  if (it == g_pins.begin()) return false;
+  --it;
+  if (a >= it->second.end) return false;
+  if (dev) *dev = reinterpret_cast<void*>(it->second.dev + (a - it->first));
+  return true;
+}
+
+}  // namespace tfscrc
+
 static_assert(sizeof(tfs_crc_desc) == 16 && sizeof(tfs_crc_vdesc) == 16, "descriptor ABI");
 static_assert(sizeof(tfs_raw_meta) == sizeof(tfscrc::RawMeta), "RawMeta ABI");
 static_assert(sizeof(tfs_file_info) == 36, "FileInfo ABI");
@@ -105,9 +145,7 @@ struct PinBuf {
   bool coherent = false;
   hipError_t reserve(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
-    if (p) (void)hipHostFree(p);
-    p = nullptr;
-    cap = 0;
+    release();
     size_t want = std::max<size_t>(bytes, 4096);
     want = (want + 0xFFFF) & ~size_t(0xFFFF);
     hipError_t e = hipHostMalloc(&p, want, coherent ? hipHostMallocCoherent : hipHostMallocDefault);
@@ -120,11 +158,15 @@ struct PinBuf {
         dev = nullptr;
         (void)hipGetLastError();
       }
+      pin_register(p, cap, dev);
     }
     return e;
   }
   void release() {
-    if (p) (void)hipHostFree(p);
+    if (p) {
+      pin_unregister(p);
+      (void)hipHostFree(p);
+    }
     p = nullptr;
     dev = nullptr;
     cap = 0;
@@ -316,12 +358,23 @@ void build_tables(Tables* t) {
 }
 
 bool is_pinned_host(const void* p) {
+  if (pin_lookup(p, nullptr)) return true;  // allocated here: no runtime query
   hipPointerAttribute_t a;
   if (hipPointerGetAttributes(&a, p) != hipSuccess) {
     (void)hipGetLastError();
     return false;
   }
   return a.type == hipMemoryTypeHost;
+}
+
+// Device-visible address of page-locked host address p: the registry, else the
+// runtime.
+bool host_dev_ptr(const void* p, void** dev) {
+  if (pin_lookup(p, dev)) return true;
+  if (hipHostGetDevicePointer(dev, const_cast<void*>(p), 0) == hipSuccess) return true;
+  (void)hipGetLastError();
+  *dev = nullptr;
+  return false;
 }
 
 // Range of base actually touched by n descriptors (offset, len pairs).
@@ -821,7 +874,7 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
     memcpy(s.h_desc.p, d, size_t(n) * sizeof(Desc));
     void *zb = nullptr, *zd = s.h_desc.dev, *zcrc = s.h_crc.dev, *zok = s.h_ok.dev, *zflag = s.h_flag.dev;
     if (host_span == s.h_data.p) zb = s.h_data.dev;
-    else if (hipHostGetDevicePointer(&zb, host_span, 0) != hipSuccess) zb = nullptr;
+    else if (!host_dev_ptr(host_span, &zb)) zb = nullptr;
     if (zb && zd && zcrc && zok && zflag) {
       s.seq = g_flag_seq.fetch_add(1) + 1u;
       if (s.seq == 0) s.seq = g_flag_seq.fetch_add(1) + 1u;  // 0 is the words' initial value
@@ -1264,8 +1317,7 @@ int tfs_block_verify(tfs_crc_ctx* ctx, const void* image, uint64_t image_len, co
   // whole-block copy.  Pageable images are staged.
   const uint8_t* d_base = nullptr;
   void* zc = nullptr;
-  if (ctx->variant != kVariantDmaCompact && is_pinned_host(image) &&
-      hipHostGetDevicePointer(&zc, const_cast<void*>(image), 0) == hipSuccess) {
+  if (ctx->variant != kVariantDmaCompact && is_pinned_host(image) && host_dev_ptr(image, &zc)) {
     d_base = static_cast<const uint8_t*>(zc);
   } else {
     (void)hipGetLastError();
@@ -1357,11 +1409,7 @@ static int compact_enqueue(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job
   }
   void* zc_src = nullptr;
   void* zc_dst = nullptr;
-  if (zc && (hipHostGetDevicePointer(&zc_src, const_cast<void*>(job->src_image), 0) != hipSuccess ||
-             hipHostGetDevicePointer(&zc_dst, job->dest_image, 0) != hipSuccess)) {
-    (void)hipGetLastError();
-    zc = false;
-  }
+  if (zc && (!host_dev_ptr(job->src_image, &zc_src) || !host_dev_ptr(job->dest_image, &zc_dst))) zc = false;
   uint8_t* da = static_cast<uint8_t*>(cs.d_aux.p);
   int64_t* d_doff = reinterpret_cast<int64_t*>(da);
   RawMeta* d_metas = reinterpret_cast<RawMeta*>(da + ob);
@@ -1831,12 +1879,16 @@ int tfs_crc32_host_malloc_pinned(tfs_crc_ctx* ctx, uint64_t bytes, void** h_ptr)
   *h_ptr = nullptr;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   HIP_TRY(ctx, hipHostMalloc(h_ptr, bytes ? bytes : 1, hipHostMallocDefault));
+  void* dev = nullptr;
+  if (hipHostGetDevicePointer(&dev, *h_ptr, 0) == hipSuccess) pin_register(*h_ptr, bytes ? bytes : 1, dev);
+  else (void)hipGetLastError();
   return TFS_SUCCESS;
 }
 
 int tfs_crc32_host_free_pinned(tfs_crc_ctx* ctx, void* h_ptr) {
   if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
   if (!h_ptr) return TFS_SUCCESS;
+  pin_unregister(h_ptr);
   HIP_TRY(ctx, hipHostFree(h_ptr));
   return TFS_SUCCESS;
 }
@@ -1844,6 +1896,7 @@ int tfs_crc32_host_free_pinned(tfs_crc_ctx* ctx, void* h_ptr) {
 int tfs_crc32_host_device_ptr(tfs_crc_ctx* ctx, const void* h_ptr, void** d_ptr) {
   if (!ctx || !h_ptr || !d_ptr) return TFS_EXIT_PARAMETER_ERROR;
   *d_ptr = nullptr;
+  if (pin_lookup(h_ptr, d_ptr)) return TFS_SUCCESS;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   HIP_TRY(ctx, hipHostGetDevicePointer(d_ptr, const_cast<void*>(h_ptr), 0));
   return TFS_SUCCESS;

@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "../../include/tfs_crc.h"
+#include "pin_registry.h"
 
 namespace {
 
@@ -227,6 +228,8 @@ int tfs_crc_group_host_malloc(tfs_crc_group* g, uint32_t i, uint64_t bytes, void
   run_on_members(one, [&](uint32_t) {
     hipError_t e = hipSetDevice(m->device);
     if (e == hipSuccess) e = hipHostMalloc(p, bytes ? bytes : 1, hipHostMallocNumaUser | hipHostMallocPortable);
+    void* dev = nullptr;
+    if (e == hipSuccess && hipHostGetDevicePointer(&dev, *p, 0) == hipSuccess) tfscrc::pin_register(*p, bytes ? bytes : 1, dev);
     if (e != hipSuccess) {
       (void)hipGetLastError();
       *p = nullptr;
@@ -239,6 +242,7 @@ int tfs_crc_group_host_malloc(tfs_crc_group* g, uint32_t i, uint64_t bytes, void
 
 int tfs_crc_group_host_free(tfs_crc_group* g, uint32_t i, void* p) {
   if (!g || i >= g->members.size()) return TFS_EXIT_PARAMETER_ERROR;
+  if (p) tfscrc::pin_unregister(p);
   if (p && hipHostFree(p) != hipSuccess) return TFS_CRC_EXIT_DEVICE_ERROR;
   return TFS_SUCCESS;
 }

@@ -112,9 +112,15 @@ def main():
             raise SystemExit("ab_compact: variant %d on %s reports bad records" % (v, js))
     times = {"%d_%s" % c: [] for c in cases}
     times["copy_52114"] = []
-    copies = [53104, 53116, 53004, 53016]  # wave-contiguous chunks: nt / plain stores, 64 / 256 KiB
-    for pat in copies:
-        times["copy_%d" % pat] = []
+    # wave-contiguous chunks: nt / plain stores, 64 / 256 KiB (256 workgroups); AB_COPIES
+    # adds "pattern:grid" pairs (e.g. 52114:8192, the grid-stride copy over 8,192 workgroups)
+    copies = [(53104, 0), (53116, 0), (53004, 0), (53016, 0)]
+    for x in os.environ.get("AB_COPIES", "").split(","):
+        if x:
+            pg = x.split(":")
+            copies.append((int(pg[0]), int(pg[1]) if len(pg) > 1 else 0))
+    for pat, grid in copies:
+        times["copy_%d%s" % (pat, "_g%d" % grid if grid else "")] = []
     for v in vcases:
         d_bad.zero()
         ctxs[v].blocks_verify_device(img, total, d_allj, n, None, d_vst, d_bad)
@@ -152,15 +158,15 @@ def main():
         e1.record()
         ctx.sync()
         times["copy_52114"].append(e0.elapsed_ms(e1) / 3)
-        for pat in copies:
+        for pat, grid in copies:
             e0, e1 = crc.Event(ctx), crc.Event(ctx)
-            ctx.membench_device(pat, img, None, 0, cb, d_dst)
+            ctx.membench_device(pat, img, None, 0, cb, d_dst, grid=grid)
             e0.record()
             for _ in range(3):
-                ctx.membench_device(pat, img, None, 0, cb, d_dst)
+                ctx.membench_device(pat, img, None, 0, cb, d_dst, grid=grid)
             e1.record()
             ctx.sync()
-            times["copy_%d" % pat].append(e0.elapsed_ms(e1) / 3)
+            times["copy_%d%s" % (pat, "_g%d" % grid if grid else "")].append(e0.elapsed_ms(e1) / 3)
         print("round %d done" % r, file=sys.stderr, flush=True)
     res = {}
     for name, v in times.items():
