@@ -621,6 +621,35 @@ def test_small_pinned_batches_read_in_place(gpu_ctx, oracle):
         pin.free()
 
 
+def test_pinned_registry_interior_bases_and_recycled_buffers(gpu_ctx, oracle):
+    """Page-locked buffers the library allocated are found through its own registry
+    (no HIP runtime query): a base in the middle of one is read in place at the right
+    device address, and buffers freed and allocated again (maybe at the same address,
+    with another size) are looked up afresh; pageable copies of the same bytes agree."""
+    import tfs_amd.crc as crc
+    rng = np.random.default_rng(5150)
+    for rnd, size in enumerate((1 << 20, 3 << 19, 1 << 20, 5000)):
+        pin = crc.PinnedBuffer(gpu_ctx, size)
+        try:
+            data = rng.integers(0, 256, size, dtype=np.uint8)
+            pin.array[:] = data
+            for skew in (0, 13, 4096 + 3):
+                view = pin.array[skew:]
+                n = 40
+                lens = rng.integers(0, max(2, (size - skew) // n), n).astype(np.uint32)
+                offs = np.zeros(n, np.uint64)
+                offs[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+                assert int(offs[-1] + lens[-1]) <= view.size
+                exp = np.array([ocrc(oracle, 0, view[int(o):int(o) + int(l)].tobytes()) for o, l in zip(offs, lens)],
+                               np.uint32)
+                c, ok, nb, rc = gpu_ctx.verify(view, offs, lens, exp)
+                assert (c == exp).all() and ok.all() and nb == 0 and rc == 0, (rnd, skew)
+                c2 = gpu_ctx.batch(view.copy(), offs, lens, np.zeros(n, np.uint32))
+                assert (c2 == exp).all()
+        finally:
+            pin.free()
+
+
 def test_device_resident_max_len_and_64bit_offsets(gpu_ctx, oracle):
     """Maximum sizes: one file of INT32_MAX bytes (Func::crc's `len` is int32, func.h:90)
     with a non-zero seed, a file straddling the 4 GiB offset boundary and one past 5 GiB

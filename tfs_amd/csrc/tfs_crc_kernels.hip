@@ -2408,8 +2408,50 @@ __global__ void __launch_bounds__(kBlock) membench_wg_chunk_kernel(const uint8_t
   if (acc == 0x9E3779B9u) out[0] = acc;  // keep the loads alive
 }
 
+// Calibration: copy form of the workgroup-contiguous chunks (the access shape a
+// workgroup-per-record compaction would have): chunk c to workgroup c mod G; wave
+// w copies 1 KiB stripes w, w+16, ... of it, PF in flight, nt loads and stores.
+template <int PF>
+__global__ void __launch_bounds__(kBlock) membench_wg_copy_kernel(const uint8_t* __restrict__ src,
+                                                                  uint8_t* __restrict__ dst, uint64_t nbytes,
+                                                                  uint64_t ch) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uint64_t nch = nbytes / ch;
+  const uint64_t nst = ch / 1024u;
+  const uintptr_t s = reinterpret_cast<uintptr_t>(src), d = reinterpret_cast<uintptr_t>(dst);
+  for (uint64_t c = blockIdx.x; c < nch; c += gridDim.x) {
+    const uint64_t b = c * ch + 16u * uint64_t(lane);
+    for (uint64_t st = wave; st < nst; st += 16u * PF) {
+      uint4 v[PF];
+#pragma unroll
+      for (int k = 0; k < PF; ++k) {
+        const uint64_t sk = st + 16u * uint64_t(k);
+        if (sk < nst) v[k] = ld128s<true>(s + b + 1024u * sk);
+      }
+#pragma unroll
+      for (int k = 0; k < PF; ++k) {
+        const uint64_t sk = st + 16u * uint64_t(k);
+        if (sk < nst) st128_nt(d + b + 1024u * sk, v[k]);
+      }
+    }
+  }
+}
+
 hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, uint32_t n, uint64_t nbytes,
                            uint32_t* out, unsigned grid, hipStream_t stream) {
+  if (pattern >= 57000 && pattern < 58000) {
+    // 57PCC: workgroup-contiguous chunk copy into `out`, CC = chunk in 16 KiB units, P = stripes in flight per wave
+    const int P = (pattern / 100) % 10, CC = pattern % 100;
+    const uint64_t ch = uint64_t(CC ? CC : 4) * 16384u;
+    const dim3 g(grid ? grid : kMaxGrid);
+    const uint64_t nb = nbytes / ch * ch;
+    uint8_t* d = reinterpret_cast<uint8_t*>(out);
+    if (P <= 2) hipLaunchKernelGGL(membench_wg_copy_kernel<2>, g, dim3(kBlock), 0, stream, base, d, nb, ch);
+    else if (P <= 4) hipLaunchKernelGGL(membench_wg_copy_kernel<4>, g, dim3(kBlock), 0, stream, base, d, nb, ch);
+    else hipLaunchKernelGGL(membench_wg_copy_kernel<8>, g, dim3(kBlock), 0, stream, base, d, nb, ch);
+    return hipGetLastError();
+  }
   if (pattern >= 55000 && pattern < 56000) {
     // 55PCC: workgroup-contiguous chunks, CC = chunk in 16 KiB units, P = stripes in flight per wave (1-8)
     const int P = (pattern / 100) % 10, CC = pattern % 100;
