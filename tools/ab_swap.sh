@@ -4,10 +4,11 @@
 # tfs_amd/libtfs_crc.so) must load too: abtmp/TAG/libtfs_crc.so is copied over the
 # product file before each run, TAGs alternated ROUNDS times in separate
 # processes; the product file is restored at the end.  CMD's stdout goes to
-# gpurun_out/ab_swap/TAG_ROUND.json.  Measurement only (the GPU box's scratch copy).
+# gpurun_out/ab_swap/<CMD as a name>/TAG_ROUND.json.  Measurement only (the GPU
+# box's scratch copy).
 set -euo pipefail
 ROUNDS=${1:?rounds}; TAGS=${2:?tags}; shift 2
-OUT=gpurun_out/ab_swap
+OUT="gpurun_out/ab_swap/$(echo "$*" | tr -c 'A-Za-z0-9' '_' | cut -c1-60)"
 mkdir -p "$OUT"
 cp tfs_amd/libtfs_crc.so abtmp/.product.so
 trap 'cp abtmp/.product.so tfs_amd/libtfs_crc.so' EXIT
