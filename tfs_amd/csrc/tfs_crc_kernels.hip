@@ -1496,6 +1496,56 @@ __global__ void __launch_bounds__(kBlock) compact_copy_kernel(const uint8_t* __r
   }
 }
 
+// Calibration (variants 65/66, measurement only): the record list of a device
+// compaction copied by the chunk copy's loop -- per job, bursts of 8 stripes of
+// 1 KiB (16 B per lane, nt loads and stores) over the 16-aligned body, the ragged
+// ends byte by byte; no CRC, no header rewrite, no statuses.  Needs destinations
+// congruent to their sources mod AL, bodies from AL-aligned addresses (67/68: AL
+// 128, whole lines like the kernel's anchored grid).  DYN: the product's interleaved tickets;
+// else job j -> wave j mod W (53104's order).  Where the record kernel trails the
+// chunk copy of the same bytes, this says whether the record list or the kernel's
+// own schedule costs it.
+template <bool DYN, uint32_t AL = 16>
+__global__ void __launch_bounds__(kBlock) compact_probe_copy_kernel(const uint8_t* __restrict__ src,
+                                                                    const CompactJob* __restrict__ jobs, uint32_t n,
+                                                                    uint8_t* __restrict__ dst, uint32_t* sched) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint32_t wpb = kBlock / kWave;
+  Tickets<kIL> tk;
+  tk.ctr = sched;
+  tk.n = n;
+  tk.group = blockIdx.x & 7u;
+  tk.init_static(gridDim.x * wpb, blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave));
+  if (!DYN) tk.dyn = false;
+  for (;;) {
+    const uint32_t f = tk.resolve(tk.issue(lane), lane);
+    if (f >= n) break;
+    const CompactJob j = jobs[f];
+    const uintptr_t s0 = reinterpret_cast<uintptr_t>(src) + j.src_offset;
+    const intptr_t delta = intptr_t(reinterpret_cast<uintptr_t>(dst) + j.dest_offset) - intptr_t(s0);
+    const uintptr_t s1 = s0 + uint32_t(j.size);
+    const uintptr_t a0 = (s0 + AL - 1u) & ~uintptr_t(AL - 1u), a1 = s1 & ~uintptr_t(AL - 1u);
+    for (uintptr_t i = uintptr_t(lane); i < a0 - s0; i += kWave)
+      *reinterpret_cast<uint8_t*>(s0 + i + delta) = *reinterpret_cast<const uint8_t*>(s0 + i);
+    for (uintptr_t i = uintptr_t(lane); i < s1 - a1; i += kWave)
+      *reinterpret_cast<uint8_t*>(a1 + i + delta) = *reinterpret_cast<const uint8_t*>(a1 + i);
+    for (uintptr_t o = a0; o < a1; o += 8u * 1024u) {
+      uint4 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uintptr_t q = o + 1024u * k + 16u * uint32_t(lane);
+        if (q < a1) v[k] = ld128s<true>(q);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uintptr_t q = o + 1024u * k + 16u * uint32_t(lane);
+        if (q < a1) st128_kind<1>(q + delta, u32x4{v[k].x, v[k].y, v[k].z, v[k].w});
+      }
+    }
+  }
+  if (lane == 0) launch_exit(sched, gridDim.x * wpb, nullptr, 0u);
+}
+
 // Fused compaction: one read of each live record computes its
 // payload CRC (the re-CRC verify) and, from the same registers, writes the
 // record to its new offset with offset_/size_/usize_/flag_ rewritten
@@ -1730,7 +1780,12 @@ __device__ __forceinline__ void copy_unaligned(const uint8_t* s, uint8_t* d, uin
 // CRC by copy_unaligned instead of through the chain (DIAG bit 5), 32 = byte-
 // shifted records stored as each lane's 16 bytes at their byte address instead
 // of line-aligned alignbyte chunks (DIAG bit 6), 36 = sc1 copy-through stores
-// (DIAG bit 7).  CPF: stripes in flight per wave (variants 33-35, 37: 6, 7, 8, 4).
+// (DIAG bit 7), 60/61 = static record assignment r -> wave r mod W (DIAG bit 8),
+// with / without the payload CRC steps, 62-64 = the ring refilled in bursts of
+// CPF stripes (DIAG bit 9: CPF loads out together after CPF stripes are used,
+// as the chunk copy does; 64 also skips the CRC steps and the header/tail
+// stores).  CPF: stripes in flight per wave
+// (variants 33-35, 37: 6, 7, 8, 4).
 constexpr int kCompactDiag = 4 | 8;
 template <bool WIDE, bool DPPSH = true, bool VERIFY = false, int DIAG = kCompactDiag, int CPF = kPF, int CF = 1,
           int TS = 0>
@@ -1755,6 +1810,7 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
   Tickets<kIL>& tk = fc.tk;
   fc.init(sched, n, blockIdx.x & 7u, gridDim.x * wpb,
           blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave));
+  if (DIAG & 256) tk.dyn = false;  // measurement: static record r -> wave r mod W (the chunk copy's order)
   if (CF > 1) fc.start(lane);
   uint32_t bad = 0;
   do {
@@ -1770,8 +1826,8 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
     for (;;) {
       // DIAG bit 5 (variant 31, measurement): byte-shifted records copy after the CRC (copy_unaligned)
       const bool chain_copy = !(DIAG & 32) || (st.delta & 3) == 0;
-      uint32_t c = st.g.nstripes ? lane_chain<kRun, CPF, LNT, kS8, !VERIFY, 1, DPPSH, SK, (DIAG & 2) != 0, !(DIAG & 16),
-                                            (DIAG & 64) != 0>(
+      uint32_t c = st.g.nstripes ? lane_chain<kRun, CPF, LNT, kS8, !VERIFY, (DIAG & 512) ? CPF : 1, DPPSH, SK,
+                                            (DIAG & 2) != 0, !(DIAG & 16), (DIAG & 64) != 0>(
                                      lds_tables, lb, st.g, st.h, buf, lane, junk, st.delta, chain_copy)
                                  : 0u;
       // The next record's loads go out before this one is finished.
@@ -2262,6 +2318,20 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
   else if (variant == 35) TFS_CJ(true, true, false, kCompactDiag, 8);
   else if (variant == 36) TFS_CJ(true, true, false, kCompactDiag | 128);
   else if (variant == 37) TFS_CJ(true, true, false, kCompactDiag, 4);
+  else if (variant == 60) TFS_CJ(true, true, false, kCompactDiag | 256);      // static records, product otherwise
+  else if (variant == 61) TFS_CJ(true, true, false, kCompactDiag | 256 | 2);  // static, no payload CRC steps
+  else if (variant == 62) TFS_CJ(true, true, false, kCompactDiag | 512);      // ring refilled in bursts of CPF
+  else if (variant == 63) TFS_CJ(true, true, false, kCompactDiag | 512, 8);   // bursts of 8 (the chunk copy's)
+  else if (variant == 64) TFS_CJ(true, true, false, kCompactDiag | 512 | 2 | 16, 8);  // bursts of 8, copy only
+  else if (variant >= 65 && variant <= 68)  // the record list through the chunk copy's loop (calibration)
+    hipLaunchKernelGGL((variant == 65   ? compact_probe_copy_kernel<true>
+                        : variant == 66 ? compact_probe_copy_kernel<false>
+                        : variant == 67 ? compact_probe_copy_kernel<true, 128>
+                                        : compact_probe_copy_kernel<false, 128>),
+                       grid, dim3(kBlock), 0, stream, src, jobs, n, dst, sched);
+  else if (variant == 69 || variant == 70)  // 67 over 512 / 2,048 workgroups (two resident per CU, no LDS)
+    hipLaunchKernelGGL((compact_probe_copy_kernel<true, 128>), dim3(variant == 69 ? 512 : 2048), dim3(kBlock), 0,
+                       stream, src, jobs, n, dst, sched);
   else if (variant == 39) TFS_CJ(true, true, false, kCompactDiag, kPF, 2, 0);  // chunked tickets (as crc_files 39-45)
   else if (variant == 40) TFS_CJ(true, true, false, kCompactDiag, kPF, 4, 0);
   else if (variant == 42) TFS_CJ(true, true, false, kCompactDiag, kPF, 4, 3);

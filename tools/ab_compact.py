@@ -64,7 +64,9 @@ def main():
     ctx.sync()
     for b in (d_desc, d_roff, d_len, d_crc):
         b.free()
-    live1 = np.nonzero(bench._fragmented_flags(nfiles) == 0)[0]
+    # AB_LIVE=all: every record live (a dense source, the copy's read shape)
+    live1 = (np.arange(nfiles) if os.environ.get("AB_LIVE") == "all"
+             else np.nonzero(bench._fragmented_flags(nfiles) == 0)[0])
     nl = live1.size
     bidx = np.repeat(np.arange(nblocks, dtype=np.uint64), nl)
     soff = bidx * blk + np.tile(live1.astype(np.uint64) * rec, nblocks)
@@ -88,7 +90,9 @@ def main():
     ctxs = {0: ctx}
     for v in want:
         ctxs[v] = ctx_for(v)
-    cases = [(0, "packed")] + [(v, "packed") for v in want if v not in (31, 32)] + [(0, "dst128")]
+    # 65/66: the record list through the chunk copy's loop -- destinations congruent mod 16 only
+    cases = ([(0, "packed")] + [(v, "packed") for v in want if v not in (31, 32, 65, 66, 67, 68, 69, 70)] + [(0, "dst128")] +
+             [(v, "dst128") for v in want if v in (65, 66, 67, 68, 69, 70)])
     if 31 in want or 32 in want:
         cases += [(0, "shift1")] + [(v, "shift1") for v in want if v in (31, 32)]
     # verify-on-read of every record of the resident blocks (tfs_blocks_verify_device)
@@ -103,7 +107,7 @@ def main():
     # correctness of the product cases (the diagnostic variants 26 and 30 compute
     # no CRCs / skip stores)
     for v, js in cases:
-        if v in (26, 30):
+        if v in (26, 30, 61, 64, 65, 66, 67, 68, 69, 70):
             continue
         d_bad.zero()
         ctxs[v].compact_jobs_device(img, total, jobsets[js], nj, d_dst, None, d_st, d_bad)
@@ -113,14 +117,19 @@ def main():
     times = {"%d_%s" % c: [] for c in cases}
     times["copy_52114"] = []
     # wave-contiguous chunks: nt / plain stores, 64 / 256 KiB (256 workgroups); AB_COPIES
-    # adds "pattern:grid" pairs (e.g. 52114:8192, the grid-stride copy over 8,192 workgroups)
-    copies = [(53104, 0), (53116, 0), (53004, 0), (53016, 0)]
+    # adds "pattern:grid[:dskew[:sskew]]" (e.g. 52114:8192, the grid-stride copy over 8,192
+    # workgroups; skews: bytes added to the destination / source pointers, multiples of 16)
+    copies = [(53104, 0, 0, 0), (53116, 0, 0, 0), (53004, 0, 0, 0), (53016, 0, 0, 0)]
     for x in os.environ.get("AB_COPIES", "").split(","):
         if x:
-            pg = x.split(":")
-            copies.append((int(pg[0]), int(pg[1]) if len(pg) > 1 else 0))
-    for pat, grid in copies:
-        times["copy_%d%s" % (pat, "_g%d" % grid if grid else "")] = []
+            pg = [int(v) for v in x.split(":")] + [0, 0, 0]
+            copies.append(tuple(pg[:4]))
+
+    def cname(pat, grid, dsk, ssk):
+        return "copy_%d%s%s%s" % (pat, "_g%d" % grid if grid else "", "_d%d" % dsk if dsk else "",
+                                  "_s%d" % ssk if ssk else "")
+    for c in copies:
+        times[cname(*c)] = []
     for v in vcases:
         d_bad.zero()
         ctxs[v].blocks_verify_device(img, total, d_allj, n, None, d_vst, d_bad)
@@ -158,15 +167,16 @@ def main():
         e1.record()
         ctx.sync()
         times["copy_52114"].append(e0.elapsed_ms(e1) / 3)
-        for pat, grid in copies:
+        for pat, grid, dsk, ssk in copies:
             e0, e1 = crc.Event(ctx), crc.Event(ctx)
-            ctx.membench_device(pat, img, None, 0, cb, d_dst, grid=grid)
+            nb = cb - max(dsk, ssk) // 16 * 16
+            ctx.membench_device(pat, img.ptr + ssk, None, 0, nb, d_dst.ptr + dsk, grid=grid)
             e0.record()
             for _ in range(3):
-                ctx.membench_device(pat, img, None, 0, cb, d_dst, grid=grid)
+                ctx.membench_device(pat, img.ptr + ssk, None, 0, nb, d_dst.ptr + dsk, grid=grid)
             e1.record()
             ctx.sync()
-            times["copy_%d%s" % (pat, "_g%d" % grid if grid else "")].append(e0.elapsed_ms(e1) / 3)
+            times[cname(pat, grid, dsk, ssk)].append(e0.elapsed_ms(e1) / 3 * cb / nb)
         print("round %d done" % r, file=sys.stderr, flush=True)
     res = {}
     for name, v in times.items():
