@@ -2220,12 +2220,13 @@ def bench_loopback(args):
     # preallocates its blocks), so the final verify reads the block in place.
     pool = ds.BlockImagePool(ctx, 2, n * (L + FILEINFO) + 4096)
 
-    # One CloseBatcher per thread count, created once (DataService::initialize).
-    # Batches of a quarter of the closing threads (2 of 8, 4 of 64): several
-    # batches are in flight at once, their round trips overlapping; with the
-    # resident kernel a batch costs no launch, so smaller batches pay
-    # (tools/loopback_probe.py, profiles/r02/resident/loopback_probe.json).
-    close_batch = {8: 2, 64: 4}
+    # One CloseBatcher per thread count, created once (DataService::initialize),
+    # with the harness's rule (CloseBatcher::batch_for): one lease per batch up to
+    # 8 threads, threads/16 beyond (4 of 64).  Several batches are in flight at
+    # once, their round trips overlapping; with the resident kernel a batch costs
+    # no launch, so small batches pay (tools/loopback_probe.py,
+    # profiles/r03/s2/loopback_batches/).
+    close_batch = {8: 1, 64: 4}
     batchers = {t: ds.CloseBatcher(ctx, max_batch=b, max_wait_us=100) for t, b in close_batch.items()}
 
     def gpu_once(threads=8):

@@ -208,7 +208,7 @@ struct Slot {
 std::atomic<uint32_t> g_flag_seq{0};
 
 constexpr int kSlots = 4;
-constexpr int kSyncSlots = 8;
+constexpr int kSyncSlots = 16;  // synchronous host calls in flight at once (CloseBatcher kMaxInFlight)
 
 struct CompactSlot {
   hipStream_t stream = nullptr;

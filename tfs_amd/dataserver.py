@@ -56,6 +56,7 @@ def lib():
             "tfs_ds_block_metas": (ctypes.c_int, [vp, vp, vp, u32]),
             "tfs_ds_close_write_file": (ctypes.c_int, [vp, u64, u32, vp]),
             "tfs_ds_batcher_new": (vp, [vp, u32, ctypes.c_int]),
+            "tfs_ds_batcher_new2": (vp, [vp, u32, ctypes.c_int, ctypes.c_int]),
             "tfs_ds_batcher_free": (None, [vp]),
             "tfs_ds_batcher_batches": (u64, [vp]),
             "tfs_ds_batcher_close": (ctypes.c_int, [vp, vp, u64, u32, vp]),
@@ -239,8 +240,11 @@ class LogicBlock:
 class CloseBatcher:
     """Batches close_write_file CRC checks from many threads into one GPU verify."""
 
-    def __init__(self, ctx, max_batch=64, max_wait_us=200):
-        self.h = lib().tfs_ds_batcher_new(_ctx(ctx), max_batch, max_wait_us)
+    def __init__(self, ctx, max_batch=64, max_wait_us=200, in_flight=None):
+        if in_flight is None:
+            self.h = lib().tfs_ds_batcher_new(_ctx(ctx), max_batch, max_wait_us)
+        else:  # batches in use at once, 1..16 (default 8)
+            self.h = lib().tfs_ds_batcher_new2(_ctx(ctx), max_batch, max_wait_us, in_flight)
 
     def close(self, block, file_id, client_crc, df):
         return lib().tfs_ds_batcher_close(self.h, block.h, file_id, client_crc, df.h)

@@ -78,6 +78,10 @@ int tfs_ds_close_write_file(void* block, uint64_t file_id, uint32_t client_crc, 
 void* tfs_ds_batcher_new(tfs_crc_ctx* ctx, uint32_t max_batch, int max_wait_us) {
   return new CloseBatcher(ctx, max_batch, max_wait_us);
 }
+// in_flight: batches in use at once (1..16; the constructor's default is 8).
+void* tfs_ds_batcher_new2(tfs_crc_ctx* ctx, uint32_t max_batch, int max_wait_us, int in_flight) {
+  return new CloseBatcher(ctx, max_batch, max_wait_us, in_flight);
+}
 void tfs_ds_batcher_free(void* b) { delete static_cast<CloseBatcher*>(b); }
 uint64_t tfs_ds_batcher_batches(void* b) { return static_cast<CloseBatcher*>(b)->batches(); }
 int tfs_ds_batcher_close(void* batcher, void* block, uint64_t file_id, uint32_t client_crc, void* df) {
@@ -162,7 +166,7 @@ int tfs_ds_loopback_block_with(tfs_crc_ctx* ctx, void* batcher, const char* payl
   const auto t_begin = now();
   {
     std::unique_ptr<CloseBatcher> own;
-    if (!batcher) own.reset(new CloseBatcher(ctx, size_t(nthreads), 100));
+    if (!batcher) own.reset(new CloseBatcher(ctx, CloseBatcher::batch_for(size_t(nthreads)), 100));
     CloseBatcher& bat = batcher ? *static_cast<CloseBatcher*>(batcher) : *own;
     std::vector<std::thread> workers;
     for (int t = 0; t < nthreads; ++t)
@@ -225,7 +229,7 @@ int tfs_ds_close_latency(tfs_crc_ctx* ctx, int nleases, int iters, int32_t len, 
   blk.reserve(total);
   std::atomic<int> err{0};
   {
-    CloseBatcher batcher(ctx, size_t(nleases), 100);
+    CloseBatcher batcher(ctx, CloseBatcher::batch_for(size_t(nleases)), 100);
     std::vector<std::thread> workers;
     for (int t = 0; t < nleases; ++t)
       workers.emplace_back([&, t] {
@@ -270,7 +274,7 @@ int tfs_ds_close_stream(tfs_crc_ctx* ctx, int nleases, int32_t len, const volati
   std::atomic<int> err{0};
   std::atomic<uint64_t> done{0};
   {
-    CloseBatcher batcher(ctx, size_t(nleases), 100);
+    CloseBatcher batcher(ctx, CloseBatcher::batch_for(size_t(nleases)), 100);
     std::vector<std::thread> workers;
     for (int t = 0; t < nleases; ++t)
       workers.emplace_back([&, t] {

@@ -323,13 +323,15 @@ void spin_until(P pred) {
 }
 }  // namespace
 
-CloseBatcher::CloseBatcher(tfs_crc_ctx* ctx, size_t max_batch, int max_wait_us)
+CloseBatcher::CloseBatcher(tfs_crc_ctx* ctx, size_t max_batch, int max_wait_us, int in_flight)
     : ctx_(ctx), max_batch_(max_batch ? max_batch : 1), max_wait_us_(max_wait_us),
       gather_cap_(std::min<size_t>(std::max<size_t>(max_batch_ * (256u << 10), 4u << 20), 16u << 20)),
+      nbatches_(std::min(std::max(in_flight, 1), kMaxInFlight)),
+      batches_buf_(new Batch[size_t(nbatches_)]),
       trace_(getenv("TFS_DS_TRACE") != nullptr) {
   // The gather buffers are page-locked once, here (DataService::initialize),
   // never on a close.
-  for (Batch& b : batches_buf_) {
+  for (Batch& b : all_batches()) {
     void* p = nullptr;
     if (tfs_crc32_host_malloc_pinned(ctx_, gather_cap_, &p) == TFS_SUCCESS) {
       b.gather = static_cast<char*>(p);
@@ -344,7 +346,7 @@ CloseBatcher::CloseBatcher(tfs_crc_ctx* ctx, size_t max_batch, int max_wait_us)
 }
 
 CloseBatcher::~CloseBatcher() {
-  for (Batch& b : batches_buf_)
+  for (Batch& b : all_batches())
     if (b.gather && b.fallback.empty()) tfs_crc32_host_free_pinned(ctx_, b.gather);
   if (getenv("TFS_DS_TRACE"))
     fprintf(stderr,
@@ -357,7 +359,7 @@ CloseBatcher::~CloseBatcher() {
 
 CloseBatcher::Batch* CloseBatcher::take_batch(std::unique_lock<std::mutex>& lk) {
   for (;;) {
-    for (Batch& b : batches_buf_) {
+    for (Batch& b : all_batches()) {
       if (!b.free) continue;
       b.free = false;
       b.n = 0;

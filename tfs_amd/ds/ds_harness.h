@@ -12,6 +12,7 @@
 //   BlockCrcChecker       src/dataserver/block_checker.cpp:58-182, block_status.h:40-52
 //   compact_block         src/dataserver/task.cpp:713-836 (+ re-CRC verify)
 #pragma once
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -191,19 +192,26 @@ int close_write_file(const CloseFileInfo& info, DataFile& df, LogicBlockImage& b
 // zero-copy launch over the page-locked gather buffer).  Each member copies its
 // own payload into the gather buffer (the copies run side by side) and waits
 // spinning for the verdict -- no hand-off thread, no condition-variable wake-up
-// on the critical path.  Up to kBatches batches are in use at once, so the next
-// batch forms while one is on the GPU.  Each member then gets the status
+// on the critical path.  Up to `in_flight` batches (default kBatches) are in use
+// at once, so the next batch forms while one is on the GPU.  Each member then gets the status
 // close_write_file would have returned and persists its own record.  Payloads
 // larger than kMaxBatched take the unbatched close.
 class CloseBatcher {
  public:
-  CloseBatcher(tfs_crc_ctx* ctx, size_t max_batch, int max_wait_us);
+  CloseBatcher(tfs_crc_ctx* ctx, size_t max_batch, int max_wait_us, int in_flight = kBatches);
   ~CloseBatcher();
   // Blocks until this close has been checked (and persisted on success).
   int close(const CloseFileInfo& info, DataFile& df, LogicBlockImage& block);
   uint64_t batches() const { return batches_.load(); }
 
+  // Leases per batch for `leases` closing threads: with the resident kernel a
+  // batch costs no launch, so up to 8 threads close one file per batch (10.4 vs
+  // 9.5 GiB/s in configs[0] against batches of 2 on one box; 9.1 vs 8.1 on
+  // another); more threads batch leases/16 (64 -> 4: 9.1-10.4 GiB/s against 8.1-10.3
+  // for 2 and 8.4-9.6 for 8), tools/loopback_probe.py, DESIGN.md §5.2.
+  static size_t batch_for(size_t leases) { return leases <= 8 ? 1 : std::max<size_t>(1, leases / 16); }
   static constexpr int kBatches = 8;
+  static constexpr int kMaxInFlight = 16;  // the context's synchronous slots (tfs_crc_abi.cpp kSyncSlots)
   static constexpr int32_t kMaxBatched = 2 * 1024 * 1024;  // DataFile's in-memory limit (data_file.h:78)
 
  private:
@@ -232,7 +240,14 @@ class CloseBatcher {
   size_t gather_cap_;  // per batch: max_batch x 256 KiB, within [4 MiB, 16 MiB]
   std::mutex mu_;
   std::condition_variable free_cv_;
-  Batch batches_buf_[kBatches];
+  int nbatches_;
+  std::unique_ptr<Batch[]> batches_buf_;
+  struct Span {
+    Batch *b, *e;
+    Batch* begin() const { return b; }
+    Batch* end() const { return e; }
+  };
+  Span all_batches() { return Span{batches_buf_.get(), batches_buf_.get() + nbatches_}; }
   Batch* cur_ = nullptr;  // the batch taking members (under mu_)
   std::atomic<uint64_t> batches_{0};
   std::atomic<int64_t> verify_us_{0};  // TFS_DS_TRACE diagnostics

@@ -29,9 +29,14 @@ def main():
     pay = synth_bytes(0x9E3779B97F4A7C15, n * L)
     client = ctx.batch(pay, np.arange(n, dtype=np.uint64) * L, np.full(n, L, np.uint32))
     pool = ds.BlockImagePool(ctx, 2, n * (L + 36) + 4096)
-    cases = [(8, 8), (8, 4), (8, 2), (8, 1), (64, 16), (64, 8), (64, 4), (64, 2)]
-    batchers = {c: ds.CloseBatcher(ctx, max_batch=c[1], max_wait_us=100) for c in cases}
-    times = {"%d_threads_batch_%d" % c: [] for c in cases}
+    cases = [(8, 8, 8), (8, 4, 8), (8, 2, 8), (8, 1, 8), (64, 16, 8), (64, 8, 8), (64, 4, 8), (64, 2, 8)]
+    if os.environ.get("LB_CASES"):  # "threads:batch[:in_flight],..." (in_flight: batches in use at once, 1-16)
+        cases = [tuple(int(v) for v in (c.split(":") + ["8"])[:3]) for c in os.environ["LB_CASES"].split(",")]
+    batchers = {c: ds.CloseBatcher(ctx, max_batch=c[1], max_wait_us=100, in_flight=c[2]) for c in cases}
+
+    def key(c):
+        return "%d_threads_batch_%d%s" % (c[0], c[1], "_inflight_%d" % c[2] if c[2] != 8 else "")
+    times = {key(c): [] for c in cases}
     for _ in range(2):  # warm-up
         for c in cases:
             blk = ds.LogicBlock(1, pool=pool)
@@ -44,7 +49,7 @@ def main():
                 blk = ds.LogicBlock(1, pool=pool)
                 assert ds.loopback_block(ctx, pay, n, L, client, c[0], blk, batchers[c]) == 0
                 blk.free()
-            times["%d_threads_batch_%d" % c].append((time.perf_counter() - t0) / 4)
+            times[key(c)].append((time.perf_counter() - t0) / 4)
         print("round %d" % r, file=sys.stderr, flush=True)
     res = {k: {"GiBs_median": n * L / sorted(v)[len(v) // 2] / 2**30, "GiBs_best": n * L / min(v) / 2**30}
            for k, v in times.items()}
