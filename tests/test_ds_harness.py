@@ -181,6 +181,66 @@ def test_batched_closes_from_threads(gpu_ctx, ds, oracle, tmp_path):
     batcher.free()
 
 
+@pytest.mark.parametrize("max_batch", [1, 4])
+def test_pooled_leases_checked_in_place(gpu_ctx, ds, oracle, tmp_path, max_batch):
+    """Leases whose DataFile buffers come from a page-locked LeaseBufferPool close
+    through a CloseBatcher on that pool with no gather copy (each member's payload
+    checked where set_data put it, the batch spread over the pool).  Wrong client
+    CRCs get -8013, the rest are persisted byte for byte; leases past the pool's
+    size take heap buffers and the unbatched close, with the same verdicts; a spill
+    (> 2 MiB) lease from the pool is checked from its tmp file; every buffer is back
+    in the pool at the end."""
+    pool = ds.LeaseBufferPool(gpu_ctx, 6)  # fewer buffers than 8 threads: some leases fall back to the heap
+    batcher = ds.CloseBatcher(gpu_ctx, max_batch=max_batch, max_wait_us=300, pool=pool)
+    blk = ds.LogicBlock(510)
+    nthreads, per = 8, 30
+    results, pooled = {}, []
+    lock = threading.Lock()
+
+    def worker(t):
+        for k in range(per):
+            fid = 1 + t * per + k
+            d = synth_bytes(fid * 7, 3000 + 911 * k + 13 * t).tobytes()
+            df = ds.DataFile(gpu_ctx, fid, str(tmp_path), pool=pool)
+            df.set_data(d, 0)
+            client = ocrc(oracle, 0, d)
+            if fid % 11 == 0:
+                client ^= 0x4
+            rc = batcher.close(blk, fid, client, df)
+            with lock:
+                results[fid] = (rc, fid % 11 == 0, d)
+                pooled.append(df.pooled())
+            df.free()
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(nthreads)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    assert len(results) == nthreads * per and any(pooled)
+    for fid, (rc, bad, _) in results.items():
+        assert rc == (-8013 if bad else 0), fid
+    m, _ = blk.metas()
+    assert len(m) == sum(1 for rc, bad, _ in results.values() if not bad)
+    raw = blk.raw()
+    for rec in m:
+        fid = int(rec["file_id"])
+        d = results[fid][2]
+        o = int(rec["offset"])
+        assert raw[o + FILEINFO:o + FILEINFO + len(d)].tobytes() == d
+        assert _file_info(raw, o)["crc_"] == ocrc(oracle, 0, d)
+    nbad, _ = ds.verify_block(gpu_ctx, blk)
+    assert nbad == 0
+    # a spill lease from the pool (> 2 MiB): re-read from its tmp file in 2 MiB chunks
+    big = synth_bytes(4242, (2 << 20) + 12345).tobytes()
+    df = ds.DataFile(gpu_ctx, 9999, str(tmp_path), pool=pool)
+    df.set_data(big, 0)
+    assert batcher.close(blk, 9999, ocrc(oracle, 0, big), df) == 0
+    df.free()
+    assert pool.in_use() == 0
+    batcher.free()
+    blk.free()
+    pool.free()
+
+
 def test_verify_block_crc_errors_drive_repair(gpu_ctx, ds, oracle, tmp_path):
     """Verify-on-read finds corrupted payloads; BlockChecker counts crc_error_ per
     block and asks for repair at max_crc_error_nums (default 4, parameter.cpp:256)."""

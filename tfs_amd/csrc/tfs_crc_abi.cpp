@@ -868,9 +868,17 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
   // host spins on the flag instead of an event.  Pageable payloads are first
   // copied into the slot's page-locked staging buffer.  Such calls are bound by
   // latency, not bandwidth.
-  if (ctx->variant != kVariantDmaCompact && hi - lo <= kZeroCopySpan) {
+  // A few files far apart in one page-locked buffer (a CloseBatcher batch of
+  // leases in a LeaseBufferPool) are read in place too: only their bytes cross
+  // PCIe, however wide the span.
+  const bool wide = hi - lo > kZeroCopySpan;
+  const bool pinned = ctx->variant != kVariantDmaCompact && (!wide || n <= kWgMaxFiles) && is_pinned_host(base);
+  uint64_t wide_bytes = 0;
+  if (wide && pinned)
+    for (uint32_t i = 0; i < n; ++i) wide_bytes += dd[i].len;
+  if (ctx->variant != kVariantDmaCompact && (!wide || (pinned && wide_bytes <= kZeroCopySpan))) {
     void* host_span = nullptr;  // page-locked host address of base + lo
-    if (is_pinned_host(base)) {
+    if (pinned) {
       host_span = const_cast<uint8_t*>(static_cast<const uint8_t*>(base) + lo);
     } else {
       (void)hipGetLastError();

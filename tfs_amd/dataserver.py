@@ -38,6 +38,8 @@ def lib():
         vp, u32, i32, u64, i64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_int64
         sig = {
             "tfs_ds_datafile_new": (vp, [vp, u64, ctypes.c_char_p]),
+            "tfs_ds_datafile_new2": (vp, [vp, u64, ctypes.c_char_p, vp]),
+            "tfs_ds_datafile_pooled": (ctypes.c_int, [vp]),
             "tfs_ds_datafile_free": (None, [vp]),
             "tfs_ds_datafile_set_data": (ctypes.c_int, [vp, vp, i32, i32]),
             "tfs_ds_datafile_length": (i32, [vp]),
@@ -57,6 +59,10 @@ def lib():
             "tfs_ds_close_write_file": (ctypes.c_int, [vp, u64, u32, vp]),
             "tfs_ds_batcher_new": (vp, [vp, u32, ctypes.c_int]),
             "tfs_ds_batcher_new2": (vp, [vp, u32, ctypes.c_int, ctypes.c_int]),
+            "tfs_ds_batcher_new3": (vp, [vp, u32, ctypes.c_int, ctypes.c_int, vp]),
+            "tfs_ds_lease_pool_new": (vp, [vp, u32]),
+            "tfs_ds_lease_pool_free": (None, [vp]),
+            "tfs_ds_lease_pool_in_use": (u32, [vp]),
             "tfs_ds_batcher_free": (None, [vp]),
             "tfs_ds_batcher_batches": (u64, [vp]),
             "tfs_ds_batcher_close": (ctypes.c_int, [vp, vp, u64, u32, vp]),
@@ -119,8 +125,15 @@ def lib():
 class DataFile:
     """DataFile (src/dataserver/data_file.h:33-96)."""
 
-    def __init__(self, ctx, fn, tmp_dir="/tmp"):
-        self.h = lib().tfs_ds_datafile_new(_ctx(ctx), fn, tmp_dir.encode())
+    def __init__(self, ctx, fn, tmp_dir="/tmp", pool=None):
+        if pool is None:
+            self.h = lib().tfs_ds_datafile_new(_ctx(ctx), fn, tmp_dir.encode())
+        else:  # the buffer from a LeaseBufferPool (the heap when it is exhausted)
+            self.pool = pool
+            self.h = lib().tfs_ds_datafile_new2(_ctx(ctx), fn, tmp_dir.encode(), pool.h)
+
+    def pooled(self):
+        return bool(lib().tfs_ds_datafile_pooled(self.h))
 
     def set_data(self, data, offset):
         b = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8))
@@ -237,11 +250,32 @@ class LogicBlock:
             pass
 
 
+class LeaseBufferPool:
+    """Page-locked DataFile buffers (2 MiB each) in one allocation: a CloseBatcher
+    on the pool checks each lease's payload where set_data put it."""
+
+    def __init__(self, ctx, nbuffers):
+        self.h = lib().tfs_ds_lease_pool_new(_ctx(ctx), nbuffers)
+        if not self.h:
+            raise RuntimeError("tfs_ds_lease_pool_new(%d) failed" % nbuffers)
+
+    def in_use(self):
+        return lib().tfs_ds_lease_pool_in_use(self.h)
+
+    def free(self):
+        if self.h:
+            lib().tfs_ds_lease_pool_free(self.h)
+            self.h = None
+
+
 class CloseBatcher:
     """Batches close_write_file CRC checks from many threads into one GPU verify."""
 
-    def __init__(self, ctx, max_batch=64, max_wait_us=200, in_flight=None):
-        if in_flight is None:
+    def __init__(self, ctx, max_batch=64, max_wait_us=200, in_flight=None, pool=None):
+        if pool is not None:  # keep the pool alive as long as the batcher
+            self.pool = pool
+            self.h = lib().tfs_ds_batcher_new3(_ctx(ctx), max_batch, max_wait_us, in_flight or 8, pool.h)
+        elif in_flight is None:
             self.h = lib().tfs_ds_batcher_new(_ctx(ctx), max_batch, max_wait_us)
         else:  # batches in use at once, 1..16 (default 8)
             self.h = lib().tfs_ds_batcher_new2(_ctx(ctx), max_batch, max_wait_us, in_flight)

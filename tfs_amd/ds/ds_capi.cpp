@@ -22,6 +22,12 @@ extern "C" {
 void* tfs_ds_datafile_new(tfs_crc_ctx* ctx, uint64_t fn, const char* tmp_dir) {
   return new DataFile(fn, tmp_dir ? tmp_dir : "/tmp", ctx);
 }
+// The same with its buffer from a LeaseBufferPool (tfs_ds_lease_pool_new; the heap
+// when the pool is exhausted or NULL).
+void* tfs_ds_datafile_new2(tfs_crc_ctx* ctx, uint64_t fn, const char* tmp_dir, void* pool) {
+  return new DataFile(fn, tmp_dir ? tmp_dir : "/tmp", ctx, static_cast<LeaseBufferPool*>(pool));
+}
+int tfs_ds_datafile_pooled(void* df) { return static_cast<DataFile*>(df)->pool() != nullptr; }
 void tfs_ds_datafile_free(void* df) { delete static_cast<DataFile*>(df); }
 int tfs_ds_datafile_set_data(void* df, const char* data, int32_t len, int32_t offset) {
   return static_cast<DataFile*>(df)->set_data(data, len, offset);
@@ -82,6 +88,20 @@ void* tfs_ds_batcher_new(tfs_crc_ctx* ctx, uint32_t max_batch, int max_wait_us) 
 void* tfs_ds_batcher_new2(tfs_crc_ctx* ctx, uint32_t max_batch, int max_wait_us, int in_flight) {
   return new CloseBatcher(ctx, max_batch, max_wait_us, in_flight);
 }
+// pool (a tfs_ds_lease_pool_new handle, may be NULL): closes of DataFiles made
+// on it are checked where their payload is, with no gather copy.
+void* tfs_ds_batcher_new3(tfs_crc_ctx* ctx, uint32_t max_batch, int max_wait_us, int in_flight, void* pool) {
+  return new CloseBatcher(ctx, max_batch, max_wait_us, in_flight, static_cast<LeaseBufferPool*>(pool));
+}
+void* tfs_ds_batcher_pool(void* b) { return static_cast<CloseBatcher*>(b)->pool(); }
+
+// Page-locked DataFile buffers (LeaseBufferPool); NULL when the allocation fails.
+void* tfs_ds_lease_pool_new(tfs_crc_ctx* ctx, uint32_t nbuffers) {
+  std::unique_ptr<LeaseBufferPool> p(new LeaseBufferPool(ctx, nbuffers));
+  return p->ok() ? p.release() : nullptr;
+}
+void tfs_ds_lease_pool_free(void* p) { delete static_cast<LeaseBufferPool*>(p); }
+uint32_t tfs_ds_lease_pool_in_use(void* p) { return static_cast<LeaseBufferPool*>(p)->in_use(); }
 void tfs_ds_batcher_free(void* b) { delete static_cast<CloseBatcher*>(b); }
 uint64_t tfs_ds_batcher_batches(void* b) { return static_cast<CloseBatcher*>(b)->batches(); }
 int tfs_ds_batcher_close(void* batcher, void* block, uint64_t file_id, uint32_t client_crc, void* df) {
@@ -173,7 +193,7 @@ int tfs_ds_loopback_block_with(tfs_crc_ctx* ctx, void* batcher, const char* payl
       workers.emplace_back([&, t] {
         for (uint32_t i = uint32_t(t); i < n; i += uint32_t(nthreads)) {
           const auto t0 = now();
-          std::unique_ptr<DataFile> df(new DataFile(i + 1, "/tmp", ctx));
+          std::unique_ptr<DataFile> df(new DataFile(i + 1, "/tmp", ctx, bat.pool()));
           const auto t1 = now();
           if (df->set_data(payloads + size_t(i) * size_t(len), len, 0) < 0) {
             err = TFS_EXIT_PARAMETER_ERROR;

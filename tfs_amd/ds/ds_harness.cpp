@@ -26,14 +26,55 @@ void put_file_info(char* dst, const tfs_file_info& fi) { memcpy(dst, &fi, kFileI
 
 // ---------------- DataFile (data_file.cpp) ----------------
 
-DataFile::DataFile(uint64_t fn, const std::string& tmp_dir, tfs_crc_ctx* ctx)
-    : data_(new char[WRITE_DATA_TMPBUF_SIZE]), ctx_(ctx) {
+DataFile::DataFile(uint64_t fn, const std::string& tmp_dir, tfs_crc_ctx* ctx, LeaseBufferPool* pool)
+    : ctx_(ctx) {
+  if (pool && (data_ = pool->take()) != nullptr) pool_ = pool;
+  else data_ = new char[WRITE_DATA_TMPBUF_SIZE];
   char name[512];
   snprintf(name, sizeof name, "%s/%llu.dat", tmp_dir.c_str(), static_cast<unsigned long long>(fn));
   tmp_file_name_ = name;
 }
 
-DataFile::~DataFile() { set_over(); }
+DataFile::~DataFile() {
+  set_over();
+  if (pool_) pool_->give(data_);
+  else delete[] data_;
+}
+
+// ---------------- LeaseBufferPool ----------------
+
+LeaseBufferPool::LeaseBufferPool(tfs_crc_ctx* ctx, uint32_t nbuffers) : ctx_(ctx) {
+  void* p = nullptr;
+  if (nbuffers && tfs_crc32_host_malloc_pinned(ctx_, uint64_t(nbuffers) * uint64_t(DataFile::WRITE_DATA_TMPBUF_SIZE),
+                                               &p) == TFS_SUCCESS) {
+    base_ = static_cast<char*>(p);
+    n_ = nbuffers;
+    free_.reserve(n_);
+    for (uint32_t i = n_; i-- > 0;) free_.push_back(base_ + size_t(i) * size_t(DataFile::WRITE_DATA_TMPBUF_SIZE));
+  }
+}
+
+LeaseBufferPool::~LeaseBufferPool() {
+  if (base_) tfs_crc32_host_free_pinned(ctx_, base_);
+}
+
+char* LeaseBufferPool::take() {
+  std::lock_guard<std::mutex> g(mu_);
+  if (free_.empty()) return nullptr;
+  char* p = free_.back();
+  free_.pop_back();
+  return p;
+}
+
+void LeaseBufferPool::give(char* p) {
+  std::lock_guard<std::mutex> g(mu_);
+  free_.push_back(p);
+}
+
+uint32_t LeaseBufferPool::in_use() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return n_ - uint32_t(free_.size());
+}
 
 void DataFile::set_over() {
   length_ = 0;
@@ -51,12 +92,12 @@ int DataFile::set_data(const char* data, int32_t len, int32_t offset) {
     if (fd_ == -1) {
       fd_ = open(tmp_file_name_.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0600);
       if (fd_ == -1) return -1;
-      if (write(fd_, data_.get(), length_) != length_) return -1;
+      if (write(fd_, data_, length_) != length_) return -1;
     }
     if (lseek(fd_, offset, SEEK_SET) == -1) return -1;
     if (write(fd_, data, len) != len) return -1;
   } else {
-    memcpy(data_.get() + offset, data, len);
+    memcpy(data_ + offset, data, len);
   }
   if (length > length_) length_ = length;
   return len;
@@ -73,7 +114,7 @@ char* DataFile::get_data(char* data, int32_t* len, int32_t offset) {
       return nullptr;
     }
     if (data == nullptr) {
-      data = data_.get();
+      data = data_;
       *len = WRITE_DATA_TMPBUF_SIZE;
     }
     const ssize_t r = read(fd_, data, *len);
@@ -85,11 +126,11 @@ char* DataFile::get_data(char* data, int32_t* len, int32_t offset) {
     return data;
   }
   if (data == nullptr) {
-    data = data_.get() + offset;
+    data = data_ + offset;
     *len = length_ - offset;
   } else {
     if (*len > length_ - offset) *len = length_ - offset;
-    memcpy(data, data_.get() + offset, *len);
+    memcpy(data, data_ + offset, *len);
   }
   return data;
 }
@@ -105,17 +146,17 @@ uint32_t DataFile::get_crc() {
     if (fd_ == -1 || lseek(fd_, 0, SEEK_SET) == -1) return crc_;
     uint32_t run = 0;
     ssize_t rlen;
-    while ((rlen = read(fd_, data_.get(), WRITE_DATA_TMPBUF_SIZE)) > 0) {
+    while ((rlen = read(fd_, data_, WRITE_DATA_TMPBUF_SIZE)) > 0) {
       tfs_crc_desc d{0, uint32_t(rlen), run};
       uint32_t out = 0;
-      status_ = tfs_crc32_batch(ctx_, &d, 1, data_.get(), uint64_t(rlen), &out);
+      status_ = tfs_crc32_batch(ctx_, &d, 1, data_, uint64_t(rlen), &out);
       if (status_ != TFS_SUCCESS) return 0;
       run = out;
     }
     crc_ = run;
   } else {
     uint32_t out = 0;
-    status_ = tfs_datafile_get_crc(ctx_, data_.get(), length_, &out);
+    status_ = tfs_datafile_get_crc(ctx_, data_, length_, &out);
     if (status_ != TFS_SUCCESS) return 0;
     crc_ = out;
   }
@@ -323,15 +364,21 @@ void spin_until(P pred) {
 }
 }  // namespace
 
-CloseBatcher::CloseBatcher(tfs_crc_ctx* ctx, size_t max_batch, int max_wait_us, int in_flight)
+CloseBatcher::CloseBatcher(tfs_crc_ctx* ctx, size_t max_batch, int max_wait_us, int in_flight,
+                           LeaseBufferPool* pool)
     : ctx_(ctx), max_batch_(max_batch ? max_batch : 1), max_wait_us_(max_wait_us),
       gather_cap_(std::min<size_t>(std::max<size_t>(max_batch_ * (256u << 10), 4u << 20), 16u << 20)),
+      pool_(pool && pool->ok() ? pool : nullptr),
       nbatches_(std::min(std::max(in_flight, 1), kMaxInFlight)),
       batches_buf_(new Batch[size_t(nbatches_)]),
       trace_(getenv("TFS_DS_TRACE") != nullptr) {
   // The gather buffers are page-locked once, here (DataService::initialize),
-  // never on a close.
+  // never on a close.  A batcher on a lease pool gathers nothing.
   for (Batch& b : all_batches()) {
+    b.desc.resize(max_batch_);
+    b.crc.resize(max_batch_);
+    b.ok.resize(max_batch_);
+    if (pool_) continue;
     void* p = nullptr;
     if (tfs_crc32_host_malloc_pinned(ctx_, gather_cap_, &p) == TFS_SUCCESS) {
       b.gather = static_cast<char*>(p);
@@ -339,9 +386,6 @@ CloseBatcher::CloseBatcher(tfs_crc_ctx* ctx, size_t max_batch, int max_wait_us, 
       b.fallback.resize(gather_cap_);
       b.gather = b.fallback.data();
     }
-    b.desc.resize(max_batch_);
-    b.crc.resize(max_batch_);
-    b.ok.resize(max_batch_);
   }
 }
 
@@ -394,7 +438,10 @@ void CloseBatcher::lead(Batch* b) {
   const auto t0 = std::chrono::steady_clock::now();
   if (trace_) t_lead_wait_ += std::chrono::duration_cast<std::chrono::microseconds>(t0 - b->opened).count();
   uint32_t nbad = 0;
-  b->rc = tfs_crc32_verify(ctx_, b->desc.data(), n, b->gather, b->bytes, b->crc.data(), b->ok.data(), &nbad);
+  // Pooled batches: each member's payload is read in its own lease buffer.
+  b->rc = pool_ ? tfs_crc32_verify(ctx_, b->desc.data(), n, pool_->base(), pool_->bytes(), b->crc.data(),
+                                   b->ok.data(), &nbad)
+                : tfs_crc32_verify(ctx_, b->desc.data(), n, b->gather, b->bytes, b->crc.data(), b->ok.data(), &nbad);
   verify_us_ += std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
   ++batches_;
   b->done.store(1, std::memory_order_release);
@@ -402,7 +449,10 @@ void CloseBatcher::lead(Batch* b) {
 
 int CloseBatcher::close(const CloseFileInfo& info, DataFile& df, LogicBlockImage& block) {
   const int32_t len = df.get_length();
-  if (len > kMaxBatched || size_t(len) > gather_cap_) return close_write_file(info, df, block);  // unbatched
+  const char* own = df.in_memory_payload();
+  const bool pooled = pool_ && own && pool_->owns(own);
+  if (len > kMaxBatched || (pool_ ? !pooled : size_t(len) > gather_cap_))
+    return close_write_file(info, df, block);  // unbatched
   using clk = std::chrono::steady_clock;
   auto us = [](clk::time_point a, clk::time_point b2) {
     return int64_t(std::chrono::duration_cast<std::chrono::microseconds>(b2 - a).count());
@@ -413,7 +463,7 @@ int CloseBatcher::close(const CloseFileInfo& info, DataFile& df, LogicBlockImage
   uint64_t off;
   {
     std::unique_lock<std::mutex> lk(mu_);
-    if (cur_ && cur_->bytes + uint64_t(len) > gather_cap_) {  // no room: close it, its leader fires it
+    if (cur_ && !pooled && cur_->bytes + uint64_t(len) > gather_cap_) {  // no room: close it, its leader fires it
       cur_->closed = true;
       cur_ = nullptr;
     }
@@ -429,8 +479,13 @@ int CloseBatcher::close(const CloseFileInfo& info, DataFile& df, LogicBlockImage
     }
   }
   const auto c1 = trace_ ? clk::now() : clk::time_point();
-  // This lease's payload into the batch's gather buffer (data_file.cpp:115-166).
+  // This lease's payload into the batch's gather buffer (data_file.cpp:115-166),
+  // or, from a lease pool, read where it is.
   int32_t got = 0;
+  if (pooled) {
+    got = len;
+    off = uint64_t(own - pool_->base());
+  }
   while (got < len) {
     int32_t rl = len - got;
     if (!df.get_data(b->gather + off + got, &rl, got) || rl <= 0) break;

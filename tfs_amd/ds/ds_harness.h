@@ -34,11 +34,16 @@ namespace dataserver {
 
 // DataFile (data_file.h:33-96): per-lease payload buffer, 2 MiB in memory,
 // spilled to work_dir/tmp/<fn>.dat beyond that (data_file.cpp:73-101).
+class LeaseBufferPool;
+
 class DataFile {
  public:
   static const int32_t WRITE_DATA_TMPBUF_SIZE = 2 * 1024 * 1024;  // data_file.h:78
 
-  DataFile(uint64_t fn, const std::string& tmp_dir, tfs_crc_ctx* ctx);
+  // pool: the lease's 2 MiB buffer comes from it when one is free (page-locked,
+  // so the close's GPU check reads the payload where set_data put it), else from
+  // the heap as in the reference.
+  DataFile(uint64_t fn, const std::string& tmp_dir, tfs_crc_ctx* ctx, LeaseBufferPool* pool = nullptr);
   ~DataFile();
   DataFile(const DataFile&) = delete;
   DataFile& operator=(const DataFile&) = delete;
@@ -54,18 +59,49 @@ class DataFile {
   uint32_t get_crc();
   int last_status() const { return status_; }
   void set_over();
-  const char* buffer() const { return data_.get(); }
+  const char* buffer() const { return data_; }
   // The staged payload when it never spilled to the tmp file (length <= 2 MiB).
-  const char* in_memory_payload() const { return fd_ == -1 ? data_.get() : nullptr; }
+  const char* in_memory_payload() const { return fd_ == -1 ? data_ : nullptr; }
+  // The pool the buffer came from (nullptr: heap).
+  LeaseBufferPool* pool() const { return pool_; }
 
  private:
   int32_t length_ = 0;
-  std::unique_ptr<char[]> data_;  // data_file.h:83: a plain char array, not zero-filled
+  char* data_ = nullptr;  // data_file.h:83: a plain char array, not zero-filled
+  LeaseBufferPool* pool_ = nullptr;
   uint32_t crc_ = 0;
   int fd_ = -1;
   std::string tmp_file_name_;
   tfs_crc_ctx* ctx_;
   int status_ = TFS_SUCCESS;
+};
+
+// Page-locked DataFile buffers (WRITE_DATA_TMPBUF_SIZE each) in one allocation,
+// made once (DataService::initialize) like the block images of a BlockImagePool:
+// a lease's payload stays where set_data copied it (data_file.cpp:104) and the
+// close's GPU check reads it there, so a CloseBatcher on this pool has no
+// gather copy (each member's descriptor is its buffer's offset in the pool).
+class LeaseBufferPool {
+ public:
+  LeaseBufferPool(tfs_crc_ctx* ctx, uint32_t nbuffers);
+  ~LeaseBufferPool();
+  LeaseBufferPool(const LeaseBufferPool&) = delete;
+  LeaseBufferPool& operator=(const LeaseBufferPool&) = delete;
+  bool ok() const { return base_ != nullptr; }
+  char* take();  // nullptr when every buffer is in use
+  void give(char* p);
+  bool owns(const char* p) const { return p >= base_ && p < base_ + bytes(); }
+  const char* base() const { return base_; }
+  uint64_t bytes() const { return uint64_t(n_) * uint64_t(DataFile::WRITE_DATA_TMPBUF_SIZE); }
+  uint32_t size() const { return n_; }
+  uint32_t in_use() const;
+
+ private:
+  tfs_crc_ctx* ctx_;
+  char* base_ = nullptr;
+  uint32_t n_ = 0;
+  mutable std::mutex mu_;
+  std::vector<char*> free_;
 };
 
 struct CloseFileInfo {  // internal.h:716-726
@@ -198,11 +234,15 @@ int close_write_file(const CloseFileInfo& info, DataFile& df, LogicBlockImage& b
 // larger than kMaxBatched take the unbatched close.
 class CloseBatcher {
  public:
-  CloseBatcher(tfs_crc_ctx* ctx, size_t max_batch, int max_wait_us, int in_flight = kBatches);
+  // pool: closes of DataFiles whose buffers are in it are checked in place (no
+  // gather copy); other closes through this batcher then take the unbatched path.
+  CloseBatcher(tfs_crc_ctx* ctx, size_t max_batch, int max_wait_us, int in_flight = kBatches,
+               LeaseBufferPool* pool = nullptr);
   ~CloseBatcher();
   // Blocks until this close has been checked (and persisted on success).
   int close(const CloseFileInfo& info, DataFile& df, LogicBlockImage& block);
   uint64_t batches() const { return batches_.load(); }
+  LeaseBufferPool* pool() const { return pool_; }
 
   // Leases per batch for `leases` closing threads: with the resident kernel a
   // batch costs no launch, so up to 8 threads close one file per batch (10.4 vs
@@ -240,6 +280,7 @@ class CloseBatcher {
   size_t gather_cap_;  // per batch: max_batch x 256 KiB, within [4 MiB, 16 MiB]
   std::mutex mu_;
   std::condition_variable free_cv_;
+  LeaseBufferPool* pool_;
   int nbatches_;
   std::unique_ptr<Batch[]> batches_buf_;
   struct Span {

@@ -29,13 +29,19 @@ def main():
     pay = synth_bytes(0x9E3779B97F4A7C15, n * L)
     client = ctx.batch(pay, np.arange(n, dtype=np.uint64) * L, np.full(n, L, np.uint32))
     pool = ds.BlockImagePool(ctx, 2, n * (L + 36) + 4096)
-    cases = [(8, 8, 8), (8, 4, 8), (8, 2, 8), (8, 1, 8), (64, 16, 8), (64, 8, 8), (64, 4, 8), (64, 2, 8)]
-    if os.environ.get("LB_CASES"):  # "threads:batch[:in_flight],..." (in_flight: batches in use at once, 1-16)
-        cases = [tuple(int(v) for v in (c.split(":") + ["8"])[:3]) for c in os.environ["LB_CASES"].split(",")]
-    batchers = {c: ds.CloseBatcher(ctx, max_batch=c[1], max_wait_us=100, in_flight=c[2]) for c in cases}
+    cases = [(8, 8, 8, 0), (8, 4, 8, 0), (8, 2, 8, 0), (8, 1, 8, 0), (64, 16, 8, 0), (64, 8, 8, 0), (64, 4, 8, 0),
+             (64, 2, 8, 0)]
+    if os.environ.get("LB_CASES"):
+        # "threads:batch[:in_flight[:pool]],..." (in_flight: batches in use at once, 1-16; pool 1: the
+        # DataFile buffers from a page-locked LeaseBufferPool, checked in place)
+        cases = [tuple(int(v) for v in (c.split(":") + ["8", "0"])[:4]) for c in os.environ["LB_CASES"].split(",")]
+    lease_pool = ds.LeaseBufferPool(ctx, 128)
+    batchers = {c: ds.CloseBatcher(ctx, max_batch=c[1], max_wait_us=100, in_flight=c[2],
+                                   pool=lease_pool if c[3] else None) for c in cases}
 
     def key(c):
-        return "%d_threads_batch_%d%s" % (c[0], c[1], "_inflight_%d" % c[2] if c[2] != 8 else "")
+        return "%d_threads_batch_%d%s%s" % (c[0], c[1], "_inflight_%d" % c[2] if c[2] != 8 else "",
+                                          "_pool" if c[3] else "")
     times = {key(c): [] for c in cases}
     for _ in range(2):  # warm-up
         for c in cases:
