@@ -165,8 +165,11 @@ static_assert(sizeof(FileInfoHdr) == kFileInfoSize, "FileInfo must be 36 bytes")
 // (seed 0, into ext_crc); the fold (split_fold_kernel) joins them:
 // crc = shift(...shift(crc_head, S) ^ crc_1 ..., S) ^ crc_{K-1}, shift by S
 // bytes from one table.
-constexpr uint32_t kSegBytes = 128u << 10;
-constexpr uint32_t kSplitMin = 128u << 10;
+#ifndef TFS_SEG_KIB
+#define TFS_SEG_KIB 128  // measurement builds may set another segment size
+#endif
+constexpr uint32_t kSegBytes = uint32_t(TFS_SEG_KIB) << 10;
+constexpr uint32_t kSplitMin = kSegBytes;
 constexpr uint32_t kNoSplit = 0xffffffffu;
 constexpr uint32_t kSplitMaxUnits = 4u << 20;  // ext units per launch at most (files past it stay whole)
 // One allocation per plan (3 SGPRs in the kernels' arguments instead of a
