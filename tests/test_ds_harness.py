@@ -234,6 +234,9 @@ def test_pooled_leases_checked_in_place(gpu_ctx, ds, oracle, tmp_path, max_batch
     df = ds.DataFile(gpu_ctx, 9999, str(tmp_path), pool=pool)
     df.set_data(big, 0)
     assert batcher.close(blk, 9999, ocrc(oracle, 0, big), df) == 0
+    assert pool.in_use() == 1
+    with pytest.raises(RuntimeError):
+        pool.free()  # refused while a DataFile holds a buffer
     df.free()
     assert pool.in_use() == 0
     batcher.free()

@@ -263,7 +263,10 @@ class LeaseBufferPool:
         return lib().tfs_ds_lease_pool_in_use(self.h)
 
     def free(self):
+        """Refused while a DataFile still holds one of the buffers."""
         if self.h:
+            if self.in_use():
+                raise RuntimeError("LeaseBufferPool.free: %d buffers still held by DataFiles" % self.in_use())
             lib().tfs_ds_lease_pool_free(self.h)
             self.h = None
 

@@ -81,6 +81,7 @@ class DataFile {
 // a lease's payload stays where set_data copied it (data_file.cpp:104) and the
 // close's GPU check reads it there, so a CloseBatcher on this pool has no
 // gather copy (each member's descriptor is its buffer's offset in the pool).
+// The pool must outlive every DataFile made on it and every CloseBatcher given it.
 class LeaseBufferPool {
  public:
   LeaseBufferPool(tfs_crc_ctx* ctx, uint32_t nbuffers);
