@@ -166,7 +166,9 @@ static void launch_chunk(const EcArgs& a, int og, dim3 g, dim3 b, hipStream_t st
 #endif  // TFS_CRC_MEASURE
 
 // The product: the grid-stride tile kernel.  Measurement build (TFS_EC_VARIANT
-// 1, 2, 3): the chunked form with K = 2, 4, 8 tiles per wave step.
+// 1, 2, 3): the chunked form with K = 2, 4, 8 tiles per wave step; 4, 6: the
+// product's kernel over 8,192 / 2,048 workgroups striding (the product launches
+// one grid step per wave).
 hipError_t launch_ec_apply(const EcArgs& a, int og, int variant, hipStream_t stream) {
   if (a.units == 0) return hipSuccess;
   const uint64_t ntiles = (a.units + 3) / 4;
@@ -184,8 +186,16 @@ hipError_t launch_ec_apply(const EcArgs& a, int og, int variant, hipStream_t str
 #else
   (void)variant;
 #endif
+  // One grid step per wave: a workgroup per 4 tiles of 4, far more workgroups than
+  // fit at once, each gone after one step (8.8 % faster than a grid of 2,048
+  // striding over the members, the round-2 form).
   uint64_t blocks = (ntiles + 3) / 4;
-  if (blocks > 2048) blocks = 2048;
+  uint64_t cap = uint64_t(1) << 30;
+#ifdef TFS_CRC_MEASURE
+  if (variant == 4) cap = 8192;       // measurement: 8,192 workgroups striding
+  else if (variant == 6) cap = 2048;  // measurement: the round-2 product (2,048 striding)
+#endif
+  if (blocks > cap) blocks = cap;
   const dim3 g(static_cast<unsigned>(blocks)), b(256);
   switch (og) {
     case 1: hipLaunchKernelGGL(ec_apply_kernel<1>, g, b, 0, stream, a, a.masks); break;
