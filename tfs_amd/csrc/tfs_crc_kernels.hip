@@ -2332,6 +2332,9 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
   else if (variant == 69 || variant == 70)  // 67 over 512 / 2,048 workgroups (two resident per CU, no LDS)
     hipLaunchKernelGGL((compact_probe_copy_kernel<true, 128>), dim3(variant == 69 ? 512 : 2048), dim3(kBlock), 0,
                        stream, src, jobs, n, dst, sched);
+  else if (variant == 71)  // 68 with one record per wave: n / 16 workgroups, each gone after one step
+    hipLaunchKernelGGL((compact_probe_copy_kernel<false, 128>), dim3((n + 15u) / 16u), dim3(kBlock), 0, stream, src,
+                       jobs, n, dst, sched);
   else if (variant == 39) TFS_CJ(true, true, false, kCompactDiag, kPF, 2, 0);  // chunked tickets (as crc_files 39-45)
   else if (variant == 40) TFS_CJ(true, true, false, kCompactDiag, kPF, 4, 0);
   else if (variant == 42) TFS_CJ(true, true, false, kCompactDiag, kPF, 4, 3);

@@ -91,8 +91,8 @@ def main():
     for v in want:
         ctxs[v] = ctx_for(v)
     # 65/66: the record list through the chunk copy's loop -- destinations congruent mod 16 only
-    cases = ([(0, "packed")] + [(v, "packed") for v in want if v not in (31, 32, 65, 66, 67, 68, 69, 70)] + [(0, "dst128")] +
-             [(v, "dst128") for v in want if v in (65, 66, 67, 68, 69, 70)])
+    cases = ([(0, "packed")] + [(v, "packed") for v in want if v not in (31, 32, 65, 66, 67, 68, 69, 70, 71)] + [(0, "dst128")] +
+             [(v, "dst128") for v in want if v in (65, 66, 67, 68, 69, 70, 71)])
     if 31 in want or 32 in want:
         cases += [(0, "shift1")] + [(v, "shift1") for v in want if v in (31, 32)]
     # verify-on-read of every record of the resident blocks (tfs_blocks_verify_device)
@@ -107,7 +107,7 @@ def main():
     # correctness of the product cases (the diagnostic variants 26 and 30 compute
     # no CRCs / skip stores)
     for v, js in cases:
-        if v in (26, 30, 61, 64, 65, 66, 67, 68, 69, 70):
+        if v in (26, 30, 61, 64, 65, 66, 67, 68, 69, 70, 71):
             continue
         d_bad.zero()
         ctxs[v].compact_jobs_device(img, total, jobsets[js], nj, d_dst, None, d_st, d_bad)
