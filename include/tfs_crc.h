@@ -426,8 +426,7 @@ int tfs_crc32_event_create(tfs_crc_ctx* ctx, void** ev);
 int tfs_crc32_event_record(tfs_crc_ctx* ctx, void* ev, void* stream);
 int tfs_crc32_event_elapsed_ms(tfs_crc_ctx* ctx, void* ev_start, void* ev_end, float* ms);
 int tfs_crc32_event_destroy(tfs_crc_ctx* ctx, void* ev);
-/* The ctx's HIP stream (as void*) and a synchronize on it (and on the streams of the
-   context's staged host batches). */
+/* The ctx's HIP stream (as void*) and a synchronize on it. */
 void* tfs_crc32_stream(tfs_crc_ctx* ctx);
 int tfs_crc32_sync(tfs_crc_ctx* ctx);
 /* Fault injection (tests of the callers' error paths, like the reference's
