@@ -97,6 +97,21 @@ def launch_ranks(args):
     return subprocess.call(cmd, env=env)
 
 
+def _init_gloo(dist):
+    """init_process_group(gloo) with the process's stdout pointed at stderr meanwhile:
+    gloo prints "[Gloo] Rank r is connected to ..." on stdout in every rank, and the
+    line the driver reads from rank 0's stdout must be the only one there."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        dist.init_process_group(backend="gloo")
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def launch_check(args):
     """--launch-check: the rank plumbing of --gpus N without any GPU work."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -105,7 +120,7 @@ def launch_check(args):
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group(backend="gloo")
+        _init_gloo(dist)
         got = [None] * world
         dist.all_gather_object(got, [rank, local, os.getpid()])
         dist.destroy_process_group()
@@ -552,7 +567,7 @@ def _dist_init():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group(backend="gloo")
+        _init_gloo(dist)
     _bind_numa(local)
     return world, rank, local, dist
 

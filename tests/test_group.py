@@ -170,6 +170,7 @@ def test_bench_two_ranks_partitioned_by_block(tmp_path):
     r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert [ln for ln in r.stdout.splitlines() if ln.strip()] == lines, r.stdout  # only the line on stdout
     assert len(lines) == 1
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["value"] > 0 and res["end_to_end"]["value"] > 0
@@ -191,6 +192,7 @@ def test_bench_gpus_2_self_launched(tmp_path):
     r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert [ln for ln in r.stdout.splitlines() if ln.strip()] == lines, r.stdout  # only the line on stdout
     assert len(lines) == 1, r.stdout[-2000:]
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["value"] > 0 and res["end_to_end"]["value"] > 0

@@ -69,6 +69,8 @@ def test_bench_gpus_n_starts_its_own_ranks():
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
+    # the JSON line is all there is on stdout (gloo's per-rank connection messages go to stderr)
+    assert [ln for ln in r.stdout.splitlines() if ln.strip()] == lines, r.stdout
     chk = json.loads(lines[0])["launch_check"]
     assert chk["world"] == 3 and chk["gpus"] == 3
     assert sorted(x[0] for x in chk["ranks"]) == [0, 1, 2]
