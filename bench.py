@@ -306,7 +306,7 @@ def main():
     for b in range(0, nblocks, max(1, args.parity_every)):
         host = img.download(np.uint8, block_bytes, b * block_bytes)
         ora.oracle_crc_batch_mt(bd.ctypes.data, FILES_PER_BLOCK, host.ctypes.data, bout.ctypes.data,
-                                _cpu_budget())
+                                _cpu_budget(shared=True))
         mism += int((bout != expected[b * FILES_PER_BLOCK:(b + 1) * FILES_PER_BLOCK]).sum())
         checked += FILES_PER_BLOCK
     if mism:
@@ -361,7 +361,10 @@ def main():
                  "covers": bool(np.array_equal(np.sort(allb), np.arange(nblocks * world)))}
     payload_bytes = float(world) * args.steps * nfiles * FILE_SIZE
     value = payload_bytes / elapsed / 2**30
-    avg_kern_s = float(np.mean(kern_ms)) / 1e3
+    # Every rank's mean kernel time (HIP events on its own launch stream); the
+    # roofline is priced at the slowest GPU's, with the spread beside it.
+    rank_kms = _gather_floats(dist, world, float(np.mean(kern_ms)))
+    avg_kern_s = max(rank_kms) / 1e3
     achieved = nfiles * ALGO_BYTES_PER_FILE / avg_kern_s / 1e9
 
     if args.ab:
@@ -439,10 +442,18 @@ def main():
             "traffic_source": pmc.get("source"), "traffic_measured_in_this_run": False, "traffic_note": TRAFFIC_NOTE,
             "kernel": "crc_files_kernel<1> (verify)",
             "kernel_ms_avg": avg_kern_s * 1e3,
+            "kernel_ms_per_rank": {"ms": rank_kms, "min": min(rank_kms), "max": max(rank_kms),
+                                   "frac_at_min": nfiles * ALGO_BYTES_PER_FILE / (min(rank_kms) / 1e3) / 1e9
+                                   / HBM_PEAK_GBS,
+                                   "note": "mean kernel ms of each rank (HIP events on its stream); achieved and "
+                                           "frac are priced at the slowest rank (max)"},
             "algorithmic_bytes_per_launch": nfiles * ALGO_BYTES_PER_FILE,
         },
     }
-    if rank == 0 and world == 1 and not args.no_cpu:
+    # The reference CRC on the host cores, in the same run at every N: rank 0 times
+    # it after the timed loops while the other ranks wait at a barrier (idle), so
+    # its all-core leg has the box's CPU quota to itself.
+    if rank == 0 and not args.no_cpu:
         ns = min(2048, nfiles)
         idx = np.linspace(0, nfiles - 1, ns).astype(np.int64)
         # copy the sampled payloads (identical bytes) to host
@@ -452,13 +463,17 @@ def main():
             sample[j * FILE_SIZE:(j + 1) * FILE_SIZE] = img.download(np.uint8, FILE_SIZE, o)
         result["cpu_baseline"] = cpu_baseline(sample, np.arange(ns) * FILE_SIZE, np.full(ns, FILE_SIZE),
                                               expected[idx], args.cpu_seconds)
+        result["cpu_baseline"]["run"] = ("rank 0 of %d, after the timed loops, the other ranks waiting at a barrier"
+                                         % world)
+    if dist and not args.no_cpu:
+        dist.barrier()
     if args.e2e:
         print(json.dumps({"e2e": e2e_rate(ctx)}), file=sys.stderr)
     if args.e2e_blocks > 0:
         # configs[4] asks for device-resident AND end-to-end at every N: the same
         # job's PCIe-inclusive rate, reported beside `value` (never as `value`).
         gibs, pcie, el = e2e_blocks(ctx, dist, world, rank, args.e2e_blocks)
-        ceil = pcie_ceiling(ctx)
+        ceil = pcie_ceiling(ctx, dist=dist)
         result["end_to_end"] = {
             "value": gibs, "unit": "GiB/s", "pcie_GBs": pcie, "ms_per_block": el / args.e2e_blocks * 1e3,
             "workload": "%d pinned host 64 MiB block images per GPU -> H2D -> verify -> verdicts back, "
@@ -597,6 +612,16 @@ def _bind_numa(device):
             _NUMA.update(bound=True, cpus=len(mine))
     except (OSError, ValueError):
         pass
+
+
+def _gather_floats(dist, world, v):
+    """[v of rank 0, v of rank 1, ...] (gloo all_gather; [v] without dist)."""
+    if not dist:
+        return [float(v)]
+    import torch
+    out = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(out, torch.tensor([float(v)], dtype=torch.float64))
+    return [float(t.item()) for t in out]
 
 
 def _max_over_ranks(dist, v):
@@ -1013,7 +1038,7 @@ def bench_compact(args):
     # Zero-copy form: the kernel reads only the live records from the pinned
     # source image and writes the new block into the pinned destination.
     pcie_block = 2 * live * rec
-    ceil = pcie_ceiling(ctx)
+    ceil = pcie_ceiling(ctx, dist=dist)
     pcie_gbs = float(nblocks) * pcie_block / el / 1e9
     res = {
         "metric": "GiB/s of live payload compacted (re-read + re-CRC + repack), host block images, PCIe included",
@@ -1340,7 +1365,7 @@ def bench_block_verify(args):
         out[name] = (_max_over_ranks(dist, time.perf_counter() - t0), nb)
     ctx_dma.close()
     el, nb = out["zero_copy"]
-    ceil = pcie_ceiling(ctx)
+    ceil = pcie_ceiling(ctx, dist=dist)
     pcie_gbs = float(nb) * live.size * rec / el / 1e9
     res = {
         "metric": "GiB/s of live payload verified on read from fragmented blocks in page-locked host memory",
@@ -2094,14 +2119,32 @@ def _ref_crc_fn():
 _PCIE = {}
 
 
-def pcie_ceiling(ctx, nbytes=256 << 20):
+def pcie_ceiling(ctx, nbytes=256 << 20, dist=None):
     """The link's measured DMA ceiling, this run: best of 5 pinned hipMemcpyAsync
     of 256 MiB host->device and device->host after 0.1 s of the same copies (the
     `peak` of the PCIe-bound lines),
     and the duplex rate: both directions at once on two streams (best of 3, the
-    sum of the bytes moved over the longer of the two)."""
+    sum of the bytes moved over the longer of the two).  With N ranks (dist) each
+    rank measures its own link in turn while the others wait at a barrier, so the
+    peak is the per-GPU link's, not N links sharing the host at once."""
     if _PCIE:
         return _PCIE
+    if dist is not None:
+        world, rank = dist.get_world_size(), dist.get_rank()
+        for r in range(world):
+            dist.barrier()
+            if r == rank:
+                _pcie_measure(ctx, nbytes)
+        dist.barrier()
+        _PCIE["measured"] = "by each of the %d ranks in turn (the others waiting at a barrier)" % world
+        _PCIE["source"] += "; per GPU link, " + _PCIE["measured"]
+        return _PCIE
+    _pcie_measure(ctx, nbytes)
+    _PCIE["measured"] = "one rank"
+    return _PCIE
+
+
+def _pcie_measure(ctx, nbytes):
     import tfs_amd.crc as crc
     h = crc.PinnedBuffer(ctx, nbytes)
     h.array[:] = 1
@@ -2140,20 +2183,31 @@ def pcie_ceiling(ctx, nbytes=256 << 20):
     out["duplex_source"] = ("measured: 256 MiB H2D and 256 MiB D2H issued together on two streams, "
                             "best of 3, 512 MiB over the wall time")
     _PCIE.update(out)
-    return _PCIE
 
 
-def _cpu_budget():
+def _cpu_budget(shared=False):
     """Host CPUs this process may use: the scheduler affinity capped by the cgroup
-    quota (cpu.max) -- on the GPU box 16 of the machine's 256 hardware threads."""
+    quota (cpu.max) -- on the GPU box 16 of the machine's 256 hardware threads.
+    shared: a leg every local rank runs at the same time (the parity oracle) gets
+    its share of the container-wide quota, quota / LOCAL_WORLD_SIZE, so N ranks
+    never ask for N times the quota (cpu.max throttles the whole container)."""
     n = len(os.sched_getaffinity(0))
+    quota_cpus = None
     try:
         with open("/sys/fs/cgroup/cpu.max") as fh:
             quota, period = fh.read().split()[:2]
         if quota != "max":
-            n = min(n, max(1, int(int(quota) // int(period))))
+            quota_cpus = max(1, int(int(quota) // int(period)))
     except (OSError, ValueError):
         pass
+    if shared:
+        local_world = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1"))))
+        if quota_cpus is not None:
+            quota_cpus = max(1, quota_cpus // local_world)
+        else:
+            n = max(1, min(n, (os.cpu_count() or n) // local_world))
+    if quota_cpus is not None:
+        n = min(n, quota_cpus)
     return n
 
 
@@ -2336,7 +2390,7 @@ def bench_loopback(args):
     # PCIe bytes of one loopback: every payload crosses once for the close check
     # (zero-copy reads of the lease buffers) and once for the whole-block verify.
     pcie_bytes = 2.0 * n * L
-    ceil = pcie_ceiling(ctx)
+    ceil = pcie_ceiling(ctx, dist=dist)
     res["roofline"] = {"bound": "pcie", "achieved": reps * pcie_bytes / el / 1e9, "peak": ceil["h2d_GBs"],
                        "unit": "GB/s (per GPU)", "frac": reps * pcie_bytes / el / 1e9 / ceil["h2d_GBs"],
                        "traffic": None, "peak_source": ceil["source"],
@@ -2465,7 +2519,7 @@ def bench_e2e(args):
         "config": {"workload": "pinned host blocks -> GPU verify, %d in flight, %d blocks" % (inflight, nsub)},
         "pcie_GBs": pcie,
     }
-    ceil = pcie_ceiling(ctx)
+    ceil = pcie_ceiling(ctx, dist=dist)
     res["roofline"] = {"bound": "pcie", "achieved": pcie / world, "peak": ceil["h2d_GBs"], "unit": "GB/s (per GPU)",
                        "frac": pcie / world / ceil["h2d_GBs"], "peak_source": ceil["source"], "traffic": None}
     if "v" in cpu_res:

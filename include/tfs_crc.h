@@ -128,9 +128,12 @@ uint32_t tfs_crc32_e(uint32_t crc, const char* data, int32_t len, int* err);
 uint64_t tfs_crc32_error_count(void);
 /* Choose the scalar context: for the whole process (NULL = back to device 0's
  * default), or for the calling thread only (a packet worker serving one GPU's
- * blocks binds that group member's context; NULL unbinds).  The caller keeps the
- * context alive while it is selected; destroying it clears the process default
- * and the destroying thread's binding. */
+ * blocks binds that group member's context; NULL unbinds).  Destroying a
+ * context clears the process default and every thread's binding to it (each
+ * thread drops it on its next scalar call, which then uses the process default);
+ * binding a context that is not live returns TFS_EXIT_PARAMETER_ERROR.  A scalar
+ * call running while another thread destroys its context is the caller's to
+ * avoid. */
 int tfs_crc32_set_default_ctx(tfs_crc_ctx* ctx);
 int tfs_crc32_bind_thread(tfs_crc_ctx* ctx);
 /* The context the scalar calls of this thread use (created on first use), or
@@ -365,7 +368,10 @@ tfs_crc_ctx* tfs_crc_group_ctx_for_block(tfs_crc_group* g, uint32_t block_id);
 int tfs_crc_group_numa_node(const tfs_crc_group* g, uint32_t i);
 int tfs_crc_group_member_bound(const tfs_crc_group* g, uint32_t i);
 /* Page-locked host memory allocated on member i's NUMA node (block images,
- * receive buffers of that GPU's blocks). */
+ * receive buffers of that GPU's blocks).  Free it only with
+ * tfs_crc_group_host_free: the library keeps its own registry of the page-locked
+ * memory it allocated (no runtime query per call), which hipHostFree would leave
+ * stale. */
 int tfs_crc_group_host_malloc(tfs_crc_group* g, uint32_t i, uint64_t bytes, void** p);
 int tfs_crc_group_host_free(tfs_crc_group* g, uint32_t i, void* p);
 
@@ -415,6 +421,9 @@ int tfs_crc32_membench_device(tfs_crc_ctx* ctx, int pattern, const void* d_base,
  * synchronous, otherwise asynchronous on `stream`. */
 int tfs_crc32_dev_malloc(tfs_crc_ctx* ctx, uint64_t bytes, void** d_ptr);
 int tfs_crc32_dev_free(tfs_crc_ctx* ctx, void* d_ptr);
+/* Page-locked memory from tfs_crc32_host_malloc_pinned is freed only with
+ * tfs_crc32_host_free_pinned (see tfs_crc_group_host_malloc: the library's
+ * registry of its page-locked allocations). */
 int tfs_crc32_host_malloc_pinned(tfs_crc_ctx* ctx, uint64_t bytes, void** h_ptr);
 int tfs_crc32_host_free_pinned(tfs_crc_ctx* ctx, void* h_ptr);
 /* Device address of page-locked host memory (hipHostGetDevicePointer), for
@@ -426,7 +435,9 @@ int tfs_crc32_event_create(tfs_crc_ctx* ctx, void** ev);
 int tfs_crc32_event_record(tfs_crc_ctx* ctx, void* ev, void* stream);
 int tfs_crc32_event_elapsed_ms(tfs_crc_ctx* ctx, void* ev_start, void* ev_end, float* ms);
 int tfs_crc32_event_destroy(tfs_crc_ctx* ctx, void* ev);
-/* The ctx's HIP stream (as void*) and a synchronize on it. */
+/* The ctx's HIP stream (as void*); tfs_crc32_sync drains it and the ctx's
+ * latency stream (the zero-copy small batches and async submissions launched
+ * there), i.e. every launch the ctx queued on its own streams. */
 void* tfs_crc32_stream(tfs_crc_ctx* ctx);
 int tfs_crc32_sync(tfs_crc_ctx* ctx);
 /* Fault injection (tests of the callers' error paths, like the reference's
@@ -483,6 +494,16 @@ int tfs_crc32_throughput_grid(tfs_crc_ctx* ctx);
  * tfs_crc32_stream_create), and launches so far on streams the ctx does not own
  * (each of those takes a pooled slot zeroed on its stream before the kernel). */
 int tfs_crc32_sched_stats(tfs_crc_ctx* ctx, uint32_t* owned_streams, uint64_t* foreign_launches);
+/* The latest split throughput launch of ctx (debug/test hook; call it with no
+ * other launch of ctx in flight): split launches so far, ext units its plan
+ * reserved (`used`: segments of files > 128 KiB; files past `cap` stayed whole),
+ * its files, the plan's capacity and the workgroups it ran on.  The launch's
+ * work units are files + min(used, cap); it takes dynamic chunked tickets when
+ * those units come to >= 16 tickets per wave.  Waits for that
+ * launch.  Each scheduler slot (stream) has its own plan, so split launches on
+ * different streams overlap. */
+int tfs_crc32_split_stats(tfs_crc_ctx* ctx, uint64_t* launches, uint64_t* used, uint32_t* files, uint32_t* cap,
+                          uint32_t* grid);
 
 #ifdef __cplusplus
 }

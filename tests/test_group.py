@@ -184,11 +184,13 @@ def test_bench_gpus_2_self_launched(tmp_path):
     """Plain `python3 bench.py --gpus 2` -- no launcher around it, as a driver may
     run it: bench.py starts the two ranks itself (both on the one GPU here,
     TFS_BENCH_SHARE_DEVICE=1) and relays rank 0's line: n_gpus 2, the ranks'
-    blocks disjoint and covering, every pass clean, parity checked."""
+    blocks disjoint and covering, every pass clean, parity checked; the line at
+    N > 1 carries the host-core baseline (rank 0, the other rank waiting) and
+    every rank's kernel time (VERDICT r3 next #4)."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
     env.update(TFS_BENCH_SHARE_DEVICE="1", OMP_NUM_THREADS="2")
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--blocks", "32", "--steps", "2",
-           "--warmup", "1", "--no-cpu", "--e2e-blocks", "4", "--parity-every", "8"]
+           "--warmup", "1", "--cpu-seconds", "1", "--e2e-blocks", "4", "--parity-every", "8"]
     r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -201,3 +203,8 @@ def test_bench_gpus_2_self_launched(tmp_path):
     assert res["parity"]["files_checked"] >= 4 * 1024 and res["parity"]["mismatches"] == 0
     assert res["parity"]["verdicts_all_ok"]
     assert "starting 2 ranks" in r.stderr
+    cb = res["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] == 1 and cb["allcore"]["cores"] >= 1 and "rank 0 of 2" in cb["run"]
+    kr = res["roofline"]["kernel_ms_per_rank"]
+    assert len(kr["ms"]) == 2 and kr["min"] <= kr["max"] and res["roofline"]["kernel_ms_avg"] == kr["max"]
+    assert "in turn" in res["end_to_end"]["roofline"]["peak_source"]

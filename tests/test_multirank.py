@@ -22,6 +22,8 @@ mine = bench.rank_blocks(1024 * world, world, rank)
 assert len(mine) == 1024 and (mine % world == rank).all()
 t = bench._max_over_ranks(dist, 1.0 + rank)
 assert t == float(world), t
+g = bench._gather_floats(dist, world, 10.0 + rank)  # per-rank kernel times of the roofline
+assert g == [10.0 + r for r in range(world)], g
 import torch
 allb = [None] * world
 dist.all_gather_object(allb, mine.tolist())
@@ -88,3 +90,20 @@ def test_bench_refuses_world_size_mismatch(world, gpus):
     assert r.returncode != 0
     assert "WORLD_SIZE=%d but --gpus %d" % (world, gpus) in r.stderr
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+@pytest.mark.parametrize("local_world", [1, 2, 8])
+def test_cpu_budget_split_by_local_world(monkeypatch, local_world):
+    """Legs every local rank runs at once (the parity oracle) get quota / LOCAL_WORLD_SIZE
+    CPUs, so N ranks never ask for N times the container's cpu.max quota; the
+    baseline leg (other ranks waiting at a barrier) keeps the whole budget."""
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", str(local_world))
+    whole = bench._cpu_budget()
+    share = bench._cpu_budget(shared=True)
+    assert whole >= 1 and 1 <= share <= whole
+    if local_world == 1:
+        assert share == whole
+    else:
+        assert share <= max(1, whole // local_world) or share == 1

@@ -72,7 +72,7 @@ EXPORTED = [
     "tfs_crc32_resident_stats", "tfs_crc32_error_count", "tfs_crc32_set_default_ctx", "tfs_crc32_bind_thread",
     "tfs_crc32_default_ctx", "tfs_crc32_set_cu_reserve", "tfs_crc32_throughput_grid", "tfs_crc32_sched_stats",
     "tfs_crc32_debug_state", "tfs_crc32_debug_poison_resident",
-    "tfs_crc32_set_split",
+    "tfs_crc32_set_split", "tfs_crc32_split_stats",
     "tfs_crc_group_create", "tfs_crc_group_destroy", "tfs_crc_group_last_error", "tfs_crc_group_size",
     "tfs_crc_group_ctx", "tfs_crc_group_member_of", "tfs_crc_group_ctx_for_block", "tfs_crc_group_numa_node",
     "tfs_crc_group_member_bound", "tfs_crc_group_host_malloc", "tfs_crc_group_host_free",
@@ -165,6 +165,9 @@ def lib(measure=False):
             "tfs_crc32_default_ctx": (vp, []),
             "tfs_crc32_set_cu_reserve": (ctypes.c_int, [vp, ctypes.c_int]),
             "tfs_crc32_set_split": (ctypes.c_int, [vp, ctypes.c_int]),
+            "tfs_crc32_split_stats": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64),
+                                                     ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32),
+                                                     ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
             "tfs_crc32_throughput_grid": (ctypes.c_int, [vp]),
             "tfs_crc32_sched_stats": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint32),
                                                      ctypes.POINTER(ctypes.c_uint64)]),
@@ -303,6 +306,15 @@ class Context:
     def set_split(self, on):
         """Split files > 128 KiB of throughput launches over several waves (on, the default) or not."""
         self._check(self.L.tfs_crc32_set_split(self.handle, 1 if on else 0), "set_split")
+
+    def split_stats(self):
+        """The latest split throughput launch: {launches, used, files, cap, grid, units} (waits for it)."""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        c, d, e = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        self._check(self.L.tfs_crc32_split_stats(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c),
+                                                 ctypes.byref(d), ctypes.byref(e)), "split_stats")
+        return {"launches": a.value, "used": b.value, "files": c.value, "cap": d.value, "grid": e.value,
+                "units": c.value + min(b.value, d.value)}
 
     def throughput_grid(self):
         """Workgroups the next throughput launch of this context would use."""

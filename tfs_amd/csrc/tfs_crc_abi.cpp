@@ -249,6 +249,7 @@ constexpr uint32_t kZeroCopyOutFiles = 65536;   // staged batches up to this man
 
 struct tfs_crc_ctx {
   int device = -1;
+  uint64_t id = 0;  // process-unique (live-context registry)
   hipStream_t stream = nullptr;
   // The latency path's streams (zero-copy small batches; the resident kernel's
   // res_stream) have the device's greatest priority: they never queue behind
@@ -286,15 +287,21 @@ struct tfs_crc_ctx {
   static constexpr int variant = 0;  // the product library holds one form of each kernel
 #endif
   unsigned cus = kMaxGrid;  // compute units of the device: throughput grids are at most this
-  // Split files (tfs_crc_device.h SplitArgs): one scratch per context, used by one
-  // throughput launch at a time: split_mu is held from the plan's setup to the
-  // event recorded after the fold, and a launch on another stream waits for it.
-  std::mutex split_mu;
-  DevBuf split_plan;
-  hipEvent_t split_done = nullptr;
-  bool split_pending = false;
-  bool cu_reserve = true;   // leave a live resident kernel's CUs out of throughput launches
-  bool split_files = true;  // throughput launches split files > kSplitMin (tfs_crc32_set_split)
+  // Split files (tfs_crc_device.h SplitArgs): one plan per scheduler slot, so a
+  // launch orders only behind the earlier launches of its own slot -- the same
+  // stream for an owned slot, the slot's previous lease (waited for by
+  // sched_acquire) for a foreign one -- and split launches on different streams
+  // overlap.  plan_mu[k] is held from the plan's setup to the launch.
+  DevBuf plans[kSchedSlots];
+  hipEvent_t plan_done[kSchedSlots] = {};  // behind the latest split launch of slot k
+  std::mutex plan_mu[kSchedSlots];
+  // The latest split launch (tfs_crc32_split_stats): its slot, stream, files and grid.
+  std::mutex last_split_mu;
+  int last_split_slot = -1;
+  uint32_t last_split_n = 0, last_split_cap = 0, last_split_grid = 0;
+  uint64_t split_launches = 0;
+  std::atomic<bool> cu_reserve{true};   // leave a live resident kernel's CUs out of throughput launches
+  std::atomic<bool> split_files{true};  // throughput launches split files > kSplitMin (tfs_crc32_set_split)
   std::atomic<uint32_t> inject_skip{0}, inject_count{0};  // tfs_crc32_inject_device_error
   DevBuf packet_scratch;  // device-resident packet calls (parse descriptors, verdicts)
   hipStream_t packet_scratch_stream = nullptr;
@@ -620,7 +627,7 @@ int resident_setup(tfs_crc_ctx* ctx) {
 // (one per XCD).
 unsigned throughput_cap(const tfs_crc_ctx* ctx) {
   const unsigned cap = ctx->cus < kMaxGrid ? ctx->cus : kMaxGrid;
-  if (!ctx->cu_reserve) return cap;
+  if (!ctx->cu_reserve.load(std::memory_order_relaxed)) return cap;
   const int64_t now = now_ns();
   unsigned held = 0;
   {
@@ -648,45 +655,64 @@ unsigned cap_for(const tfs_crc_ctx* ctx, uint32_t n) { return n <= kWgMaxFiles ?
     if (const int r2_ = sched_release((ctx), (st), lease_, le_, (what))) return r2_; \
   } while (0)
 
-// (Caller holds split_mu.)  The split plan for a throughput crc_files launch of
-// n files on st (tfs_crc_device.h: one allocation, up to cap ext units).
-int split_prepare(tfs_crc_ctx* ctx, hipStream_t st, uint32_t n, SplitArgs* sa) {
+// Scheduler slot index of a lease.
+uint32_t slot_index(const tfs_crc_ctx* ctx, const SchedLease& L) {
+  return uint32_t((L.slot - ctx->d_sched) / (kSchedSlotBytes / 4u));
+}
+
+// (Caller holds plan_mu[k].)  Slot k's split plan for a throughput crc_files
+// launch of n files on st (tfs_crc_device.h: one allocation, up to cap ext
+// units).  The earlier launches using this plan are ordered before st's: they
+// ran on st itself (owned slot) or were waited for when the slot was leased
+// (foreign slot).  Growing frees the plan, so st is drained first.
+int split_prepare(tfs_crc_ctx* ctx, hipStream_t st, uint32_t k, uint32_t n, SplitArgs* sa) {
   const uint32_t cap = uint32_t(std::min<uint64_t>(std::max<uint64_t>(2ull * n, 65536ull), kSplitMaxUnits));
   const uint64_t bytes = split_bytes(n, cap);
-  if (ctx->split_pending) {
-    // The previous split launch (maybe on another stream) still owns the plan:
-    // growing frees it, so wait for that launch; otherwise order after it.
-    if (bytes > ctx->split_plan.cap) HIP_TRY(ctx, hipEventSynchronize(ctx->split_done));
-    else HIP_TRY(ctx, hipStreamWaitEvent(st, ctx->split_done, 0));
-  }
-  HIP_TRY(ctx, ctx->split_plan.reserve(bytes));
-  if (!ctx->split_done) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->split_done, hipEventDisableTiming));
-  HIP_TRY(ctx, hipMemsetAsync(ctx->split_plan.p, 0, 8u, st));  // `used`
-  *sa = SplitArgs{static_cast<uint8_t*>(ctx->split_plan.p), cap};
+  DevBuf& plan = ctx->plans[k];
+  if (bytes > plan.cap && plan.p) HIP_TRY(ctx, hipStreamSynchronize(st));
+  HIP_TRY(ctx, plan.reserve(bytes));
+  HIP_TRY(ctx, hipMemsetAsync(plan.p, 0, 8u, st));  // `used`
+  *sa = SplitArgs{static_cast<uint8_t*>(plan.p), cap};
   return TFS_SUCCESS;
 }
 
 // A crc_files launch of n files on st (no completion flag): throughput launches
-// (n > kWgMaxFiles) get their split plan, a scheduler slot and the CU cap of
-// their device; batches of at most kWgMaxFiles files take the latency form.
+// (n > kWgMaxFiles) get a scheduler slot, that slot's split plan and the CU cap
+// of their device; batches of at most kWgMaxFiles files take the latency form.
 int files_launch(tfs_crc_ctx* ctx, hipStream_t st, int mode, const uint8_t* base, const Desc* desc, uint32_t n,
                  uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t vseed) {
-  std::unique_lock<std::mutex> lk(ctx->split_mu, std::defer_lock);
+  SchedLease lease;
+  if (const int r = sched_acquire(ctx, st, &lease)) return r;
+  const uint32_t k = slot_index(ctx, lease);
+  std::unique_lock<std::mutex> lk(ctx->plan_mu[k], std::defer_lock);
   SplitArgs sa{nullptr, 0u};
   const SplitArgs* split = nullptr;
-  if (n > kWgMaxFiles && ctx->split_files) {
+  int rc = TFS_SUCCESS;
+  if (n > kWgMaxFiles && ctx->split_files.load(std::memory_order_relaxed)) {
     lk.lock();
-    if (const int rc = split_prepare(ctx, st, n, &sa)) return rc;
-    split = &sa;
+    rc = split_prepare(ctx, st, k, n, &sa);
+    if (rc == TFS_SUCCESS) split = &sa;
   }
-  SCHED_LAUNCH(ctx, st, "crc_files",
-               launch_crc_files(mode, base, desc, n, ctx->d_tables, out_crc, out_ok, n_bad, sched, st, ctx->variant,
-                                vseed, nullptr, 0u, cap_for(ctx, n), split));
-  if (split) {
-    HIP_TRY(ctx, hipEventRecord(ctx->split_done, st));
-    ctx->split_pending = true;
+  const unsigned cap = cap_for(ctx, n);
+  const hipError_t le = rc == TFS_SUCCESS ? launch_crc_files(mode, base, desc, n, ctx->d_tables, out_crc, out_ok, n_bad,
+                                                             lease.slot, st, ctx->variant, vseed, nullptr, 0u, cap, split)
+                                          : hipSuccess;
+  if (split && le == hipSuccess) {
+    hipEvent_t& ev = ctx->plan_done[k];
+    if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ev = nullptr;
+    if (ev && hipEventRecord(ev, st) != hipSuccess) {
+      (void)hipEventDestroy(ev);
+      ev = nullptr;
+    }
+    std::lock_guard<std::mutex> g(ctx->last_split_mu);
+    ctx->last_split_slot = int(k);
+    ctx->last_split_n = n;
+    ctx->last_split_cap = sa.cap;
+    ctx->last_split_grid = cap;  // a split launch takes the whole capped grid (launch_variant)
+    ++ctx->split_launches;
   }
-  return TFS_SUCCESS;
+  const int r2 = sched_release(ctx, st, lease, le, "crc_files");
+  return rc != TFS_SUCCESS ? rc : r2;
 }
 
 // (Caller holds ctx->mu.)  Launch the resident kernel unless one is running.
@@ -1008,9 +1034,43 @@ tfs_crc_ctx* default_ctx(int* rc) {
 thread_local tfs_crc_ctx* t_scalar_ctx = nullptr;
 std::atomic<tfs_crc_ctx*> g_scalar_ctx{nullptr};
 
+// Live contexts and their ids: a thread binding names its context by
+// pointer and id, so a binding to a destroyed context is dropped on the thread's
+// next scalar call instead of being used, even if a new context reuses the
+// address.  The registry is consulted only after some context was destroyed
+// since the binding was last checked (one relaxed load on the common path).
+std::mutex g_live_mu;
+std::map<const tfs_crc_ctx*, uint64_t> g_live;
+std::atomic<uint64_t> g_ctx_ids{0}, g_destroy_epoch{0};
+thread_local uint64_t t_scalar_id = 0, t_scalar_epoch = 0;
+
+void live_add(const tfs_crc_ctx* c, uint64_t id) {
+  std::lock_guard<std::mutex> g(g_live_mu);
+  g_live[c] = id;
+}
+
+void live_remove(const tfs_crc_ctx* c) {
+  std::lock_guard<std::mutex> g(g_live_mu);
+  g_live.erase(c);
+  g_destroy_epoch.fetch_add(1, std::memory_order_release);
+}
+
+uint64_t live_id(const tfs_crc_ctx* c) {
+  std::lock_guard<std::mutex> g(g_live_mu);
+  auto it = g_live.find(c);
+  return it == g_live.end() ? 0 : it->second;
+}
+
 tfs_crc_ctx* scalar_ctx(int* rc) {
   if (rc) *rc = TFS_SUCCESS;
-  if (t_scalar_ctx) return t_scalar_ctx;
+  if (t_scalar_ctx) {
+    const uint64_t e = g_destroy_epoch.load(std::memory_order_acquire);
+    if (e != t_scalar_epoch) {
+      if (live_id(t_scalar_ctx) != t_scalar_id) t_scalar_ctx = nullptr;  // destroyed since it was bound
+      t_scalar_epoch = e;
+    }
+    if (t_scalar_ctx) return t_scalar_ctx;
+  }
   if (tfs_crc_ctx* c = g_scalar_ctx.load(std::memory_order_acquire)) return c;
   return default_ctx(rc);
 }
@@ -1051,6 +1111,8 @@ int tfs_crc32_ctx_create(int device, tfs_crc_ctx** out) {
   if (device < 0 || device >= ndev) return TFS_EXIT_PARAMETER_ERROR;
   auto* ctx = new tfs_crc_ctx();
   ctx->device = device;
+  ctx->id = g_ctx_ids.fetch_add(1, std::memory_order_relaxed) + 1;
+  live_add(ctx, ctx->id);
 #ifdef TFS_CRC_MEASURE
   if (const char* v = getenv("TFS_CRC_VARIANT")) ctx->variant = atoi(v);
 #endif
@@ -1103,9 +1165,10 @@ int tfs_crc32_ctx_create(int device, tfs_crc_ctx** out) {
 int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx) {
   if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
   {
-    tfs_crc_ctx* expect = ctx;  // no longer the scalar default (a thread binding is the caller's to clear)
+    tfs_crc_ctx* expect = ctx;  // no longer the scalar default; other threads' bindings drop it on next use
     g_scalar_ctx.compare_exchange_strong(expect, nullptr);
     if (t_scalar_ctx == ctx) t_scalar_ctx = nullptr;
+    live_remove(ctx);
   }
   if (ctx->device >= 0) (void)hipSetDevice(ctx->device);
   resident_teardown(ctx);
@@ -1123,9 +1186,13 @@ int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx) {
     ev = nullptr;
   }
   ctx->packet_scratch.release();
-  if (ctx->split_done) (void)hipEventSynchronize(ctx->split_done);
-  ctx->split_plan.release();
-  if (ctx->split_done) (void)hipEventDestroy(ctx->split_done);
+  for (uint32_t k = 0; k < kSchedSlots; ++k) {  // split launches on any stream, callers' included
+    if (ctx->plan_done[k]) {
+      (void)hipEventSynchronize(ctx->plan_done[k]);
+      (void)hipEventDestroy(ctx->plan_done[k]);
+    }
+    ctx->plans[k].release();
+  }
   if (ctx->d_tables) (void)hipFree(ctx->d_tables);
   if (ctx->d_sched) (void)hipFree(ctx->d_sched);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -1136,7 +1203,7 @@ int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx) {
 
 const char* tfs_crc32_last_error(const tfs_crc_ctx* ctx) {
   if (!ctx) {
-    if (t_scalar_ctx) return t_scalar_ctx->last_error;
+    if (t_scalar_ctx && live_id(t_scalar_ctx) == t_scalar_id) return t_scalar_ctx->last_error;
     if (const tfs_crc_ctx* c = g_scalar_ctx.load()) return c->last_error;
     if (g_default) return g_default->last_error;
     return g_default_err.c_str();
@@ -1152,7 +1219,11 @@ int tfs_crc32_set_default_ctx(tfs_crc_ctx* ctx) {
 }
 
 int tfs_crc32_bind_thread(tfs_crc_ctx* ctx) {
+  const uint64_t id = ctx ? live_id(ctx) : 0;
+  if (ctx && id == 0) return TFS_EXIT_PARAMETER_ERROR;  // not a live context
   t_scalar_ctx = ctx;
+  t_scalar_id = id;
+  t_scalar_epoch = g_destroy_epoch.load(std::memory_order_acquire);
   return TFS_SUCCESS;
 }
 
@@ -1991,6 +2062,8 @@ int tfs_crc32_sync(tfs_crc_ctx* ctx) {
   if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  // the zero-copy small batches launched on the latency stream
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->lat_stream));
   return TFS_SUCCESS;
 }
 
@@ -2038,15 +2111,43 @@ int tfs_crc32_debug_poison_resident(tfs_crc_ctx* ctx, uint32_t done) {
 
 int tfs_crc32_set_cu_reserve(tfs_crc_ctx* ctx, int on) {
   if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
-  std::lock_guard<std::mutex> g(ctx->mu);
-  ctx->cu_reserve = on != 0;
+  ctx->cu_reserve.store(on != 0, std::memory_order_relaxed);
   return TFS_SUCCESS;
 }
 
 int tfs_crc32_set_split(tfs_crc_ctx* ctx, int on) {
   if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
-  std::lock_guard<std::mutex> g(ctx->split_mu);
-  ctx->split_files = on != 0;
+  ctx->split_files.store(on != 0, std::memory_order_relaxed);
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_split_stats(tfs_crc_ctx* ctx, uint64_t* launches, uint64_t* used, uint32_t* files, uint32_t* cap,
+                          uint32_t* grid) {
+  if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
+  int k;
+  uint32_t n, c, g;
+  uint64_t nl;
+  {
+    std::lock_guard<std::mutex> lg(ctx->last_split_mu);
+    k = ctx->last_split_slot;
+    n = ctx->last_split_n;
+    c = ctx->last_split_cap;
+    g = ctx->last_split_grid;
+    nl = ctx->split_launches;
+  }
+  uint64_t u = 0;
+  if (k >= 0) {
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    std::lock_guard<std::mutex> pg(ctx->plan_mu[k]);
+    if (!ctx->plan_done[k]) return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "split_stats: no event behind the plan");
+    HIP_TRY(ctx, hipEventSynchronize(ctx->plan_done[k]));
+    HIP_TRY(ctx, hipMemcpy(&u, ctx->plans[k].p, 8, hipMemcpyDeviceToHost));
+  }
+  if (launches) *launches = nl;
+  if (used) *used = u;
+  if (files) *files = n;
+  if (cap) *cap = c;
+  if (grid) *grid = g;
   return TFS_SUCCESS;
 }
 

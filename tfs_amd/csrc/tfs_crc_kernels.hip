@@ -2180,10 +2180,13 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
     return hipGetLastError();
   }
   if (!sched) return hipErrorInvalidValue;
-  const dim3 grid(grid_for(n, cap)), block(kBlock);
   // Split files (tfs_crc_device.h): the plan before the main kernel, the fold
   // after it, all on `stream`; the completion-flag form (done_flag) never splits.
   const SplitArgs sa = split && !done_flag ? *split : SplitArgs{nullptr, 0u};
+  // A split launch's work is its files plus the ext units the plan makes on the
+  // device (a few hundred 64 MiB files are ~150 k units), so it takes the whole
+  // capped grid; the tickets hand out any number of units.
+  const dim3 grid(sa.plan ? (cap < kMaxGrid ? cap : kMaxGrid) : grid_for(n, cap)), block(kBlock);
   if (sa.plan) {
     hipLaunchKernelGGL((split_plan_kernel<MODE>), dim3((n + 255u) / 256u), dim3(256), 0, stream, desc, n, vseed, sa);
     if (const hipError_t e = hipGetLastError()) return e;
