@@ -1,0 +1,167 @@
+"""bench.py --workload compact_device: SURVEY §8 f3, the compaction data pass
+(CompactTask::real_compact, src/dataserver/task.cpp:713-836) fused with the
+re-CRC on device-resident blocks."""
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+from benchlines.common import *  # noqa: F401,F403
+
+
+def bench_compact_device(args):
+    """the compaction data pass on device-resident blocks -- one
+    fused kernel re-CRCs every live record and writes it to its new offset
+    (one read + one write of live bytes), every live record of every resident
+    block in one tfs_compact_jobs_device launch (64-bit offsets)."""
+    import tfs_amd.crc as crc
+    world, rank, local, dist = _dist_init()
+    ctx = crc.Context(local)
+    nfiles, rec = FILES_PER_BLOCK, FILEINFO + FILE_SIZE
+    blk = nfiles * rec
+    nblocks = args.blocks
+    total = nblocks * blk
+    img = crc.DeviceBuffer(ctx, (total + 4095) // 4096 * 4096)
+    ctx.synth_fill_device(img, (total + 7) // 8 * 8, 0xC0DE + rank, 0)
+    n = nblocks * nfiles
+    desc = np.zeros(n, crc.DESC_DTYPE)
+    rec_off = np.arange(n, dtype=np.uint64) * rec
+    desc["offset"], desc["len"] = rec_off + FILEINFO, FILE_SIZE
+    d_desc = crc.DeviceBuffer(ctx, desc.nbytes).upload(desc)
+    d_crc = crc.DeviceBuffer(ctx, 4 * n)
+    ctx.batch_device(d_desc, n, img, d_crc)
+    d_roff = crc.DeviceBuffer(ctx, rec_off.nbytes).upload(rec_off)
+    d_len = crc.DeviceBuffer(ctx, 4 * n).upload(np.full(n, FILE_SIZE, np.uint32))
+    ctx.write_headers_device(img, d_roff, d_len, d_crc, 1, n)  # file id = 1 + global index
+    ctx.sync()
+    for b in (d_desc, d_roff, d_len):
+        b.free()
+    flags1 = _fragmented_flags(nfiles)
+    live1 = np.nonzero(flags1 == 0)[0]
+    d_bad = crc.DeviceBuffer(ctx, 4)
+    # The product form: every live record of every block in ONE launch
+    # (tfs_compact_jobs_device); block b's live records are packed into its own
+    # destination block at b * blk.
+    nlive1 = live1.size
+    jobs = np.zeros(nblocks * nlive1, crc.COMPACT_JOB_DTYPE)
+    bidx = np.repeat(np.arange(nblocks, dtype=np.uint64), nlive1)
+    loc = np.tile(np.arange(nlive1, dtype=np.uint64) * rec, nblocks)
+    jobs["src_offset"] = bidx * blk + np.tile(live1.astype(np.uint64) * rec, nblocks)
+    jobs["dest_offset"] = bidx * (nlive1 * rec) + loc
+    jobs["file_id"] = 1 + bidx * nfiles + np.tile(live1.astype(np.uint64), nblocks)
+    jobs["size"] = rec
+    jobs["new_offset"] = loc.astype(np.int32)
+    d_jobs = crc.DeviceBuffer(ctx, jobs.nbytes).upload(jobs)
+    d_jdst = crc.DeviceBuffer(ctx, nblocks * nlive1 * rec + 64)
+    d_jst = crc.DeviceBuffer(ctx, 4 * jobs.size)
+
+    def step_jobs(c):
+        c.compact_jobs_device(img, total, d_jobs, int(jobs.size), d_jdst, None, d_jst, d_bad)
+
+    d_bad.zero()
+    for _ in range(max(1, args.warmup)):
+        step_jobs(ctx)
+    ctx.sync()
+    if int(d_bad.download(np.uint32, 1)[0]) != 0:
+        raise SystemExit("compact_device: CRC mismatches on clean blocks")
+    # parity (test infrastructure): every (parity_every / 4)-th block's new block
+    # byte for byte against the oracle's real_compact restatement of its source
+    ora = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle_crc.so"))
+    ora.oracle_compact.restype = ctypes.c_int64
+    ora.oracle_compact.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint32] + [ctypes.c_void_p] * 4
+    mo = (np.arange(nfiles) * rec).astype(np.int64)
+    ms = np.full(nfiles, rec, np.int32)
+    odest = np.zeros(blk, np.uint8)
+    doff = np.zeros(nfiles, np.int64)
+    dsz = np.zeros(nfiles, np.int32)
+    ook = np.zeros(nfiles, np.uint8)
+    every = max(1, args.parity_every // 4)
+    blocks_checked = 0
+    for b in range(0, nblocks, every):
+        host = img.download(np.uint8, blk, b * blk)
+        wlen = ora.oracle_compact(host.ctypes.data, mo.ctypes.data, ms.ctypes.data, flags1.ctypes.data, nfiles,
+                                  odest.ctypes.data, doff.ctypes.data, dsz.ctypes.data, ook.ctypes.data)
+        # the bench writes flag_ = 0 for every live file (flags1 is 0 on live files) -> identical bytes
+        if wlen != nlive1 * rec or not (d_jdst.download(np.uint8, int(wlen), b * nlive1 * rec) == odest[:wlen]).all():
+            raise SystemExit("compact_device: GPU repack of block %d disagrees with oracle" % b)
+        blocks_checked += 1
+
+    def timed(c, fn):
+        ev0, ev1 = crc.Event(c), crc.Event(c)
+        if dist:
+            dist.barrier()
+        c.sync()
+        t0 = time.perf_counter()
+        ev0.record()
+        for _ in range(args.steps):
+            fn(c)
+        ev1.record()
+        c.sync()
+        if dist:
+            dist.barrier()
+        return _max_over_ranks(dist, time.perf_counter() - t0), ev0.elapsed_ms(ev1) / args.steps
+
+    el, kms = timed(ctx, step_jobs)
+    nlive = int(jobs.size)
+    live_bytes = float(nlive) * rec
+    algo = 2 * live_bytes + nlive * (40 + 4)  # read + write live records, 40 B CompactJob + 4 B status
+    live_payload = float(nlive) * FILE_SIZE
+    cd_traffic, cd_src = _pmc_traffic("profiles/r03/compact_device/pmc_summary.json",
+                                      "compact_pipe_kernel<true, true, false, 12, 5, 1, 0", nblocks == 1024)
+    res = {
+        "metric": "GiB/s of live payload compacted on the device (re-CRC + repack of live files)",
+        "value": world * args.steps * live_payload / el / 2**30, "unit": "GiB/s of live payload", "n_gpus": world,
+        "source_block_GiBs": world * args.steps * float(total) / el / 2**30,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic 64 KiB files, 1024 per block, evens + every 3rd of the rest deleted",
+        "config": {"workload": "SURVEY §8 f3: %d resident blocks, %d live files (%.1f GiB live)" % (
+            nblocks, nlive, live_bytes / 2**30)},
+        "parity": {"blocks_checked": blocks_checked, "mismatches": 0,
+                   "method": "every %d-th new block byte for byte against oracle_compact of its source" % every},
+        "roofline": {"bound": "hbm", "achieved": algo / (kms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": algo / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": cd_traffic, "traffic_source": cd_src, "traffic_measured_in_this_run": False, "traffic_note": TRAFFIC_NOTE,
+                     "kernel": "compact_pipe_kernel<WIDE> (one launch)", "kernel_ms_avg": kms,
+                     "algorithmic_bytes_per_launch": algo},
+    }
+    if rank == 0 and not args.no_cpu:
+        # CPU restatement of real_compact + re-CRC (oracle_compact) over block 0 of the same image, one thread
+        ora = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle_crc.so"))
+        ora.oracle_compact.restype = ctypes.c_int64
+        ora.oracle_compact.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint32] + [ctypes.c_void_p] * 4
+        src = img.download(np.uint8, blk)
+        mo = np.arange(nfiles, dtype=np.int64) * rec
+        ms = np.full(nfiles, rec, np.int32)
+        odest = np.zeros(blk, np.uint8)
+        doff = np.zeros(nfiles, np.int64)
+        dsz = np.zeros(nfiles, np.int32)
+        ook = np.zeros(nfiles, np.uint8)
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            ora.oracle_compact(src.ctypes.data, mo.ctypes.data, ms.ctypes.data, flags1.ctypes.data, nfiles,
+                               odest.ctypes.data, doff.ctypes.data, dsz.ctypes.data, ook.ctypes.data)
+            reps += 1
+            if time.perf_counter() - t0 >= args.cpu_seconds:
+                break
+        dt = time.perf_counter() - t0
+        if not (ook[flags1 == 0] == 1).all():
+            raise SystemExit("compact_device: oracle re-CRC disagrees with the GPU-written headers")
+        res["cpu_baseline"] = {
+            "value": reps * len(live1) * FILE_SIZE / dt / 2**30, "unit": "GiB/s of live payload", "cores": 1,
+            "kind": "port", "source_block_GiBs": reps * blk / dt / 2**30,
+            "sample": "%d compactions of resident block 0 copied to host (re-CRC of %d live files + repack), "
+                      "oracle_compact single thread, %.1f s" % (reps, len(live1), dt),
+            "allcore": _compact_allcore(ora, [src.ctypes.data], mo, ms, flags1, nfiles, blk, None,
+                                        len(live1) * FILE_SIZE, blk, min(3.0, args.cpu_seconds))}
+    if dist and not args.no_cpu:
+        dist.barrier()
+    emit(rank, res)
+    for b in (img, d_crc, d_bad, d_jobs, d_jdst, d_jst):
+        b.free()
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+

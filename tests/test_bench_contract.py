@@ -50,8 +50,9 @@ def test_default_line_contract_small():
 def test_zipf_and_compact_lines_carry_cpu_baseline():
     z = _run(["--workload", "zipf", "--blocks", "8", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0.3"])
     assert z["roofline"]["bound"] == "hbm" and z["cpu_baseline"]["value"] > 0
+    assert z["parity"]["files_checked"] > 100 and z["parity"]["mismatches"] == 0
     c = _run(["--workload", "compact", "--compact-blocks", "16", "--cpu-seconds", "0.3"])
-    assert c["value"] > 0 and c["cpu_baseline"]["kind"] == "port" and c["ab"]["speedup"] > 0
+    assert c["value"] > 0 and c["cpu_baseline"]["kind"] == "port"
     assert c["unit"] == "GiB/s of live payload" and c["source_block_GiBs"] > c["value"]
     assert c["roofline"]["bound"] == "pcie" and 0 < c["roofline"]["frac"] < 1.2
     assert c["cpu_baseline"]["allcore"]["value"] > 0 and c["cpu_baseline"]["allcore"]["cores"] >= 1
