@@ -89,6 +89,39 @@ def test_scalar_context_selectable_per_process_and_thread(oracle):
     assert L.tfs_crc32_default_ctx() not in (None, 0)  # back to device 0's own default
 
 
+def test_thread_binding_to_a_destroyed_context_is_dropped(oracle):
+    """a context destroyed on another thread no longer leaves this
+    thread's binding dangling -- the next scalar call finds it gone and runs on the
+    process default; binding a context that is not live is refused."""
+    import tfs_amd.crc as crc
+    L = crc.lib()
+    data = synth_bytes(1602, 65536).tobytes()
+    want = ocrc(oracle, 3, data)
+    a = crc.Context(0)
+    stale = a.handle.value
+    res = {}
+    go, done = threading.Event(), threading.Event()
+
+    def worker():
+        L.tfs_crc32_bind_thread(a.handle)
+        res["bound"] = (L.tfs_crc32_default_ctx(), crc.func_crc(3, data))
+        go.set()
+        done.wait(60)
+        res["after"] = (L.tfs_crc32_default_ctx(), crc.func_crc(3, data), _scalar_e(L, 3, data))
+        L.tfs_crc32_bind_thread(None)
+
+    t = threading.Thread(target=worker)
+    t.start()
+    assert go.wait(60)
+    a.close()  # destroyed on this thread while the worker is still bound to it
+    done.set()
+    t.join(120)
+    assert res["bound"] == (stale, want)
+    d, v, ve = res["after"]
+    assert d not in (None, 0) and v == want and ve == (want, 0)
+    assert L.tfs_crc32_bind_thread(ctypes.c_void_p(stale)) == -1016  # TFS_EXIT_PARAMETER_ERROR: not live
+
+
 def test_packet_decode_device_error_is_not_a_crc_mismatch(oracle):
     """BasePacket::decode's CRC check (base_packet.cpp:141) through the batched
     receive path and the C++ PacketDecoder: an injected device error is -20001."""

@@ -35,7 +35,10 @@ __device__ __forceinline__ uint32_t xand(uint32_t acc, uint32_t in, uint32_t m) 
   return __builtin_amdgcn_bitop3_b32(acc, in, m, 0x78);
 }
 
-template <int OG>
+// MATH = false (measurement build, TFS_EC_VARIANT 7): the same loads, stores and
+// schedule with one XOR per output row instead of the bitmatrix product -- the
+// kernel's memory shape without its VALU work (wrong parity: timing only).
+template <int OG, bool MATH = true>
 __global__ void __launch_bounds__(256) ec_apply_kernel(EcArgs a, const uint32_t* __restrict__ masks) {
   const int lane = threadIdx.x & 63;
   const uint32_t u = uint32_t(lane) >> 4;
@@ -66,6 +69,11 @@ __global__ void __launch_bounds__(256) ec_apply_kernel(EcArgs a, const uint32_t*
       for (int o = 0; o < OG; ++o)
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
+          if constexpr (!MATH) {
+            acc[o][r].x ^= in[r].x;
+            acc[o][r].y ^= in[r].y;
+            continue;
+          }
           const uint32_t* m = masks + ((uint32_t(o) * 8u + uint32_t(r)) * a.S + s) * 8u;
 #pragma unroll
           for (int c = 0; c < 8; ++c) {
@@ -168,7 +176,7 @@ static void launch_chunk(const EcArgs& a, int og, dim3 g, dim3 b, hipStream_t st
 // The product: the grid-stride tile kernel.  Measurement build (TFS_EC_VARIANT
 // 1, 2, 3): the chunked form with K = 2, 4, 8 tiles per wave step; 4, 6: the
 // product's kernel over 8,192 / 2,048 workgroups striding (the product launches
-// one grid step per wave).
+// one grid step per wave); 7: the product's shape without the bitmatrix product.
 hipError_t launch_ec_apply(const EcArgs& a, int og, int variant, hipStream_t stream) {
   if (a.units == 0) return hipSuccess;
   const uint64_t ntiles = (a.units + 3) / 4;
@@ -197,6 +205,17 @@ hipError_t launch_ec_apply(const EcArgs& a, int og, int variant, hipStream_t str
 #endif
   if (blocks > cap) blocks = cap;
   const dim3 g(static_cast<unsigned>(blocks)), b(256);
+#ifdef TFS_CRC_MEASURE
+  if (variant == 7) {  // measurement: the memory shape without the bitmatrix product
+    switch (og) {
+      case 1: hipLaunchKernelGGL((ec_apply_kernel<1, false>), g, b, 0, stream, a, a.masks); break;
+      case 2: hipLaunchKernelGGL((ec_apply_kernel<2, false>), g, b, 0, stream, a, a.masks); break;
+      case 3: hipLaunchKernelGGL((ec_apply_kernel<3, false>), g, b, 0, stream, a, a.masks); break;
+      default: hipLaunchKernelGGL((ec_apply_kernel<4, false>), g, b, 0, stream, a, a.masks); break;
+    }
+    return hipGetLastError();
+  }
+#endif
   switch (og) {
     case 1: hipLaunchKernelGGL(ec_apply_kernel<1>, g, b, 0, stream, a, a.masks); break;
     case 2: hipLaunchKernelGGL(ec_apply_kernel<2>, g, b, 0, stream, a, a.masks); break;

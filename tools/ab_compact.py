@@ -75,8 +75,12 @@ def main():
             "dst16": k * 65584 + (soff & np.uint64(15)),         # delta == 0 mod 16: no lane shift
             "dst128": k * 65664 + (soff & np.uint64(127)),       # delta == 0 mod 128: whole lines per stripe
             "shift1": k * rec + np.uint64(1)}                    # delta == 1 mod 4: the unaligned copy
+    # AB_SPLIT=S[,S...] (probe for a segmented record kernel): every live record cut
+    # into consecutive pieces of about S bytes, each run as its own job -- the
+    # kernel's cost per piece and the tighter address window of S-byte units, no
+    # fold (the pieces' FileInfo checks fail: timing only)
+    splits = [int(x) for x in os.environ.get("AB_SPLIT", "").split(",") if x]
     d_dst = crc.DeviceBuffer(ctx, int(k.size) * 65664 + 256)
-    d_st = crc.DeviceBuffer(ctx, 4 * int(k.size))
     d_bad = crc.DeviceBuffer(ctx, 4)
     jobsets = {}
     for name, do in dsts.items():
@@ -86,6 +90,20 @@ def main():
         j["size"] = rec
         j["new_offset"] = (do % np.uint64(1 << 31)).astype(np.int32)
         jobsets[name] = crc.DeviceBuffer(ctx, j.nbytes).upload(j)
+    for S in splits:
+        npc = (rec + S - 1) // S
+        psz = (rec + npc - 1) // npc
+        sizes = np.full(npc, psz, np.int64)
+        sizes[-1] = rec - psz * (npc - 1)
+        po = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+        j = np.zeros(k.size * npc, crc.COMPACT_JOB_DTYPE)
+        j["src_offset"] = (soff[:, None] + po[None, :]).reshape(-1)
+        j["dest_offset"] = (dsts["packed"][:, None] + po[None, :]).reshape(-1)
+        j["file_id"] = 1
+        j["size"] = np.tile(sizes, k.size)
+        j["new_offset"] = (j["dest_offset"] % np.uint64(1 << 31)).astype(np.int32)
+        jobsets["split%d" % S] = crc.DeviceBuffer(ctx, j.nbytes).upload(j)
+        jobsets["split%d" % S].njobs = int(j.size)
     want = [int(x) for x in os.environ.get("AB_VARIANTS", "27,25,26,29,30,31,32").split(",") if x]
     ctxs = {0: ctx}
     for v in want:
@@ -95,6 +113,8 @@ def main():
              [(v, "dst128") for v in want if v in (65, 66, 67, 68, 69, 70, 71)])
     if 31 in want or 32 in want:
         cases += [(0, "shift1")] + [(v, "shift1") for v in want if v in (31, 32)]
+    cases += [(0, "split%d" % S) for S in splits]
+    d_st = crc.DeviceBuffer(ctx, 4 * max([int(k.size)] + [getattr(b, "njobs", 0) for b in jobsets.values()]))
     # verify-on-read of every record of the resident blocks (tfs_blocks_verify_device)
     allj = np.zeros(n, crc.COMPACT_JOB_DTYPE)
     allj["src_offset"], allj["file_id"], allj["size"] = rec_off, 1 + np.arange(n, dtype=np.uint64), rec
@@ -107,7 +127,7 @@ def main():
     # correctness of the product cases (the diagnostic variants 26 and 30 compute
     # no CRCs / skip stores)
     for v, js in cases:
-        if v in (26, 30, 61, 64, 65, 66, 67, 68, 69, 70, 71):
+        if v in (26, 30, 61, 64, 65, 66, 67, 68, 69, 70, 71) or js.startswith("split"):
             continue
         d_bad.zero()
         ctxs[v].compact_jobs_device(img, total, jobsets[js], nj, d_dst, None, d_st, d_bad)
@@ -142,10 +162,11 @@ def main():
         for v, js in cases:
             c = ctxs[v]
             e0, e1 = crc.Event(c), crc.Event(c)
-            c.compact_jobs_device(img, total, jobsets[js], nj, d_dst, None, d_st, d_bad)
+            nn = getattr(jobsets[js], "njobs", nj)
+            c.compact_jobs_device(img, total, jobsets[js], nn, d_dst, None, d_st, d_bad)
             e0.record()
             for _ in range(3):
-                c.compact_jobs_device(img, total, jobsets[js], nj, d_dst, None, d_st, d_bad)
+                c.compact_jobs_device(img, total, jobsets[js], nn, d_dst, None, d_st, d_bad)
             e1.record()
             c.sync()
             times["%d_%s" % (v, js)].append(e0.elapsed_ms(e1) / 3)
