@@ -8,12 +8,18 @@ and many-block forms, and zero-copy host images."""
 import numpy as np
 import pytest
 
+from conftest import ocrc
 from test_gpu_parity import _block_image, _oracle_compact
+
+
+def ocrc_payload(oracle, img, meta):
+    o = int(meta["offset"]) + 36
+    return ocrc(oracle, 0, img[o:o + int(meta["size"]) - 36].tobytes())
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[0, 22, 23, 25, 27, 29, 31, 32, 33, 35, 36, 37, 39, 40, 42, 43, 45, 60, 62, 63])
+@pytest.fixture(params=[0, 22, 23, 25, 27, 29, 31, 32, 33, 35, 36, 37, 39, 40, 42, 43, 45, 60, 62, 63, 72, 73, 74])
 def vctx(request, monkeypatch):
     import tfs_amd.crc as crc
     monkeypatch.setenv("TFS_CRC_VARIANT", str(request.param))
@@ -123,6 +129,71 @@ def test_jobs_device_many_blocks_shuffled(vctx, oracle):
     for base, od in expect:
         assert (out[base:base + od.size] == od).all()
     assert int(d_bad.download(np.uint32, 1)[0]) == 0 and (d_st.download(np.int32, len(j)) == 0).all()
+
+
+def test_jobs_device_statuses_and_split_records(vctx, oracle):
+    """tfs_compact_jobs_device over records of every size class (many longer than
+    the 8 / 16 / 32 KiB segments of the segmented forms 72-74, including exact
+    multiples and one byte past them), with rejected records on both short and
+    long records: FileInfo id, FileInfo size, payload CRC (in a later segment and
+    in the head), too short, past the image.  Statuses in the reference's order,
+    CRCs of every checked record equal to the oracle's, good records byte-exact."""
+    import tfs_amd.crc as crc
+    rng = np.random.default_rng(330)
+    sizes = [int(x) for x in rng.choice([1, 33, 1024, 8191, 8192, 8193, 16384, 16385, 32768, 32769, 65536, 70001,
+                                          200000, 300001], 160)]
+    sizes[:6] = [8193, 16385, 32769, 98304, 98305, 262144]
+    img, metas = _block_image(oracle, sizes, seed=331)
+    n = len(sizes)
+    fl = np.zeros(n, np.int32)
+    odest, doff, ook = _oracle_compact(oracle, img, metas, fl)
+    crcs = np.array([ocrc_payload(oracle, img, metas[k]) for k in range(n)], np.uint32)
+    j = np.zeros(n, crc.COMPACT_JOB_DTYPE)
+    j["src_offset"], j["dest_offset"] = metas["offset"], doff
+    j["file_id"], j["size"], j["new_offset"] = metas["file_id"], metas["size"], doff
+    big = [k for k in range(n) if sizes[k] > 40000]
+    bad = {}
+    img2 = img.copy()
+    j["file_id"][big[0]] += 7                                  # id mismatch on a long record
+    bad[big[0]] = -8016
+    img2[int(metas[big[1]]["offset"]) + 12] ^= 1               # FileInfo.size_ mismatch on a long record
+    bad[big[1]] = -8038
+    img2[int(metas[big[2]]["offset"]) + 36 + sizes[big[2]] - 5] ^= 0x10   # CRC: last segment
+    bad[big[2]] = -1010
+    img2[int(metas[big[3]]["offset"]) + 36 + 2] ^= 0x01        # CRC: head bytes
+    bad[big[3]] = -1010
+    j["size"][10] = 30                                         # shorter than a FileInfo
+    bad[10] = -8034
+    j["src_offset"][11] = img.size - 100                       # past the image
+    bad[11] = -1016
+    d_src = crc.DeviceBuffer(vctx, img2.size + 64).upload(img2)
+    d_j = crc.DeviceBuffer(vctx, j.nbytes).upload(j)
+    d_dst = crc.DeviceBuffer(vctx, odest.size + 64)
+    d_dst.zero()
+    d_st = crc.DeviceBuffer(vctx, 4 * n)
+    d_c = crc.DeviceBuffer(vctx, 4 * n)
+    d_bad = crc.DeviceBuffer(vctx, 4)
+    for rep in range(2):  # twice on one stream: the plan and the slot are reused
+        d_bad.zero()
+        vctx.compact_jobs_device(d_src, img2.size, d_j, n, d_dst, d_c, d_st, d_bad)
+        vctx.sync()
+        st = d_st.download(np.int32, n)
+        c = d_c.download(np.uint32, n)
+        out = d_dst.download(np.uint8, odest.size)
+        for k in range(n):
+            assert st[k] == bad.get(k, 0), (rep, k, sizes[k], st[k])
+            if k in (10, 11):
+                continue
+            if bad.get(k) == -1010:
+                pl = img2[int(metas[k]["offset"]) + 36:int(metas[k]["offset"]) + 36 + sizes[k]]
+                assert c[k] == ocrc(oracle, 0, pl.tobytes()), (rep, k)
+            else:
+                assert c[k] == crcs[k], (rep, k, sizes[k])
+            if k in bad:
+                continue
+            o, sz = int(doff[k]), int(metas[k]["size"])
+            assert (out[o:o + sz] == odest[o:o + sz]).all(), (rep, k, sizes[k])
+        assert int(d_bad.download(np.uint32, 1)[0]) == len(bad)
 
 
 def test_zero_copy_host_images(vctx, oracle):

@@ -46,7 +46,7 @@ hipError_t launch_compact_fused(const uint8_t* src, uint64_t src_len, const RawM
                                 int variant, unsigned cap);
 hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const CompactJob* jobs, uint32_t n, uint8_t* dst,
                                const Tables* tg, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
-                               uint32_t* sched, hipStream_t stream, int variant, unsigned cap);
+                               uint32_t* sched, hipStream_t stream, int variant, unsigned cap, const CSegArgs* seg);
 #ifdef TFS_CRC_MEASURE
 hipError_t launch_block_verify(const uint8_t* image, uint64_t image_len, const RawMeta* metas, uint32_t n,
                                const Tables* tg, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
@@ -302,6 +302,7 @@ struct tfs_crc_ctx {
   uint64_t split_launches = 0;
   std::atomic<bool> cu_reserve{true};   // leave a live resident kernel's CUs out of throughput launches
   std::atomic<bool> split_files{true};  // throughput launches split files > kSplitMin (tfs_crc32_set_split)
+  uint32_t cseg_lg = 0;  // segmented compaction: 1 KiB << cseg_lg segments, 0 = whole records
   std::atomic<uint32_t> inject_skip{0}, inject_count{0};  // tfs_crc32_inject_device_error
   DevBuf packet_scratch;  // device-resident packet calls (parse descriptors, verdicts)
   hipStream_t packet_scratch_stream = nullptr;
@@ -362,6 +363,7 @@ void build_tables(Tables* t) {
   }
   make_shift_table5(t->wg_jump, 16ull * (64ull * kWgWaves - 1ull));
   make_shift_table5(t->seg_shift, kSegBytes);
+  for (uint32_t lg = kCSegLgMin; lg <= kCSegLgMax; ++lg) make_shift_table5(t->cseg_shift[lg - kCSegLgMin], 1024ull << lg);
   for (int j = 0; j < kWgLevels; ++j) make_shift_table5(t->wg_level[j], 16ull << j);
 }
 
@@ -713,6 +715,33 @@ int files_launch(tfs_crc_ctx* ctx, hipStream_t st, int mode, const uint8_t* base
   }
   const int r2 = sched_release(ctx, st, lease, le, "crc_files");
   return rc != TFS_SUCCESS ? rc : r2;
+}
+
+// Segment size of the segmented compaction (tfs_crc_device.h CSegArgs) for ctx:
+// 1 KiB << lg, 0 = records stay whole.  Measurement build: TFS_CRC_VARIANT 72 /
+// 73 / 74 = 16 / 8 / 32 KiB segments.
+uint32_t cseg_lg(const tfs_crc_ctx* ctx) {
+#ifdef TFS_CRC_MEASURE
+  if (ctx->variant == 72) return 4u;
+  if (ctx->variant == 73) return 3u;
+  if (ctx->variant == 74) return 5u;
+#endif
+  return ctx->cseg_lg;
+}
+
+// (Caller holds plan_mu[k].)  Slot k's segmented-compaction plan for n jobs on st
+// (the same per-slot allocation and ordering rules as split_prepare).
+int cseg_prepare(tfs_crc_ctx* ctx, hipStream_t st, uint32_t k, uint32_t n, uint32_t lg, CSegArgs* cs) {
+  // room for 64 KiB records cut into segments, at least 64 K units, at most 16 M
+  const uint64_t per = std::max<uint64_t>(1u, 65536u >> (10u + lg));
+  const uint32_t cap = uint32_t(std::min<uint64_t>(std::max<uint64_t>(uint64_t(n) * per, 65536ull), 16ull << 20));
+  const uint64_t bytes = cseg_bytes(n, cap);
+  DevBuf& plan = ctx->plans[k];
+  if (bytes > plan.cap && plan.p) HIP_TRY(ctx, hipStreamSynchronize(st));
+  HIP_TRY(ctx, plan.reserve(bytes));
+  HIP_TRY(ctx, hipMemsetAsync(plan.p, 0, 8u, st));  // `used`
+  *cs = CSegArgs{static_cast<uint8_t*>(plan.p), cap, lg};
+  return TFS_SUCCESS;
 }
 
 // (Caller holds ctx->mu.)  Launch the resident kernel unless one is running.
@@ -1656,10 +1685,35 @@ int tfs_compact_jobs_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_le
   if (!ctx || (n && (!d_src || !d_jobs || !d_dest))) return TFS_EXIT_PARAMETER_ERROR;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  SCHED_LAUNCH(ctx, st, "compact_jobs", launch_compact_jobs(static_cast<const uint8_t*>(d_src), src_len,
-                                   reinterpret_cast<const CompactJob*>(d_jobs), n, static_cast<uint8_t*>(d_dest),
-                                   ctx->d_tables, d_out_crc, d_out_status, d_n_bad, sched, st, ctx->variant, throughput_cap(ctx)));
-  return TFS_SUCCESS;
+  if (n == 0) return TFS_SUCCESS;
+  SchedLease lease;
+  if (const int r = sched_acquire(ctx, st, &lease)) return r;
+  const uint32_t k = slot_index(ctx, lease);
+  std::unique_lock<std::mutex> lk(ctx->plan_mu[k], std::defer_lock);
+  CSegArgs cs{nullptr, 0u, 0u};
+  int rc = TFS_SUCCESS;
+  const uint32_t lg = cseg_lg(ctx);
+  if (lg) {
+    lk.lock();
+    rc = cseg_prepare(ctx, st, k, n, lg, &cs);
+  }
+  const hipError_t le =
+      rc == TFS_SUCCESS ? launch_compact_jobs(static_cast<const uint8_t*>(d_src), src_len,
+                                              reinterpret_cast<const CompactJob*>(d_jobs), n,
+                                              static_cast<uint8_t*>(d_dest), ctx->d_tables, d_out_crc, d_out_status,
+                                              d_n_bad, lease.slot, st, ctx->variant, throughput_cap(ctx),
+                                              cs.plan ? &cs : nullptr)
+                        : hipSuccess;
+  if (cs.plan && le == hipSuccess) {
+    hipEvent_t& ev = ctx->plan_done[k];
+    if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ev = nullptr;
+    if (ev && hipEventRecord(ev, st) != hipSuccess) {
+      (void)hipEventDestroy(ev);
+      ev = nullptr;
+    }
+  }
+  const int r2 = sched_release(ctx, st, lease, le, "compact_jobs");
+  return rc != TFS_SUCCESS ? rc : r2;
 }
 
 int tfs_block_compact(tfs_crc_ctx* ctx, const void* src_image, uint64_t src_len, const tfs_raw_meta* metas,

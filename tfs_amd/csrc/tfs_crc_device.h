@@ -188,6 +188,36 @@ constexpr uint64_t split_off_ext_crc(uint32_t n) { return 16u + 8ull * n; }
 constexpr uint64_t split_off_ext(uint32_t n, uint32_t cap) { return (16u + 8ull * n + 4ull * cap + 15u) & ~15ull; }
 constexpr uint64_t split_bytes(uint32_t n, uint32_t cap) { return split_off_ext(n, cap) + 16ull * cap; }
 
+// Segmented compaction (round 4): a throughput compaction launch
+// cuts every live record whose payload is longer than one segment into a ragged
+// head (the FileInfo and the first len - K*seg payload bytes, in the record's own
+// ticket slot) and K whole `seg`-byte payload segments appended after the jobs as
+// extra units, so the waves of a launch copy and checksum segment-sized pieces
+// (a tighter window of addresses in flight than one wave per record);
+// compact_seg_fold_kernel joins each record's CRCs and writes its CRC / status.
+// Plan (one allocation per scheduler slot, like SplitArgs):
+// [used u64 | pad][base u32 x n][head_crc u32 x n][hdr_crc u32 x n][pre i32 x n]
+// [ext_crc u32 x cap][pad to 16][CSegUnit x cap]
+struct CSegArgs {
+  uint8_t* plan;  // nullptr: records stay whole
+  uint32_t cap;   // ext units at most (records past it stay whole)
+  uint32_t lg;    // seg = 1 KiB << lg (lg 3..5: 8, 16, 32 KiB)
+};
+struct CSegUnit {  // one whole payload segment of a split record
+  uint64_t src, dst;  // payload byte offsets in the source / destination images
+  uint32_t len, job;
+  uint64_t pad;
+};
+static_assert(sizeof(CSegUnit) == 32, "segment unit layout");
+constexpr uint32_t kCSegLgMin = 3, kCSegLgMax = 5;
+constexpr uint64_t cseg_off_base() { return 16u; }
+constexpr uint64_t cseg_off_head(uint32_t n) { return 16u + 4ull * n; }
+constexpr uint64_t cseg_off_hdr(uint32_t n) { return 16u + 8ull * n; }
+constexpr uint64_t cseg_off_pre(uint32_t n) { return 16u + 12ull * n; }
+constexpr uint64_t cseg_off_ext_crc(uint32_t n) { return 16u + 16ull * n; }
+constexpr uint64_t cseg_off_ext(uint32_t n, uint32_t cap) { return (16u + 16ull * n + 4ull * cap + 15u) & ~15ull; }
+constexpr uint64_t cseg_bytes(uint32_t n, uint32_t cap) { return cseg_off_ext(n, cap) + 32ull * cap; }
+
 // Device-resident constant tables (built on the host by crc_math.h).
 struct Tables {
   uint32_t slice[4][256];                          // slice-by-4 (slice k: byte then k zero bytes)
@@ -200,6 +230,7 @@ struct Tables {
   uint32_t wg_jump[kShiftChunks][32];              // latency form: shift(c, 16 * (64 * kWgWaves - 1))
   uint32_t wg_level[kWgLevels][kShiftChunks][32];  // latency form: shift(c, 16 * 2^j)
   uint32_t seg_shift[kShiftChunks][32];            // split files: shift(c, kSegBytes)
+  uint32_t cseg_shift[kCSegLgMax - kCSegLgMin + 1][kShiftChunks][32];  // segmented compaction: shift(c, 1 KiB << lg)
 };
 
 constexpr int run_index(int run) { return run == 16 ? 0 : run == 32 ? 1 : run == 64 ? 2 : 3; }

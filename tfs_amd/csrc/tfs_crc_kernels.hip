@@ -1661,6 +1661,8 @@ struct CRec {
   uint64_t soff, doff, fid;
   int32_t size, flag, new_off;
   int32_t pre;  // kSuccess, or the status decided before reading (size / range)
+  uint32_t plen;  // payload bytes this unit covers (size - 36 for a whole record)
+  uint32_t kind;  // 0 a whole record, 1 a payload segment of a split record, 2 a split record's head
 };
 
 template <bool WIDE, bool VERIFY = false>
@@ -1690,6 +1692,36 @@ __device__ __forceinline__ CRec load_crec(uint32_t f, uint64_t src_len, const Ra
   // compaction copies an empty file like any other (task.cpp:753-798).
   const bool short_rec = VERIFY ? r.size <= kFileInfoSize : r.size < kFileInfoSize;
   r.pre = short_rec ? kExitReadFileSizeError : (range_ok ? kSuccess : kExitParameterError);
+  r.plen = r.pre == kSuccess ? uint32_t(r.size - kFileInfoSize) : 0u;
+  r.kind = 0u;
+  return r;
+}
+
+// Unit f of a segmented compaction launch (CSegArgs): jobs [0, njobs) -- a split
+// record's job is its head (FileInfo + the ragged first payload bytes) -- then
+// the ext units, whole payload segments with no FileInfo.
+__device__ __forceinline__ CRec load_cunit(uint32_t f, uint32_t njobs, uint64_t src_len,
+                                           const CompactJob* __restrict__ jobs, const uint8_t* plan, uint32_t cap,
+                                           uint32_t lg) {
+  if (f < njobs) {
+    CRec r = load_crec<true>(f, src_len, nullptr, nullptr, nullptr, jobs);
+    if (plan && reinterpret_cast<const uint32_t*>(plan + cseg_off_base())[f] != kNoSplit) {
+      const uint32_t seg = 1024u << lg;
+      r.kind = 2u;
+      r.plen -= ((r.plen - 1u) >> (10u + lg)) * seg;
+    }
+    return r;
+  }
+  const CSegUnit u = reinterpret_cast<const CSegUnit*>(plan + cseg_off_ext(njobs, cap))[f - njobs];
+  CRec r;
+  r.soff = u.src - kFileInfoSize;  // a pseudo-record whose payload is the segment
+  r.doff = u.dst - kFileInfoSize;
+  r.fid = 0;
+  r.size = int32_t(u.len) + kFileInfoSize;
+  r.flag = r.new_off = 0;
+  r.pre = kSuccess;
+  r.plen = u.len;
+  r.kind = 1u;
   return r;
 }
 
@@ -1712,12 +1744,12 @@ __device__ __forceinline__ CState issue_crec(const CRec& r, const uint8_t* src, 
   CState s;
   if (r.pre == kSuccess) {
     const uint8_t* rec = src + r.soff;
-    s.hb = lane < kFileInfoSize ? uint32_t(rec[lane]) : 0u;
+    s.hb = lane < kFileInfoSize && r.kind != 1u ? uint32_t(rec[lane]) : 0u;
     s.delta = intptr_t(dst + r.doff) - intptr_t(rec);
     uint32_t aoff = 0u;
-    if (DA && r.soff + uint64_t(uint32_t(r.size)) + 128u <= src_len)
+    if (DA && r.soff + kFileInfoSize + uint64_t(r.plen) + 128u <= src_len)
       aoff = uint32_t(-(s.delta & ~intptr_t(15))) & 127u;
-    s.g = make_geo<kRun>(rec + kFileInfoSize, uint32_t(r.size - kFileInfoSize), 0u, aoff);
+    s.g = make_geo<kRun>(rec + kFileInfoSize, r.plen, 0u, aoff);
     s.h = load_head<kRun>(s.g, lane);
   } else {  // nothing is read for a record rejected up front
     s.hb = 0u;
@@ -1788,7 +1820,7 @@ __device__ __forceinline__ void copy_unaligned(const uint8_t* s, uint8_t* d, uin
 // (variants 33-35, 37: 6, 7, 8, 4).
 constexpr int kCompactDiag = 4 | 8;
 template <bool WIDE, bool DPPSH = true, bool VERIFY = false, int DIAG = kCompactDiag, int CPF = kPF, int CF = 1,
-          int TS = 0>
+          int TS = 0, bool SEG = false>
 __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __restrict__ src, uint64_t src_len,
                                                               const RawMeta* __restrict__ metas,
                                                               const int32_t* __restrict__ flags,
@@ -1796,7 +1828,7 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
                                                               const CompactJob* __restrict__ jobs, uint32_t n,
                                                               uint8_t* __restrict__ dst, const Tables* __restrict__ tg,
                                                               uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
-                                                              uint32_t* sched) {
+                                                              uint32_t* sched, CSegArgs cs) {
   constexpr bool DA = !VERIFY && (DIAG & 4) != 0;
   constexpr bool LNT = (DIAG & 8) && !VERIFY ? false : kNT;  // the verify form keeps the headline's loads
   constexpr int SK = (DIAG & 1) ? 0 : ((DIAG & 128) ? 2 : 1);  // copy-through store kind (st128_kind)
@@ -1806,6 +1838,18 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
   const LaneBase lb = lane_base_of(lane);
   const uint32_t wpb = kBlock / kWave;
   const uintptr_t junk = reinterpret_cast<uintptr_t>(tg->slice);
+  // SEG: units are the jobs, then the ext segments of the split records (CSegArgs)
+  const uint32_t njobs = n;
+  uint8_t* plan = nullptr;  // stays null when nothing was split
+  if (SEG && cs.plan) {
+    const unsigned long long used = *reinterpret_cast<const unsigned long long*>(cs.plan);
+    n = njobs + uint32_t(used < cs.cap ? used : cs.cap);
+    if (used) plan = cs.plan;
+  }
+  auto unit = [&](uint32_t u) -> CRec {
+    if constexpr (SEG) return load_cunit(u, njobs, src_len, jobs, plan, cs.cap, cs.lg);
+    return load_crec<WIDE, VERIFY>(u, src_len, metas, flags, dest_off, jobs);
+  };
   FileCursor<kIL, 1, CF, TS> fc;  // CF > 1: chunks of CF records per ticket (measurement)
   Tickets<kIL>& tk = fc.tk;
   fc.init(sched, n, blockIdx.x & 7u, gridDim.x * wpb,
@@ -1817,11 +1861,11 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
     uint32_t f = CF > 1 ? fc.take(lane) : tk.resolve(tk.issue(lane), lane);
     if (f >= n) break;
     uint32_t fn = CF > 1 ? fc.take(lane) : tk.resolve(tk.issue(lane), lane);
-    CRec cur = load_crec<WIDE, VERIFY>(f, src_len, metas, flags, dest_off, jobs);
+    CRec cur = unit(f);
     CState st = issue_crec<DA>(cur, src, src_len, dst, lane, junk);
     uint4 buf[CPF][kRun / 16];
     load_ring<kRun, CPF, LNT>(st.g, lane, buf, junk);
-    CRec nxt = fn < n ? load_crec<WIDE, VERIFY>(fn, src_len, metas, flags, dest_off, jobs) : CRec{};
+    CRec nxt = fn < n ? unit(fn) : CRec{};
     uint32_t jv = CF == 1 && fn < n ? tk.issue(lane) : 0u;
     for (;;) {
       // DIAG bit 5 (variant 31, measurement): byte-shifted records copy after the CRC (copy_unaligned)
@@ -1840,7 +1884,7 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
         load_ring<kRun, CPF, LNT>(ns.g, lane, buf, junk);
         fnn = CF > 1 ? fc.take(lane) : tk.resolve(jv, lane);
         if (fnn < n) {
-          nxt = load_crec<WIDE, VERIFY>(fnn, src_len, metas, flags, dest_off, jobs);
+          nxt = unit(fnn);
           if (CF == 1) jv = tk.issue(lane);
         }
       }
@@ -1848,9 +1892,9 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
       if (status == kSuccess) {
         const uint8_t* rec = src + cur.soff;
         uint8_t* drec = dst + cur.doff;
-        const uint32_t len = uint32_t(cur.size - kFileInfoSize);
+        const uint32_t len = cur.plen;
         // FileInfo with offset_(8) size_(12) usize_(16) flag_(28) rewritten, the rest copied (task.cpp:753-759)
-        if (!VERIFY && !(DIAG & 16) && lane < kFileInfoSize) {
+        if (!VERIFY && !(DIAG & 16) && lane < kFileInfoSize && cur.kind != 1u) {
           const int fld = lane >> 2, sh = 8 * (lane & 3);
           uint32_t b = st.hb;
           if (fld == 2) b = uint32_t(cur.new_off) >> sh;
@@ -1873,13 +1917,23 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
         }
         c = finish_file<kRun, kS8>(lds_tables, lb, st.g, st.h, c, lane);
         const uint64_t hid = uint64_t(hdr_dword(st.hb, 0)) | uint64_t(hdr_dword(st.hb, 1)) << 32;
-        if (hid != cur.fid) status = kExitFileInfoError;
+        if (cur.kind == 1u) {
+        } else if (hid != cur.fid) status = kExitFileInfoError;
         else if (int32_t(hdr_dword(st.hb, 3)) != cur.size) status = kExitSyncFileError;
-        else if (c != hdr_dword(st.hb, 8)) status = kExitCheckCrcError;
+        else if (cur.kind == 0u && c != hdr_dword(st.hb, 8)) status = kExitCheckCrcError;
+        if (SEG && cur.kind == 2u && lane == 0) {  // the fold decides the CRC check
+          reinterpret_cast<uint32_t*>(plan + cseg_off_head(njobs))[f] = c;
+          reinterpret_cast<uint32_t*>(plan + cseg_off_hdr(njobs))[f] = hdr_dword(st.hb, 8);
+          reinterpret_cast<int32_t*>(plan + cseg_off_pre(njobs))[f] = status;
+        }
       } else {
         c = 0u;
+        if (SEG && cur.kind == 2u && lane == 0) reinterpret_cast<int32_t*>(plan + cseg_off_pre(njobs))[f] = status;
       }
-      if (lane == 0) {
+      if (SEG && cur.kind == 1u) {
+        if (lane == 0) reinterpret_cast<uint32_t*>(plan + cseg_off_ext_crc(njobs))[f - njobs] = c;
+      } else if (SEG && cur.kind == 2u) {
+      } else if (lane == 0) {
         if (out_crc) out_crc[f] = c;
         if (out_status) out_status[f] = status;
         bad += status != kSuccess ? 1u : 0u;
@@ -1893,6 +1947,99 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
   } while (false);
   if (lane == 0 && bad && n_bad) atomicAdd(n_bad, bad);
   if (lane == 0) launch_exit(sched, gridDim.x * wpb, nullptr, 0u);
+}
+
+// Segmented compaction plan (CSegArgs): one thread per job.  A live record whose
+// payload is longer than one segment keeps its FileInfo and ragged first
+// len - K*seg payload bytes in its own slot and gets K ext units for its whole
+// segments, reserved as one range per workgroup (one atomic per 256 jobs); a
+// workgroup whose range would pass `cap` leaves its records whole (and writes
+// empty units into the part below cap).  Records the kernel rejects before
+// reading (short, out of range: load_crec) are never split.
+__global__ void __launch_bounds__(256) compact_seg_plan_kernel(const CompactJob* __restrict__ jobs, uint32_t n,
+                                                               uint64_t src_len, CSegArgs cs) {
+  __shared__ uint32_t wsum[4];
+  __shared__ unsigned long long blk_base;
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint32_t w = threadIdx.x / kWave;
+  const uint32_t seg = 1024u << cs.lg;
+  CompactJob j{};
+  uint32_t K = 0;
+  if (i < n) {
+    j = jobs[i];
+    const bool ok = j.size >= kFileInfoSize && j.src_offset + uint64_t(uint32_t(j.size)) <= src_len;
+    const uint32_t L = ok ? uint32_t(j.size - kFileInfoSize) : 0u;
+    K = L > seg ? (L - 1u) >> (10u + cs.lg) : 0u;
+  }
+  uint32_t x = K;  // inclusive scan over the wave
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, kWave);
+    if (lane >= o) x += y;
+  }
+  if (lane == kWave - 1) wsum[w] = x;
+  __syncthreads();
+  uint32_t before = 0, total = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    before += k < w ? wsum[k] : 0u;
+    total += wsum[k];
+  }
+  if (threadIdx.x == 0)
+    blk_base = total ? atomicAdd(reinterpret_cast<unsigned long long*>(cs.plan), (unsigned long long)total) : 0ull;
+  __syncthreads();
+  const unsigned long long b0 = blk_base;
+  const bool fits = b0 + total <= cs.cap;
+  const unsigned long long my = b0 + before + (x - K);
+  if (i < n) reinterpret_cast<uint32_t*>(cs.plan + cseg_off_base())[i] = (K && fits) ? uint32_t(my) : kNoSplit;
+  if (!K) return;
+  CSegUnit* ext = reinterpret_cast<CSegUnit*>(cs.plan + cseg_off_ext(n, cs.cap));
+  if (fits) {
+    const uint64_t head = uint64_t(uint32_t(j.size - kFileInfoSize)) - uint64_t(K) * seg;
+    const uint64_t s0 = j.src_offset + kFileInfoSize + head, d0 = j.dest_offset + kFileInfoSize + head;
+    for (uint32_t k = 0; k < K; ++k) ext[my + k] = CSegUnit{s0 + uint64_t(k) * seg, d0 + uint64_t(k) * seg, seg, i, 0u};
+  } else {
+    for (unsigned long long u = my; u < my + K && u < cs.cap; ++u) ext[u] = CSegUnit{0, 0, 0, 0, 0};
+  }
+}
+
+// Segmented compaction fold: each split record's CRC from its head and segment
+// CRCs (crc(A||B) = shift(crc(A), |B|) ^ crc(B), seed 0), then the record's CRC,
+// status (the head's FileInfo checks first, then the CRC against the stored
+// crc_) and mismatch count, as the record kernel writes them for whole records.
+__global__ void __launch_bounds__(256) compact_seg_fold_kernel(const CompactJob* __restrict__ jobs, uint32_t n,
+                                                               const Tables* __restrict__ tg, CSegArgs cs,
+                                                               uint32_t* out_crc, int32_t* out_status,
+                                                               uint32_t* n_bad) {
+  __shared__ uint32_t T[uint32_t(kShiftChunks) * 32u];
+  if (*reinterpret_cast<const unsigned long long*>(cs.plan) == 0ull) return;  // nothing was split
+  const uint32_t* base = reinterpret_cast<const uint32_t*>(cs.plan + cseg_off_base());
+  const uint32_t* head_crc = reinterpret_cast<const uint32_t*>(cs.plan + cseg_off_head(n));
+  const uint32_t* hdr_crc = reinterpret_cast<const uint32_t*>(cs.plan + cseg_off_hdr(n));
+  const int32_t* pre = reinterpret_cast<const int32_t*>(cs.plan + cseg_off_pre(n));
+  const uint32_t* ext_crc = reinterpret_cast<const uint32_t*>(cs.plan + cseg_off_ext_crc(n));
+  const uint32_t* tab = &tg->cseg_shift[cs.lg - kCSegLgMin][0][0];
+  for (uint32_t k = threadIdx.x; k < uint32_t(kShiftChunks) * 32u; k += blockDim.x) T[k] = tab[k];
+  __syncthreads();
+  uint32_t bad = 0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t b = base[i];
+    if (b == kNoSplit) continue;
+    const uint32_t K = (uint32_t(jobs[i].size - kFileInfoSize) - 1u) >> (10u + cs.lg);
+    uint32_t c = head_crc[i];
+    for (uint32_t k = 0; k < K; ++k) c = shift5(T, 0u, c) ^ ext_crc[b + k];
+    int32_t status = pre[i];
+    if (status == kSuccess && c != hdr_crc[i]) status = kExitCheckCrcError;
+    if (out_crc) out_crc[i] = c;
+    if (out_status) out_status[i] = status;
+    bad += status != kSuccess ? 1u : 0u;
+  }
+  if (n_bad) {  // one atomic per wave
+#pragma unroll
+    for (int m = kWave / 2; m >= 1; m >>= 1) bad += __shfl_xor(bad, m, kWave);
+    if ((threadIdx.x & (kWave - 1)) == 0 && bad) atomicAdd(n_bad, bad);
+  }
 }
 
 // Synthetic payload bytes: word i = splitmix64(seed + (first_word + i + 1) * GOLDEN)
@@ -2282,14 +2429,15 @@ hipError_t launch_compact_fused(const uint8_t* src, uint64_t src_len, const RawM
                        dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad);
   else if (variant == 23)
     hipLaunchKernelGGL((compact_pipe_kernel<false, false>), grid, dim3(kBlock), 0, stream, src, src_len, metas, flags,
-                       dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched);
+                       dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched, CSegArgs{nullptr, 0u, 0u});
   else if (variant == 27)
     hipLaunchKernelGGL((compact_pipe_kernel<false, true, false, 0>), grid, dim3(kBlock), 0, stream, src, src_len,
-                       metas, flags, dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched);
+                       metas, flags, dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched,
+                       CSegArgs{nullptr, 0u, 0u});
   else
 #endif
     hipLaunchKernelGGL(compact_pipe_kernel<false>, grid, dim3(kBlock), 0, stream, src, src_len, metas, flags,
-                       dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched);
+                       dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched, CSegArgs{nullptr, 0u, 0u});
   (void)variant;
   return hipGetLastError();
 }
@@ -2297,13 +2445,28 @@ hipError_t launch_compact_fused(const uint8_t* src, uint64_t src_len, const RawM
 // Compaction of many blocks (CompactJob, 64-bit offsets) in one launch.
 hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const CompactJob* jobs, uint32_t n, uint8_t* dst,
                                const Tables* tg, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
-                               uint32_t* sched, hipStream_t stream, int variant, unsigned cap) {
+                               uint32_t* sched, hipStream_t stream, int variant, unsigned cap, const CSegArgs* seg) {
   if (n == 0) return hipSuccess;
   if (!sched) return hipErrorInvalidValue;
+  if (seg && seg->plan) {
+    // Segmented form: plan, the record kernel over jobs + segments (the whole
+    // capped grid: the units are made on the device), fold -- all on `stream`.
+    const CSegArgs cs = *seg;
+    hipLaunchKernelGGL(compact_seg_plan_kernel, dim3((n + 255u) / 256u), dim3(256), 0, stream, jobs, n, src_len, cs);
+    if (const hipError_t e = hipGetLastError()) return e;
+    hipLaunchKernelGGL((compact_pipe_kernel<true, true, false, kCompactDiag, kPF, 1, 0, true>),
+                       dim3(cap < kMaxGrid ? cap : kMaxGrid), dim3(kBlock), 0, stream, src, src_len, nullptr, nullptr,
+                       nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad, sched, cs);
+    if (const hipError_t e = hipGetLastError()) return e;
+    const uint32_t fg = (n + 255u) / 256u;
+    hipLaunchKernelGGL(compact_seg_fold_kernel, dim3(fg < 1024u ? fg : 1024u), dim3(256), 0, stream, jobs, n, tg, cs,
+                       out_crc, out_status, n_bad);
+    return hipGetLastError();
+  }
   const dim3 grid(grid_for(n, cap));
 #define TFS_CJ(...)                                                                                                  \
   hipLaunchKernelGGL((compact_pipe_kernel<__VA_ARGS__>), grid, dim3(kBlock), 0, stream, src, src_len, nullptr, nullptr, \
-                     nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad, sched)
+                     nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad, sched, CSegArgs{nullptr, 0u, 0u})
 #ifdef TFS_CRC_MEASURE
   if (variant == 22)
     hipLaunchKernelGGL(compact_fused_kernel<true>, grid, dim3(kBlock), 0, stream, src, src_len, nullptr, nullptr,
@@ -2364,7 +2527,7 @@ hipError_t launch_block_verify_pipe(const uint8_t* image, uint64_t image_len, co
 #define TFS_BV(...)                                                                                                  \
   hipLaunchKernelGGL((compact_pipe_kernel<true, true, true, kCompactDiag, kPF, __VA_ARGS__>), grid, dim3(kBlock), 0, \
                      stream, image, image_len, nullptr, nullptr, nullptr, jobs, n, nullptr, tg, out_crc, out_status,   \
-                     n_bad, sched)
+                     n_bad, sched, CSegArgs{nullptr, 0u, 0u})
 #ifdef TFS_CRC_MEASURE
   if (jobs && variant == 39) TFS_BV(2, 0);
   else if (jobs && variant == 40) TFS_BV(4, 0);
@@ -2379,7 +2542,8 @@ hipError_t launch_block_verify_pipe(const uint8_t* image, uint64_t image_len, co
                        out_status, n_bad);
   else if (!jobs && variant == 50)
     hipLaunchKernelGGL((compact_pipe_kernel<false, true, true>), grid, dim3(kBlock), 0, stream, image, image_len, metas,
-                       nullptr, nullptr, nullptr, n, nullptr, tg, out_crc, out_status, n_bad, sched);
+                       nullptr, nullptr, nullptr, n, nullptr, tg, out_crc, out_status, n_bad, sched,
+                       CSegArgs{nullptr, 0u, 0u});
   else
 #endif
   if (jobs)
@@ -2387,7 +2551,7 @@ hipError_t launch_block_verify_pipe(const uint8_t* image, uint64_t image_len, co
   else
     hipLaunchKernelGGL((compact_pipe_kernel<false, true, true, kCompactDiag, kPF, kCF, kTS>), grid, dim3(kBlock), 0,
                        stream, image, image_len, metas, nullptr, nullptr, nullptr, n, nullptr, tg, out_crc, out_status,
-                       n_bad, sched);
+                       n_bad, sched, CSegArgs{nullptr, 0u, 0u});
 #undef TFS_BV
   (void)variant;
   return hipGetLastError();
