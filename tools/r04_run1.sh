@@ -5,6 +5,8 @@ set -u
 mkdir -p gpurun_out/r04
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
   tests/test_zipf_parity.py tests/test_split_files.py tests/test_scalar_and_streams.py \
+  tests/test_compaction_kernels.py::test_jobs_device_statuses_and_split_records \
+  tests/test_compaction_kernels.py::test_jobs_device_many_blocks_shuffled \
   > gpurun_out/r04/tests1.log 2>&1
 rc=$?
 echo "pytest rc=$rc"
