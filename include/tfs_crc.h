@@ -489,6 +489,13 @@ int tfs_crc32_set_cu_reserve(tfs_crc_ctx* ctx, int on);
  * GPU: one wave never streams a long file alone.  Results are
  * identical either way; on = 0 keeps every file on one wave (A/B). */
 int tfs_crc32_set_split(tfs_crc_ctx* ctx, int on);
+/* Device compaction (tfs_compact_jobs_device, and the block-file compactor that
+ * calls it) cuts every live record whose payload is longer than `seg_bytes` into a
+ * ragged head and whole seg_bytes payload segments that separate waves copy and
+ * checksum, then folds the segment CRCs into the record's CRC and status on the
+ * GPU.  seg_bytes: 8192, 16384 or 32768; 0 keeps every record on
+ * one wave.  Output bytes, CRCs and statuses are identical either way. */
+int tfs_crc32_set_compact_segment(tfs_crc_ctx* ctx, uint32_t seg_bytes);
 int tfs_crc32_throughput_grid(tfs_crc_ctx* ctx);
 /* Scheduler slots: ctx-owned streams bound (the ctx stream, compaction streams,
  * tfs_crc32_stream_create), and launches so far on streams the ctx does not own

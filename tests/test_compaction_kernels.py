@@ -132,6 +132,23 @@ def test_jobs_device_many_blocks_shuffled(vctx, oracle):
 
 
 def test_jobs_device_statuses_and_split_records(vctx, oracle):
+    _jobs_statuses_case(vctx, oracle)
+
+
+@pytest.mark.parametrize("seg", [8192, 16384, 32768, 0])
+def test_product_segmented_compaction_toggle(gpu_ctx, oracle, seg):
+    """The product library with tfs_crc32_set_compact_segment: every segment size
+    and back to whole records on the same context, same results."""
+    gpu_ctx.set_compact_segment(seg)
+    try:
+        _jobs_statuses_case(gpu_ctx, oracle)
+    finally:
+        gpu_ctx.set_compact_segment(0)
+    with pytest.raises(Exception):
+        gpu_ctx.set_compact_segment(12345)
+
+
+def _jobs_statuses_case(vctx, oracle):
     """tfs_compact_jobs_device over records of every size class (many longer than
     the 8 / 16 / 32 KiB segments of the segmented forms 72-74, including exact
     multiples and one byte past them), with rejected records on both short and

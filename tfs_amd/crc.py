@@ -72,7 +72,7 @@ EXPORTED = [
     "tfs_crc32_resident_stats", "tfs_crc32_error_count", "tfs_crc32_set_default_ctx", "tfs_crc32_bind_thread",
     "tfs_crc32_default_ctx", "tfs_crc32_set_cu_reserve", "tfs_crc32_throughput_grid", "tfs_crc32_sched_stats",
     "tfs_crc32_debug_state", "tfs_crc32_debug_poison_resident",
-    "tfs_crc32_set_split", "tfs_crc32_split_stats",
+    "tfs_crc32_set_split", "tfs_crc32_split_stats", "tfs_crc32_set_compact_segment",
     "tfs_crc_group_create", "tfs_crc_group_destroy", "tfs_crc_group_last_error", "tfs_crc_group_size",
     "tfs_crc_group_ctx", "tfs_crc_group_member_of", "tfs_crc_group_ctx_for_block", "tfs_crc_group_numa_node",
     "tfs_crc_group_member_bound", "tfs_crc_group_host_malloc", "tfs_crc_group_host_free",
@@ -165,6 +165,7 @@ def lib(measure=False):
             "tfs_crc32_default_ctx": (vp, []),
             "tfs_crc32_set_cu_reserve": (ctypes.c_int, [vp, ctypes.c_int]),
             "tfs_crc32_set_split": (ctypes.c_int, [vp, ctypes.c_int]),
+            "tfs_crc32_set_compact_segment": (ctypes.c_int, [vp, u32]),
             "tfs_crc32_split_stats": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64),
                                                      ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32),
                                                      ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
@@ -306,6 +307,11 @@ class Context:
     def set_split(self, on):
         """Split files > 128 KiB of throughput launches over several waves (on, the default) or not."""
         self._check(self.L.tfs_crc32_set_split(self.handle, 1 if on else 0), "set_split")
+
+    def set_compact_segment(self, seg_bytes):
+        """Segmented device compaction: records longer than seg_bytes (8/16/32 KiB) are cut
+        into segments on separate waves; 0 keeps every record on one wave."""
+        self._check(self.L.tfs_crc32_set_compact_segment(self.handle, int(seg_bytes)), "set_compact_segment")
 
     def split_stats(self):
         """The latest split throughput launch: {launches, used, files, cap, grid, units} (waits for it)."""

@@ -302,7 +302,7 @@ struct tfs_crc_ctx {
   uint64_t split_launches = 0;
   std::atomic<bool> cu_reserve{true};   // leave a live resident kernel's CUs out of throughput launches
   std::atomic<bool> split_files{true};  // throughput launches split files > kSplitMin (tfs_crc32_set_split)
-  uint32_t cseg_lg = 0;  // segmented compaction: 1 KiB << cseg_lg segments, 0 = whole records
+  std::atomic<uint32_t> cseg_lg{0};  // segmented compaction: 1 KiB << cseg_lg segments, 0 = whole records
   std::atomic<uint32_t> inject_skip{0}, inject_count{0};  // tfs_crc32_inject_device_error
   DevBuf packet_scratch;  // device-resident packet calls (parse descriptors, verdicts)
   hipStream_t packet_scratch_stream = nullptr;
@@ -726,7 +726,7 @@ uint32_t cseg_lg(const tfs_crc_ctx* ctx) {
   if (ctx->variant == 73) return 3u;
   if (ctx->variant == 74) return 5u;
 #endif
-  return ctx->cseg_lg;
+  return ctx->cseg_lg.load(std::memory_order_relaxed);
 }
 
 // (Caller holds plan_mu[k].)  Slot k's segmented-compaction plan for n jobs on st
@@ -2172,6 +2172,17 @@ int tfs_crc32_set_cu_reserve(tfs_crc_ctx* ctx, int on) {
 int tfs_crc32_set_split(tfs_crc_ctx* ctx, int on) {
   if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
   ctx->split_files.store(on != 0, std::memory_order_relaxed);
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_set_compact_segment(tfs_crc_ctx* ctx, uint32_t seg_bytes) {
+  if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
+  uint32_t lg = 0;
+  if (seg_bytes == 8192u) lg = 3;
+  else if (seg_bytes == 16384u) lg = 4;
+  else if (seg_bytes == 32768u) lg = 5;
+  else if (seg_bytes != 0u) return TFS_EXIT_PARAMETER_ERROR;
+  ctx->cseg_lg.store(lg, std::memory_order_relaxed);
   return TFS_SUCCESS;
 }
 

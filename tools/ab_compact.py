@@ -114,6 +114,10 @@ def main():
     if 31 in want or 32 in want:
         cases += [(0, "shift1")] + [(v, "shift1") for v in want if v in (31, 32)]
     cases += [(0, "split%d" % S) for S in splits]
+    # AB_SEG=S[,S...]: the segmented compaction (tfs_crc32_set_compact_segment) on the
+    # product context itself, toggled around its rounds (no second context's placement)
+    segs = [int(x) for x in os.environ.get("AB_SEG", "").split(",") if x]
+    cases += [("seg%d" % S, "packed") for S in segs]
     d_st = crc.DeviceBuffer(ctx, 4 * max([int(k.size)] + [getattr(b, "njobs", 0) for b in jobsets.values()]))
     # verify-on-read of every record of the resident blocks (tfs_blocks_verify_device)
     allj = np.zeros(n, crc.COMPACT_JOB_DTYPE)
@@ -126,15 +130,23 @@ def main():
     algo = 2 * live_bytes + nj * (40 + 4)
     # correctness of the product cases (the diagnostic variants 26 and 30 compute
     # no CRCs / skip stores)
+    def ctx_of(v):
+        if isinstance(v, str):
+            ctx.set_compact_segment(int(v[3:]))
+            return ctx
+        ctx.set_compact_segment(0)
+        return ctxs[v]
+
     for v, js in cases:
         if v in (26, 30, 61, 64, 65, 66, 67, 68, 69, 70, 71) or js.startswith("split"):
             continue
         d_bad.zero()
-        ctxs[v].compact_jobs_device(img, total, jobsets[js], nj, d_dst, None, d_st, d_bad)
-        ctxs[v].sync()
+        c = ctx_of(v)
+        c.compact_jobs_device(img, total, jobsets[js], nj, d_dst, None, d_st, d_bad)
+        c.sync()
         if int(d_bad.download(np.uint32, 1)[0]) != 0:
-            raise SystemExit("ab_compact: variant %d on %s reports bad records" % (v, js))
-    times = {"%d_%s" % c: [] for c in cases}
+            raise SystemExit("ab_compact: variant %s on %s reports bad records" % (v, js))
+    times = {"%s_%s" % c: [] for c in cases}
     times["copy_52114"] = []
     # wave-contiguous chunks: nt / plain stores, 64 / 256 KiB (256 workgroups); AB_COPIES
     # adds "pattern:grid[:dskew[:sskew]]" (e.g. 52114:8192, the grid-stride copy over 8,192
@@ -160,7 +172,7 @@ def main():
     cb = int(live_bytes) // 16 * 16
     for r in range(rounds):
         for v, js in cases:
-            c = ctxs[v]
+            c = ctx_of(v)
             e0, e1 = crc.Event(c), crc.Event(c)
             nn = getattr(jobsets[js], "njobs", nj)
             c.compact_jobs_device(img, total, jobsets[js], nn, d_dst, None, d_st, d_bad)
@@ -169,7 +181,8 @@ def main():
                 c.compact_jobs_device(img, total, jobsets[js], nn, d_dst, None, d_st, d_bad)
             e1.record()
             c.sync()
-            times["%d_%s" % (v, js)].append(e0.elapsed_ms(e1) / 3)
+            times["%s_%s" % (v, js)].append(e0.elapsed_ms(e1) / 3)
+        ctx.set_compact_segment(0)
         for v in vcases:
             c = ctxs[v]
             e0, e1 = crc.Event(c), crc.Event(c)
