@@ -1,7 +1,9 @@
 """Split files: a throughput launch (more than 256
 files) cuts every file longer than 128 KiB into a ragged head and 128 KiB
 segments that separate waves checksum; the segment CRCs are folded on the GPU
-(crc(A||B) = shift(crc(A), |B|) ^ crc(B), the seed on the head).  Results must
+(crc(A||B) = shift(crc(A), |B|) ^ crc(B), the seed on the head).  Every test
+runs under both unit orders: segments appended after the files (round 3) and
+every unit in address order (round 4).  Results must
 be bit-identical to Func::crc (src/common/func.cpp:426-435) whatever the split:
 against the oracle, and against the same context with splitting off."""
 import numpy as np
@@ -14,6 +16,14 @@ from tfs_amd.synth import synth_bytes
 pytestmark = pytest.mark.gpu
 
 KSEG = 128 * 1024
+
+
+@pytest.fixture(autouse=True, params=[1, 2], ids=["appended", "address_ordered"])
+def split_form(request, gpu_ctx):
+    """Every test under both split forms (tfs_crc32_set_split 1 and 2) on the session context."""
+    gpu_ctx.set_split(request.param)
+    yield request.param
+    gpu_ctx.set_split(1)
 
 
 def _edge_lengths():

@@ -40,6 +40,14 @@ SEG = 128 * 1024
 NBLOCKS = 320
 
 
+@pytest.fixture(params=[1, 2], ids=["appended", "address_ordered"])
+def split_form(request, gpu_ctx):
+    """Both unit orders of the split plan (tfs_crc32_set_split 1 / 2) on the session context."""
+    gpu_ctx.set_split(request.param)
+    yield request.param
+    gpu_ctx.set_split(1)
+
+
 def _oracle_mt(oracle, host, offs, lens, seeds):
     import tfs_amd.crc as crc
     d = np.zeros(len(offs), crc.DESC_DTYPE)
@@ -77,7 +85,7 @@ def zipf_image(gpu_ctx, oracle):
     img.free()
 
 
-def test_zipf_production_launch_compute_with_seeds(gpu_ctx, oracle, zipf_image):
+def test_zipf_production_launch_compute_with_seeds(gpu_ctx, oracle, zipf_image, split_form):
     import tfs_amd.crc as crc
     img, host, offs, lens, crc0 = zipf_image
     n = len(lens)
@@ -110,7 +118,7 @@ def test_zipf_production_launch_compute_with_seeds(gpu_ctx, oracle, zipf_image):
         d_out.free()
 
 
-def test_zipf_production_launch_verify_wrong_expectations(gpu_ctx, oracle, zipf_image):
+def test_zipf_production_launch_verify_wrong_expectations(gpu_ctx, oracle, zipf_image, split_form):
     import tfs_amd.crc as crc
     img, host, offs, lens, crc0 = zipf_image
     n = len(lens)
@@ -142,7 +150,7 @@ def test_zipf_production_launch_verify_wrong_expectations(gpu_ctx, oracle, zipf_
             b.free()
 
 
-def test_split_launches_on_two_streams_overlap_and_agree(gpu_ctx, zipf_image):
+def test_split_launches_on_two_streams_overlap_and_agree(gpu_ctx, zipf_image, split_form):
     """Split launches of one context queued on two of its streams at once, each
     stream's scheduler slot with its own plan (no launch waits on the other
     stream's plan any more): every launch's CRCs exact."""

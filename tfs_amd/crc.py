@@ -305,8 +305,9 @@ class Context:
         self._check(self.L.tfs_crc32_set_cu_reserve(self.handle, 1 if on else 0), "set_cu_reserve")
 
     def set_split(self, on):
-        """Split files > 128 KiB of throughput launches over several waves (on, the default) or not."""
-        self._check(self.L.tfs_crc32_set_split(self.handle, 1 if on else 0), "set_split")
+        """Split files > 128 KiB of throughput launches over several waves: 0/False whole files,
+        1/True segments appended after the files, 2 every unit in address order."""
+        self._check(self.L.tfs_crc32_set_split(self.handle, int(on)), "set_split")
 
     def set_compact_segment(self, seg_bytes):
         """Segmented device compaction: records longer than seg_bytes (8/16/32 KiB) are cut

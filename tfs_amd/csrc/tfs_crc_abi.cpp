@@ -299,9 +299,11 @@ struct tfs_crc_ctx {
   std::mutex last_split_mu;
   int last_split_slot = -1;
   uint32_t last_split_n = 0, last_split_cap = 0, last_split_grid = 0;
+  bool last_split_ao = false;
   uint64_t split_launches = 0;
   std::atomic<bool> cu_reserve{true};   // leave a live resident kernel's CUs out of throughput launches
-  std::atomic<bool> split_files{true};  // throughput launches split files > kSplitMin (tfs_crc32_set_split)
+  std::atomic<int> split_files{1};  // throughput launches split files > kSplitMin (tfs_crc32_set_split): 0 off,
+                                   // 1 segments appended after the files, 2 address-ordered units
   std::atomic<uint32_t> cseg_lg{0};  // segmented compaction: 1 KiB << cseg_lg segments, 0 = whole records
   std::atomic<uint32_t> inject_skip{0}, inject_count{0};  // tfs_crc32_inject_device_error
   DevBuf packet_scratch;  // device-resident packet calls (parse descriptors, verdicts)
@@ -669,12 +671,15 @@ uint32_t slot_index(const tfs_crc_ctx* ctx, const SchedLease& L) {
 // (foreign slot).  Growing frees the plan, so st is drained first.
 int split_prepare(tfs_crc_ctx* ctx, hipStream_t st, uint32_t k, uint32_t n, SplitArgs* sa) {
   const uint32_t cap = uint32_t(std::min<uint64_t>(std::max<uint64_t>(2ull * n, 65536ull), kSplitMaxUnits));
-  const uint64_t bytes = split_bytes(n, cap);
+  const bool ao = ctx->split_files.load(std::memory_order_relaxed) == 2;
+  // address-ordered form: the plan's capacity counts every unit (files + segments)
+  const uint32_t ucap = ao ? uint32_t(std::min<uint64_t>(uint64_t(n) + cap, 0xffffffffull)) : cap;
+  const uint64_t bytes = ao ? ao_bytes(n, ucap) : split_bytes(n, cap);
   DevBuf& plan = ctx->plans[k];
   if (bytes > plan.cap && plan.p) HIP_TRY(ctx, hipStreamSynchronize(st));
   HIP_TRY(ctx, plan.reserve(bytes));
-  HIP_TRY(ctx, hipMemsetAsync(plan.p, 0, 8u, st));  // `used`
-  *sa = SplitArgs{static_cast<uint8_t*>(plan.p), cap};
+  if (!ao) HIP_TRY(ctx, hipMemsetAsync(plan.p, 0, 8u, st));  // `used` (the scan kernel writes the ao header)
+  *sa = SplitArgs{static_cast<uint8_t*>(plan.p), ucap, ao ? 1u : 0u};
   return TFS_SUCCESS;
 }
 
@@ -687,10 +692,10 @@ int files_launch(tfs_crc_ctx* ctx, hipStream_t st, int mode, const uint8_t* base
   if (const int r = sched_acquire(ctx, st, &lease)) return r;
   const uint32_t k = slot_index(ctx, lease);
   std::unique_lock<std::mutex> lk(ctx->plan_mu[k], std::defer_lock);
-  SplitArgs sa{nullptr, 0u};
+  SplitArgs sa{nullptr, 0u, 0u};
   const SplitArgs* split = nullptr;
   int rc = TFS_SUCCESS;
-  if (n > kWgMaxFiles && ctx->split_files.load(std::memory_order_relaxed)) {
+  if (n > kWgMaxFiles && ctx->split_files.load(std::memory_order_relaxed) != 0) {
     lk.lock();
     rc = split_prepare(ctx, st, k, n, &sa);
     if (rc == TFS_SUCCESS) split = &sa;
@@ -709,7 +714,8 @@ int files_launch(tfs_crc_ctx* ctx, hipStream_t st, int mode, const uint8_t* base
     std::lock_guard<std::mutex> g(ctx->last_split_mu);
     ctx->last_split_slot = int(k);
     ctx->last_split_n = n;
-    ctx->last_split_cap = sa.cap;
+    ctx->last_split_cap = sa.ao ? sa.cap - n : sa.cap;  // ext units the plan had room for
+    ctx->last_split_ao = sa.ao != 0;
     ctx->last_split_grid = cap;  // a split launch takes the whole capped grid (launch_variant)
     ++ctx->split_launches;
   }
@@ -2170,8 +2176,8 @@ int tfs_crc32_set_cu_reserve(tfs_crc_ctx* ctx, int on) {
 }
 
 int tfs_crc32_set_split(tfs_crc_ctx* ctx, int on) {
-  if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
-  ctx->split_files.store(on != 0, std::memory_order_relaxed);
+  if (!ctx || on < 0 || on > 2) return TFS_EXIT_PARAMETER_ERROR;
+  ctx->split_files.store(on, std::memory_order_relaxed);
   return TFS_SUCCESS;
 }
 
@@ -2206,7 +2212,13 @@ int tfs_crc32_split_stats(tfs_crc_ctx* ctx, uint64_t* launches, uint64_t* used, 
     std::lock_guard<std::mutex> pg(ctx->plan_mu[k]);
     if (!ctx->plan_done[k]) return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "split_stats: no event behind the plan");
     HIP_TRY(ctx, hipEventSynchronize(ctx->plan_done[k]));
-    HIP_TRY(ctx, hipMemcpy(&u, ctx->plans[k].p, 8, hipMemcpyDeviceToHost));
+    if (ctx->last_split_ao) {  // header {units, nosplit, ext}
+      uint32_t hdr[3] = {0u, 0u, 0u};
+      HIP_TRY(ctx, hipMemcpy(hdr, ctx->plans[k].p, 12, hipMemcpyDeviceToHost));
+      u = hdr[1] ? 0u : hdr[2];
+    } else {
+      HIP_TRY(ctx, hipMemcpy(&u, ctx->plans[k].p, 8, hipMemcpyDeviceToHost));
+    }
   }
   if (launches) *launches = nl;
   if (used) *used = u;

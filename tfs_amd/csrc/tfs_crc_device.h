@@ -180,13 +180,37 @@ constexpr uint32_t kSplitMaxUnits = 4u << 20;  // ext units per launch at most (
 // cap, the files past it stay whole).
 struct SplitArgs {
   uint8_t* plan;  // nullptr: no split plan
-  uint32_t cap;
+  uint32_t cap;   // appended form: ext units at most; address-ordered form: units (files + segments) at most
+  uint32_t ao;    // 1: the address-ordered form (SplitUnit list), 0: segments appended after the files
 };
 constexpr uint64_t split_off_base() { return 16u; }
 constexpr uint64_t split_off_head(uint32_t n) { return 16u + 4ull * n; }
 constexpr uint64_t split_off_ext_crc(uint32_t n) { return 16u + 8ull * n; }
 constexpr uint64_t split_off_ext(uint32_t n, uint32_t cap) { return (16u + 8ull * n + 4ull * cap + 15u) & ~15ull; }
 constexpr uint64_t split_bytes(uint32_t n, uint32_t cap) { return split_off_ext(n, cap) + 16ull * cap; }
+
+// Address-ordered split plan (round 4): the same cut (ragged head
+// + whole kSegBytes segments), but every unit of the launch -- whole files,
+// heads and segments -- sits in one list in address order (file i's head, then
+// its segments, then file i + 1), so the waves' tickets walk the image once
+// instead of twice (files and heads first, the big files' segments after).  The
+// unit list is built by a three-kernel scan (split_ao_count / _scan / _write).
+// [total u32 | nosplit u32 | ext u32 | pad][blk u32 x nblk][ubase u32 x n]
+// [ucrc u32 x ucap][pad to 16][SplitUnit x ucap], nblk = ceil(n / 256).
+struct SplitUnit {
+  uint64_t offset;
+  uint32_t len, aux;   // aux: the file's seed / expected CRC on a whole file or head, 0 on a segment
+  uint32_t file, kind; // kind 0 a whole file, 1 a segment, 2 a split file's head
+  uint64_t pad;
+};
+static_assert(sizeof(SplitUnit) == 32, "split unit layout");
+constexpr uint32_t kAoBlock = 256;
+constexpr uint32_t ao_nblk(uint32_t n) { return (n + kAoBlock - 1u) / kAoBlock; }
+constexpr uint64_t ao_off_blk() { return 16u; }
+constexpr uint64_t ao_off_ubase(uint32_t n) { return 16u + 4ull * ao_nblk(n); }
+constexpr uint64_t ao_off_ucrc(uint32_t n) { return ao_off_ubase(n) + 4ull * n; }
+constexpr uint64_t ao_off_units(uint32_t n, uint32_t ucap) { return (ao_off_ucrc(n) + 4ull * ucap + 15u) & ~15ull; }
+constexpr uint64_t ao_bytes(uint32_t n, uint32_t ucap) { return ao_off_units(n, ucap) + 32ull * ucap; }
 
 // Segmented compaction (round 4): a throughput compaction launch
 // cuts every live record whose payload is longer than one segment into a ragged

@@ -790,7 +790,7 @@ __device__ __forceinline__ void launch_exit(uint32_t* sched, uint32_t units, uin
 // n >> TS files are ticketed one by one (chunks only while much work is left,
 // so a chunk of large files cannot become the launch's tail).
 template <int MODE, int RUN, int PF, bool NT, bool DYN, bool S8, int G = 1, bool HV = false, bool IL = false,
-          int W = 1, bool XF = false, bool BLK = false, int CF = 1, int TS = 0>
+          int W = 1, bool XF = false, bool BLK = false, int CF = 1, int TS = 0, int SPL = 0>
 __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __restrict__ base,
                                                            const Desc* __restrict__ desc, uint32_t n,
                                                            const Tables* __restrict__ tg, uint32_t* out_crc,
@@ -803,13 +803,34 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
   // files (tfs_crc_device.h SplitArgs); a split file itself is skipped here.
   const uint32_t nfiles = n;
   uint8_t* plan = nullptr;  // stays null when the plan split nothing: no per-file lookup
+  const SplitUnit* aou = nullptr;  // SPL 1: the address-ordered unit list (null: nothing split)
+  uint32_t* ucrc = nullptr;
   if (sa.plan) {
-    const unsigned long long used = *reinterpret_cast<const unsigned long long*>(sa.plan);
-    n = nfiles + uint32_t(used < sa.cap ? used : sa.cap);
-    if (used) plan = sa.plan;
+    if constexpr (SPL == 1) {
+      const uint32_t* hdr = reinterpret_cast<const uint32_t*>(sa.plan);
+      if (hdr[1] == 0u) {
+        n = hdr[0];
+        aou = reinterpret_cast<const SplitUnit*>(sa.plan + ao_off_units(nfiles, sa.cap));
+        ucrc = reinterpret_cast<uint32_t*>(sa.plan + ao_off_ucrc(nfiles));
+      }
+    } else {
+      const unsigned long long used = *reinterpret_cast<const unsigned long long*>(sa.plan);
+      n = nfiles + uint32_t(used < sa.cap ? used : sa.cap);
+      if (used) plan = sa.plan;
+    }
   }
-  // kind: 0 a file, 1 an ext unit (a whole segment), 2 a split file's ragged head
-  auto unit = [&](uint32_t u, uint32_t& kind) -> Desc {
+  // kind: 0 a file, 1 an ext unit (a whole segment), 2 a split file's ragged head;
+  // fi: the file whose output a kind-0 unit writes
+  auto unit = [&](uint32_t u, uint32_t& kind, uint32_t& fi) -> Desc {
+    fi = u;
+    if constexpr (SPL == 1) {
+      kind = 0u;
+      if (!aou) return desc[u];
+      const SplitUnit U = aou[u];
+      kind = U.kind;
+      fi = U.file;
+      return Desc{U.offset, U.len, U.aux};
+    }
     if (u >= nfiles) {
       kind = 1u;
       return reinterpret_cast<const Desc*>(plan + split_off_ext(nfiles, sa.cap))[u - nfiles];
@@ -858,19 +879,19 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
     if (f >= n) break;
     fn = f + stride;
   }
-  uint32_t kcur = 0, knxt = 0;
-  Desc cur = unit(f, kcur);
+  uint32_t kcur = 0, knxt = 0, ocur = 0, onxt = 0;
+  Desc cur = unit(f, kcur, ocur);
   FileGeo<RUN> g = make_geo<RUN>(base + cur.offset, cur.len, seed_of(cur, kcur));
   Head<RUN> h = load_head<RUN, HV>(g, lane);
   const uintptr_t junk = reinterpret_cast<uintptr_t>(tg->slice);
   uint4 buf[PF][RUN / 16];
   load_ring<RUN, PF, NT>(g, lane, buf, junk);
-  Desc nxt = fn < n ? unit(fn, knxt) : Desc{0, 0, 0};
+  Desc nxt = fn < n ? unit(fn, knxt, onxt) : Desc{0, 0, 0};
   uint32_t jv = DYN && CF == 1 && fn < n ? tk.issue(lane) : 0u;  // ticket of the file after next, in flight
   for (;;) {
     const bool more = fn < n;
     const Desc ncur = nxt;
-    const uint32_t kn = knxt;
+    const uint32_t kn = knxt, on = onxt;
     // XF: the next file's geometry first -- this file's ring refills run into it.
     FileGeo<RUN> ng = XF ? make_geo<RUN>(more ? base + ncur.offset : reinterpret_cast<const uint8_t*>(junk),
                                          more ? ncur.len : 0u, seed_of(ncur, kn))
@@ -888,20 +909,22 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
       if (!XF || !g.nstripes) load_ring<RUN, PF, NT>(ng, lane, buf, junk);
       fnn = DYN ? (CF > 1 ? take() : tk.resolve(jv, lane))
                 : (BLK ? (fn + 1u < blk_end ? fn + 1u : n) : fn + stride);
-      if (fnn < n) nxt = unit(fnn, knxt);
+      if (fnn < n) nxt = unit(fnn, knxt, onxt);
       if (DYN && CF == 1 && fnn < n) jv = tk.issue(lane);
     }
     const uint32_t crc = finish_file<RUN, S8>(lds_tables, lb, g, h, c, lane);
     if (lane == 0) {
-      if (kcur == 1u) {
+      if (SPL == 1 && kcur != 0u) {
+        ucrc[f] = crc;  // a head or a segment: the fold joins them
+      } else if (kcur == 1u) {
         reinterpret_cast<uint32_t*>(plan + split_off_ext_crc(nfiles))[f - nfiles] = crc;
       } else if (kcur == 2u) {
         reinterpret_cast<uint32_t*>(plan + split_off_head(nfiles))[f] = crc;
       } else {
-        if (out_crc) out_crc[f] = crc;
+        if (out_crc) out_crc[ocur] = crc;
         if (MODE == 1) {
           const bool ok = crc == cur.aux;
-          if (out_ok) out_ok[f] = ok ? 1 : 0;
+          if (out_ok) out_ok[ocur] = ok ? 1 : 0;
           bad += ok ? 0u : 1u;
         }
       }
@@ -911,6 +934,7 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
     fn = fnn;
     cur = ncur;
     kcur = kn;
+    ocur = on;
     g = ng;
     h = nh;
   }
@@ -991,6 +1015,129 @@ __global__ void __launch_bounds__(256) split_fold_kernel(const Desc* __restrict_
     const uint32_t K = (d.len - 1u) / kSegBytes;
     uint32_t c = head_crc[i];
     for (uint32_t j = 0; j < K; ++j) c = shift5(T, 0u, c) ^ ext_crc[b + j];
+    if (out_crc) out_crc[i] = c;
+    if (MODE == 1) {
+      const bool ok = c == d.aux;
+      if (out_ok) out_ok[i] = ok ? 1 : 0;
+      bad += ok ? 0u : 1u;
+    }
+  }
+  if (MODE == 1 && n_bad) {  // one atomic per wave
+#pragma unroll
+    for (int m = kWave / 2; m >= 1; m >>= 1) bad += __shfl_xor(bad, m, kWave);
+    if ((threadIdx.x & (kWave - 1)) == 0 && bad) atomicAdd(n_bad, bad);
+  }
+}
+
+// Address-ordered split plan (SplitUnit list, tfs_crc_device.h), step 1 of 3: the
+// number of whole segments of each block of kAoBlock files.
+__device__ __forceinline__ uint32_t ao_segments(const Desc& d) {
+  return d.len > kSplitMin ? (d.len - 1u) / kSegBytes : 0u;
+}
+
+__global__ void __launch_bounds__(kAoBlock) split_ao_count_kernel(const Desc* __restrict__ desc, uint32_t n,
+                                                                  SplitArgs sa) {
+  __shared__ uint32_t wsum[kAoBlock / kWave];
+  const uint32_t i = blockIdx.x * kAoBlock + threadIdx.x;
+  uint32_t K = i < n ? ao_segments(desc[i]) : 0u;
+#pragma unroll
+  for (int m = kWave / 2; m >= 1; m >>= 1) K += __shfl_xor(K, m, kWave);
+  if ((threadIdx.x & (kWave - 1)) == 0) wsum[threadIdx.x / kWave] = K;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (uint32_t w = 0; w < kAoBlock / kWave; ++w) t += wsum[w];
+    reinterpret_cast<uint32_t*>(sa.plan + ao_off_blk())[blockIdx.x] = t;
+  }
+}
+
+// Step 2 (one workgroup): exclusive scan of the block counts in place; the
+// header gets the launch's unit count, or `nosplit` when nothing was split or the
+// segments would pass the plan's capacity (every file then stays whole).
+__global__ void __launch_bounds__(1024) split_ao_scan_kernel(uint32_t n, SplitArgs sa) {
+  __shared__ uint32_t part[1024];
+  uint32_t* blk = reinterpret_cast<uint32_t*>(sa.plan + ao_off_blk());
+  const uint32_t nb = ao_nblk(n);
+  const uint32_t per = (nb + 1023u) / 1024u;
+  const uint32_t b0 = threadIdx.x * per, b1 = min(b0 + per, nb);
+  uint32_t t = 0;
+  for (uint32_t b = b0; b < b1; ++b) t += blk[b];
+  part[threadIdx.x] = t;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024u; o <<= 1) {  // inclusive scan of the per-thread sums
+    const uint32_t v = threadIdx.x >= o ? part[threadIdx.x - o] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[threadIdx.x] - t;
+  for (uint32_t b = b0; b < b1; ++b) {
+    const uint32_t v = blk[b];
+    blk[b] = run;
+    run += v;
+  }
+  if (threadIdx.x == 1023u) {
+    const uint64_t ext = part[1023];
+    uint32_t* hdr = reinterpret_cast<uint32_t*>(sa.plan);
+    const bool fits = ext > 0u && uint64_t(n) + ext <= uint64_t(sa.cap);
+    hdr[0] = fits ? uint32_t(n + ext) : n;
+    hdr[1] = fits ? 0u : 1u;
+    hdr[2] = uint32_t(ext);
+  }
+}
+
+// Step 3: every file's units at its place in address order: file i starts at
+// unit i + (segments of the files before it).
+__global__ void __launch_bounds__(kAoBlock) split_ao_write_kernel(const Desc* __restrict__ desc, uint32_t n,
+                                                                  SplitArgs sa) {
+  __shared__ uint32_t wsum[kAoBlock / kWave];
+  if (reinterpret_cast<const uint32_t*>(sa.plan)[1] != 0u) return;  // nothing split: the kernel reads desc
+  const uint32_t i = blockIdx.x * kAoBlock + threadIdx.x;
+  const int lane = threadIdx.x & (kWave - 1);
+  const uint32_t w = threadIdx.x / kWave;
+  Desc d{0, 0, 0};
+  if (i < n) d = desc[i];
+  const uint32_t K = i < n ? ao_segments(d) : 0u;
+  uint32_t x = K;  // inclusive scan over the wave
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, kWave);
+    if (lane >= o) x += y;
+  }
+  if (lane == kWave - 1) wsum[w] = x;
+  __syncthreads();
+  if (i >= n) return;
+  uint32_t before = reinterpret_cast<const uint32_t*>(sa.plan + ao_off_blk())[blockIdx.x] + (x - K);
+  for (uint32_t k = 0; k < w; ++k) before += wsum[k];
+  const uint32_t base = i + before;
+  reinterpret_cast<uint32_t*>(sa.plan + ao_off_ubase(n))[i] = base;
+  SplitUnit* U = reinterpret_cast<SplitUnit*>(sa.plan + ao_off_units(n, sa.cap));
+  const uint32_t head = d.len - K * kSegBytes;
+  U[base] = SplitUnit{d.offset, head, d.aux, i, K ? 2u : 0u, 0u};
+  for (uint32_t k = 0; k < K; ++k)
+    U[base + 1u + k] = SplitUnit{d.offset + head + uint64_t(k) * kSegBytes, kSegBytes, 0u, i, 1u, 0u};
+}
+
+// Fold of the address-ordered form: a split file's CRC from its head (unit
+// ubase[i]) and segments (the K units after it).
+template <int MODE>
+__global__ void __launch_bounds__(256) split_ao_fold_kernel(const Desc* __restrict__ desc, uint32_t n,
+                                                            const Tables* __restrict__ tg, SplitArgs sa,
+                                                            uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad) {
+  __shared__ uint32_t T[uint32_t(kShiftChunks) * 32u];
+  if (reinterpret_cast<const uint32_t*>(sa.plan)[1] != 0u) return;  // nothing was split
+  const uint32_t* ubase = reinterpret_cast<const uint32_t*>(sa.plan + ao_off_ubase(n));
+  const uint32_t* ucrc = reinterpret_cast<const uint32_t*>(sa.plan + ao_off_ucrc(n));
+  for (uint32_t k = threadIdx.x; k < uint32_t(kShiftChunks) * 32u; k += blockDim.x) T[k] = (&tg->seg_shift[0][0])[k];
+  __syncthreads();
+  uint32_t bad = 0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const Desc d = desc[i];
+    const uint32_t K = ao_segments(d);
+    if (K == 0u) continue;
+    const uint32_t b = ubase[i];
+    uint32_t c = ucrc[b];
+    for (uint32_t j = 1; j <= K; ++j) c = shift5(T, 0u, c) ^ ucrc[b + j];
     if (out_crc) out_crc[i] = c;
     if (MODE == 1) {
       const bool ok = c == d.aux;
@@ -2329,11 +2476,26 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
   if (!sched) return hipErrorInvalidValue;
   // Split files (tfs_crc_device.h): the plan before the main kernel, the fold
   // after it, all on `stream`; the completion-flag form (done_flag) never splits.
-  const SplitArgs sa = split && !done_flag ? *split : SplitArgs{nullptr, 0u};
+  const SplitArgs sa = split && !done_flag ? *split : SplitArgs{nullptr, 0u, 0u};
   // A split launch's work is its files plus the ext units the plan makes on the
   // device (a few hundred 64 MiB files are ~150 k units), so it takes the whole
   // capped grid; the tickets hand out any number of units.
   const dim3 grid(sa.plan ? (cap < kMaxGrid ? cap : kMaxGrid) : grid_for(n, cap)), block(kBlock);
+  if (sa.plan && sa.ao) {
+    // Address-ordered form: count, scan, write the unit list; the product kernel
+    // over it; the fold (round 4).
+    const uint32_t nb = ao_nblk(n);
+    hipLaunchKernelGGL(split_ao_count_kernel, dim3(nb), dim3(kAoBlock), 0, stream, desc, n, sa);
+    hipLaunchKernelGGL(split_ao_scan_kernel, dim3(1), dim3(1024), 0, stream, n, sa);
+    hipLaunchKernelGGL(split_ao_write_kernel, dim3(nb), dim3(kAoBlock), 0, stream, desc, n, sa);
+    hipLaunchKernelGGL(
+        (crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, kCF, kTS, 1>), grid,
+        block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
+    const uint32_t fg = (n + 255u) / 256u;
+    hipLaunchKernelGGL((split_ao_fold_kernel<MODE>), dim3(fg < 1024u ? fg : 1024u), dim3(256), 0, stream, desc, n, tg,
+                       sa, out_crc, out_ok, n_bad);
+    return hipGetLastError();
+  }
   if (sa.plan) {
     hipLaunchKernelGGL((split_plan_kernel<MODE>), dim3((n + 255u) / 256u), dim3(256), 0, stream, desc, n, vseed, sa);
     if (const hipError_t e = hipGetLastError()) return e;

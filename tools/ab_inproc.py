@@ -9,10 +9,11 @@ drops out.
 
   python tools/ab_inproc.py OTHER_SO[,OTHER_SO...] [ROUNDS] [mode]   mode: verify (default) | zipf
 
-A second entry, "product_nosplit", is the product library's SAME context with
-file splitting switched off (tfs_crc32_set_split) for its rounds, so split on
-vs off shares one stream and one scratch set: the per-context placement noise
-(up to +-2 % between two contexts of one library) drops out of that pair.
+Two more entries, "product_nosplit" and "product_ao", are the product library's
+SAME context with file splitting switched off / set to the address-ordered unit
+list (tfs_crc32_set_split 0 / 2) for their rounds, so the split forms share one
+stream and one scratch set: the per-context placement noise (up to +-2 % between
+two contexts of one library) drops out.  OTHER_SO "-" compares only those.
 """
 import ctypes
 import json
@@ -50,8 +51,8 @@ def main():
     ctx = crc.Context(0)
     prod = bind(crc.LIB_PATH)
     prod[0].tfs_crc32_set_split.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    libs = {"product": prod, "product_nosplit": prod}
-    for i, o in enumerate(other.split(",")):
+    libs = {"product": prod, "product_nosplit": prod, "product_ao": prod}
+    for i, o in enumerate(x for x in other.split(",") if x and x != "-"):
         libs["other%d" % i] = bind(os.path.abspath(o))
     if mode == "zipf":
         blocks = bench.zipf_sizes(42, 1024)
@@ -89,8 +90,8 @@ def main():
     times = {k: [] for k in libs}
     for r in range(rounds):
         for name, (L, h) in libs.items():
-            if name.startswith("product"):
-                assert L.tfs_crc32_set_split(h, int(name == "product")) == 0
+            if name.startswith("product"):  # split form of the one product context: 1, 0 or 2 (address order)
+                assert L.tfs_crc32_set_split(h, {"product": 1, "product_nosplit": 0, "product_ao": 2}[name]) == 0
             e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
             L.tfs_crc32_event_create(h, ctypes.byref(e0))
             L.tfs_crc32_event_create(h, ctypes.byref(e1))

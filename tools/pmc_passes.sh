@@ -22,10 +22,10 @@ declare -A G=(
   [write]="WRITE_SIZE"
   [tccs]="TCC_EA0_WRREQ_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_BUSY_sum"
 )
-GROUPS=${PMC_GROUPS:-sq1,sq2,tcp,tccw,fetch,write,tccs}
+PGROUPS=${PMC_GROUPS:-sq1,sq2,tcp,tccw,fetch,write,tccs}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$D/trace" -o run --output-format csv -- "$@" \
   > "$D/trace.out" 2> "$D/trace.err"
-for g in ${GROUPS//,/ }; do
+for g in ${PGROUPS//,/ }; do
   timeout -s KILL 150 rocprofv3 --pmc ${G[$g]} --kernel-include-regex "$KRE" -d "$D/pmc_$g" -o run \
     --output-format csv -- "$@" > "$D/pmc_$g.out" 2> "$D/pmc_$g.err"
   echo "$NAME $g done"
