@@ -87,6 +87,9 @@ def main():
     d["aux"] = out.download(np.uint32)
     d_vdesc = crc.DeviceBuffer(ctx, d.nbytes).upload(d)
     ok = crc.DeviceBuffer(ctx, n)
+    only = [x for x in os.environ.get("AB_ONLY", "").split(",") if x]  # e.g. AB_ONLY=product,product_ao
+    if only:
+        libs = {k: v for k, v in libs.items() if k in only}
     times = {k: [] for k in libs}
     for r in range(rounds):
         for name, (L, h) in libs.items():

@@ -11,4 +11,5 @@ PMC_GROUPS=sq1,tcp,tccw,fetch,write,tccs tools/pmc_passes.sh $O copy53101 "membe
 tools/pmc_passes.sh $O ec "ec_apply_kernel" -- python bench.py --workload ec --no-cpu --steps 2 --warmup 1
 AB_VARIANTS="" AB_SEG=8192,16384,32768 AB_SPLIT=16384 timeout -k 10 600 python tools/ab_compact.py 4 > gpurun_out/r04/ab_compact_split.json 2> gpurun_out/r04/ab_compact_split.err
 timeout -k 10 300 python tools/ab_ec.py 7,6 8 > gpurun_out/r04/ab_ec.json 2> gpurun_out/r04/ab_ec.err
+AB_ONLY=product,product_ao PMC_GROUPS=tcp,sq1,tccs tools/pmc_passes.sh $O zipf_forms "crc_files_kernel<0" -- python tools/ab_inproc.py - 2 zipf
 echo ALLDONE
