@@ -57,7 +57,7 @@ TRAFFIC_NOTE = ("quoted: HBM bytes per launch from the committed rocprofv3 PMC p
                 "run; null when this run is not the profiled configuration")
 
 
-HEADLINE_KERNEL = "crc_files_kernel<1, 16, 5, true, true, true, 1, false, true, 1, false, false, 4, 3"
+HEADLINE_KERNEL = "crc_files_kernel<1, 16, 5, true, true, true, 1, false, true, 1, false, false, 4, 3, 1"
 
 
 PACKET_PIPELINE = ("packet pipeline: packet_parse_kernel + crc_files_kernel<1, ..., 4, 3> + "

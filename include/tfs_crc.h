@@ -487,9 +487,11 @@ int tfs_crc32_set_cu_reserve(tfs_crc_ctx* ctx, int on);
  * every file longer than 128 KiB into a ragged head and 128 KiB segments that
  * separate waves checksum, then fold the segment CRCs into the file's CRC on the
  * GPU: one wave never streams a long file alone.  Results are
- * identical either way; on = 0 keeps every file on one wave (A/B), 1 appends the
- * segments after the files, 2 lists every unit in address order (each file's
- * head, then its segments, then the next file). */
+ * identical either way; on = 0 keeps every file on one wave (A/B).  The
+ * launch's units -- whole files, heads and segments -- form one list in address
+ * order (each file's head, then its segments, then the next file), so the waves
+ * walk the image once (round 4; the measurement build's on = 2 is round 3's form,
+ * segments appended after all files). */
 int tfs_crc32_set_split(tfs_crc_ctx* ctx, int on);
 /* Device compaction (tfs_compact_jobs_device, and the block-file compactor that
  * calls it) cuts every live record whose payload is longer than `seg_bytes` into a

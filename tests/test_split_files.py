@@ -2,8 +2,8 @@
 files) cuts every file longer than 128 KiB into a ragged head and 128 KiB
 segments that separate waves checksum; the segment CRCs are folded on the GPU
 (crc(A||B) = shift(crc(A), |B|) ^ crc(B), the seed on the head).  Every test
-runs under both unit orders: segments appended after the files (round 3) and
-every unit in address order (round 4).  Results must
+runs under both unit orders: every unit in address order (the product, round 4)
+and segments appended after the files (round 3's form, measurement build).  Results must
 be bit-identical to Func::crc (src/common/func.cpp:426-435) whatever the split:
 against the oracle, and against the same context with splitting off."""
 import numpy as np
@@ -18,12 +18,18 @@ pytestmark = pytest.mark.gpu
 KSEG = 128 * 1024
 
 
-@pytest.fixture(autouse=True, params=[1, 2], ids=["appended", "address_ordered"])
-def split_form(request, gpu_ctx):
-    """Every test under both split forms (tfs_crc32_set_split 1 and 2) on the session context."""
-    gpu_ctx.set_split(request.param)
-    yield request.param
-    gpu_ctx.set_split(1)
+@pytest.fixture(params=["address_ordered", "appended"])
+def sctx(request, gpu_ctx):
+    """The product context (the address-ordered unit list), and a measurement-build
+    context set to round 3's appended form (tfs_crc32_set_split 2)."""
+    import tfs_amd.crc as crc
+    if request.param == "address_ordered":
+        yield gpu_ctx
+        return
+    c = crc.Context(0, measure=True)
+    c.set_split(2)
+    yield c
+    c.close()
 
 
 def _edge_lengths():
@@ -32,7 +38,7 @@ def _edge_lengths():
     return L
 
 
-def test_split_batch_matches_oracle_and_unsplit(gpu_ctx, oracle):
+def test_split_batch_matches_oracle_and_unsplit(sctx, oracle):
     """300+ files mixing the split edges (K*128 KiB +- 1, ragged heads of every
     size), small files and 1-9 MiB files, every alignment, seeds (compute) --
     one host batch (throughput form): oracle-exact, and equal to split off."""
@@ -47,7 +53,7 @@ def test_split_batch_matches_oracle_and_unsplit(gpu_ctx, oracle):
     buf = synth_bytes(3031, int(offs[-1] + lens[-1]) + 256)
     seeds = np.where(rng.integers(0, 2, n) == 0, 0, rng.integers(0, 2**32, n)).astype(np.uint32)
     exp = _oracle_batch(oracle, buf, offs, lens, seeds)
-    got = gpu_ctx.batch(buf, offs, lens, seeds)
+    got = sctx.batch(buf, offs, lens, seeds)
     bad = np.nonzero(got != exp)[0]
     assert bad.size == 0, [(int(i), int(lens[i]), int(offs[i]) % 16) for i in bad[:10]]
     c2 = crc.Context(0)
@@ -58,7 +64,7 @@ def test_split_batch_matches_oracle_and_unsplit(gpu_ctx, oracle):
         c2.close()
 
 
-def test_split_verify_device_wrong_expectations(gpu_ctx, oracle):
+def test_split_verify_device_wrong_expectations(sctx, oracle):
     """Device-resident verify with split files: wrong expectations on split and
     whole files alike are found exactly (n_bad, verdicts, CRCs)."""
     import tfs_amd.crc as crc
@@ -67,23 +73,23 @@ def test_split_verify_device_wrong_expectations(gpu_ctx, oracle):
     lens = np.where(rng.integers(0, 3, n) == 0, rng.integers(KSEG, 3 << 20, n), rng.integers(0, 200000, n)).astype(np.uint32)
     offs = np.cumsum(np.concatenate([[0], lens[:-1]]).astype(np.uint64) + rng.integers(0, 64, n).astype(np.uint64))
     total = int(offs[-1] + lens[-1]) + 256
-    img = crc.DeviceBuffer(gpu_ctx, (total + 7) // 8 * 8)
-    gpu_ctx.synth_fill_device(img, (total + 7) // 8 * 8, 3033, 0)
+    img = crc.DeviceBuffer(sctx, (total + 7) // 8 * 8)
+    sctx.synth_fill_device(img, (total + 7) // 8 * 8, 3033, 0)
     host = img.download(np.uint8, total)
     exp = _oracle_batch(oracle, host, offs, lens, np.zeros(n, np.uint32))
     wrong = np.sort(rng.choice(n, 97, replace=False))
     d = np.zeros(n, crc.DESC_DTYPE)
     d["offset"], d["len"], d["aux"] = offs, lens, exp
     d["aux"][wrong] ^= 0x80000000
-    dd = crc.DeviceBuffer(gpu_ctx, d.nbytes).upload(d)
-    dc, dok, dnb = crc.DeviceBuffer(gpu_ctx, 4 * n), crc.DeviceBuffer(gpu_ctx, n), crc.DeviceBuffer(gpu_ctx, 4)
+    dd = crc.DeviceBuffer(sctx, d.nbytes).upload(d)
+    dc, dok, dnb = crc.DeviceBuffer(sctx, 4 * n), crc.DeviceBuffer(sctx, n), crc.DeviceBuffer(sctx, 4)
     try:
         assert int((lens[wrong] > KSEG).sum()) > 10
         for rep in range(2):
             dok.zero()
             dnb.zero()
-            gpu_ctx.verify_device(dd, n, img, dc, dok, dnb)
-            gpu_ctx.sync()
+            sctx.verify_device(dd, n, img, dc, dok, dnb)
+            sctx.sync()
             assert int(dnb.download(np.uint32)[0]) == wrong.size, rep
             ok = dok.download(np.uint8, n)
             assert (np.nonzero(ok == 0)[0] == wrong).all() and (ok[np.setdiff1d(np.arange(n), wrong)] == 1).all()
@@ -93,15 +99,15 @@ def test_split_verify_device_wrong_expectations(gpu_ctx, oracle):
             b.free()
 
 
-def test_split_capacity_overflow_keeps_files_whole(gpu_ctx, oracle):
+def test_split_capacity_overflow_keeps_files_whole(sctx, oracle):
     """The plan holds max(2n, 65,536) units: 400 files of 9 MiB (28,800
     segments) all split; 1,000 of them need 72,000, so the files of the
     workgroups that do not fit stay whole.  Every CRC exact either way."""
     import tfs_amd.crc as crc
     rng = np.random.default_rng(3034)
     L = 9 * (1 << 20) + 3
-    src = crc.DeviceBuffer(gpu_ctx, L + 4096)
-    gpu_ctx.synth_fill_device(src, (L + 4096) // 8 * 8, 3035, 0)
+    src = crc.DeviceBuffer(sctx, L + 4096)
+    sctx.synth_fill_device(src, (L + 4096) // 8 * 8, 3035, 0)
     host = src.download(np.uint8, L + 4096)
     for n in (400, 1000):
         offs = rng.integers(0, 4000, n).astype(np.uint64)  # overlapping files over one 9 MiB region
@@ -109,11 +115,11 @@ def test_split_capacity_overflow_keeps_files_whole(gpu_ctx, oracle):
         seeds = rng.integers(0, 2**32, n).astype(np.uint32)
         d = np.zeros(n, crc.DESC_DTYPE)
         d["offset"], d["len"], d["aux"] = offs, lens, seeds
-        dd = crc.DeviceBuffer(gpu_ctx, d.nbytes).upload(d)
-        out = crc.DeviceBuffer(gpu_ctx, 4 * n)
+        dd = crc.DeviceBuffer(sctx, d.nbytes).upload(d)
+        out = crc.DeviceBuffer(sctx, 4 * n)
         try:
-            gpu_ctx.batch_device(dd, n, src, out)
-            gpu_ctx.sync()
+            sctx.batch_device(dd, n, src, out)
+            sctx.sync()
             got = out.download(np.uint32, n)
             idx = np.linspace(0, n - 1, 40).astype(np.int64)
             exp = _oracle_batch(oracle, host, offs[idx], lens[idx], seeds[idx])
@@ -124,7 +130,7 @@ def test_split_capacity_overflow_keeps_files_whole(gpu_ctx, oracle):
     src.free()
 
 
-def test_split_packet_bodies(gpu_ctx, oracle):
+def test_split_packet_bodies(sctx, oracle):
     """Packet frames with bodies over 128 KiB (a write of 1 MiB is one frame):
     the decode CRC (seed TFS_PACKET_FLAG_V1, base_packet.cpp:141) through the
     split launch equals the oracle's statuses and CRCs."""
@@ -142,6 +148,6 @@ def test_split_packet_bodies(gpu_ctx, oracle):
         pos += gap + len(f)
     raw = b"".join(parts)
     buf = np.frombuffer(raw, np.uint8)
-    c, st, nbad, rc = gpu_ctx.packet_verify(buf, [f[0] for f in frames], [f[1] for f in frames])
+    c, st, nbad, rc = sctx.packet_verify(buf, [f[0] for f in frames], [f[1] for f in frames])
     oc, ost, obad = tp.o_verify(oracle, buf, frames)
     assert np.array_equal(st, ost) and np.array_equal(c, oc) and nbad == obad == 6

@@ -20,9 +20,11 @@ forms, each checked file by file against the oracle over the device's own bytes:
   n_bad == 1,000, verdict 0 at exactly those files, CRCs equal to the oracle's.
 
 tfs_crc32_split_stats proves the launch took that path (the plan split files;
-units / tickets from the plan's own `used`).  A second test runs two split
-launches on two streams of one context at once (one plan per
-scheduler slot) and checks both.
+units / tickets from the plan's own count).  A third test runs split launches on
+two streams of one context at once (one plan per scheduler slot) and
+checks them.  Every test runs on the product context (the address-ordered unit
+list, round 4) and on a measurement-build context set to round 3's form
+(segments appended after the files).
 
 References: Func::crc src/common/func.cpp:426-435; the running-seed identity the
 fold relies on, DataFile::get_crc src/dataserver/data_file.cpp:183-186; the
@@ -40,12 +42,18 @@ SEG = 128 * 1024
 NBLOCKS = 320
 
 
-@pytest.fixture(params=[1, 2], ids=["appended", "address_ordered"])
-def split_form(request, gpu_ctx):
-    """Both unit orders of the split plan (tfs_crc32_set_split 1 / 2) on the session context."""
-    gpu_ctx.set_split(request.param)
-    yield request.param
-    gpu_ctx.set_split(1)
+@pytest.fixture(params=["address_ordered", "appended"])
+def sctx(request, gpu_ctx):
+    """The product context (the address-ordered unit list), and a measurement-build
+    context set to round 3's appended form (tfs_crc32_set_split 2)."""
+    import tfs_amd.crc as crc
+    if request.param == "address_ordered":
+        yield gpu_ctx
+        return
+    c = crc.Context(0, measure=True)
+    c.set_split(2)
+    yield c
+    c.close()
 
 
 def _oracle_mt(oracle, host, offs, lens, seeds):
@@ -85,7 +93,7 @@ def zipf_image(gpu_ctx, oracle):
     img.free()
 
 
-def test_zipf_production_launch_compute_with_seeds(gpu_ctx, oracle, zipf_image, split_form):
+def test_zipf_production_launch_compute_with_seeds(sctx, oracle, zipf_image):
     import tfs_amd.crc as crc
     img, host, offs, lens, crc0 = zipf_image
     n = len(lens)
@@ -96,11 +104,11 @@ def test_zipf_production_launch_compute_with_seeds(gpu_ctx, oracle, zipf_image, 
     seeds[np.nonzero(big)[0][:200]] = 0xFFFFFFFF  # all-ones seed on some split files
     d = np.zeros(n, crc.DESC_DTYPE)
     d["offset"], d["len"], d["aux"] = offs, lens, seeds
-    d_d = crc.DeviceBuffer(gpu_ctx, d.nbytes).upload(d)
-    d_out = crc.DeviceBuffer(gpu_ctx, 4 * n)
+    d_d = crc.DeviceBuffer(sctx, d.nbytes).upload(d)
+    d_out = crc.DeviceBuffer(sctx, 4 * n)
     try:
-        gpu_ctx.batch_device(d_d, n, img, d_out)
-        st = gpu_ctx.split_stats()
+        sctx.batch_device(d_d, n, img, d_out)
+        st = sctx.split_stats()
         got = d_out.download(np.uint32, n)
         exp = _oracle_mt(oracle, host, offs, lens, seeds)
         bad = np.nonzero(got != exp)[0]
@@ -118,7 +126,7 @@ def test_zipf_production_launch_compute_with_seeds(gpu_ctx, oracle, zipf_image, 
         d_out.free()
 
 
-def test_zipf_production_launch_verify_wrong_expectations(gpu_ctx, oracle, zipf_image, split_form):
+def test_zipf_production_launch_verify_wrong_expectations(sctx, oracle, zipf_image):
     import tfs_amd.crc as crc
     img, host, offs, lens, crc0 = zipf_image
     n = len(lens)
@@ -130,16 +138,16 @@ def test_zipf_production_launch_verify_wrong_expectations(gpu_ctx, oracle, zipf_
     d = np.zeros(n, crc.DESC_DTYPE)
     d["offset"], d["len"], d["aux"] = offs, lens, crc0
     d["aux"][wrong] ^= (1 << rng.integers(0, 32, wrong.size)).astype(np.uint32)
-    d_v = crc.DeviceBuffer(gpu_ctx, d.nbytes).upload(d)
-    d_ok = crc.DeviceBuffer(gpu_ctx, n)
-    d_c = crc.DeviceBuffer(gpu_ctx, 4 * n)
-    d_nb = crc.DeviceBuffer(gpu_ctx, 4)
+    d_v = crc.DeviceBuffer(sctx, d.nbytes).upload(d)
+    d_ok = crc.DeviceBuffer(sctx, n)
+    d_c = crc.DeviceBuffer(sctx, 4 * n)
+    d_nb = crc.DeviceBuffer(sctx, 4)
     try:
         for rep in range(2):  # twice on one stream: the slot and the plan are reused
             d_ok.zero()
             d_nb.zero()
-            gpu_ctx.verify_device(d_v, n, img, d_c, d_ok, d_nb)
-            st = gpu_ctx.split_stats()
+            sctx.verify_device(d_v, n, img, d_c, d_ok, d_nb)
+            st = sctx.split_stats()
             assert st["used"] > 0 and _tickets(st["units"]) >= 16 * st["grid"] * 16, st
             assert int(d_nb.download(np.uint32)[0]) == 1000, rep
             ok = d_ok.download(np.uint8, n)
@@ -150,7 +158,7 @@ def test_zipf_production_launch_verify_wrong_expectations(gpu_ctx, oracle, zipf_
             b.free()
 
 
-def test_split_launches_on_two_streams_overlap_and_agree(gpu_ctx, zipf_image, split_form):
+def test_split_launches_on_two_streams_overlap_and_agree(sctx, zipf_image):
     """Split launches of one context queued on two of its streams at once, each
     stream's scheduler slot with its own plan (no launch waits on the other
     stream's plan any more): every launch's CRCs exact."""
@@ -159,24 +167,24 @@ def test_split_launches_on_two_streams_overlap_and_agree(gpu_ctx, zipf_image, sp
     n = len(lens)
     half = n // 2
     parts = [(0, half), (half, n)]
-    s1, s2 = gpu_ctx.stream_create(), gpu_ctx.stream_create()
+    s1, s2 = sctx.stream_create(), sctx.stream_create()
     bufs = []
     try:
         outs = []
         for (a, b), s in zip(parts + parts, [s1, s2, s2, s1]):
             d = np.zeros(b - a, crc.DESC_DTYPE)
             d["offset"], d["len"] = offs[a:b], lens[a:b]
-            d_d = crc.DeviceBuffer(gpu_ctx, d.nbytes).upload(d)
-            d_o = crc.DeviceBuffer(gpu_ctx, 4 * (b - a))
+            d_d = crc.DeviceBuffer(sctx, d.nbytes).upload(d)
+            d_o = crc.DeviceBuffer(sctx, 4 * (b - a))
             bufs += [d_d, d_o]
-            gpu_ctx.batch_device(d_d, b - a, img, d_o, stream=s)
+            sctx.batch_device(d_d, b - a, img, d_o, stream=s)
             outs.append((a, b, d_o))
-        gpu_ctx.stream_sync(s1)
-        gpu_ctx.stream_sync(s2)
+        sctx.stream_sync(s1)
+        sctx.stream_sync(s2)
         for a, b, d_o in outs:
             assert np.array_equal(d_o.download(np.uint32, b - a), crc0[a:b]), (a, b)
     finally:
         for x in bufs:
             x.free()
-        gpu_ctx.stream_destroy(s1)
-        gpu_ctx.stream_destroy(s2)
+        sctx.stream_destroy(s1)
+        sctx.stream_destroy(s2)

@@ -303,7 +303,8 @@ struct tfs_crc_ctx {
   uint64_t split_launches = 0;
   std::atomic<bool> cu_reserve{true};   // leave a live resident kernel's CUs out of throughput launches
   std::atomic<int> split_files{1};  // throughput launches split files > kSplitMin (tfs_crc32_set_split): 0 off,
-                                   // 1 segments appended after the files, 2 address-ordered units
+                                   // 1 address-ordered units (product), 2 segments appended after the files
+                                   // (round 3's form, measurement build)
   std::atomic<uint32_t> cseg_lg{0};  // segmented compaction: 1 KiB << cseg_lg segments, 0 = whole records
   std::atomic<uint32_t> inject_skip{0}, inject_count{0};  // tfs_crc32_inject_device_error
   DevBuf packet_scratch;  // device-resident packet calls (parse descriptors, verdicts)
@@ -671,7 +672,9 @@ uint32_t slot_index(const tfs_crc_ctx* ctx, const SchedLease& L) {
 // (foreign slot).  Growing frees the plan, so st is drained first.
 int split_prepare(tfs_crc_ctx* ctx, hipStream_t st, uint32_t k, uint32_t n, SplitArgs* sa) {
   const uint32_t cap = uint32_t(std::min<uint64_t>(std::max<uint64_t>(2ull * n, 65536ull), kSplitMaxUnits));
-  const bool ao = ctx->split_files.load(std::memory_order_relaxed) == 2;
+  // the product's address-ordered unit list; the measurement build's appended
+  // form (set_split 2) and kernel variants (which read the appended layout)
+  const bool ao = ctx->split_files.load(std::memory_order_relaxed) == 1 && ctx->variant == 0;
   // address-ordered form: the plan's capacity counts every unit (files + segments)
   const uint32_t ucap = ao ? uint32_t(std::min<uint64_t>(uint64_t(n) + cap, 0xffffffffull)) : cap;
   const uint64_t bytes = ao ? ao_bytes(n, ucap) : split_bytes(n, cap);
@@ -2176,7 +2179,12 @@ int tfs_crc32_set_cu_reserve(tfs_crc_ctx* ctx, int on) {
 }
 
 int tfs_crc32_set_split(tfs_crc_ctx* ctx, int on) {
-  if (!ctx || on < 0 || on > 2) return TFS_EXIT_PARAMETER_ERROR;
+#ifdef TFS_CRC_MEASURE
+  const int top = 2;  // 2: round 3's appended form (measurement build)
+#else
+  const int top = 1;
+#endif
+  if (!ctx || on < 0 || on > top) return TFS_EXIT_PARAMETER_ERROR;
   ctx->split_files.store(on, std::memory_order_relaxed);
   return TFS_SUCCESS;
 }

@@ -950,6 +950,7 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
 // workgroup whose range would pass `cap` leaves its files whole (and writes
 // empty units into the part of its range below cap, so every unit the main
 // kernel takes is valid).
+#ifdef TFS_CRC_MEASURE
 template <int MODE>
 __global__ void __launch_bounds__(256) split_plan_kernel(const Desc* __restrict__ desc, uint32_t n, uint32_t vseed,
                                                          SplitArgs sa) {
@@ -1028,6 +1029,7 @@ __global__ void __launch_bounds__(256) split_fold_kernel(const Desc* __restrict_
     if ((threadIdx.x & (kWave - 1)) == 0 && bad) atomicAdd(n_bad, bad);
   }
 }
+#endif  // TFS_CRC_MEASURE
 
 // Address-ordered split plan (SplitUnit list, tfs_crc_device.h), step 1 of 3: the
 // number of whole segments of each block of kAoBlock files.
@@ -2482,40 +2484,50 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
   // capped grid; the tickets hand out any number of units.
   const dim3 grid(sa.plan ? (cap < kMaxGrid ? cap : kMaxGrid) : grid_for(n, cap)), block(kBlock);
   if (sa.plan && sa.ao) {
-    // Address-ordered form: count, scan, write the unit list; the product kernel
-    // over it; the fold (round 4).
+    // Address-ordered split (the product, round 4): count, scan
+    // and write the unit list before the main kernel, the fold after it.
     const uint32_t nb = ao_nblk(n);
     hipLaunchKernelGGL(split_ao_count_kernel, dim3(nb), dim3(kAoBlock), 0, stream, desc, n, sa);
     hipLaunchKernelGGL(split_ao_scan_kernel, dim3(1), dim3(1024), 0, stream, n, sa);
     hipLaunchKernelGGL(split_ao_write_kernel, dim3(nb), dim3(kAoBlock), 0, stream, desc, n, sa);
-    hipLaunchKernelGGL(
-        (crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, kCF, kTS, 1>), grid,
-        block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
-    const uint32_t fg = (n + 255u) / 256u;
-    hipLaunchKernelGGL((split_ao_fold_kernel<MODE>), dim3(fg < 1024u ? fg : 1024u), dim3(256), 0, stream, desc, n, tg,
-                       sa, out_crc, out_ok, n_bad);
-    return hipGetLastError();
-  }
-  if (sa.plan) {
-    hipLaunchKernelGGL((split_plan_kernel<MODE>), dim3((n + 255u) / 256u), dim3(256), 0, stream, desc, n, vseed, sa);
     if (const hipError_t e = hipGetLastError()) return e;
   }
   bool launched = false;
 #ifdef TFS_CRC_MEASURE
+  // Measurement build: round 3's appended split (segments after the files,
+  // tfs_crc32_set_split 2) and the kernel variants, which read that layout.
+  if (sa.plan && !sa.ao) {
+    hipLaunchKernelGGL((split_plan_kernel<MODE>), dim3((n + 255u) / 256u), dim3(256), 0, stream, desc, n, vseed, sa);
+    if (const hipError_t e = hipGetLastError()) return e;
+  }
   launched = variant != 0 && launch_measure_variant<MODE>(variant, grid, block, base, desc, n, tg, out_crc, out_ok,
                                                           n_bad, sched, stream, vseed, done_flag, seq, sa);
-#endif
-  // The product: chunked interleaved tickets (kCF files per ticket, the last
-  // n >> kTS one by one), PF stripes in flight.
-  if (!launched)
+  if (!launched && sa.plan && !sa.ao) {
     hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, kCF, kTS>),
                        grid, block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq,
                        sa);
-  if (const hipError_t e = hipGetLastError()) return e;
-  if (sa.plan) {
+    launched = true;
+  }
+  if (launched && sa.plan && !sa.ao) {
+    if (const hipError_t e = hipGetLastError()) return e;
     const uint32_t fg = (n + 255u) / 256u;
     hipLaunchKernelGGL((split_fold_kernel<MODE>), dim3(fg < 1024u ? fg : 1024u), dim3(256), 0, stream, desc, n, tg, sa,
                        out_crc, out_ok, n_bad);
+    return hipGetLastError();
+  }
+#endif
+  // The product: chunked interleaved tickets (kCF files per ticket, the last
+  // n >> kTS one by one), PF stripes in flight, the address-ordered unit list
+  // when the plan split files.
+  if (!launched)
+    hipLaunchKernelGGL(
+        (crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, kCF, kTS, 1>), grid, block,
+        0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
+  if (const hipError_t e = hipGetLastError()) return e;
+  if (sa.plan && sa.ao) {
+    const uint32_t fg = (n + 255u) / 256u;
+    hipLaunchKernelGGL((split_ao_fold_kernel<MODE>), dim3(fg < 1024u ? fg : 1024u), dim3(256), 0, stream, desc, n, tg,
+                       sa, out_crc, out_ok, n_bad);
   }
   return hipGetLastError();
 }

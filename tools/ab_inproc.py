@@ -9,11 +9,12 @@ drops out.
 
   python tools/ab_inproc.py OTHER_SO[,OTHER_SO...] [ROUNDS] [mode]   mode: verify (default) | zipf
 
-Two more entries, "product_nosplit" and "product_ao", are the product library's
-SAME context with file splitting switched off / set to the address-ordered unit
-list (tfs_crc32_set_split 0 / 2) for their rounds, so the split forms share one
-stream and one scratch set: the per-context placement noise (up to +-2 % between
-two contexts of one library) drops out.  OTHER_SO "-" compares only those.
+Two more entries: "product_nosplit" is the product library's SAME context with
+file splitting switched off (tfs_crc32_set_split 0) for its rounds, so split on
+vs off shares one stream and one scratch set and the per-context placement
+noise (up to +-2 % between two contexts of one library) drops out of that pair;
+"appended" is a measurement-build context in round 3's split form (segments
+after all files, set_split 2).  OTHER_SO "-" compares only those.
 """
 import ctypes
 import json
@@ -51,7 +52,9 @@ def main():
     ctx = crc.Context(0)
     prod = bind(crc.LIB_PATH)
     prod[0].tfs_crc32_set_split.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    libs = {"product": prod, "product_nosplit": prod, "product_ao": prod}
+    meas = bind(os.path.join(os.path.dirname(crc.LIB_PATH), "libtfs_crc_measure.so"))
+    meas[0].tfs_crc32_set_split.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    libs = {"product": prod, "product_nosplit": prod, "appended": meas}
     for i, o in enumerate(x for x in other.split(",") if x and x != "-"):
         libs["other%d" % i] = bind(os.path.abspath(o))
     if mode == "zipf":
@@ -93,8 +96,8 @@ def main():
     times = {k: [] for k in libs}
     for r in range(rounds):
         for name, (L, h) in libs.items():
-            if name.startswith("product"):  # split form of the one product context: 1, 0 or 2 (address order)
-                assert L.tfs_crc32_set_split(h, {"product": 1, "product_nosplit": 0, "product_ao": 2}[name]) == 0
+            if name in ("product", "product_nosplit", "appended"):  # split forms (tfs_crc32_set_split)
+                assert L.tfs_crc32_set_split(h, {"product": 1, "product_nosplit": 0, "appended": 2}[name]) == 0
             e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
             L.tfs_crc32_event_create(h, ctypes.byref(e0))
             L.tfs_crc32_event_create(h, ctypes.byref(e1))
