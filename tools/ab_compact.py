@@ -115,7 +115,8 @@ def main():
         cases += [(0, "shift1")] + [(v, "shift1") for v in want if v in (31, 32)]
     cases += [(0, "split%d" % S) for S in splits]
     # AB_SEG=S[,S...]: the segmented compaction (tfs_crc32_set_compact_segment) on the
-    # product context itself, toggled around its rounds (no second context's placement)
+    # product context itself, toggled around its rounds (no second context's placement);
+    # the other cases run it with whole records (set_compact_segment 0)
     segs = [int(x) for x in os.environ.get("AB_SEG", "").split(",") if x]
     cases += [("seg%d" % S, "packed") for S in segs]
     d_st = crc.DeviceBuffer(ctx, 4 * max([int(k.size)] + [getattr(b, "njobs", 0) for b in jobsets.values()]))
