@@ -2743,7 +2743,11 @@ hipError_t launch_synth_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, uint
 // Calibration: copy by wave-contiguous chunks of CH bytes (the record kernel's
 // shape: one wave streams one range), chunk c to wave c mod W; each wave moves
 // PF 1 KiB stripes per step (16 B per lane, nt loads, store kind SK).
-template <int PF, int SK>
+// HOLE (round 4, partial-line writes): 1 leaves the chunk's first 16 bytes
+// unwritten (one partial line per chunk), 2 also its last 16 bytes, 3 writes
+// those two 16-byte pieces as byte stores (whole lines, assembled from partial
+// stores of one wave) -- the record kernel's boundary-line pattern on a dense copy.
+template <int PF, int SK, int HOLE = 0>
 __global__ void __launch_bounds__(kBlock) membench_copy_chunk_kernel(const uint8_t* __restrict__ src,
                                                                      uint8_t* __restrict__ dst, uint64_t nbytes,
                                                                      uint64_t ch) {
@@ -2762,6 +2766,17 @@ __global__ void __launch_bounds__(kBlock) membench_copy_chunk_kernel(const uint8
       for (int k = 0; k < PF; ++k) {
         const u32x4 w = {v[k].x, v[k].y, v[k].z, v[k].w};
         gu128wp a = reinterpret_cast<gu128wp>(d + b + o + 1024u * k);
+        const bool first = o == 0 && k == 0 && lane == 0;
+        const bool last = o + 1024u * (k + 1) >= ch && k == PF - 1 && lane == kWave - 1;
+        if (HOLE && (first || (HOLE >= 2 && last))) {
+          if (HOLE == 3) {
+            uint8_t* bp = reinterpret_cast<uint8_t*>(d + b + o + 1024u * k);
+            const uint32_t ww[4] = {w[0], w[1], w[2], w[3]};
+#pragma unroll
+            for (int i = 0; i < 16; ++i) bp[i] = uint8_t(ww[i >> 2] >> (8 * (i & 3)));
+          }
+          continue;
+        }
         if (SK == 1) __builtin_nontemporal_store(w, a);
         else *a = w;
       }
@@ -2894,6 +2909,12 @@ hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, u
     uint8_t* d = reinterpret_cast<uint8_t*>(out);
     if (S == 1)
       hipLaunchKernelGGL((membench_copy_chunk_kernel<8, 1>), g, dim3(kBlock), 0, stream, base, d, nb, ch);
+    else if (S == 2)  // nt stores, one 16-byte hole per chunk (partial-line writes, round 4)
+      hipLaunchKernelGGL((membench_copy_chunk_kernel<8, 1, 1>), g, dim3(kBlock), 0, stream, base, d, nb, ch);
+    else if (S == 3)  // nt stores, holes at both ends of each chunk
+      hipLaunchKernelGGL((membench_copy_chunk_kernel<8, 1, 2>), g, dim3(kBlock), 0, stream, base, d, nb, ch);
+    else if (S == 4)  // nt stores, both ends written as byte stores
+      hipLaunchKernelGGL((membench_copy_chunk_kernel<8, 1, 3>), g, dim3(kBlock), 0, stream, base, d, nb, ch);
     else
       hipLaunchKernelGGL((membench_copy_chunk_kernel<8, 0>), g, dim3(kBlock), 0, stream, base, d, nb, ch);
     return hipGetLastError();
