@@ -71,6 +71,9 @@ def main():
     bidx = np.repeat(np.arange(nblocks, dtype=np.uint64), nl)
     soff = bidx * blk + np.tile(live1.astype(np.uint64) * rec, nblocks)
     k = np.arange(nblocks * nl, dtype=np.uint64)
+    # AB_ALIGNED=1 adds "aligned64k": the same number of jobs over a dense, 64 KiB-aligned
+    # record list (src = dest = j * 65,536, size 65,536) -- the dense copy's own layout
+    # through the record kernel (timing only: the FileInfo checks fail)
     dsts = {"packed": k * rec,                                   # the product workload (contiguous new blocks)
             "dst16": k * 65584 + (soff & np.uint64(15)),         # delta == 0 mod 16: no lane shift
             "dst128": k * 65664 + (soff & np.uint64(127)),       # delta == 0 mod 128: whole lines per stripe
@@ -90,6 +93,11 @@ def main():
         j["size"] = rec
         j["new_offset"] = (do % np.uint64(1 << 31)).astype(np.int32)
         jobsets[name] = crc.DeviceBuffer(ctx, j.nbytes).upload(j)
+    if os.environ.get("AB_ALIGNED"):
+        j = np.zeros(k.size, crc.COMPACT_JOB_DTYPE)
+        j["src_offset"] = j["dest_offset"] = k * np.uint64(65536)
+        j["file_id"], j["size"] = 1, 65536
+        jobsets["aligned64k"] = crc.DeviceBuffer(ctx, j.nbytes).upload(j)
     for S in splits:
         npc = (rec + S - 1) // S
         psz = (rec + npc - 1) // npc
@@ -114,6 +122,8 @@ def main():
     if 31 in want or 32 in want:
         cases += [(0, "shift1")] + [(v, "shift1") for v in want if v in (31, 32)]
     cases += [(0, "split%d" % S) for S in splits]
+    if os.environ.get("AB_ALIGNED"):
+        cases += [(0, "aligned64k")]
     # AB_SEG=S[,S...]: the segmented compaction (tfs_crc32_set_compact_segment) on the
     # product context itself, toggled around its rounds (no second context's placement);
     # the other cases run it with whole records (set_compact_segment 0)
@@ -139,7 +149,7 @@ def main():
         return ctxs[v]
 
     for v, js in cases:
-        if v in (26, 30, 61, 64, 65, 66, 67, 68, 69, 70, 71) or js.startswith("split"):
+        if v in (26, 30, 61, 64, 65, 66, 67, 68, 69, 70, 71) or js.startswith("split") or js == "aligned64k":
             continue
         d_bad.zero()
         c = ctx_of(v)
