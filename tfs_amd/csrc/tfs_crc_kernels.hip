@@ -2658,6 +2658,8 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
   else if (variant == 35) TFS_CJ(true, true, false, kCompactDiag, 8);
   else if (variant == 36) TFS_CJ(true, true, false, kCompactDiag | 128);
   else if (variant == 37) TFS_CJ(true, true, false, kCompactDiag, 4);
+  else if (variant == 75) TFS_CJ(true, true, false, kCompactDiag | 1, 8);  // plain stores, PF 8 (round 4)
+  else if (variant == 76) TFS_CJ(true, true, false, kCompactDiag | 1, 6);  // plain stores, PF 6
   else if (variant == 60) TFS_CJ(true, true, false, kCompactDiag | 256);      // static records, product otherwise
   else if (variant == 61) TFS_CJ(true, true, false, kCompactDiag | 256 | 2);  // static, no payload CRC steps
   else if (variant == 62) TFS_CJ(true, true, false, kCompactDiag | 512);      // ring refilled in bursts of CPF
