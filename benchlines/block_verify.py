@@ -164,6 +164,10 @@ def bench_block_verify_device(args):
             checked += 1
     def timed(c, fn):
         e0, e1 = crc.Event(c), crc.Event(c)
+        # warm up again right before the clock: the parity pass above leaves the GPU
+        # idle for seconds, and the first launches after an idle gap run slower
+        for _ in range(max(1, args.warmup)):
+            fn(c)
         if dist:
             dist.barrier()
         c.sync()
