@@ -181,6 +181,7 @@ def main():
             raise SystemExit("ab_compact: verify variant %d reports bad records" % v)
         times["verify_%d" % v] = []
     cb = int(live_bytes) // 16 * 16
+    reps = int(os.environ.get("AB_REPS", "3"))  # back-to-back launches per timing (sustained load: 16)
     for r in range(rounds):
         for v, js in cases:
             c = ctx_of(v)
@@ -188,11 +189,11 @@ def main():
             nn = getattr(jobsets[js], "njobs", nj)
             c.compact_jobs_device(img, total, jobsets[js], nn, d_dst, None, d_st, d_bad)
             e0.record()
-            for _ in range(3):
+            for _ in range(reps):
                 c.compact_jobs_device(img, total, jobsets[js], nn, d_dst, None, d_st, d_bad)
             e1.record()
             c.sync()
-            times["%s_%s" % (v, js)].append(e0.elapsed_ms(e1) / 3)
+            times["%s_%s" % (v, js)].append(e0.elapsed_ms(e1) / reps)
         ctx.set_compact_segment(0)
         for v in vcases:
             c = ctxs[v]
@@ -217,11 +218,11 @@ def main():
             nb = cb - max(dsk, ssk) // 16 * 16
             ctx.membench_device(pat, img.ptr + ssk, None, 0, nb, d_dst.ptr + dsk, grid=grid)
             e0.record()
-            for _ in range(3):
+            for _ in range(reps):
                 ctx.membench_device(pat, img.ptr + ssk, None, 0, nb, d_dst.ptr + dsk, grid=grid)
             e1.record()
             ctx.sync()
-            times[cname(pat, grid, dsk, ssk)].append(e0.elapsed_ms(e1) / 3 * cb / nb)
+            times[cname(pat, grid, dsk, ssk)].append(e0.elapsed_ms(e1) / reps * cb / nb)
         print("round %d done" % r, file=sys.stderr, flush=True)
     res = {}
     for name, v in times.items():
