@@ -177,15 +177,29 @@ def test_gpu_statuses_and_device_form(gpu_ctx, ec_oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 6])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 6, 8])
 def test_gpu_kernel_forms_ragged_sizes(gpu_ctx, ec_oracle, variant, monkeypatch):
     """Every kernel form (TFS_EC_VARIANT 0: one grid step of tiles per wave; 1-3:
     chunks of 2, 4, 8 tiles per wave step with the cross-tile prefetch; 4, 6: the
     tile kernel striding over 8,192 / 2,048 workgroups) on unit counts that leave
     partial tiles, partial chunks and a grid stride larger than the work:
-    encode and a 3-member decode byte-exact against the oracle."""
+    encode and a 3-member decode byte-exact against the oracle; 8: 16 bytes per
+    lane, 8 units per wave step.  The forms live in the measurement build
+    (the product library never reads TFS_EC_VARIANT), so a variant runs on a
+    measurement-build context."""
+    import tfs_amd.crc as crc
     from tfs_amd.ec import ErasureCode
     monkeypatch.setenv("TFS_EC_VARIANT", str(variant))
+    vctx = crc.Context(0, measure=True) if variant else gpu_ctx
+    try:
+        _ec_forms_case(vctx, ec_oracle, variant)
+    finally:
+        if variant:
+            vctx.close()
+
+
+def _ec_forms_case(gpu_ctx, ec_oracle, variant):
+    from tfs_amd.ec import ErasureCode
     k, m = 5, 3
     for units in (1, 3, 5, 17, 33, 1031, 70001):
         size = units * 1024

@@ -94,6 +94,71 @@ __global__ void __launch_bounds__(256) ec_apply_kernel(EcArgs a, const uint32_t*
   }
 }
 
+#ifdef TFS_CRC_MEASURE
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4v* gu128p;
+typedef __attribute__((address_space(1))) u32x4v* gu128wp;
+
+// Wide form (measurement, TFS_EC_VARIANT 8, round 4): 16 bytes per lane, so
+// lane l owns bytes 16*(l & 7) of packet c of unit (l >> 3) and a wave step
+// covers 8 units (8 KiB of every member): half the memory instructions of the
+// product for the same bytes, at more VGPRs (fewer waves per SIMD).
+template <int OG>
+__global__ void __launch_bounds__(256) ec_apply_wide_kernel(EcArgs a, const uint32_t* __restrict__ masks) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t u = uint32_t(lane) >> 3;
+  const uint32_t off = 16u * uint32_t(lane & 7);
+  const uint64_t ntiles = (a.units + 7) / 8;
+  const uint64_t wave = uint64_t(blockIdx.x) * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t nwaves = uint64_t(gridDim.x) * (blockDim.x / 64);
+  for (uint64_t t = wave; t < ntiles; t += nwaves) {
+    const uint64_t unit = t * 8 + u;
+    const bool ok = unit < a.units;
+    const uint64_t base = unit * 1024u + off;
+    u32x4v acc[OG][8];
+#pragma unroll
+    for (int o = 0; o < OG; ++o)
+#pragma unroll
+      for (int r = 0; r < 8; ++r) acc[o][r] = u32x4v{0u, 0u, 0u, 0u};
+    u32x4v in[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      in[c] = ok ? __builtin_nontemporal_load(reinterpret_cast<gu128p>(reinterpret_cast<uintptr_t>(a.src[0] + base + 128u * c)))
+                 : u32x4v{0u, 0u, 0u, 0u};
+    for (uint32_t s = 0; s < a.S; ++s) {
+      u32x4v nx[8];
+      const bool more = s + 1 < a.S;
+      const uint8_t* np = a.src[more ? s + 1 : s];
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        nx[c] = (ok && more) ? __builtin_nontemporal_load(reinterpret_cast<gu128p>(reinterpret_cast<uintptr_t>(np + base + 128u * c)))
+                             : u32x4v{0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int o = 0; o < OG; ++o)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const uint32_t* m = masks + ((uint32_t(o) * 8u + uint32_t(r)) * a.S + s) * 8u;
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            const uint32_t mk = m[c];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[o][r][q] = xand(acc[o][r][q], in[c][q], mk);
+          }
+        }
+#pragma unroll
+      for (int c = 0; c < 8; ++c) in[c] = nx[c];
+    }
+    if (ok) {
+#pragma unroll
+      for (int o = 0; o < OG; ++o)
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          __builtin_nontemporal_store(acc[o][r], reinterpret_cast<gu128wp>(reinterpret_cast<uintptr_t>(a.dst[o] + base + 128u * r)));
+    }
+  }
+}
+#endif  // TFS_CRC_MEASURE
+
 // Chunked form (K > 1): a wave takes K consecutive tiles (4K KiB of every
 // member) per step of its grid stride, and the next tile's first member is
 // loaded while the current tile's last member is combined, so the loads never
@@ -206,6 +271,17 @@ hipError_t launch_ec_apply(const EcArgs& a, int og, int variant, hipStream_t str
   if (blocks > cap) blocks = cap;
   const dim3 g(static_cast<unsigned>(blocks)), b(256);
 #ifdef TFS_CRC_MEASURE
+  if (variant == 8) {  // measurement: 16 bytes per lane, 8 units per wave step
+    const uint64_t t8 = (a.units + 7) / 8;
+    const dim3 g8(static_cast<unsigned>((t8 + 3) / 4)), b8(256);
+    switch (og) {
+      case 1: hipLaunchKernelGGL(ec_apply_wide_kernel<1>, g8, b8, 0, stream, a, a.masks); break;
+      case 2: hipLaunchKernelGGL(ec_apply_wide_kernel<2>, g8, b8, 0, stream, a, a.masks); break;
+      case 3: hipLaunchKernelGGL(ec_apply_wide_kernel<3>, g8, b8, 0, stream, a, a.masks); break;
+      default: hipLaunchKernelGGL(ec_apply_wide_kernel<4>, g8, b8, 0, stream, a, a.masks); break;
+    }
+    return hipGetLastError();
+  }
   if (variant == 7) {  // measurement: the memory shape without the bitmatrix product
     switch (og) {
       case 1: hipLaunchKernelGGL((ec_apply_kernel<1, false>), g, b, 0, stream, a, a.masks); break;
