@@ -60,7 +60,7 @@ TRAFFIC_NOTE = ("quoted: HBM bytes per launch from the committed rocprofv3 PMC p
 HEADLINE_KERNEL = "crc_files_kernel<1, 16, 5, true, true, true, 1, false, true, 1, false, false, 4, 3, 1"
 
 
-PACKET_PIPELINE = ("packet pipeline: packet_parse_kernel + crc_files_kernel<1, ..., 4, 3> + "
+PACKET_PIPELINE = ("packet pipeline: packet_parse_kernel + crc_files_kernel<1, ..., 4, 3, 1> + "
                    "packet_finish_kernel")
 
 

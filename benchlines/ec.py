@@ -62,7 +62,7 @@ def bench_ec(args):
         kms = e0.elapsed_ms(e1) / args.steps
         out[name] = {"ms": kms, "GiBs_data": world * args.steps * k * size / el / 2**30,
                      "hbm_GBs": (rd + wr) * size / (kms / 1e3) / 1e9}
-    e_traffic, e_src = _pmc_traffic("profiles/r02_s4/ec/pmc_summary.json", "ec_apply_kernel<3>", args.ec_mib == 1536)
+    e_traffic, e_src = _pmc_traffic("profiles/r04/final/ec/pmc_summary.json", "ec_apply_kernel<3, true>", args.ec_mib == 1536)
     res = {
         "metric": "GiB/s of data encoded (ErasureCode k=5 m=3, Cauchy bitmatrix w=8 ps=128), device-resident",
         "value": out["encode"]["GiBs_data"], "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
@@ -72,7 +72,7 @@ def bench_ec(args):
         "roofline": {"bound": "hbm", "achieved": out["encode"]["hbm_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": out["encode"]["hbm_GBs"] / HBM_PEAK_GBS, "traffic": e_traffic, "traffic_source": e_src, "traffic_measured_in_this_run": False, "traffic_note": TRAFFIC_NOTE,
                      "algorithmic_bytes_per_launch": float(k + m) * size,
-                     "kernel": "ec_apply_kernel<3>", "kernel_ms_avg": out["encode"]["ms"]},
+                     "kernel": "ec_apply_kernel<3, true>", "kernel_ms_avg": out["encode"]["ms"]},
         "decode": out["decode"],
     }
     if rank == 0 and not args.no_cpu:

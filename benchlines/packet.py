@@ -70,7 +70,7 @@ def bench_packet(args):
     # the CRC kernel reads the body and its descriptor and writes crc + ok; finish
     # reads pre-status/ok and writes status (and crc).
     algo = n * (float(frame) + 16 + 16 + 4 + 16 + 4 + 1 + 4 + 4 + 1 + 4)
-    p_traffic, p_src = _pmc_traffic("profiles/r02_s4/packet/pmc_summary.json", PACKET_PIPELINE, n == 1048576)
+    p_traffic, p_src = _pmc_traffic("profiles/r04/final/packet/pmc_summary.json", PACKET_PIPELINE, n == 1048576)
     res = {
         "metric": "GiB/s packet bytes CRC-verified (BasePacket::decode), device-resident V1 frames",
         "value": world * args.steps * n * frame / el / 2**30, "unit": "GiB/s", "n_gpus": world,
