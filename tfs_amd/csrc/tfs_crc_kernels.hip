@@ -1969,7 +1969,7 @@ __device__ __forceinline__ void copy_unaligned(const uint8_t* s, uint8_t* d, uin
 // (variants 33-35, 37: 6, 7, 8, 4).
 constexpr int kCompactDiag = 4 | 8;
 template <bool WIDE, bool DPPSH = true, bool VERIFY = false, int DIAG = kCompactDiag, int CPF = kPF, int CF = 1,
-          int TS = 0, bool SEG = false>
+          int TS = 0, bool SEG = false, int WW = 1>
 __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __restrict__ src, uint64_t src_len,
                                                               const RawMeta* __restrict__ metas,
                                                               const int32_t* __restrict__ flags,
@@ -1999,8 +1999,10 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
     if constexpr (SEG) return load_cunit(u, njobs, src_len, jobs, plan, cs.cap, cs.lg);
     return load_crec<WIDE, VERIFY>(u, src_len, metas, flags, dest_off, jobs);
   };
-  FileCursor<kIL, 1, CF, TS> fc;  // CF > 1: chunks of CF records per ticket (measurement)
-  Tickets<kIL>& tk = fc.tk;
+  // CF > 1: chunks of CF records per ticket; WW > 1: WW consecutive records per
+  // ticket-group slot, so an XCD's waves walk WW-record runs (measurement)
+  FileCursor<kIL, WW, CF, TS> fc;
+  auto& tk = fc.tk;
   fc.init(sched, n, blockIdx.x & 7u, gridDim.x * wpb,
           blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave));
   if (DIAG & 256) tk.dyn = false;  // measurement: static record r -> wave r mod W (the chunk copy's order)
@@ -2660,6 +2662,8 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
   else if (variant == 37) TFS_CJ(true, true, false, kCompactDiag, 4);
   else if (variant == 75) TFS_CJ(true, true, false, kCompactDiag | 1, 8);  // plain stores, PF 8 (round 4)
   else if (variant == 76) TFS_CJ(true, true, false, kCompactDiag | 1, 6);  // plain stores, PF 6
+  else if (variant == 77) TFS_CJ(true, true, false, kCompactDiag, kPF, 1, 0, false, 4);   // 4 records per group slot
+  else if (variant == 78) TFS_CJ(true, true, false, kCompactDiag, kPF, 1, 0, false, 16);  // 16 records per group slot
   else if (variant == 60) TFS_CJ(true, true, false, kCompactDiag | 256);      // static records, product otherwise
   else if (variant == 61) TFS_CJ(true, true, false, kCompactDiag | 256 | 2);  // static, no payload CRC steps
   else if (variant == 62) TFS_CJ(true, true, false, kCompactDiag | 512);      // ring refilled in bursts of CPF

@@ -123,7 +123,10 @@ def main():
         cases += [(0, "shift1")] + [(v, "shift1") for v in want if v in (31, 32)]
     cases += [(0, "split%d" % S) for S in splits]
     if os.environ.get("AB_ALIGNED"):
-        cases += [(0, "aligned64k")]
+        # every requested variant on the dense layout too (the probe copies 65-71
+        # and the kernel reduced to a copy, 64, included): where the 8 % between
+        # the kernel and the chunk copy of the same layout goes
+        cases += [(0, "aligned64k")] + [(v, "aligned64k") for v in want if v not in (31, 32)]
     # AB_SEG=S[,S...]: the segmented compaction (tfs_crc32_set_compact_segment) on the
     # product context itself, toggled around its rounds (no second context's placement);
     # the other cases run it with whole records (set_compact_segment 0)
