@@ -2662,6 +2662,8 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
   else if (variant == 37) TFS_CJ(true, true, false, kCompactDiag, 4);
   else if (variant == 75) TFS_CJ(true, true, false, kCompactDiag | 1, 8);  // plain stores, PF 8 (round 4)
   else if (variant == 76) TFS_CJ(true, true, false, kCompactDiag | 1, 6);  // plain stores, PF 6
+  else if (variant == 79) TFS_CJ(true, true, false, 4 | 512 | 2 | 16, 8);        // 64 with non-temporal loads
+  else if (variant == 80) TFS_CJ(true, true, false, kCompactDiag | 512 | 2 | 16 | 256, 8);  // 64, static order
   else if (variant == 77) TFS_CJ(true, true, false, kCompactDiag, kPF, 1, 0, false, 4);   // 4 records per group slot
   else if (variant == 78) TFS_CJ(true, true, false, kCompactDiag, kPF, 1, 0, false, 16);  // 16 records per group slot
   else if (variant == 60) TFS_CJ(true, true, false, kCompactDiag | 256);      // static records, product otherwise
