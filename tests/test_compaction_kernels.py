@@ -19,7 +19,7 @@ def ocrc_payload(oracle, img, meta):
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[0, 22, 23, 25, 27, 29, 31, 32, 33, 35, 36, 37, 39, 40, 42, 43, 45, 60, 62, 63, 72, 73, 74, 75, 76, 77, 78])
+@pytest.fixture(params=[0, 22, 23, 25, 27, 29, 31, 32, 33, 35, 36, 37, 39, 40, 42, 43, 45, 60, 62, 63, 72, 73, 74, 75, 76, 77, 78, 81, 82, 83])
 def vctx(request, monkeypatch):
     import tfs_amd.crc as crc
     monkeypatch.setenv("TFS_CRC_VARIANT", str(request.param))

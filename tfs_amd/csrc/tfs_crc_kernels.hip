@@ -1887,24 +1887,34 @@ struct CState {
 // new block instead of splitting two lines with its neighbours (a split line
 // leaves the chip as two partial writes).  Needs a destination congruent to the
 // source mod 4 and 128 readable bytes past the record inside the source.
+// The payload geometry of a record (and its copy distance): wave-uniform, no loads.
 template <bool DA>
+__device__ __forceinline__ FileGeo<kRun> crec_geo(const CRec& r, const uint8_t* src, uint64_t src_len, uint8_t* dst,
+                                                  uintptr_t junk, intptr_t& delta) {
+  if (r.pre != kSuccess) {  // nothing is read for a record rejected up front
+    delta = 0;
+    return make_geo<kRun>(reinterpret_cast<const uint8_t*>(junk), 0u, 0u);
+  }
+  const uint8_t* rec = src + r.soff;
+  delta = intptr_t(dst + r.doff) - intptr_t(rec);
+  uint32_t aoff = 0u;
+  if (DA && r.soff + kFileInfoSize + uint64_t(r.plen) + 128u <= src_len)
+    aoff = uint32_t(-(delta & ~intptr_t(15))) & 127u;
+  return make_geo<kRun>(rec + kFileInfoSize, r.plen, 0u, aoff);
+}
+
+// HV (measurement): stripe 0 and the tail as one dwordx4 per lane each (load_head).
+template <bool DA, bool HV = false>
 __device__ __forceinline__ CState issue_crec(const CRec& r, const uint8_t* src, uint64_t src_len, uint8_t* dst,
                                              int lane, uintptr_t junk) {
   CState s;
+  s.g = crec_geo<DA>(r, src, src_len, dst, junk, s.delta);
   if (r.pre == kSuccess) {
-    const uint8_t* rec = src + r.soff;
-    s.hb = lane < kFileInfoSize && r.kind != 1u ? uint32_t(rec[lane]) : 0u;
-    s.delta = intptr_t(dst + r.doff) - intptr_t(rec);
-    uint32_t aoff = 0u;
-    if (DA && r.soff + kFileInfoSize + uint64_t(r.plen) + 128u <= src_len)
-      aoff = uint32_t(-(s.delta & ~intptr_t(15))) & 127u;
-    s.g = make_geo<kRun>(rec + kFileInfoSize, r.plen, 0u, aoff);
-    s.h = load_head<kRun>(s.g, lane);
-  } else {  // nothing is read for a record rejected up front
+    s.hb = lane < kFileInfoSize && r.kind != 1u ? uint32_t(src[r.soff + uint32_t(lane)]) : 0u;
+    s.h = load_head<kRun, HV>(s.g, lane);
+  } else {
     s.hb = 0u;
-    s.g = make_geo<kRun>(reinterpret_cast<const uint8_t*>(junk), 0u, 0u);
     s.h = Head<kRun>{};
-    s.delta = 0;
   }
   return s;
 }
@@ -1966,7 +1976,11 @@ __device__ __forceinline__ void copy_unaligned(const uint8_t* s, uint8_t* d, uin
 // CPF stripes (DIAG bit 9: CPF loads out together after CPF stripes are used,
 // as the chunk copy does; 64 also skips the CRC steps and the header/tail
 // stores).  CPF: stripes in flight per wave
-// (variants 33-35, 37: 6, 7, 8, 4).
+// (variants 33-35, 37: 6, 7, 8, 4).  Round 4, measurement: DIAG bit 10 the
+// cross-record ring (lane_chain XF: a ring slot freed past this record's last
+// stripe takes the next record's stripe, so the wave's loads stay in HBM across
+// the record boundary; variant 81), bit 11 stripe 0 and the tail loaded as one
+// dwordx4 per lane (load_head HV; 82), both (83).
 constexpr int kCompactDiag = 4 | 8;
 template <bool WIDE, bool DPPSH = true, bool VERIFY = false, int DIAG = kCompactDiag, int CPF = kPF, int CF = 1,
           int TS = 0, bool SEG = false, int WW = 1>
@@ -1981,6 +1995,8 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
   constexpr bool DA = !VERIFY && (DIAG & 4) != 0;
   constexpr bool LNT = (DIAG & 8) && !VERIFY ? false : kNT;  // the verify form keeps the headline's loads
   constexpr int SK = (DIAG & 1) ? 0 : ((DIAG & 128) ? 2 : 1);  // copy-through store kind (st128_kind)
+  constexpr bool XF = (DIAG & 1024) != 0 && !(DIAG & 512);
+  constexpr bool HV = (DIAG & 2048) != 0;
   __shared__ uint32_t lds_tables[LdsLayout<kS8>::bytes / 4];
   load_tables<kRun, kPAR, kS8>(lds_tables, tg);
   const int lane = threadIdx.x & (kWave - 1);
@@ -2013,7 +2029,7 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
     if (f >= n) break;
     uint32_t fn = CF > 1 ? fc.take(lane) : tk.resolve(tk.issue(lane), lane);
     CRec cur = unit(f);
-    CState st = issue_crec<DA>(cur, src, src_len, dst, lane, junk);
+    CState st = issue_crec<DA, HV>(cur, src, src_len, dst, lane, junk);
     uint4 buf[CPF][kRun / 16];
     load_ring<kRun, CPF, LNT>(st.g, lane, buf, junk);
     CRec nxt = fn < n ? unit(fn) : CRec{};
@@ -2021,18 +2037,23 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
     for (;;) {
       // DIAG bit 5 (variant 31, measurement): byte-shifted records copy after the CRC (copy_unaligned)
       const bool chain_copy = !(DIAG & 32) || (st.delta & 3) == 0;
-      uint32_t c = st.g.nstripes ? lane_chain<kRun, CPF, LNT, kS8, !VERIFY, (DIAG & 512) ? CPF : 1, DPPSH, SK,
-                                            (DIAG & 2) != 0, !(DIAG & 16), (DIAG & 64) != 0>(
-                                     lds_tables, lb, st.g, st.h, buf, lane, junk, st.delta, chain_copy)
-                                 : 0u;
-      // The next record's loads go out before this one is finished.
       const bool more = fn < n;
       const CRec ncur = nxt;
+      // XF: the next record's geometry first -- this record's ring refills run into it.
+      intptr_t ndelta = 0;
+      FileGeo<kRun> ng = st.g;
+      if constexpr (XF) ng = crec_geo<DA>(more ? ncur : CRec{0, 0, 0, 0, 0, 0, kExitParameterError, 0u, 0u}, src,
+                                         src_len, dst, junk, ndelta);
+      uint32_t c = st.g.nstripes ? lane_chain<kRun, CPF, LNT, kS8, !VERIFY, (DIAG & 512) ? CPF : 1, DPPSH, SK,
+                                            (DIAG & 2) != 0, !(DIAG & 16), (DIAG & 64) != 0, XF>(
+                                     lds_tables, lb, st.g, st.h, buf, lane, junk, st.delta, chain_copy, &ng)
+                                 : 0u;
+      // The next record's loads go out before this one is finished.
       CState ns = st;
       uint32_t fnn = n;
       if (more) {
-        ns = issue_crec<DA>(ncur, src, src_len, dst, lane, junk);
-        load_ring<kRun, CPF, LNT>(ns.g, lane, buf, junk);
+        ns = issue_crec<DA, HV>(ncur, src, src_len, dst, lane, junk);
+        if (!XF || !st.g.nstripes) load_ring<kRun, CPF, LNT>(ns.g, lane, buf, junk);
         fnn = CF > 1 ? fc.take(lane) : tk.resolve(jv, lane);
         if (fnn < n) {
           nxt = unit(fnn);
@@ -2664,6 +2685,9 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
   else if (variant == 76) TFS_CJ(true, true, false, kCompactDiag | 1, 6);  // plain stores, PF 6
   else if (variant == 79) TFS_CJ(true, true, false, 4 | 512 | 2 | 16, 8);        // 64 with non-temporal loads
   else if (variant == 80) TFS_CJ(true, true, false, kCompactDiag | 512 | 2 | 16 | 256, 8);  // 64, static order
+  else if (variant == 81) TFS_CJ(true, true, false, kCompactDiag | 1024);         // cross-record ring
+  else if (variant == 82) TFS_CJ(true, true, false, kCompactDiag | 2048);         // stripe 0 / tail as dwordx4
+  else if (variant == 83) TFS_CJ(true, true, false, kCompactDiag | 1024 | 2048);  // both
   else if (variant == 77) TFS_CJ(true, true, false, kCompactDiag, kPF, 1, 0, false, 4);   // 4 records per group slot
   else if (variant == 78) TFS_CJ(true, true, false, kCompactDiag, kPF, 1, 0, false, 16);  // 16 records per group slot
   else if (variant == 60) TFS_CJ(true, true, false, kCompactDiag | 256);      // static records, product otherwise
