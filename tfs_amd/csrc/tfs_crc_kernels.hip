@@ -1980,7 +1980,9 @@ __device__ __forceinline__ void copy_unaligned(const uint8_t* s, uint8_t* d, uin
 // cross-record ring (lane_chain XF: a ring slot freed past this record's last
 // stripe takes the next record's stripe, so the wave's loads stay in HBM across
 // the record boundary; variant 81), bit 11 stripe 0 and the tail loaded as one
-// dwordx4 per lane (load_head HV; 82), both (83).
+// dwordx4 per lane (load_head HV; 82), both (83); bit 12 no per-record combine
+// (finish_file skipped: wrong CRCs and statuses, timing only; 84, and 85 on the
+// copy-only form 64).
 constexpr int kCompactDiag = 4 | 8;
 template <bool WIDE, bool DPPSH = true, bool VERIFY = false, int DIAG = kCompactDiag, int CPF = kPF, int CF = 1,
           int TS = 0, bool SEG = false, int WW = 1>
@@ -2087,7 +2089,7 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
         } else {  // tiny payload, or a destination not congruent mod 4
           copy_unaligned(rec + kFileInfoSize, drec + kFileInfoSize, len, lane);
         }
-        c = finish_file<kRun, kS8>(lds_tables, lb, st.g, st.h, c, lane);
+        if (!(DIAG & 4096)) c = finish_file<kRun, kS8>(lds_tables, lb, st.g, st.h, c, lane);
         const uint64_t hid = uint64_t(hdr_dword(st.hb, 0)) | uint64_t(hdr_dword(st.hb, 1)) << 32;
         if (cur.kind == 1u) {
         } else if (hid != cur.fid) status = kExitFileInfoError;
@@ -2685,6 +2687,8 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
   else if (variant == 76) TFS_CJ(true, true, false, kCompactDiag | 1, 6);  // plain stores, PF 6
   else if (variant == 79) TFS_CJ(true, true, false, 4 | 512 | 2 | 16, 8);        // 64 with non-temporal loads
   else if (variant == 80) TFS_CJ(true, true, false, kCompactDiag | 512 | 2 | 16 | 256, 8);  // 64, static order
+  else if (variant == 84) TFS_CJ(true, true, false, kCompactDiag | 4096);                  // no combine
+  else if (variant == 85) TFS_CJ(true, true, false, kCompactDiag | 512 | 2 | 16 | 4096, 8);  // 64, no combine
   else if (variant == 81) TFS_CJ(true, true, false, kCompactDiag | 1024);         // cross-record ring
   else if (variant == 82) TFS_CJ(true, true, false, kCompactDiag | 2048);         // stripe 0 / tail as dwordx4
   else if (variant == 83) TFS_CJ(true, true, false, kCompactDiag | 1024 | 2048);  // both

@@ -152,7 +152,7 @@ def main():
         return ctxs[v]
 
     for v, js in cases:
-        if v in (26, 30, 61, 64, 65, 66, 67, 68, 69, 70, 71, 79, 80) or js.startswith("split") or js == "aligned64k":
+        if v in (26, 30, 61, 64, 65, 66, 67, 68, 69, 70, 71, 79, 80, 84, 85) or js.startswith("split") or js == "aligned64k":
             continue
         d_bad.zero()
         c = ctx_of(v)
