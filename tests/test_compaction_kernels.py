@@ -19,7 +19,7 @@ def ocrc_payload(oracle, img, meta):
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[0, 22, 23, 25, 27, 29, 31, 32, 33, 35, 36, 37, 39, 40, 42, 43, 45, 60, 62, 63, 72, 73, 74, 75, 76, 77, 78, 81, 82, 83])
+@pytest.fixture(params=[0, 22, 23, 25, 27, 29, 31, 32, 33, 35, 36, 37, 39, 40, 42, 43, 45, 60, 62, 63, 72, 73, 74, 75, 76, 77, 78, 81, 82, 83, 86, 87, 88])
 def vctx(request, monkeypatch):
     import tfs_amd.crc as crc
     monkeypatch.setenv("TFS_CRC_VARIANT", str(request.param))
@@ -399,3 +399,56 @@ def test_dynamic_tickets_many_records(chunk_ctx, oracle, many_records):
     chunk_ctx.sync()
     assert int(d_bad.download(np.uint32, 1)[0]) == 0 and (d_st.download(np.int32, n) == 0).all()
     assert (d_c.download(np.uint32, n) == c).all()
+
+
+@pytest.mark.parametrize("variant", [86, 87, 88])
+def test_hybrid_static_then_ticket_order_long_launch(oracle, variant, monkeypatch):
+    """Measurement variants 86-88 (FileCursor HS): a launch of >= 16 records per
+    wave hands the first n - (n >> HS) records out statically and the rest by
+    tickets -- both phases must cover every record exactly once: 100 k records of
+    0.5-2 KiB payload, every fourth deleted, byte-exact against the oracle's
+    real_compact with CRCs and statuses."""
+    import tfs_amd.crc as crc
+    from tfs_amd.synth import synth_bytes
+    from test_headline_parity import _oracle_mt
+    monkeypatch.setenv("TFS_CRC_VARIANT", str(variant))
+    ctx = crc.Context(0)
+    monkeypatch.setenv("TFS_CRC_VARIANT", "0")
+    rng = np.random.default_rng(variant)
+    n = 100_000
+    sizes = rng.integers(512, 2049, n)
+    recs = sizes + 36
+    offs = np.concatenate([[0], np.cumsum(recs)[:-1]]).astype(np.int64)
+    img = synth_bytes(3000 + variant, int(recs.sum()) + 256)
+    c = _oracle_mt(oracle, img, offs + 36, sizes)
+    fi = np.zeros(n, crc.FILEINFO_DTYPE)
+    fi["id_"] = 9000 + np.arange(n)
+    fi["offset_"], fi["size_"], fi["usize_"], fi["crc_"] = offs, recs, recs, c
+    img[offs[:, None] + np.arange(36)[None, :]] = fi.view(np.uint8).reshape(n, 36)
+    metas = np.zeros(n, crc.META_DTYPE)
+    metas["file_id"], metas["offset"], metas["size"] = 9000 + np.arange(n), offs, recs
+    fl = np.zeros(n, np.int32)
+    fl[1::4] = 1
+    odest, doff, _ = _oracle_compact(oracle, img, metas, fl)
+    live = np.nonzero(fl == 0)[0]
+    assert live.size >= 16 * 4096
+    j = np.zeros(live.size, crc.COMPACT_JOB_DTYPE)
+    j["src_offset"], j["dest_offset"] = metas["offset"][live], doff[live]
+    j["file_id"], j["size"], j["new_offset"] = metas["file_id"][live], metas["size"][live], doff[live]
+    bufs = [crc.DeviceBuffer(ctx, img.size).upload(img), crc.DeviceBuffer(ctx, j.nbytes).upload(j),
+            crc.DeviceBuffer(ctx, odest.size + 64), crc.DeviceBuffer(ctx, 4 * live.size),
+            crc.DeviceBuffer(ctx, 4 * live.size), crc.DeviceBuffer(ctx, 4)]
+    d_src, d_j, d_dst, d_c, d_st, d_nb = bufs
+    try:
+        d_dst.zero()
+        d_nb.zero()
+        d_st.zero()
+        ctx.compact_jobs_device(d_src, img.size, d_j, live.size, d_dst, d_c, d_st, d_nb)
+        ctx.sync()
+        assert int(d_nb.download(np.uint32)[0]) == 0 and (d_st.download(np.int32, live.size) == 0).all()
+        assert (d_c.download(np.uint32, live.size) == c[live]).all()
+        assert (d_dst.download(np.uint8, odest.size) == odest).all()
+    finally:
+        for b in bufs:
+            b.free()
+        ctx.close()

@@ -712,10 +712,15 @@ struct Tickets {
 // for dynamic tickets over chunks (fewer than kDynMinPerWave chunks per wave:
 // a block of 1,024 files, a small batch) takes single files as before, so its
 // files stay spread over all waves.
-template <bool IL, int W, int CF, int TS>
+// HS (measurement, compaction): a long launch hands its first n - (n >> HS) files
+// out statically (wave w takes w, w+W, ...: one contiguous window, 16 consecutive
+// files per workgroup) and only the rest by single-file tickets, which even out the
+// waves' ends.
+template <bool IL, int W, int CF, int TS, int HS = 0>
 struct FileCursor {
   Tickets<IL, W> tk;
   uint32_t n = 0, cf = 1, nA = 0, nt = 0, jv = 0, next = 0, end = 0;
+  uint32_t hbase = 0, hnext = 0, hstride = 0;  // HS: the static phase covers files [0, hbase)
   bool done = false;
   __device__ __forceinline__ void init(uint32_t* sched, uint32_t n_, uint32_t group, uint32_t waves_total,
                                        uint32_t global_wave) {
@@ -727,14 +732,27 @@ struct FileCursor {
       cf = 1u;
       nA = nt = n;
     }
+    if (HS > 0 && uint64_t(n) >= uint64_t(kDynMinPerWave) * waves_total) {
+      hbase = uint32_t((n - (n >> HS)) / waves_total * waves_total);
+      hnext = global_wave;
+      hstride = waves_total;
+      cf = 1u;
+      nA = nt = n - hbase;
+    }
     tk.ctr = sched;
     tk.n = nt;
     tk.group = group;
     tk.init_static(waves_total, global_wave);
+    if (hbase) tk.dyn = true;  // the tail goes by tickets however short it is
   }
   __device__ __forceinline__ void start(int lane) { jv = tk.issue(lane); }
   __device__ __forceinline__ uint32_t take(int lane) {  // next file of this wave, n = none left
     if (next < end) return next++;
+    if (HS > 0 && hnext < hbase) {
+      const uint32_t f = hnext;
+      hnext += hstride;
+      return f;
+    }
     if (done) return n;
     const uint32_t c = tk.resolve(jv, lane);
     if (c >= nt) {
@@ -742,7 +760,7 @@ struct FileCursor {
       return n;
     }
     if (c < nA) {
-      next = c * cf;
+      next = hbase + c * cf;
       end = min(next + cf, n);
     } else {
       next = nA * cf + (c - nA);
@@ -1985,7 +2003,7 @@ __device__ __forceinline__ void copy_unaligned(const uint8_t* s, uint8_t* d, uin
 // copy-only form 64).
 constexpr int kCompactDiag = 4 | 8;
 template <bool WIDE, bool DPPSH = true, bool VERIFY = false, int DIAG = kCompactDiag, int CPF = kPF, int CF = 1,
-          int TS = 0, bool SEG = false, int WW = 1>
+          int TS = 0, bool SEG = false, int WW = 1, int HS = 0>
 __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __restrict__ src, uint64_t src_len,
                                                               const RawMeta* __restrict__ metas,
                                                               const int32_t* __restrict__ flags,
@@ -2019,23 +2037,24 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
   };
   // CF > 1: chunks of CF records per ticket; WW > 1: WW consecutive records per
   // ticket-group slot, so an XCD's waves walk WW-record runs (measurement)
-  FileCursor<kIL, WW, CF, TS> fc;
+  FileCursor<kIL, WW, CF, TS, HS> fc;
+  constexpr bool FC = CF > 1 || HS > 0;  // files come from the cursor (chunks / the static phase)
   auto& tk = fc.tk;
   fc.init(sched, n, blockIdx.x & 7u, gridDim.x * wpb,
           blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave));
   if (DIAG & 256) tk.dyn = false;  // measurement: static record r -> wave r mod W (the chunk copy's order)
-  if (CF > 1) fc.start(lane);
+  if (FC) fc.start(lane);
   uint32_t bad = 0;
   do {
-    uint32_t f = CF > 1 ? fc.take(lane) : tk.resolve(tk.issue(lane), lane);
+    uint32_t f = FC ? fc.take(lane) : tk.resolve(tk.issue(lane), lane);
     if (f >= n) break;
-    uint32_t fn = CF > 1 ? fc.take(lane) : tk.resolve(tk.issue(lane), lane);
+    uint32_t fn = FC ? fc.take(lane) : tk.resolve(tk.issue(lane), lane);
     CRec cur = unit(f);
     CState st = issue_crec<DA, HV>(cur, src, src_len, dst, lane, junk);
     uint4 buf[CPF][kRun / 16];
     load_ring<kRun, CPF, LNT>(st.g, lane, buf, junk);
     CRec nxt = fn < n ? unit(fn) : CRec{};
-    uint32_t jv = CF == 1 && fn < n ? tk.issue(lane) : 0u;
+    uint32_t jv = !FC && fn < n ? tk.issue(lane) : 0u;
     for (;;) {
       // DIAG bit 5 (variant 31, measurement): byte-shifted records copy after the CRC (copy_unaligned)
       const bool chain_copy = !(DIAG & 32) || (st.delta & 3) == 0;
@@ -2056,10 +2075,10 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
       if (more) {
         ns = issue_crec<DA, HV>(ncur, src, src_len, dst, lane, junk);
         if (!XF || !st.g.nstripes) load_ring<kRun, CPF, LNT>(ns.g, lane, buf, junk);
-        fnn = CF > 1 ? fc.take(lane) : tk.resolve(jv, lane);
+        fnn = FC ? fc.take(lane) : tk.resolve(jv, lane);
         if (fnn < n) {
           nxt = unit(fnn);
-          if (CF == 1) jv = tk.issue(lane);
+          if (!FC) jv = tk.issue(lane);
         }
       }
       int32_t status = cur.pre;
@@ -2687,6 +2706,9 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
   else if (variant == 76) TFS_CJ(true, true, false, kCompactDiag | 1, 6);  // plain stores, PF 6
   else if (variant == 79) TFS_CJ(true, true, false, 4 | 512 | 2 | 16, 8);        // 64 with non-temporal loads
   else if (variant == 80) TFS_CJ(true, true, false, kCompactDiag | 512 | 2 | 16 | 256, 8);  // 64, static order
+  else if (variant == 86) TFS_CJ(true, true, false, kCompactDiag, kPF, 1, 0, false, 1, 3);  // static 7/8, tickets after
+  else if (variant == 87) TFS_CJ(true, true, false, kCompactDiag, kPF, 1, 0, false, 1, 5);  // static 31/32
+  else if (variant == 88) TFS_CJ(true, true, false, kCompactDiag, kPF, 1, 0, false, 1, 2);  // static 3/4
   else if (variant == 84) TFS_CJ(true, true, false, kCompactDiag | 4096);                  // no combine
   else if (variant == 85) TFS_CJ(true, true, false, kCompactDiag | 512 | 2 | 16 | 4096, 8);  // 64, no combine
   else if (variant == 81) TFS_CJ(true, true, false, kCompactDiag | 1024);         // cross-record ring
