@@ -401,7 +401,7 @@ def test_dynamic_tickets_many_records(chunk_ctx, oracle, many_records):
     assert (d_c.download(np.uint32, n) == c).all()
 
 
-@pytest.mark.parametrize("variant", [86, 87, 88])
+@pytest.mark.parametrize("variant", [86, 87, 88, 89])
 def test_hybrid_static_then_ticket_order_long_launch(oracle, variant, monkeypatch):
     """Measurement variants 86-88 (FileCursor HS): a launch of >= 16 records per
     wave hands the first n - (n >> HS) records out statically and the rest by

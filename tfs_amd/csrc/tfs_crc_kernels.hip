@@ -2709,6 +2709,7 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
   else if (variant == 86) TFS_CJ(true, true, false, kCompactDiag, kPF, 1, 0, false, 1, 3);  // static 7/8, tickets after
   else if (variant == 87) TFS_CJ(true, true, false, kCompactDiag, kPF, 1, 0, false, 1, 5);  // static 31/32
   else if (variant == 88) TFS_CJ(true, true, false, kCompactDiag, kPF, 1, 0, false, 1, 2);  // static 3/4
+  else if (variant == 89) TFS_CJ(true, true, false, kCompactDiag, kPF, 1, 0, false, 1, 1);  // static 1/2
   else if (variant == 84) TFS_CJ(true, true, false, kCompactDiag | 4096);                  // no combine
   else if (variant == 85) TFS_CJ(true, true, false, kCompactDiag | 512 | 2 | 16 | 4096, 8);  // 64, no combine
   else if (variant == 81) TFS_CJ(true, true, false, kCompactDiag | 1024);         // cross-record ring
