@@ -19,7 +19,7 @@ def ocrc_payload(oracle, img, meta):
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[0, 22, 23, 25, 27, 29, 31, 32, 33, 35, 36, 37, 39, 40, 42, 43, 45, 60, 62, 63, 72, 73, 74, 75, 76, 77, 78, 81, 82, 83, 86, 87, 88])
+@pytest.fixture(params=[0, 22, 23, 25, 27, 29, 31, 32, 33, 35, 36, 37, 39, 40, 42, 43, 45, 60, 62, 63, 72, 73, 74, 75, 76, 77, 78, 81, 82, 83, 86, 87, 88, 89, 90])
 def vctx(request, monkeypatch):
     import tfs_amd.crc as crc
     monkeypatch.setenv("TFS_CRC_VARIANT", str(request.param))
@@ -401,12 +401,14 @@ def test_dynamic_tickets_many_records(chunk_ctx, oracle, many_records):
     assert (d_c.download(np.uint32, n) == c).all()
 
 
-@pytest.mark.parametrize("variant", [86, 87, 88, 89])
+@pytest.mark.parametrize("variant", [86, 87, 88, 89, 90])
 def test_hybrid_static_then_ticket_order_long_launch(oracle, variant, monkeypatch):
-    """Measurement variants 86-88 (FileCursor HS): a launch of >= 16 records per
+    """Measurement variants 86-89 (FileCursor HS): a launch of >= 16 records per
     wave hands the first n - (n >> HS) records out statically and the rest by
-    tickets -- both phases must cover every record exactly once: 100 k records of
-    0.5-2 KiB payload, every fourth deleted, byte-exact against the oracle's
+    tickets -- both phases must cover every record exactly once; 90: the same
+    order over the segmented form's units (jobs, then 32 KiB payload segments).
+    100 k records, most of 0.5-2 KiB payload and one in twenty of 33-100 KiB (cut
+    into segments by 90), every fourth deleted, byte-exact against the oracle's
     real_compact with CRCs and statuses."""
     import tfs_amd.crc as crc
     from tfs_amd.synth import synth_bytes
@@ -417,6 +419,8 @@ def test_hybrid_static_then_ticket_order_long_launch(oracle, variant, monkeypatc
     rng = np.random.default_rng(variant)
     n = 100_000
     sizes = rng.integers(512, 2049, n)
+    big = rng.random(n) < 0.05
+    sizes[big] = rng.integers(33 << 10, 100 << 10, int(big.sum()))
     recs = sizes + 36
     offs = np.concatenate([[0], np.cumsum(recs)[:-1]]).astype(np.int64)
     img = synth_bytes(3000 + variant, int(recs.sum()) + 256)

@@ -742,6 +742,7 @@ uint32_t cseg_lg(const tfs_crc_ctx* ctx, uint32_t n) {
   if (ctx->variant == 72) return 4u;
   if (ctx->variant == 73) return 3u;
   if (ctx->variant == 74) return 5u;
+  if (ctx->variant == 90) return n >= kCSegAutoJobs ? kCSegAutoLg : 0u;  // the auto rule, hybrid unit order
   if (ctx->variant != 0) return 0u;  // the other compaction variants: whole records
 #endif
   if (ctx->cseg_auto.load(std::memory_order_relaxed)) return n >= kCSegAutoJobs ? kCSegAutoLg : 0u;

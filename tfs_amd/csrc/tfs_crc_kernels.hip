@@ -2672,6 +2672,13 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
     const CSegArgs cs = *seg;
     hipLaunchKernelGGL(compact_seg_plan_kernel, dim3((n + 255u) / 256u), dim3(256), 0, stream, jobs, n, src_len, cs);
     if (const hipError_t e = hipGetLastError()) return e;
+#ifdef TFS_CRC_MEASURE
+    if (variant == 90)  // segments with the hybrid unit order (static 3/4, tickets after; measurement)
+      hipLaunchKernelGGL((compact_pipe_kernel<true, true, false, kCompactDiag, kPF, 1, 0, true, 1, 2>),
+                         dim3(cap < kMaxGrid ? cap : kMaxGrid), dim3(kBlock), 0, stream, src, src_len, nullptr,
+                         nullptr, nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad, sched, cs);
+    else
+#endif
     hipLaunchKernelGGL((compact_pipe_kernel<true, true, false, kCompactDiag, kPF, 1, 0, true>),
                        dim3(cap < kMaxGrid ? cap : kMaxGrid), dim3(kBlock), 0, stream, src, src_len, nullptr, nullptr,
                        nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad, sched, cs);
