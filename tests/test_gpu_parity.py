@@ -403,7 +403,7 @@ def test_cross_file_pipeline_many_files(oracle, variant, monkeypatch):
         ctx.close()
 
 
-@pytest.mark.parametrize("variant", [0, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 50, 51, 52, 53, 54, 55, 56, 57, 58])
+@pytest.mark.parametrize("variant", [0, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 50, 51, 52, 53, 54, 55, 56, 57, 58, 91, 92, 93])
 def test_dynamic_tickets_million_files(oracle, variant, monkeypatch):
     """> 16 files (or chunks of CF files, variants 39-41) per wave, so the launch
     takes the dynamic-ticket path with stealing across the eight groups: 1 M short

@@ -733,11 +733,13 @@ struct FileCursor {
       nA = nt = n;
     }
     if (HS > 0 && uint64_t(n) >= uint64_t(kDynMinPerWave) * waves_total) {
-      hbase = uint32_t((n - (n >> HS)) / waves_total * waves_total);
+      // static chunks [0, hbase) of CF files, the rest by chunk tickets (no TS tail)
+      const uint32_t nc = (n + uint32_t(CF) - 1u) / uint32_t(CF);
+      hbase = (nc - (nc >> HS)) / waves_total * waves_total;
       hnext = global_wave;
       hstride = waves_total;
-      cf = 1u;
-      nA = nt = n - hbase;
+      cf = uint32_t(CF);
+      nA = nt = nc - hbase;
     }
     tk.ctr = sched;
     tk.n = nt;
@@ -749,9 +751,10 @@ struct FileCursor {
   __device__ __forceinline__ uint32_t take(int lane) {  // next file of this wave, n = none left
     if (next < end) return next++;
     if (HS > 0 && hnext < hbase) {
-      const uint32_t f = hnext;
+      next = hnext * cf;
+      end = min(next + cf, n);
       hnext += hstride;
-      return f;
+      return next++;
     }
     if (done) return n;
     const uint32_t c = tk.resolve(jv, lane);
@@ -760,7 +763,7 @@ struct FileCursor {
       return n;
     }
     if (c < nA) {
-      next = hbase + c * cf;
+      next = (hbase + c) * cf;
       end = min(next + cf, n);
     } else {
       next = nA * cf + (c - nA);
@@ -808,7 +811,7 @@ __device__ __forceinline__ void launch_exit(uint32_t* sched, uint32_t units, uin
 // n >> TS files are ticketed one by one (chunks only while much work is left,
 // so a chunk of large files cannot become the launch's tail).
 template <int MODE, int RUN, int PF, bool NT, bool DYN, bool S8, int G = 1, bool HV = false, bool IL = false,
-          int W = 1, bool XF = false, bool BLK = false, int CF = 1, int TS = 0, int SPL = 0>
+          int W = 1, bool XF = false, bool BLK = false, int CF = 1, int TS = 0, int SPL = 0, int HS = 0>
 __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __restrict__ base,
                                                            const Desc* __restrict__ desc, uint32_t n,
                                                            const Tables* __restrict__ tg, uint32_t* out_crc,
@@ -868,7 +871,7 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
   const uint32_t wpb = kBlock / kWave;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t stride = gridDim.x * wpb;
-  FileCursor<IL, W, CF, TS> cur_files;
+  FileCursor<IL, W, CF, TS, HS> cur_files;  // HS (measurement, CF > 1): static chunks first (FileCursor)
   Tickets<IL, W>& tk = cur_files.tk;
   cur_files.init(sched, n, blockIdx.x & 7u, stride, blockIdx.x * wpb + wave);
   if (CF > 1 && DYN) cur_files.start(lane);
@@ -2490,6 +2493,13 @@ static bool launch_measure_variant(int variant, dim3 grid, dim3 block, const uin
 #define TFS_LAUNCH_CW(WW)                                                                                           \
   hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, WW, false, false, kCF, kTS>), \
                      grid, block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa)
+#define TFS_LAUNCH_HS(HS_)                                                                                           \
+  hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, kCF, 0, 0, HS_>), \
+                     grid, block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa)
+    case 91: TFS_LAUNCH_HS(2); break;  // chunks of 4: the first 3/4 static (wave w: chunks w, w+W, ...), tickets after
+    case 92: TFS_LAUNCH_HS(1); break;  // the first 1/2 static
+    case 93: TFS_LAUNCH_HS(3); break;  // the first 7/8 static
+#undef TFS_LAUNCH_HS
     case 56: TFS_LAUNCH_CW(2); break;  // chunked tickets, WW consecutive chunks per group slot (one XCD)
     case 57: TFS_LAUNCH_CW(8); break;
     case 58: TFS_LAUNCH_CW(4); break;

@@ -15,6 +15,8 @@ vs off shares one stream and one scratch set and the per-context placement
 noise (up to +-2 % between two contexts of one library) drops out of that pair;
 "appended" is a measurement-build context in round 3's split form (segments
 after all files, set_split 2).  OTHER_SO "-" compares only those.
+AB_VARIANTS=v[,v...] adds measurement-build contexts running kernel variant v
+(TFS_CRC_VARIANT) as entries "v<v>".
 """
 import ctypes
 import json
@@ -93,6 +95,13 @@ def main():
     only = [x for x in os.environ.get("AB_ONLY", "").split(",") if x]  # e.g. AB_ONLY=product,product_ao
     if only:
         libs = {k: v for k, v in libs.items() if k in only}
+    keep = []  # the variant contexts stay alive for the run
+    for v in [int(x) for x in os.environ.get("AB_VARIANTS", "").split(",") if x]:
+        os.environ["TFS_CRC_VARIANT"] = str(v)
+        vc = crc.Context(0, measure=True)
+        os.environ["TFS_CRC_VARIANT"] = "0"
+        keep.append(vc)
+        libs["v%d" % v] = (vc.L, vc.handle)
     times = {k: [] for k in libs}
     for r in range(rounds):
         for name, (L, h) in libs.items():
