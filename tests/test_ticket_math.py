@@ -67,3 +67,33 @@ def test_interleaved_slots_of_w_tickets(w):
     for n in [1, 5, 8 * w - 1, 8 * w, 8 * w + 1, 65536 + 13, 1 << 18, (1 << 18) + 8 * w * 3 + 5]:
         t = np.concatenate([file_of_w(g, np.arange(gcount_w(n, g, w), dtype=np.int64), w) for g in range(8)])
         assert np.array_equal(np.sort(t), np.arange(n)), (w, n)
+
+
+def hybrid_files(n, cf, hs, waves):  # FileCursor<..., CF, TS, HS>: static chunks, then chunk tickets
+    """Files each wave takes in the HS form (measurement variants 86-93): static
+    chunks w, w+W, ... below hbase, then tickets over the remaining chunks."""
+    if n < K_DYN_MIN_PER_WAVE * waves:
+        return None  # short launches keep the plain cursor
+    nc = (n + cf - 1) // cf
+    hbase = (nc - (nc >> hs)) // waves * waves
+    static_chunks = np.arange(hbase, dtype=np.int64)          # wave w: chunks w, w + W, ... (all of them)
+    assert np.array_equal(np.sort(static_chunks % waves), np.repeat(np.arange(waves), hbase // waves))
+    nt = nc - hbase
+    tickets = np.concatenate([file_of(g, np.arange(gcount(nt, g), dtype=np.int64)) for g in range(8)])
+    chunks = np.concatenate([static_chunks, hbase + tickets])
+    first = np.repeat(chunks * cf, cf) + np.tile(np.arange(cf), chunks.size)
+    return first[first < n], hbase, nt
+
+
+@pytest.mark.parametrize("cf,hs", [(1, 1), (1, 2), (1, 3), (1, 5), (4, 1), (4, 2), (4, 3)])
+def test_hybrid_static_then_tickets_every_file_once(cf, hs):
+    waves = 4096
+    for n in [65535, 65536, 65536 * 4 + 3, 349184, 1 << 20, (1 << 20) + 777]:
+        r = hybrid_files(n, cf, hs, waves)
+        if r is None:
+            assert n < K_DYN_MIN_PER_WAVE * waves
+            continue
+        files, hbase, nt = r
+        seen = np.bincount(files, minlength=n)
+        assert seen.size == n and (seen == 1).all(), (n, cf, hs)
+        assert hbase % waves == 0 and nt >= ((n + cf - 1) // cf) >> hs
