@@ -1536,6 +1536,16 @@ __device__ __forceinline__ uint32_t ld_le32(const uint8_t* p) {
   return uint32_t(p[0]) | uint32_t(p[1]) << 8 | uint32_t(p[2]) << 16 | uint32_t(p[3]) << 24;
 }
 __device__ __forceinline__ int32_t ld_le16s(const uint8_t* p) { return int16_t(uint16_t(p[0] | p[1] << 8)); }
+// Header words at any byte address (HSA unaligned access mode: one global_load_dwordx4 /
+// _dword whatever the alignment) -- two loads per frame instead of sixteen byte loads.
+typedef const __attribute__((address_space(1))) u32x4u* gu128ucp;
+typedef const __attribute__((address_space(1))) u32u* gu32ucp;
+__device__ __forceinline__ u32x4 ld128u(const uint8_t* p) {
+  return *reinterpret_cast<gu128ucp>(reinterpret_cast<uintptr_t>(p));
+}
+__device__ __forceinline__ uint32_t ld32u(const uint8_t* p) {
+  return *reinterpret_cast<gu32ucp>(reinterpret_cast<uintptr_t>(p));
+}
 
 // mode 1 = verify (desc.aux = stored crc), 0 = seal (desc.aux = seed).
 __global__ void packet_parse_kernel(const uint8_t* __restrict__ base, const PacketDesc* __restrict__ pd, uint32_t n,
@@ -1549,9 +1559,13 @@ __global__ void packet_parse_kernel(const uint8_t* __restrict__ base, const Pack
   if (f.len < uint32_t(kPacketHeaderV0Size)) {
     st = kPacketIncomplete;  // getPacketInfo:49
   } else {
-    const uint32_t flag = ld_le32(p);
-    const int32_t length = int32_t(ld_le32(p + 4));
-    const int32_t type = ld_le16s(p + 8), check = ld_le16s(p + 10);
+    // A frame of at least 24 bytes (every frame whose crc field is read) takes its
+    // header as one 16-byte and one 4-byte load; shorter ones byte by byte.
+    const bool wide = f.len >= uint32_t(kPacketHeaderV0Size + kPacketHeaderDiffSize);
+    const u32x4 h = wide ? ld128u(p) : u32x4{ld_le32(p), ld_le32(p + 4), ld_le32(p + 8), 0u};
+    const uint32_t flag = h.x;
+    const int32_t length = int32_t(h.y);
+    const int32_t type = int16_t(uint16_t(h.z)), check = int16_t(uint16_t(h.z >> 16));
     const bool v1 = flag == kPacketFlagV1;
     if (v1 && f.len < uint32_t(kPacketHeaderV0Size + kPacketHeaderDiffSize)) {
       st = kPacketIncomplete;  // :65-69, the V1 header's last 12 bytes are not there yet
@@ -1571,7 +1585,7 @@ __global__ void packet_parse_kernel(const uint8_t* __restrict__ base, const Pack
           // decode: id (8) and crc (4) follow the V0 header, the body after them (:117-141).
           d.offset = f.offset + kPacketHeaderV0Size + kPacketHeaderDiffSize;
           d.len = uint32_t(data_len - kPacketHeaderDiffSize);
-          d.aux = mode == 1 ? ld_le32(p + kPacketHeaderV0Size + 8) : kPacketFlagV1;
+          d.aux = mode == 1 ? ld32u(p + kPacketHeaderV0Size + 8) : kPacketFlagV1;  // f.len >= 24 here
           st = kPacketPending;
         }
       }
