@@ -2,7 +2,7 @@
 # Round 4, closing tree after the measurement-variant work: the -m gpu suite,
 # smoke and the default line.
 set -u
-O=gpurun_out/r04/final2
+O=gpurun_out/r04/${FINAL_DIR:-final2}
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gputests.log 2>&1
 rc=$?
