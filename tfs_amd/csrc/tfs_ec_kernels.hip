@@ -95,6 +95,63 @@ __global__ void __launch_bounds__(256) ec_apply_kernel(EcArgs a, const uint32_t*
 }
 
 #ifdef TFS_CRC_MEASURE
+// Narrow form (measurement, TFS_EC_VARIANT 9, round 4): 4 bytes per lane, so lane
+// l owns bytes 4*(l & 31) of packet c of unit (l >> 5) and a wave step covers 2
+// units: twice the memory instructions of the product for the same bytes, at
+// about half its VGPRs (more waves per SIMD) -- the other side of the wide form.
+typedef const __attribute__((address_space(1))) uint32_t* gu32p;
+typedef __attribute__((address_space(1))) uint32_t* gu32wp;
+template <int OG>
+__global__ void __launch_bounds__(256) ec_apply_narrow_kernel(EcArgs a, const uint32_t* __restrict__ masks) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t u = uint32_t(lane) >> 5;
+  const uint32_t off = 4u * uint32_t(lane & 31);
+  const uint64_t ntiles = (a.units + 1) / 2;
+  const uint64_t wave = uint64_t(blockIdx.x) * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t nwaves = uint64_t(gridDim.x) * (blockDim.x / 64);
+  for (uint64_t t = wave; t < ntiles; t += nwaves) {
+    const uint64_t unit = t * 2 + u;
+    const bool ok = unit < a.units;
+    const uint64_t base = unit * 1024u + off;
+    uint32_t acc[OG][8];
+#pragma unroll
+    for (int o = 0; o < OG; ++o)
+#pragma unroll
+      for (int r = 0; r < 8; ++r) acc[o][r] = 0u;
+    auto ld = [&](const uint8_t* p) -> uint32_t {
+      return __builtin_nontemporal_load(reinterpret_cast<gu32p>(reinterpret_cast<uintptr_t>(p)));
+    };
+    uint32_t in[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) in[c] = ok ? ld(a.src[0] + base + 128u * c) : 0u;
+    for (uint32_t s = 0; s < a.S; ++s) {
+      uint32_t nx[8];
+      const bool more = s + 1 < a.S;
+      const uint8_t* np = a.src[more ? s + 1 : s];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) nx[c] = (ok && more) ? ld(np + base + 128u * c) : 0u;
+#pragma unroll
+      for (int o = 0; o < OG; ++o)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const uint32_t* m = masks + ((uint32_t(o) * 8u + uint32_t(r)) * a.S + s) * 8u;
+#pragma unroll
+          for (int c = 0; c < 8; ++c) acc[o][r] = xand(acc[o][r], in[c], m[c]);
+        }
+#pragma unroll
+      for (int c = 0; c < 8; ++c) in[c] = nx[c];
+    }
+    if (ok) {
+#pragma unroll
+      for (int o = 0; o < OG; ++o)
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          __builtin_nontemporal_store(acc[o][r],
+                                      reinterpret_cast<gu32wp>(reinterpret_cast<uintptr_t>(a.dst[o] + base + 128u * r)));
+    }
+  }
+}
+
 typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(1))) u32x4v* gu128p;
 typedef __attribute__((address_space(1))) u32x4v* gu128wp;
@@ -279,6 +336,17 @@ hipError_t launch_ec_apply(const EcArgs& a, int og, int variant, hipStream_t str
       case 2: hipLaunchKernelGGL(ec_apply_wide_kernel<2>, g8, b8, 0, stream, a, a.masks); break;
       case 3: hipLaunchKernelGGL(ec_apply_wide_kernel<3>, g8, b8, 0, stream, a, a.masks); break;
       default: hipLaunchKernelGGL(ec_apply_wide_kernel<4>, g8, b8, 0, stream, a, a.masks); break;
+    }
+    return hipGetLastError();
+  }
+  if (variant == 9) {  // measurement: 4 bytes per lane, 2 units per wave step
+    const uint64_t t2 = (a.units + 1) / 2;
+    const dim3 g2(static_cast<unsigned>((t2 + 3) / 4)), b2(256);
+    switch (og) {
+      case 1: hipLaunchKernelGGL(ec_apply_narrow_kernel<1>, g2, b2, 0, stream, a, a.masks); break;
+      case 2: hipLaunchKernelGGL(ec_apply_narrow_kernel<2>, g2, b2, 0, stream, a, a.masks); break;
+      case 3: hipLaunchKernelGGL(ec_apply_narrow_kernel<3>, g2, b2, 0, stream, a, a.masks); break;
+      default: hipLaunchKernelGGL(ec_apply_narrow_kernel<4>, g2, b2, 0, stream, a, a.masks); break;
     }
     return hipGetLastError();
   }
