@@ -38,8 +38,10 @@ __device__ __forceinline__ uint32_t xand(uint32_t acc, uint32_t in, uint32_t m) 
 // MATH = false (measurement build, TFS_EC_VARIANT 7): the same loads, stores and
 // schedule with one XOR per output row instead of the bitmatrix product -- the
 // kernel's memory shape without its VALU work (wrong parity: timing only).
-template <int OG, bool MATH = true>
-__global__ void __launch_bounds__(256) ec_apply_kernel(EcArgs a, const uint32_t* __restrict__ masks) {
+// PREF = false (measurement, TFS_EC_VARIANT 11): no next-member prefetch -- fewer
+// VGPRs (more waves per SIMD) for fewer bytes in flight per wave.
+template <int OG, bool MATH = true, bool PREF = true>
+__device__ __forceinline__ void ec_apply_body(const EcArgs& a, const uint32_t* __restrict__ masks) {
   const int lane = threadIdx.x & 63;
   const uint32_t u = uint32_t(lane) >> 4;
   const uint32_t off = 8u * uint32_t(lane & 15);
@@ -63,8 +65,13 @@ __global__ void __launch_bounds__(256) ec_apply_kernel(EcArgs a, const uint32_t*
       u32x2 nx[8];
       const bool more = s + 1 < a.S;
       const uint8_t* np = a.src[more ? s + 1 : s];
+      if constexpr (PREF) {
 #pragma unroll
-      for (int c = 0; c < 8; ++c) nx[c] = (ok && more) ? ld64nt(np + base + 128u * c) : u32x2{0u, 0u};
+        for (int c = 0; c < 8; ++c) nx[c] = (ok && more) ? ld64nt(np + base + 128u * c) : u32x2{0u, 0u};
+      } else if (s > 0) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) in[c] = ok ? ld64nt(a.src[s] + base + 128u * c) : u32x2{0u, 0u};
+      }
 #pragma unroll
       for (int o = 0; o < OG; ++o)
 #pragma unroll
@@ -82,8 +89,10 @@ __global__ void __launch_bounds__(256) ec_apply_kernel(EcArgs a, const uint32_t*
             acc[o][r].y = xand(acc[o][r].y, in[c].y, mk);
           }
         }
+      if constexpr (PREF) {
 #pragma unroll
-      for (int c = 0; c < 8; ++c) in[c] = nx[c];
+        for (int c = 0; c < 8; ++c) in[c] = nx[c];
+      }
     }
     if (ok) {
 #pragma unroll
@@ -92,6 +101,11 @@ __global__ void __launch_bounds__(256) ec_apply_kernel(EcArgs a, const uint32_t*
         for (int r = 0; r < 8; ++r) st64nt(a.dst[o] + base + 128u * r, acc[o][r]);
     }
   }
+}
+
+template <int OG, bool MATH = true>
+__global__ void __launch_bounds__(256) ec_apply_kernel(EcArgs a, const uint32_t* __restrict__ masks) {
+  ec_apply_body<OG, MATH>(a, masks);
 }
 
 #ifdef TFS_CRC_MEASURE
@@ -150,6 +164,18 @@ __global__ void __launch_bounds__(256) ec_apply_narrow_kernel(EcArgs a, const ui
                                       reinterpret_cast<gu32wp>(reinterpret_cast<uintptr_t>(a.dst[o] + base + 128u * r)));
     }
   }
+}
+
+// The product body held to 6 waves per SIMD (measurement, TFS_EC_VARIANT 10: 80 VGPRs,
+// 36 bytes of scratch spills per lane), and without the next-member prefetch (11).
+template <int OG>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) ec_apply_w6_kernel(
+    EcArgs a, const uint32_t* __restrict__ masks) {
+  ec_apply_body<OG, true>(a, masks);
+}
+template <int OG>
+__global__ void __launch_bounds__(256) ec_apply_w7_kernel(EcArgs a, const uint32_t* __restrict__ masks) {
+  ec_apply_body<OG, true, false>(a, masks);
 }
 
 typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
@@ -337,6 +363,19 @@ hipError_t launch_ec_apply(const EcArgs& a, int og, int variant, hipStream_t str
       case 3: hipLaunchKernelGGL(ec_apply_wide_kernel<3>, g8, b8, 0, stream, a, a.masks); break;
       default: hipLaunchKernelGGL(ec_apply_wide_kernel<4>, g8, b8, 0, stream, a, a.masks); break;
     }
+    return hipGetLastError();
+  }
+  if (variant == 10 || variant == 11) {  // measurement: the product body at 6 / 7 waves per SIMD
+#define TFS_EC_W(K)                                                                            \
+  if (variant == 10) hipLaunchKernelGGL(ec_apply_w6_kernel<K>, g, b, 0, stream, a, a.masks); \
+  else hipLaunchKernelGGL(ec_apply_w7_kernel<K>, g, b, 0, stream, a, a.masks)
+    switch (og) {
+      case 1: TFS_EC_W(1); break;
+      case 2: TFS_EC_W(2); break;
+      case 3: TFS_EC_W(3); break;
+      default: TFS_EC_W(4); break;
+    }
+#undef TFS_EC_W
     return hipGetLastError();
   }
   if (variant == 9) {  // measurement: 4 bytes per lane, 2 units per wave step
