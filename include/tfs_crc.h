@@ -498,9 +498,9 @@ int tfs_crc32_set_split(tfs_crc_ctx* ctx, int on);
  * ragged head and whole seg_bytes payload segments that separate waves copy and
  * checksum, then folds the segment CRCs into the record's CRC and status on the
  * GPU.  seg_bytes: 8192, 16384 or 32768 for every launch; 0 keeps
- * every record on one wave; 1 restores the default rule: 32 KiB segments for
- * launches of at least 65,536 records, whole records below that.  Output
- * bytes, CRCs and statuses are identical either way. */
+ * every record on one wave; 1 restores the default: whole records (segments
+ * averaged -0.4 % over seven boxes).  Output bytes, CRCs and
+ * statuses are identical either way. */
 int tfs_crc32_set_compact_segment(tfs_crc_ctx* ctx, uint32_t seg_bytes);
 int tfs_crc32_throughput_grid(tfs_crc_ctx* ctx);
 /* Scheduler slots: ctx-owned streams bound (the ctx stream, compaction streams,

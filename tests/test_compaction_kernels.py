@@ -143,7 +143,7 @@ def test_product_segmented_compaction_toggle(gpu_ctx, oracle, seg):
     try:
         _jobs_statuses_case(gpu_ctx, oracle)
     finally:
-        gpu_ctx.set_compact_segment(1)  # the default rule again (32 KiB segments for >= 65,536 records)
+        gpu_ctx.set_compact_segment(1)  # the default again (whole records)
     with pytest.raises(Exception):
         gpu_ctx.set_compact_segment(12345)
 

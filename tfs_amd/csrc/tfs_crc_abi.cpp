@@ -730,13 +730,15 @@ int files_launch(tfs_crc_ctx* ctx, hipStream_t st, int mode, const uint8_t* base
 // Segment size of the segmented compaction (tfs_crc_device.h CSegArgs) for ctx:
 // 1 KiB << lg, 0 = records stay whole.  Measurement build: TFS_CRC_VARIANT 72 /
 // 73 / 74 = 16 / 8 / 32 KiB segments.
-// The product default (cseg_auto): 32 KiB segments for launches of at least
-// kCSegAutoJobs records -- the launches long enough for dynamic tickets, where
-// halving the unit cut the device compaction line by 0.9 % (16 KiB: 0.45 %, 8 KiB:
-// +6 %); shorter launches (a block-file window) keep whole records
-// and skip the plan and fold launches.
-constexpr uint32_t kCSegAutoJobs = 65536;
+// The product default (cseg_auto): whole records.  Round 4 first made 32 KiB segments
+// the default for launches of at least 65,536 records; over seven boxes they averaged
+// -0.4 % against whole records (+2.0 % to -1.7 %), while the hybrid record order the
+// product now launches (kCompactHS) gained 1.4 % on average.
+// Segments stay selectable per context (tfs_crc32_set_compact_segment).
+#ifdef TFS_CRC_MEASURE
+constexpr uint32_t kCSegAutoJobs = 65536;  // variant 90: the former default rule
 constexpr uint32_t kCSegAutoLg = 5;
+#endif
 uint32_t cseg_lg(const tfs_crc_ctx* ctx, uint32_t n) {
 #ifdef TFS_CRC_MEASURE
   if (ctx->variant == 72) return 4u;
@@ -745,7 +747,7 @@ uint32_t cseg_lg(const tfs_crc_ctx* ctx, uint32_t n) {
   if (ctx->variant == 90) return n >= kCSegAutoJobs ? kCSegAutoLg : 0u;  // the auto rule, hybrid unit order
   if (ctx->variant != 0) return 0u;  // the other compaction variants: whole records
 #endif
-  if (ctx->cseg_auto.load(std::memory_order_relaxed)) return n >= kCSegAutoJobs ? kCSegAutoLg : 0u;
+  if (ctx->cseg_auto.load(std::memory_order_relaxed)) return 0u;  // the default: whole records
   return ctx->cseg_lg.load(std::memory_order_relaxed);
 }
 

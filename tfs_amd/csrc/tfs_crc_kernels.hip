@@ -2019,6 +2019,11 @@ __device__ __forceinline__ void copy_unaligned(const uint8_t* s, uint8_t* d, uin
 // (finish_file skipped: wrong CRCs and statuses, timing only; 84, and 85 on the
 // copy-only form 64).
 constexpr int kCompactDiag = 4 | 8;
+// Record order of long device-compaction launches (FileCursor HS, round 4): the first
+// 3/4 of the records go statically (wave w: w, w+W, ...), the rest by tickets.  Against
+// one record per ticket, in one process on five boxes: -1.7, -1.7, 0.0, -1.8, -1.7 %
+// (measurement variant 88 before it became the product).
+constexpr int kCompactHS = 2;
 template <bool WIDE, bool DPPSH = true, bool VERIFY = false, int DIAG = kCompactDiag, int CPF = kPF, int CF = 1,
           int TS = 0, bool SEG = false, int WW = 1, int HS = 0>
 __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __restrict__ src, uint64_t src_len,
@@ -2772,7 +2777,7 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
   else if (variant == 45) TFS_CJ(true, true, false, kCompactDiag, kPF, 3, 0);
   else
 #endif
-    TFS_CJ(true);
+    TFS_CJ(true, true, false, kCompactDiag, kPF, 1, 0, false, 1, kCompactHS);
 #undef TFS_CJ
   (void)variant;
   return hipGetLastError();
