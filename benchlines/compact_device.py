@@ -113,8 +113,8 @@ def bench_compact_device(args):
     live_bytes = float(nlive) * rec
     algo = 2 * live_bytes + nlive * (40 + 4)  # read + write live records, 40 B CompactJob + 4 B status
     live_payload = float(nlive) * FILE_SIZE
-    cd_traffic, cd_src = _pmc_traffic("profiles/r04/final/compact_device/pmc_summary.json",
-                                      "compact_pipe_kernel<true, true, false, 12, 5, 1, 0, true", nblocks == 1024)
+    cd_traffic, cd_src = _pmc_traffic("profiles/r04/final/compact_device_hs/pmc_summary.json",
+                                      "compact_pipe_kernel<true, true, false, 12, 5, 1, 0, false, 1, 2", nblocks == 1024)
     res = {
         "metric": "GiB/s of live payload compacted on the device (re-CRC + repack of live files)",
         "value": world * args.steps * live_payload / el / 2**30, "unit": "GiB/s of live payload", "n_gpus": world,
@@ -128,7 +128,7 @@ def bench_compact_device(args):
                    "method": "every %d-th new block byte for byte against oracle_compact of its source" % every},
         "roofline": {"bound": "hbm", "achieved": algo / (kms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": algo / (kms / 1e3) / 1e9 / HBM_PEAK_GBS, "traffic": cd_traffic, "traffic_source": cd_src, "traffic_measured_in_this_run": False, "traffic_note": TRAFFIC_NOTE,
-                     "kernel": "compact_pipe_kernel<WIDE, SEG> (one launch: 32 KiB segments + plan/fold)",
+                     "kernel": "compact_pipe_kernel<WIDE> (whole records, hybrid order: 3/4 static, tickets after)",
                      "kernel_ms_avg": kms,
                      "algorithmic_bytes_per_launch": algo},
     }
