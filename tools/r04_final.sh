@@ -2,7 +2,7 @@
 # Round 4, closing tree: the -m gpu suite, smoke, then every bench line at full
 # default size (tools/all_lines.sh) on one box.
 set -u
-O=gpurun_out/r04/final
+O=gpurun_out/r04/${FINAL_DIR:-final}
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gputests.log 2>&1
 rc=$?
