@@ -34,6 +34,54 @@ def test_library_exports_every_declared_symbol():
     assert sorted(crc.EXPORTED + ec.EXPORTED) == names
 
 
+def _header_functions(name):
+    src = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", name)).read(), flags=re.S)
+    return set(re.findall(r"\b(tfs_\w+)\s*\(", src))
+
+
+# The dataserver boundary: context, scalar, DataFile, batch, verify,
+# device-resident, async, block images / compaction, packets (f1), the device
+# group (§8e) and the memory / stream / event helpers a caller without a HIP
+# runtime needs.  Nothing else may appear in the drop-in header.
+PRODUCT_API = {
+    "tfs_crc32_ctx_create", "tfs_crc32_ctx_destroy", "tfs_crc32_last_error", "tfs_crc32_device_count",
+    "tfs_crc32_device_numa_node",
+    "tfs_crc32", "tfs_crc32_e", "tfs_crc32_error_count", "tfs_crc32_set_default_ctx", "tfs_crc32_bind_thread",
+    "tfs_crc32_default_ctx", "tfs_datafile_get_crc",
+    "tfs_crc32_batch", "tfs_crc32_verify", "tfs_crc32_batch_device", "tfs_crc32_verify_device",
+    "tfs_crc32_submit_verify", "tfs_crc32_wait",
+    "tfs_block_verify", "tfs_block_verify_device", "tfs_block_compact", "tfs_block_compact_device",
+    "tfs_compact_jobs_device", "tfs_blocks_verify_device", "tfs_blocks_compact",
+    "tfs_packet_verify", "tfs_packet_verify_device", "tfs_packet_seal", "tfs_packet_seal_device",
+    "tfs_crc_group_create", "tfs_crc_group_destroy", "tfs_crc_group_last_error", "tfs_crc_group_size",
+    "tfs_crc_group_ctx", "tfs_crc_group_member_of", "tfs_crc_group_ctx_for_block", "tfs_crc_group_numa_node",
+    "tfs_crc_group_member_bound", "tfs_crc_group_host_malloc", "tfs_crc_group_host_free",
+    "tfs_crc_group_blocks_verify", "tfs_crc_group_blocks_compact",
+    "tfs_crc32_dev_malloc", "tfs_crc32_dev_free", "tfs_crc32_host_malloc_pinned", "tfs_crc32_host_free_pinned",
+    "tfs_crc32_host_device_ptr", "tfs_crc32_memcpy", "tfs_crc32_memset_device", "tfs_crc32_event_create",
+    "tfs_crc32_event_record", "tfs_crc32_event_elapsed_ms", "tfs_crc32_event_destroy", "tfs_crc32_stream",
+    "tfs_crc32_sync", "tfs_crc32_stream_create", "tfs_crc32_stream_sync", "tfs_crc32_stream_destroy",
+}
+
+
+def test_product_header_is_the_boundary_only():
+    """include/tfs_crc.h declares exactly the §8b families, the device group and the
+    memory / stream helpers; the test, calibration and tuning hooks live in
+    include/tfs_crc_testing.h, and INTEGRATION.md -- what a
+    dataserver maintainer reads -- names only the product header and its symbols."""
+    prod = _header_functions("tfs_crc.h")
+    test = _header_functions("tfs_crc_testing.h")
+    assert prod == PRODUCT_API, (sorted(prod - PRODUCT_API), sorted(PRODUCT_API - prod))
+    assert not prod & test
+    for hook in ("tfs_crc32_inject_device_error", "tfs_crc32_synth_fill_device", "tfs_crc32_membench_device",
+                 "tfs_crc32_debug_state", "tfs_crc32_set_split", "tfs_crc32_set_compact_segment"):
+        assert hook in test, hook
+    integ = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    assert "tfs_crc_testing.h" not in integ
+    for sym in test:
+        assert sym not in integ, sym
+
+
 def test_library_is_gfx950_code_object():
     so = os.path.join(ROOT, "tfs_amd", "libtfs_crc.so")
     blob = open(so, "rb").read()
@@ -93,7 +141,7 @@ def _kernel_symbols(so):
 def test_product_library_holds_one_form_of_each_kernel():
     """The A/B kernel forms and calibration kernels live only in the measurement
     build (libtfs_crc_measure.so, -DTFS_CRC_MEASURE): the product library holds
-    one crc_files_kernel per mode, no round-1 baselines, no membench, and never
+    one crc_files_kernel per mode, no calibration copies, no membench, and never
     names TFS_CRC_VARIANT / TFS_EC_VARIANT, so no environment variable can swap
     a dataserver's kernel."""
     prod = os.path.join(ROOT, "tfs_amd", "libtfs_crc.so")
@@ -104,9 +152,8 @@ def test_product_library_holds_one_form_of_each_kernel():
     kp, km = _kernel_symbols(prod), _kernel_symbols(meas)
     files_p = {k for k in kp if k.startswith("crc_files_kernel<")}
     assert len(files_p) == 2, files_p  # verify and compute
-    assert len({k for k in km if k.startswith("crc_files_kernel<")}) > 20
-    for name in ("membench", "block_verify_kernel", "compact_fused_kernel", "compact_copy_kernel",
-                 "ec_apply_chunk_kernel"):
+    assert len({k for k in km if k.startswith("crc_files_kernel<")}) == 4  # + one file per ticket (50)
+    for name in ("membench", "compact_probe_copy_kernel", "ec_apply_chunk_kernel"):
         assert not any(name in k for k in kp), name
         assert any(name in k for k in km), name
     # the product's kernels are all in the measurement build too (same sources)

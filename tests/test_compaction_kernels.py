@@ -1,10 +1,11 @@
 """The compaction data pass under every kernel form: the product
-pipelined kernel (dynamic tickets, next-record prefetch, DPP lane shifts), the
-same with ds_bpermute lane shifts (TFS_CRC_VARIANT=23) and round 1's
-unpipelined fused kernel (22).  Each must produce the oracle's real_compact
-bytes and statuses exactly, for every destination shift class, tiny and large
-records, rejected records (size, range, id, CRC), device-resident single-block
-and many-block forms, and zero-copy host images."""
+pipelined kernel (dynamic tickets, next-record prefetch, DPP lane shifts, the
+hybrid static/ticketed record order) and the round-5 occupancy forms of the
+measurement build (TFS_CRC_VARIANT 94-99: two workgroups per CU over 74 KiB of
+LDS tables, and its one-workgroup control 97).  Each must produce the oracle's
+real_compact bytes and statuses exactly, for every destination shift class, tiny
+and large records, rejected records (size, range, id, CRC), device-resident
+single-block and many-block forms, and zero-copy host images."""
 import numpy as np
 import pytest
 
@@ -19,7 +20,7 @@ def ocrc_payload(oracle, img, meta):
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[0, 22, 23, 25, 27, 29, 31, 32, 33, 35, 36, 37, 39, 40, 42, 43, 45, 60, 62, 63, 72, 73, 74, 75, 76, 77, 78, 81, 82, 83, 86, 87, 88, 89, 90])
+@pytest.fixture(params=[0, 94, 95, 96, 97, 98, 99])
 def vctx(request, monkeypatch):
     import tfs_amd.crc as crc
     monkeypatch.setenv("TFS_CRC_VARIANT", str(request.param))
@@ -150,7 +151,7 @@ def test_product_segmented_compaction_toggle(gpu_ctx, oracle, seg):
 
 def _jobs_statuses_case(vctx, oracle):
     """tfs_compact_jobs_device over records of every size class (many longer than
-    the 8 / 16 / 32 KiB segments of the segmented forms 72-74, including exact
+    the 8 / 16 / 32 KiB segments of the segmented form, including exact
     multiples and one byte past them), with rejected records on both short and
     long records: FileInfo id, FileInfo size, payload CRC (in a later segment and
     in the head), too short, past the image.  Statuses in the reference's order,
@@ -237,10 +238,10 @@ def test_zero_copy_host_images(vctx, oracle):
         dst.free()
 
 
-@pytest.fixture(params=[0, 24, 50])
+@pytest.fixture(params=[0, 50])
 def vfy_ctx(request, monkeypatch):
-    """Verify-on-read forms: the pipelined record kernel (product) and round 1's
-    grid-stride block_verify_kernel (TFS_CRC_VARIANT=24)."""
+    """Verify-on-read forms: the pipelined record kernel (product: chunked tickets)
+    and one record per ticket (TFS_CRC_VARIANT=50)."""
     import tfs_amd.crc as crc
     monkeypatch.setenv("TFS_CRC_VARIANT", str(request.param))
     ctx = crc.Context(0)
@@ -356,10 +357,10 @@ def many_records(oracle):
     return img, metas, fl, c
 
 
-@pytest.fixture(params=[0, 39, 40, 42, 43, 45, 47, 48, 50])
+@pytest.fixture(params=[0, 50, 94, 99])
 def chunk_ctx(request, monkeypatch):
-    """The product record kernel and its chunked-ticket forms (TFS_CRC_VARIANT
-    39-45: 2, 4, 4 + single tail, 4 + longer single tail, 3 records per ticket)."""
+    """The product record kernel, one record per ticket on verify (50) and two
+    occupancy forms of the compaction (94, 99)."""
     import tfs_amd.crc as crc
     monkeypatch.setenv("TFS_CRC_VARIANT", str(request.param))
     ctx = crc.Context(0)
@@ -401,15 +402,14 @@ def test_dynamic_tickets_many_records(chunk_ctx, oracle, many_records):
     assert (d_c.download(np.uint32, n) == c).all()
 
 
-@pytest.mark.parametrize("variant", [86, 87, 88, 89, 90])
+@pytest.mark.parametrize("variant", [0, 94, 95, 96, 97, 98, 99])
 def test_hybrid_static_then_ticket_order_long_launch(oracle, variant, monkeypatch):
-    """Measurement variants 86-89 (FileCursor HS): a launch of >= 16 records per
+    """The product's record order (FileCursor HS): a launch of >= 16 records per
     wave hands the first n - (n >> HS) records out statically and the rest by
-    tickets -- both phases must cover every record exactly once; 90: the same
-    order over the segmented form's units (jobs, then 32 KiB payload segments).
-    100 k records, most of 0.5-2 KiB payload and one in twenty of 33-100 KiB (cut
-    into segments by 90), every fourth deleted, byte-exact against the oracle's
-    real_compact with CRCs and statuses."""
+    tickets -- both phases must cover every record exactly once, also over the
+    10-, 12- and 16-wave workgroups of the occupancy forms (94-99).  100 k records,
+    most of 0.5-2 KiB payload and one in twenty of 33-100 KiB, every fourth
+    deleted, byte-exact against the oracle's real_compact with CRCs and statuses."""
     import tfs_amd.crc as crc
     from tfs_amd.synth import synth_bytes
     from test_headline_parity import _oracle_mt

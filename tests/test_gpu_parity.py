@@ -348,10 +348,10 @@ def _stripe_edge_cases(run, count=24):
     return out[:count]
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5, 6, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21,
-                                     39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 50, 51, 52, 53, 54, 55, 56, 57, 58])
+@pytest.mark.parametrize("variant", [0, 20, 50])
 def test_kernel_variants_parity(oracle, variant, monkeypatch):
-    """Every compiled (RUN, PF) variant is bit-exact, including the stripe-0 seed edge."""
+    """The product, the latency form forced on every batch (TFS_CRC_VARIANT 20) and
+    one file per ticket (50) are bit-exact, including the stripe-0 seed edge."""
     import tfs_amd.crc as crc
     monkeypatch.setenv("TFS_CRC_VARIANT", str(variant))
     ctx = crc.Context(0)
@@ -372,7 +372,7 @@ def test_kernel_variants_parity(oracle, variant, monkeypatch):
         ctx.close()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 4, 10, 13, 14, 15, 16, 17, 18, 19, 20, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 50])
+@pytest.mark.parametrize("variant", [0, 20, 50])
 def test_cross_file_pipeline_many_files(oracle, variant, monkeypatch):
     """> 4096 files so every wave runs a sequence of files of mixed geometry
     (tiny / single-stripe / multi-stripe, any alignment, any seed): exercises
@@ -403,9 +403,9 @@ def test_cross_file_pipeline_many_files(oracle, variant, monkeypatch):
         ctx.close()
 
 
-@pytest.mark.parametrize("variant", [0, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 50, 51, 52, 53, 54, 55, 56, 57, 58, 91, 92, 93])
+@pytest.mark.parametrize("variant", [0, 50])
 def test_dynamic_tickets_million_files(oracle, variant, monkeypatch):
-    """> 16 files (or chunks of CF files, variants 39-41) per wave, so the launch
+    """> 16 files (or chunks of CF files, the product) per wave, so the launch
     takes the dynamic-ticket path with stealing across the eight groups: 1 M short
     files of every length class below 300 bytes, any alignment and seed."""
     import tfs_amd.crc as crc
@@ -698,7 +698,7 @@ def test_device_resident_max_len_and_64bit_offsets(gpu_ctx, oracle):
         img.free()
 
 
-@pytest.mark.parametrize("variant", [0, 50, 40])
+@pytest.mark.parametrize("variant", [0, 50])
 def test_dynamic_tickets_verify_counts_each_file_once(oracle, variant, monkeypatch):
     """Verify over 1 M device-resident files on the dynamic (chunked) path with
     1,000 wrong expectations: n_bad is exactly 1,000 and the verdicts are 0 at

@@ -254,6 +254,52 @@ def test_caller_streams_any_number_and_concurrent(gpu_ctx, oracle):
             b.free()
 
 
+def test_foreign_streams_share_one_split_plan(oracle):
+    """Throughput launches on many streams of the caller's own (foreign slots) use
+    ONE split plan between them: after 40 such launches on 40 streams,
+    with files long enough to be split, the context holds one plan more than its
+    owned streams' -- not one per foreign slot -- and every CRC is exact."""
+    import tfs_amd.crc as crc
+    hip = _hip()
+    ctx = crc.Context(0)
+    n = 3000
+    rng = np.random.default_rng(1703)
+    lens = np.where(rng.integers(0, 10, n) == 0, rng.integers(1 << 17, 1 << 19, n), rng.integers(0, 4000, n))
+    lens = lens.astype(np.uint32)
+    offs = np.cumsum(np.concatenate([[0], lens[:-1]]).astype(np.uint64))
+    buf = synth_bytes(1704, int(offs[-1] + lens[-1]) + 64)
+    exp = _oracle_batch(oracle, buf, offs, lens, np.zeros(n, np.uint32))
+    d = np.zeros(n, crc.DESC_DTYPE)
+    d["offset"], d["len"] = offs, lens
+    img = crc.DeviceBuffer(ctx, buf.size).upload(buf)
+    dd = crc.DeviceBuffer(ctx, d.nbytes).upload(d)
+    outs = [crc.DeviceBuffer(ctx, 4 * n) for _ in range(4)]
+    streams = []
+    try:
+        ctx.batch_device(dd, n, img, outs[0])  # the ctx stream's own plan
+        ctx.sync()
+        plans0, bytes0 = ctx.plan_stats()
+        assert plans0 == 1
+        for it in range(40):
+            s = ctypes.c_void_p()
+            assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+            streams.append(s.value)
+            ctx.batch_device(dd, n, img, outs[it % 4], stream=s.value)
+            if it % 4 == 3:  # four launches in flight on four streams at a time
+                for q in streams[-4:]:
+                    assert hip.hipStreamSynchronize(q) == 0
+                for k in range(4):
+                    assert (outs[k].download(np.uint32, n) == exp).all(), (it, k)
+        plans, nbytes = ctx.plan_stats()
+        assert plans == plans0 + 1 and nbytes <= 2 * bytes0, (plans, nbytes, bytes0)
+    finally:
+        for q in streams:
+            hip.hipStreamDestroy(q)
+        for b in outs + [img, dd]:
+            b.free()
+        ctx.close()
+
+
 def test_stream_per_thread_handle_refused(gpu_ctx, oracle):
     import tfs_amd.crc as crc
     img, dd, exp = _device_files(gpu_ctx, oracle, 100, 1701)

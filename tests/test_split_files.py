@@ -1,11 +1,10 @@
-"""Split files: a throughput launch (more than 256
-files) cuts every file longer than 128 KiB into a ragged head and 128 KiB
-segments that separate waves checksum; the segment CRCs are folded on the GPU
-(crc(A||B) = shift(crc(A), |B|) ^ crc(B), the seed on the head).  Every test
-runs under both unit orders: every unit in address order (the product, round 4)
-and segments appended after the files (round 3's form, measurement build).  Results must
-be bit-identical to Func::crc (src/common/func.cpp:426-435) whatever the split:
-against the oracle, and against the same context with splitting off."""
+"""Split files: a throughput launch (more than 256 files) cuts
+every file longer than 128 KiB into a ragged head and 128 KiB segments that
+separate waves checksum, every unit in address order; the segment CRCs are
+folded on the GPU (crc(A||B) = shift(crc(A), |B|) ^ crc(B), the seed on the
+head).  Results must be bit-identical to Func::crc (src/common/func.cpp:426-435)
+whatever the split: against the oracle, and against the same context with
+splitting off."""
 import numpy as np
 import pytest
 
@@ -18,18 +17,10 @@ pytestmark = pytest.mark.gpu
 KSEG = 128 * 1024
 
 
-@pytest.fixture(params=["address_ordered", "appended"])
-def sctx(request, gpu_ctx):
-    """The product context (the address-ordered unit list), and a measurement-build
-    context set to round 3's appended form (tfs_crc32_set_split 2)."""
-    import tfs_amd.crc as crc
-    if request.param == "address_ordered":
-        yield gpu_ctx
-        return
-    c = crc.Context(0, measure=True)
-    c.set_split(2)
-    yield c
-    c.close()
+@pytest.fixture
+def sctx(gpu_ctx):
+    """The product context (the address-ordered unit list)."""
+    yield gpu_ctx
 
 
 def _edge_lengths():
@@ -99,18 +90,20 @@ def test_split_verify_device_wrong_expectations(sctx, oracle):
             b.free()
 
 
-def test_split_capacity_overflow_keeps_files_whole(sctx, oracle):
-    """The plan holds max(2n, 65,536) units: 400 files of 9 MiB (28,800
-    segments) all split; 1,000 of them need 72,000, so the files of the
-    workgroups that do not fit stay whole.  Every CRC exact either way."""
+def test_split_capacity_overflow_splits_the_prefix_that_fits(sctx, oracle):
+    """The plan has room for max(2n, 65,536) segments.  400 files of 9 MiB (28,400
+    segments) all split; 1,000 of them need 71,000, so the longest prefix of files
+    whose segments fit is split (round 4's form split nothing then) and
+    the files after it stay whole -- split_stats reports exactly that prefix's
+    segments.  Then 300 files of 64 MiB (153,300 segments; the first 128 fit): a
+    batch of big files still spreads over the grid.  Every CRC exact."""
     import tfs_amd.crc as crc
     rng = np.random.default_rng(3034)
-    L = 9 * (1 << 20) + 3
-    src = crc.DeviceBuffer(sctx, L + 4096)
-    sctx.synth_fill_device(src, (L + 4096) // 8 * 8, 3035, 0)
-    host = src.download(np.uint8, L + 4096)
-    for n in (400, 1000):
-        offs = rng.integers(0, 4000, n).astype(np.uint64)  # overlapping files over one 9 MiB region
+    for n, L in ((400, 9 * (1 << 20) + 3), (1000, 9 * (1 << 20) + 3), (300, 64 * (1 << 20) + 5)):
+        src = crc.DeviceBuffer(sctx, L + 4096)
+        sctx.synth_fill_device(src, (L + 4096) // 8 * 8, 3035, 0)
+        host = src.download(np.uint8, L + 4096)
+        offs = rng.integers(0, 4000, n).astype(np.uint64)  # overlapping files over one region
         lens = np.full(n, L - 4000, np.uint32) - rng.integers(0, 100, n).astype(np.uint32)
         seeds = rng.integers(0, 2**32, n).astype(np.uint32)
         d = np.zeros(n, crc.DESC_DTYPE)
@@ -124,10 +117,17 @@ def test_split_capacity_overflow_keeps_files_whole(sctx, oracle):
             idx = np.linspace(0, n - 1, 40).astype(np.int64)
             exp = _oracle_batch(oracle, host, offs[idx], lens[idx], seeds[idx])
             assert (got[idx] == exp).all(), n
+            st = sctx.split_stats()
+            K = np.where(lens > KSEG, (lens.astype(np.int64) - 1) // KSEG, 0)
+            cum = np.cumsum(K)
+            fit = int((cum <= st["cap"]).sum())
+            assert st["files"] == n and st["cap"] == max(2 * n, 65536)
+            assert st["used"] == (int(cum[fit - 1]) if fit else 0) > 0, (n, st, fit)
+            assert (fit == n) == (n == 400), (n, fit)
         finally:
             dd.free()
             out.free()
-    src.free()
+            src.free()
 
 
 def test_split_packet_bodies(sctx, oracle):

@@ -5,13 +5,13 @@ BASELINE configs[2] packs Zipf(1.1)-sized files (len = 4096 k + U[0, 4095], k in
 offsets and 27 % of the files are longer than 128 KiB.  At production size the
 file kernel's launch then runs everything at once:
 
-- the split plan (split_plan_kernel): every file > 128 KiB cut into a ragged head
-  and whole 128 KiB segments ("ext units") appended after the files;
+- the split plan (split_ao_count / _scan / _write): every file > 128 KiB cut into
+  a ragged head and whole 128 KiB segments, every unit listed in address order;
 - chunked dynamic tickets (FileCursor, CF = 4, the last units >> 3 one by one):
-  taken only when the units (files + ext units) come to >= 16 tickets per wave;
-- the fold (split_fold_kernel) joining each split file's head and segment CRCs.
+  taken only when the units (files + segments) come to >= 16 tickets per wave;
+- the fold (split_ao_fold_kernel) joining each split file's head and segment CRCs.
 
-Here 320 blocks of bench.zipf_sizes (~154 k files, ~118 k ext units, ~93 k
+Here 320 blocks of bench.zipf_sizes (~154 k files, ~118 k segments, ~93 k
 tickets on 4,096 waves: the chunked path) are device-resident and run in both
 forms, each checked file by file against the oracle over the device's own bytes:
 
@@ -21,10 +21,8 @@ forms, each checked file by file against the oracle over the device's own bytes:
 
 tfs_crc32_split_stats proves the launch took that path (the plan split files;
 units / tickets from the plan's own count).  A third test runs split launches on
-two streams of one context at once (one plan per scheduler slot) and
-checks them.  Every test runs on the product context (the address-ordered unit
-list, round 4) and on a measurement-build context set to round 3's form
-(segments appended after the files).
+two streams of one context at once (one plan per owned scheduler slot) and
+checks them.
 
 References: Func::crc src/common/func.cpp:426-435; the running-seed identity the
 fold relies on, DataFile::get_crc src/dataserver/data_file.cpp:183-186; the
@@ -42,18 +40,10 @@ SEG = 128 * 1024
 NBLOCKS = 320
 
 
-@pytest.fixture(params=["address_ordered", "appended"])
-def sctx(request, gpu_ctx):
-    """The product context (the address-ordered unit list), and a measurement-build
-    context set to round 3's appended form (tfs_crc32_set_split 2)."""
-    import tfs_amd.crc as crc
-    if request.param == "address_ordered":
-        yield gpu_ctx
-        return
-    c = crc.Context(0, measure=True)
-    c.set_split(2)
-    yield c
-    c.close()
+@pytest.fixture
+def sctx(gpu_ctx):
+    """The product context (the address-ordered unit list)."""
+    yield gpu_ctx
 
 
 def _oracle_mt(oracle, host, offs, lens, seeds):

@@ -55,7 +55,8 @@ FILEINFO_DTYPE = np.dtype([("id_", "<u8"), ("offset_", "<i4"), ("size_", "<i4"),
                            ("crc_", "<u4")], align=False)
 assert DESC_DTYPE.itemsize == 16 and META_DTYPE.itemsize == 16 and FILEINFO_DTYPE.itemsize == 36
 
-# Every symbol include/tfs_crc.h declares (checked by tests/test_abi.py).
+# Every symbol include/tfs_crc.h and include/tfs_crc_testing.h declare (checked by
+# tests/test_abi.py).
 EXPORTED = [
     "tfs_crc32_ctx_create", "tfs_crc32_ctx_destroy", "tfs_crc32_last_error", "tfs_crc32_device_count",
     "tfs_crc32_device_numa_node",
@@ -70,7 +71,7 @@ EXPORTED = [
     "tfs_crc32_stream", "tfs_crc32_sync", "tfs_crc32_stream_create", "tfs_crc32_stream_sync",
     "tfs_crc32_stream_destroy", "tfs_crc32_inject_device_error", "tfs_crc32_set_resident",
     "tfs_crc32_resident_stats", "tfs_crc32_error_count", "tfs_crc32_set_default_ctx", "tfs_crc32_bind_thread",
-    "tfs_crc32_default_ctx", "tfs_crc32_set_cu_reserve", "tfs_crc32_throughput_grid", "tfs_crc32_sched_stats",
+    "tfs_crc32_default_ctx", "tfs_crc32_set_cu_reserve", "tfs_crc32_throughput_grid", "tfs_crc32_sched_stats", "tfs_crc32_plan_stats",
     "tfs_crc32_debug_state", "tfs_crc32_debug_poison_resident",
     "tfs_crc32_set_split", "tfs_crc32_split_stats", "tfs_crc32_set_compact_segment",
     "tfs_crc_group_create", "tfs_crc_group_destroy", "tfs_crc_group_last_error", "tfs_crc_group_size",
@@ -172,6 +173,8 @@ def lib(measure=False):
             "tfs_crc32_throughput_grid": (ctypes.c_int, [vp]),
             "tfs_crc32_sched_stats": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint32),
                                                      ctypes.POINTER(ctypes.c_uint64)]),
+            "tfs_crc32_plan_stats": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint32),
+                                                    ctypes.POINTER(ctypes.c_uint64)]),
             "tfs_crc32_debug_state": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_uint64),
                                                      ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_uint64)]),
             "tfs_crc32_debug_poison_resident": (ctypes.c_int, [vp, u32]),
@@ -336,6 +339,12 @@ class Context:
         self._check(self.L.tfs_crc32_sched_stats(self.handle, ctypes.byref(a), ctypes.byref(b)), "sched_stats")
         return a.value, b.value
 
+    def plan_stats(self):
+        """(split / segment plans held, their device bytes) -- test hook."""
+        a, b = ctypes.c_uint32(), ctypes.c_uint64()
+        self._check(self.L.tfs_crc32_plan_stats(self.handle, ctypes.byref(a), ctypes.byref(b)), "plan_stats")
+        return a.value, b.value
+
     def debug_state(self):
         """{sched, sched_bytes, res_state, res_state_bytes}: device addresses of the scheduler slots and
         resident-kernel state (test hook)."""
@@ -447,6 +456,12 @@ class Context:
         self._check(self.L.tfs_block_compact_device(self.handle, _ptr(d_src), src_len, _ptr(d_live_metas),
                                                    _ptr(d_flags), _ptr(d_dest_off), n, _ptr(d_dest), _ptr(d_crc),
                                                    _ptr(d_status), _ptr(d_nbad), stream), "block_compact_device")
+
+    def host_device_ptr(self, h_ptr):
+        """Device address of page-locked host memory (zero-copy operand of the *_device calls)."""
+        p = ctypes.c_void_p()
+        self._check(self.L.tfs_crc32_host_device_ptr(self.handle, _ptr(h_ptr), ctypes.byref(p)), "host_device_ptr")
+        return p.value
 
     def compact_jobs_device(self, d_src, src_len, d_jobs, n, d_dest, d_crc=None, d_status=None, d_nbad=None,
                             stream=None):

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../include/tfs_crc.h"
+#include "../../include/tfs_crc_testing.h"
 #include "crc_math.h"
 #include "pin_registry.h"
 #include "tfs_crc_device.h"
@@ -47,13 +48,6 @@ hipError_t launch_compact_fused(const uint8_t* src, uint64_t src_len, const RawM
 hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const CompactJob* jobs, uint32_t n, uint8_t* dst,
                                const Tables* tg, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
                                uint32_t* sched, hipStream_t stream, int variant, unsigned cap, const CSegArgs* seg);
-#ifdef TFS_CRC_MEASURE
-hipError_t launch_block_verify(const uint8_t* image, uint64_t image_len, const RawMeta* metas, uint32_t n,
-                               const Tables* tg, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
-                               hipStream_t stream);
-hipError_t launch_compact_copy(const uint8_t* src, const RawMeta* metas, const int32_t* flags, const int64_t* dest_off,
-                               uint32_t n, uint8_t* dst, hipStream_t stream);
-#endif
 hipError_t launch_synth_fill(uint64_t* dst, uint64_t nwords, uint64_t seed, uint64_t first_word, hipStream_t stream);
 hipError_t launch_write_headers(uint8_t* image, const uint64_t* rec_off, const uint32_t* len, const uint32_t* crc,
                                 uint64_t first_id, uint32_t n, hipStream_t stream);
@@ -233,11 +227,6 @@ constexpr uint32_t kForeignSlots = 64;    // the last 64 scheduler slots: launch
 constexpr uint32_t kOwnedSlots = kSchedSlots - kForeignSlots;
 // Measurement build only (TFS_CRC_VARIANT; the product's ctx->variant is a constant 0):
 constexpr int kVariantDmaCompact = 8;      // DMA staging for host compaction / block verify / small batches
-constexpr int kVariantZcReadDmaWrite = 38; // host compaction reads live records in place, the new block goes to
-                                           // device memory and back by a DMA copy
-#ifdef TFS_CRC_MEASURE
-constexpr int kVariantUnfusedCompact = 7;  // two-pass device compaction (A/B baseline)
-#endif
 // A context that posted a close batch this recently keeps the resident kernel's
 // CUs out of its device's throughput launches even while the kernel is between
 // lifetimes.
@@ -287,11 +276,11 @@ struct tfs_crc_ctx {
   static constexpr int variant = 0;  // the product library holds one form of each kernel
 #endif
   unsigned cus = kMaxGrid;  // compute units of the device: throughput grids are at most this
-  // Split files (tfs_crc_device.h SplitArgs): one plan per scheduler slot, so a
-  // launch orders only behind the earlier launches of its own slot -- the same
-  // stream for an owned slot, the slot's previous lease (waited for by
-  // sched_acquire) for a foreign one -- and split launches on different streams
-  // overlap.  plan_mu[k] is held from the plan's setup to the launch.
+  // Split files (tfs_crc_device.h SplitArgs): one plan per owned scheduler slot,
+  // so a launch orders only behind the earlier launches of its own stream, and
+  // split launches on different owned streams overlap; the foreign
+  // slots share the plan at index kOwnedSlots, ordered by plan_done (plan_index,
+  // ADVICE r4).  plan_mu[k] is held from the plan's setup to the launch.
   DevBuf plans[kSchedSlots];
   hipEvent_t plan_done[kSchedSlots] = {};  // behind the latest split launch of slot k
   std::mutex plan_mu[kSchedSlots];
@@ -299,12 +288,9 @@ struct tfs_crc_ctx {
   std::mutex last_split_mu;
   int last_split_slot = -1;
   uint32_t last_split_n = 0, last_split_cap = 0, last_split_grid = 0;
-  bool last_split_ao = false;
   uint64_t split_launches = 0;
   std::atomic<bool> cu_reserve{true};   // leave a live resident kernel's CUs out of throughput launches
-  std::atomic<int> split_files{1};  // throughput launches split files > kSplitMin (tfs_crc32_set_split): 0 off,
-                                   // 1 address-ordered units (product), 2 segments appended after the files
-                                   // (round 3's form, measurement build)
+  std::atomic<int> split_files{1};  // throughput launches split files > kSplitMin (tfs_crc32_set_split): 0 off
   std::atomic<uint32_t> cseg_lg{0};  // segmented compaction: 1 KiB << cseg_lg segments, 0 = whole records
   std::atomic<bool> cseg_auto{true};  // the default rule (cseg_lg()) until tfs_crc32_set_compact_segment
   std::atomic<uint32_t> inject_skip{0}, inject_count{0};  // tfs_crc32_inject_device_error
@@ -666,24 +652,32 @@ uint32_t slot_index(const tfs_crc_ctx* ctx, const SchedLease& L) {
   return uint32_t((L.slot - ctx->d_sched) / (kSchedSlotBytes / 4u));
 }
 
+// The plan a lease uses: an owned slot's own, or ONE plan shared by every foreign
+// slot (a plan per foreign slot let 64 caller-stream launches keep
+// 64 plans -- ~7 GB at 1 M files -- alive per context).  A launch on the shared
+// plan waits on its stream for the plan's previous user, which may be on any other
+// stream (plan_done); the caller holds plan_mu[index] from here to the launch.
+uint32_t plan_index(const SchedLease& L, uint32_t k) { return L.foreign >= 0 ? kOwnedSlots : k; }
+int plan_order(tfs_crc_ctx* ctx, hipStream_t st, const SchedLease& L, uint32_t pk) {
+  if (L.foreign >= 0 && ctx->plan_done[pk]) HIP_TRY(ctx, hipStreamWaitEvent(st, ctx->plan_done[pk], 0));
+  return TFS_SUCCESS;
+}
+
 // (Caller holds plan_mu[k].)  Slot k's split plan for a throughput crc_files
 // launch of n files on st (tfs_crc_device.h: one allocation, up to cap ext
 // units).  The earlier launches using this plan are ordered before st's: they
 // ran on st itself (owned slot) or were waited for when the slot was leased
 // (foreign slot).  Growing frees the plan, so st is drained first.
 int split_prepare(tfs_crc_ctx* ctx, hipStream_t st, uint32_t k, uint32_t n, SplitArgs* sa) {
+  // room for max(2n, 65,536) segments (at most 4 M); the plan's capacity counts
+  // every unit of the address-ordered list (files + segments)
   const uint32_t cap = uint32_t(std::min<uint64_t>(std::max<uint64_t>(2ull * n, 65536ull), kSplitMaxUnits));
-  // the product's address-ordered unit list; the measurement build's appended
-  // form (set_split 2) and kernel variants (which read the appended layout)
-  const bool ao = ctx->split_files.load(std::memory_order_relaxed) == 1 && ctx->variant == 0;
-  // address-ordered form: the plan's capacity counts every unit (files + segments)
-  const uint32_t ucap = ao ? uint32_t(std::min<uint64_t>(uint64_t(n) + cap, 0xffffffffull)) : cap;
-  const uint64_t bytes = ao ? ao_bytes(n, ucap) : split_bytes(n, cap);
+  const uint32_t ucap = uint32_t(std::min<uint64_t>(uint64_t(n) + cap, 0xffffffffull));
+  const uint64_t bytes = ao_bytes(n, ucap);
   DevBuf& plan = ctx->plans[k];
   if (bytes > plan.cap && plan.p) HIP_TRY(ctx, hipStreamSynchronize(st));
   HIP_TRY(ctx, plan.reserve(bytes));
-  if (!ao) HIP_TRY(ctx, hipMemsetAsync(plan.p, 0, 8u, st));  // `used` (the scan kernel writes the ao header)
-  *sa = SplitArgs{static_cast<uint8_t*>(plan.p), ucap, ao ? 1u : 0u};
+  *sa = SplitArgs{static_cast<uint8_t*>(plan.p), ucap};
   return TFS_SUCCESS;
 }
 
@@ -694,14 +688,15 @@ int files_launch(tfs_crc_ctx* ctx, hipStream_t st, int mode, const uint8_t* base
                  uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t vseed) {
   SchedLease lease;
   if (const int r = sched_acquire(ctx, st, &lease)) return r;
-  const uint32_t k = slot_index(ctx, lease);
+  const uint32_t k = plan_index(lease, slot_index(ctx, lease));
   std::unique_lock<std::mutex> lk(ctx->plan_mu[k], std::defer_lock);
-  SplitArgs sa{nullptr, 0u, 0u};
+  SplitArgs sa{nullptr, 0u};
   const SplitArgs* split = nullptr;
   int rc = TFS_SUCCESS;
   if (n > kWgMaxFiles && ctx->split_files.load(std::memory_order_relaxed) != 0) {
     lk.lock();
-    rc = split_prepare(ctx, st, k, n, &sa);
+    rc = plan_order(ctx, st, lease, k);
+    if (rc == TFS_SUCCESS) rc = split_prepare(ctx, st, k, n, &sa);
     if (rc == TFS_SUCCESS) split = &sa;
   }
   const unsigned cap = cap_for(ctx, n);
@@ -718,8 +713,7 @@ int files_launch(tfs_crc_ctx* ctx, hipStream_t st, int mode, const uint8_t* base
     std::lock_guard<std::mutex> g(ctx->last_split_mu);
     ctx->last_split_slot = int(k);
     ctx->last_split_n = n;
-    ctx->last_split_cap = sa.ao ? sa.cap - n : sa.cap;  // ext units the plan had room for
-    ctx->last_split_ao = sa.ao != 0;
+    ctx->last_split_cap = sa.cap - n;  // segments the plan had room for
     ctx->last_split_grid = cap;  // a split launch takes the whole capped grid (launch_variant)
     ++ctx->split_launches;
   }
@@ -728,25 +722,15 @@ int files_launch(tfs_crc_ctx* ctx, hipStream_t st, int mode, const uint8_t* base
 }
 
 // Segment size of the segmented compaction (tfs_crc_device.h CSegArgs) for ctx:
-// 1 KiB << lg, 0 = records stay whole.  Measurement build: TFS_CRC_VARIANT 72 /
-// 73 / 74 = 16 / 8 / 32 KiB segments.
+// 1 KiB << lg, 0 = records stay whole.
 // The product default (cseg_auto): whole records.  Round 4 first made 32 KiB segments
 // the default for launches of at least 65,536 records; over seven boxes they averaged
 // -0.4 % against whole records (+2.0 % to -1.7 %), while the hybrid record order the
 // product now launches (kCompactHS) gained 1.4 % on average.
 // Segments stay selectable per context (tfs_crc32_set_compact_segment).
-#ifdef TFS_CRC_MEASURE
-constexpr uint32_t kCSegAutoJobs = 65536;  // variant 90: the former default rule
-constexpr uint32_t kCSegAutoLg = 5;
-#endif
 uint32_t cseg_lg(const tfs_crc_ctx* ctx, uint32_t n) {
-#ifdef TFS_CRC_MEASURE
-  if (ctx->variant == 72) return 4u;
-  if (ctx->variant == 73) return 3u;
-  if (ctx->variant == 74) return 5u;
-  if (ctx->variant == 90) return n >= kCSegAutoJobs ? kCSegAutoLg : 0u;  // the auto rule, hybrid unit order
-  if (ctx->variant != 0) return 0u;  // the other compaction variants: whole records
-#endif
+  (void)n;
+  if (ctx->variant != 0) return 0u;  // the measurement variants: whole records
   if (ctx->cseg_auto.load(std::memory_order_relaxed)) return 0u;  // the default: whole records
   return ctx->cseg_lg.load(std::memory_order_relaxed);
 }
@@ -1579,16 +1563,9 @@ static int compact_enqueue(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job
   if (zc) {
     HIP_TRY(ctx, hipMemcpyAsync(da, ha, ob + mb + fb, hipMemcpyHostToDevice, cs.stream));
     uint8_t* kdst = static_cast<uint8_t*>(zc_dst);
-    const bool dma_write = ctx->variant == kVariantZcReadDmaWrite;
-    if (dma_write) {
-      HIP_TRY(ctx, cs.d_dst.reserve(uint64_t(w) + 16));
-      kdst = static_cast<uint8_t*>(cs.d_dst.p);
-    }
     SCHED_LAUNCH(ctx, cs.stream, "compact_fused", launch_compact_fused(static_cast<const uint8_t*>(zc_src), job->src_len, d_metas, d_flags, d_doff, nl,
                                       kdst, ctx->d_tables, d_crc, d_status, nullptr, sched, cs.stream, ctx->variant, throughput_cap(ctx)));
     HIP_TRY(ctx, hipMemcpyAsync(cs.h_status.p, d_status, fb, hipMemcpyDeviceToHost, cs.stream));
-    if (dma_write && w)
-      HIP_TRY(ctx, hipMemcpyAsync(job->dest_image, cs.d_dst.p, size_t(w), hipMemcpyDeviceToHost, cs.stream));
   } else {
     const int rc = compact_dma(ctx, cs, job, nl, w, da, ha, ob + mb + fb, d_metas, d_flags, d_doff, d_crc, d_status);
     if (rc != TFS_SUCCESS) return rc;
@@ -1684,16 +1661,6 @@ int tfs_block_compact_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_l
   if (!ctx || (n && (!d_src || !d_live_metas || !d_flags || !d_dest_off || !d_dest))) return TFS_EXIT_PARAMETER_ERROR;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-#ifdef TFS_CRC_MEASURE
-  if (ctx->variant == kVariantUnfusedCompact) {  // measurement build: verify, then a separate copy pass
-    HIP_TRY(ctx, launch_block_verify(static_cast<const uint8_t*>(d_src), src_len,
-                                     reinterpret_cast<const RawMeta*>(d_live_metas), n, ctx->d_tables, d_out_crc,
-                                     d_out_status, d_n_bad, st));
-    HIP_TRY(ctx, launch_compact_copy(static_cast<const uint8_t*>(d_src), reinterpret_cast<const RawMeta*>(d_live_metas),
-                                     d_flags, d_dest_off, n, static_cast<uint8_t*>(d_dest), st));
-    return TFS_SUCCESS;
-  }
-#endif
   SCHED_LAUNCH(ctx, st, "compact_fused", launch_compact_fused(static_cast<const uint8_t*>(d_src), src_len,
                                     reinterpret_cast<const RawMeta*>(d_live_metas), d_flags, d_dest_off, n,
                                     static_cast<uint8_t*>(d_dest), ctx->d_tables, d_out_crc, d_out_status, d_n_bad,
@@ -1710,14 +1677,15 @@ int tfs_compact_jobs_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_le
   if (n == 0) return TFS_SUCCESS;
   SchedLease lease;
   if (const int r = sched_acquire(ctx, st, &lease)) return r;
-  const uint32_t k = slot_index(ctx, lease);
+  const uint32_t k = plan_index(lease, slot_index(ctx, lease));
   std::unique_lock<std::mutex> lk(ctx->plan_mu[k], std::defer_lock);
   CSegArgs cs{nullptr, 0u, 0u};
   int rc = TFS_SUCCESS;
   const uint32_t lg = cseg_lg(ctx, n);
   if (lg) {
     lk.lock();
-    rc = cseg_prepare(ctx, st, k, n, lg, &cs);
+    rc = plan_order(ctx, st, lease, k);
+    if (rc == TFS_SUCCESS) rc = cseg_prepare(ctx, st, k, n, lg, &cs);
   }
   const hipError_t le =
       rc == TFS_SUCCESS ? launch_compact_jobs(static_cast<const uint8_t*>(d_src), src_len,
@@ -2192,12 +2160,7 @@ int tfs_crc32_set_cu_reserve(tfs_crc_ctx* ctx, int on) {
 }
 
 int tfs_crc32_set_split(tfs_crc_ctx* ctx, int on) {
-#ifdef TFS_CRC_MEASURE
-  const int top = 2;  // 2: round 3's appended form (measurement build)
-#else
-  const int top = 1;
-#endif
-  if (!ctx || on < 0 || on > top) return TFS_EXIT_PARAMETER_ERROR;
+  if (!ctx || on < 0 || on > 1) return TFS_EXIT_PARAMETER_ERROR;
   ctx->split_files.store(on, std::memory_order_relaxed);
   return TFS_SUCCESS;
 }
@@ -2238,19 +2201,31 @@ int tfs_crc32_split_stats(tfs_crc_ctx* ctx, uint64_t* launches, uint64_t* used, 
     std::lock_guard<std::mutex> pg(ctx->plan_mu[k]);
     if (!ctx->plan_done[k]) return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "split_stats: no event behind the plan");
     HIP_TRY(ctx, hipEventSynchronize(ctx->plan_done[k]));
-    if (ctx->last_split_ao) {  // header {units, nosplit, ext}
-      uint32_t hdr[3] = {0u, 0u, 0u};
-      HIP_TRY(ctx, hipMemcpy(hdr, ctx->plans[k].p, 12, hipMemcpyDeviceToHost));
-      u = hdr[1] ? 0u : hdr[2];
-    } else {
-      HIP_TRY(ctx, hipMemcpy(&u, ctx->plans[k].p, 8, hipMemcpyDeviceToHost));
-    }
+    uint32_t hdr[4] = {0u, 0u, 0u, 0u};  // {units, nosplit, ext, cut}
+    HIP_TRY(ctx, hipMemcpy(hdr, ctx->plans[k].p, 16, hipMemcpyDeviceToHost));
+    u = hdr[1] ? 0u : hdr[2];
   }
   if (launches) *launches = nl;
   if (used) *used = u;
   if (files) *files = n;
   if (cap) *cap = c;
   if (grid) *grid = g;
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_plan_stats(tfs_crc_ctx* ctx, uint32_t* plans, uint64_t* bytes) {
+  if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
+  uint32_t np = 0;
+  uint64_t nb = 0;
+  for (uint32_t k = 0; k < kSchedSlots; ++k) {
+    std::lock_guard<std::mutex> g(ctx->plan_mu[k]);
+    if (ctx->plans[k].p) {
+      ++np;
+      nb += ctx->plans[k].cap;
+    }
+  }
+  if (plans) *plans = np;
+  if (bytes) *bytes = nb;
   return TFS_SUCCESS;
 }
 

@@ -24,11 +24,19 @@ constexpr uint32_t kLdsStripeOff = 4u * kRepTableBytes;   // 128 KiB
 constexpr int kShiftChunks = 7;
 constexpr uint32_t kShift5Stride = 1024u;                          // 896 B table, padded
 constexpr uint32_t kShift8Stride = 4096u;                          // 4 x 256 x 4 B
-template <bool S8> struct LdsLayout {
-  static constexpr uint32_t stride = S8 ? kShift8Stride : kShift5Stride;
-  static constexpr uint32_t stripe_off = kLdsStripeOff;
-  static constexpr uint32_t level_off = kLdsStripeOff + stride;
-  static constexpr uint32_t bytes = level_off + 6u * stride;        // 135 KiB (5-bit) / 156 KiB (8-bit)
+// Table layouts (LY): 0 slice tables 32x + 5-bit shift tables (135 KiB); 1 slice
+// tables 32x + byte shift tables (156 KiB, the product's one workgroup per CU);
+// 2 slice tables 16x (64 KiB, four tables in one 256-byte bank row per byte value),
+// the per-stripe shift as byte tables and the once-per-file level shifts 5-bit:
+// 74 KiB, so two workgroups fit a CU's 160 KiB (round 5, the record kernel).
+template <int LY> struct LdsLayout {
+  static constexpr bool rep16 = LY == 2;
+  static constexpr bool stripe_s8 = LY >= 1;
+  static constexpr bool level_s8 = LY == 1;
+  static constexpr uint32_t stripe_off = rep16 ? 65536u : kLdsStripeOff;
+  static constexpr uint32_t stride = level_s8 ? kShift8Stride : kShift5Stride;  // level tables
+  static constexpr uint32_t level_off = stripe_off + (stripe_s8 ? kShift8Stride : kShift5Stride);
+  static constexpr uint32_t bytes = level_off + 6u * stride;  // 135 / 156 / 74 KiB
 };
 
 constexpr int kFileInfoSize = 36;  // sizeof(FileInfo), internal.h:432-446
@@ -154,49 +162,32 @@ struct FileInfoHdr {  // FileInfo, internal.h:432-446
 #pragma pack(pop)
 static_assert(sizeof(FileInfoHdr) == kFileInfoSize, "FileInfo must be 36 bytes");
 
-// Split files.  A throughput launch of crc_files_kernel
-// cuts every file longer than kSplitMin into a ragged head and kSegBytes
-// segments ("ext units"), appended to the launch's work after its files, so no
-// wave streams more than kSegBytes of one file alone (a wave that walks a 1 MiB
-// file alone reads slower than the moving window of the rest: Zipf +4-5 %).
-// The plan (split_plan_kernel) gives every file its first ext unit or kNoSplit;
-// the main kernel checksums a split file's ragged head in the file's own place
-// (with the file's seed, into head_crc) and its K-1 whole segments as ext units
-// (seed 0, into ext_crc); the fold (split_fold_kernel) joins them:
-// crc = shift(...shift(crc_head, S) ^ crc_1 ..., S) ^ crc_{K-1}, shift by S
-// bytes from one table.
+// Split files.  A throughput launch of crc_files_kernel cuts
+// every file longer than kSplitMin into a ragged head and kSegBytes segments, so
+// no wave streams more than kSegBytes of one file alone (a wave that walks a
+// 1 MiB file alone reads slower than the moving window of the rest: Zipf +4-5 %).
+// The plan lists every unit of the launch -- whole files, heads and segments --
+// in address order (split_ao_count / _scan / _write); the main kernel checksums a
+// head with its file's seed and each segment with seed 0, and the fold
+// (split_ao_fold_kernel) joins them: crc = shift(...shift(crc_head, S) ^ crc_1
+// ..., S) ^ crc_K, shift by S bytes from one table.
 #ifndef TFS_SEG_KIB
 #define TFS_SEG_KIB 128  // measurement builds may set another segment size
 #endif
 constexpr uint32_t kSegBytes = uint32_t(TFS_SEG_KIB) << 10;
 constexpr uint32_t kSplitMin = kSegBytes;
 constexpr uint32_t kNoSplit = 0xffffffffu;
-constexpr uint32_t kSplitMaxUnits = 4u << 20;  // ext units per launch at most (files past it stay whole)
-// One allocation per plan (3 SGPRs in the kernels' arguments instead of a
-// pointer per array): [used u64 | pad][base u32 x n][head_crc u32 x n]
-// [ext_crc u32 x cap][pad to 16][ext Desc x cap].  base: per file its first ext
-// unit, or kNoSplit; head_crc: a split file's head CRC; ext: the split files'
-// whole segments; used: ext units the plan reserved (zeroed before it; may pass
-// cap, the files past it stay whole).
+constexpr uint32_t kSplitMaxUnits = 4u << 20;  // segments per launch at most (files past the cut stay whole)
 struct SplitArgs {
   uint8_t* plan;  // nullptr: no split plan
-  uint32_t cap;   // appended form: ext units at most; address-ordered form: units (files + segments) at most
-  uint32_t ao;    // 1: the address-ordered form (SplitUnit list), 0: segments appended after the files
+  uint32_t cap;   // units (files + segments) at most
 };
-constexpr uint64_t split_off_base() { return 16u; }
-constexpr uint64_t split_off_head(uint32_t n) { return 16u + 4ull * n; }
-constexpr uint64_t split_off_ext_crc(uint32_t n) { return 16u + 8ull * n; }
-constexpr uint64_t split_off_ext(uint32_t n, uint32_t cap) { return (16u + 8ull * n + 4ull * cap + 15u) & ~15ull; }
-constexpr uint64_t split_bytes(uint32_t n, uint32_t cap) { return split_off_ext(n, cap) + 16ull * cap; }
 
-// Address-ordered split plan (round 4): the same cut (ragged head
-// + whole kSegBytes segments), but every unit of the launch -- whole files,
-// heads and segments -- sits in one list in address order (file i's head, then
-// its segments, then file i + 1), so the waves' tickets walk the image once
-// instead of twice (files and heads first, the big files' segments after).  The
-// unit list is built by a three-kernel scan (split_ao_count / _scan / _write).
-// [total u32 | nosplit u32 | ext u32 | pad][blk u32 x nblk][ubase u32 x n]
-// [ucrc u32 x ucap][pad to 16][SplitUnit x ucap], nblk = ceil(n / 256).
+// The plan (one allocation per scheduler slot):
+// [units u32 | nosplit u32 | ext u32 | cut u32][blk u32 x nblk][ubase u32 x n]
+// [ucrc u32 x ucap][pad to 16][SplitUnit x ucap], nblk = ceil(n / 256).  When the
+// segments of every file would pass the room (cap - n), only files [0, cut) are
+// split (the longest prefix whose segments fit); the rest stay whole.
 struct SplitUnit {
   uint64_t offset;
   uint32_t len, aux;   // aux: the file's seed / expected CRC on a whole file or head, 0 on a segment

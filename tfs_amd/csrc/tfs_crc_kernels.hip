@@ -87,6 +87,17 @@ __device__ __forceinline__ LaneBase lane_base_of(int lane) {
   const uint32_t l4 = uint32_t(lane & 31) * 4u;
   return LaneBase{l4, l4 | 0x80u, l4 | 0x10000u, l4 | 0x10080u};
 }
+// Layout 2 (16 copies, LdsLayout<2>): entry (table t, byte b, copy j < 16) at
+// b << 8 | tsel(t) << 6 | j << 2 with T3..T0 = tsel 0..3 -- the same v_perm
+// addressing (bits 16.. zero); lanes l, l+16, l+32, l+48 share a bank.
+template <int LY>
+__device__ __forceinline__ LaneBase lane_base_for(int lane) {
+  if constexpr (LdsLayout<LY>::rep16) {
+    const uint32_t l4 = uint32_t(lane & 15) * 4u;
+    return LaneBase{l4, l4 | 0x40u, l4 | 0x80u, l4 | 0xC0u};
+  }
+  return lane_base_of(lane);
+}
 
 // One dword of the slice-by-4 recurrence on x = c ^ w, fused with the XOR of the
 // next payload dword: returns M(x) ^ w_next.
@@ -122,9 +133,9 @@ __device__ __forceinline__ uint32_t shift_lds(const uint32_t* T, uint32_t off, u
   return S8 ? shift8(T, off, c) : shift5(T, off, c);
 }
 // shift(c, 63*RUN) (or 64*RUN in PAR form): the jump between two stripes of a lane.
-template <bool S8>
+template <int LY>
 __device__ __forceinline__ uint32_t shift_stripe(const uint32_t* T, uint32_t c) {
-  return shift_lds<S8>(T, LdsLayout<S8>::stripe_off, c);
+  return shift_lds<LdsLayout<LY>::stripe_s8>(T, LdsLayout<LY>::stripe_off, c);
 }
 
 __device__ __forceinline__ uint32_t steps16(const uint32_t* T, const LaneBase& lb, uint32_t c, const uint4& v) {
@@ -148,20 +159,32 @@ __device__ __forceinline__ void load_slice_tables(uint32_t* T, const Tables* __r
   }
 }
 
-// Stage the tables: 32 copies of each slice table (conflict-free lookups) and
-// the stripe-shift tables for RUN.  Every thread of the workgroup takes part.
-template <int RUN, bool PAR, bool S8>
+// Layout 2: 16 copies, dword index b<<6 | tsel<<4 | j; four copies per 16-byte store.
+__device__ __forceinline__ void load_slice_tables16(uint32_t* T, const Tables* __restrict__ tg) {
+  for (uint32_t q = threadIdx.x; q < 4u * 256u * 4u; q += blockDim.x) {
+    const uint32_t b = q >> 4, tsel = (q >> 2) & 3u;
+    const uint32_t v = tg->slice[3u - tsel][b];  // T3, T2, T1, T0
+    *reinterpret_cast<uint4*>(T + 4u * q) = make_uint4(v, v, v, v);
+  }
+}
+
+// Stage the tables: the copies of the slice tables (conflict-free lookups, or
+// 4-way with layout 2) and the stripe- and level-shift tables for RUN.  Every
+// thread of the workgroup takes part.
+template <int RUN, bool PAR, int LY>
 __device__ __forceinline__ void load_tables(uint32_t* T, const Tables* __restrict__ tg) {
-  load_slice_tables(T, tg);
-  using LL = LdsLayout<S8>;
+  using LL = LdsLayout<LY>;
+  if constexpr (LL::rep16) load_slice_tables16(T, tg);
+  else load_slice_tables(T, tg);
   const uint32_t ri = run_index(RUN);
-  const uint32_t nent = S8 ? 1024u : kShiftChunks * 32u;
-  const uint32_t* st = S8 ? (PAR ? tg->stripe64_8[ri][0] : tg->stripe8[ri][0])
-                          : (PAR ? tg->stripe64[ri][0] : tg->stripe[ri][0]);
-  for (uint32_t i = threadIdx.x; i < nent; i += blockDim.x) T[LL::stripe_off / 4 + i] = st[i];
-  const uint32_t* lv = S8 ? tg->level8[ri][0][0] : tg->level[ri][0][0];
-  for (uint32_t i = threadIdx.x; i < 6u * nent; i += blockDim.x) {
-    const uint32_t j = i / nent, r = i % nent;
+  const uint32_t sent = LL::stripe_s8 ? 1024u : kShiftChunks * 32u;
+  const uint32_t* st = LL::stripe_s8 ? (PAR ? tg->stripe64_8[ri][0] : tg->stripe8[ri][0])
+                                     : (PAR ? tg->stripe64[ri][0] : tg->stripe[ri][0]);
+  for (uint32_t i = threadIdx.x; i < sent; i += blockDim.x) T[LL::stripe_off / 4 + i] = st[i];
+  const uint32_t lent = LL::level_s8 ? 1024u : kShiftChunks * 32u;
+  const uint32_t* lv = LL::level_s8 ? tg->level8[ri][0][0] : tg->level[ri][0][0];
+  for (uint32_t i = threadIdx.x; i < 6u * lent; i += blockDim.x) {
+    const uint32_t j = i / lent, r = i % lent;
     T[(LL::level_off + LL::stride * j) / 4 + r] = lv[i];
   }
   __syncthreads();
@@ -216,35 +239,9 @@ struct Head {
   uint32_t tb[3];
 };
 
-// HV (measurement knob): one dwordx4 per lane for stripe 0 and one for the tail
-// instead of RUN/4 dword loads and 3 dword + 3 byte loads.  A 16-byte chunk that
-// holds at least one payload byte lies in the same page as that byte, so the
-// bytes read outside the payload cannot fault; they are masked as before.
-template <int RUN, bool HV = false>
+template <int RUN>
 __device__ __forceinline__ Head<RUN> load_head(const FileGeo<RUN>& g, int lane) {
   Head<RUN> h;
-  if constexpr (HV && RUN == 16) {
-    const uintptr_t lo = g.sb0 + uintptr_t(lane) * 16u;
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (g.nstripes && lo + 16u > g.A && lo < g.B16) v = ld128(lo);
-    const uint32_t vw[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uintptr_t q = lo + 4u * i;
-      h.w[i] = (q >= g.A && q < g.B16) ? vw[i] : 0u;
-    }
-    uint4 t = make_uint4(0u, 0u, 0u, 0u);
-    if (g.nstripes && g.end > g.B16) t = ld128(g.B16);
-    const uint32_t tw[4] = {t.x, t.y, t.z, t.w};
-#pragma unroll
-    for (int i = 0; i < 3; ++i) h.tw[i] = (g.nstripes && g.B16 + 4u * i + 4u <= g.end) ? tw[i] : 0u;
-    const uint32_t bo = uint32_t((g.end & ~uintptr_t(3)) - g.B16);  // byte offset of the last partial dword
-    const uint32_t bw = bo >= 12u ? t.w : (bo >= 8u ? t.z : (bo >= 4u ? t.y : t.x));
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-      h.tb[i] = (g.nstripes && (g.end & ~uintptr_t(3)) + i < g.end) ? ((bw >> (8 * i)) & 0xFFu) : 0u;
-    return h;
-  }
   const uintptr_t lo = g.sb0 + uintptr_t(lane) * RUN;
 #pragma unroll
   for (int i = 0; i < RUN / 4; ++i) {
@@ -435,24 +432,13 @@ __device__ __forceinline__ void store_bshift(uintptr_t chunk, uintptr_t own, con
 
 // The lane's chain over stripes 0..nstripes-1 (before the final combine).
 // COPY: also store every payload byte of [start, B16) to dst = src + delta.
-// G (measurement knob): refill the ring G slots at a time, so each wave issues G
-// consecutive stripes (G KiB contiguous) back to back instead of one per stripe.
 // NTS: non-temporal copy-through stores (product).  NOCRC (measurement only,
 // TFS_CRC_VARIANT=26: wrong CRCs): skip the payload steps, so the record kernel
 // runs its own load/store schedule without the table lookups.
-// XF (cross-file ring): a slot freed past this file's last stripe is refilled
-// with the NEXT file's stripe (`ng`) that the slot holds in that file's ring
-// (slot f always holds stripes congruent to 1 + f mod PF), so the next file's
-// first PF stripes are in flight while this one drains, and on return the ring
-// is the next file's.  Without XF those slots read the L2-resident `junk`
-// region and the caller issues the next file's ring after this one ends.
-template <int RUN, int PF, bool NT, bool S8, bool COPY = false, int G = 1, bool DPPSH = false, int NTS = 1,
-          bool NOCRC = false, bool HEADST = true, bool BSU = false, bool XF = false>
+template <int RUN, int PF, bool NT, int LY, bool COPY = false, bool DPPSH = false, int NTS = 1, bool NOCRC = false>
 __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase& lb, const FileGeo<RUN>& g,
                                                const Head<RUN>& h, uint4 (&buf)[PF][RUN / 16], int lane,
-                                               uintptr_t junk, intptr_t delta = 0, bool copy_on = false,
-                                               const FileGeo<RUN>* ng = nullptr) {
-  static_assert(!XF || G == 1, "the cross-file ring refills one slot at a time");
+                                               uintptr_t junk, intptr_t delta = 0, bool copy_on = false) {
   constexpr uint32_t kStripe = 64u * RUN;
   constexpr int kVec = RUN / 16;
   // Stripe 0: mask the bytes before `start` in the dword at A and inject the
@@ -470,7 +456,7 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
     for (int i = 0; i < RUN / 4; ++i) {
       const uintptr_t q = lo + 4u * i;
       uint32_t w = h.w[i];
-      if (COPY && HEADST && copy_on) {
+      if (COPY && copy_on) {
         if (q >= g.start && q < g.B16) {
           st32u(q + delta, w);
         } else if (q == g.A && g.s) {  // the dword holding `start`: its payload bytes only
@@ -488,7 +474,7 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
     const uint32_t last = g.nstripes - 1;
     const bool lane_in_last = uint32_t(lane) < g.nvalid;
     // Copy-through of stripe st (COPY only): whole dwordx4 stores at any
-    // destination shift congruent mod 4 (store_shifted).
+    // destination shift (store_shifted, store_bshift).
     const uint32_t kshift = uint32_t(delta >> 2) & 3u;
     const bool bshift = (delta & 3) != 0;  // wave-uniform
     ShiftCarry carry{0u, 0u, 0u, false, 0u};
@@ -496,7 +482,7 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
     auto copy_stripe = [&](uint32_t st, const uint4& v) {
       const bool valid = !(st == last && !lane_in_last);
       const uintptr_t q = g.sb0 + uintptr_t(st) * kStripe + uintptr_t(lane) * RUN;
-      if (bshift && !BSU) {  // byte shift: line-aligned chunks built by alignbyte
+      if (bshift) {  // byte shift: line-aligned chunks built by alignbyte
         const uintptr_t chunk = q + uintptr_t(delta & ~intptr_t(15));
         const uint32_t sh = 4u - uint32_t(delta & 3);
         const bool fl = st == last && uint32_t(lane) + 1u == g.nvalid;
@@ -504,13 +490,11 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
         else if (kshift == 1u) store_bshift<1, NTS>(chunk, q + delta, v, sh, lane, carry, valid, fl);
         else if (kshift == 2u) store_bshift<2, NTS>(chunk, q + delta, v, sh, lane, carry, valid, fl);
         else store_bshift<3, NTS>(chunk, q + delta, v, sh, lane, carry, valid, fl);
-      } else if (bshift) {  // BSU (measurement): the lane's 16 bytes at their byte address
-        if (valid) st128u<NTS>(q + delta, v);
       } else if (kshift == 0u) {
         if (valid) st128_nt<NTS>(q + delta, v);
       } else {
         store_shifted<DPPSH, NTS>(q + uintptr_t(delta) - 4u * kshift, v, kshift, lane, carry, valid,
-                             st == last && uint32_t(lane) + 1u == g.nvalid);
+                                  st == last && uint32_t(lane) + 1u == g.nvalid);
       }
     };
     uint32_t r = 1;
@@ -518,7 +502,7 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
 #pragma unroll
       for (int f = 0; f < PF; ++f) {
         const uint32_t c_old = c;
-        c = shift_stripe<S8>(T, c);
+        c = shift_stripe<LY>(T, c);
         if (f == 0) {
           c ^= inj;  // XOR into the stripe's first dword == XOR into the register before its step
           inj = 0;
@@ -527,50 +511,30 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
         for (int v = 0; v < kVec; ++v) c = NOCRC ? c ^ buf[f][v].x : steps16(T, lb, c, buf[f][v]);
         c = (r + f == last && !lane_in_last) ? c_old : c;  // run past B16: not part of the chain
         if (COPY && copy_on) copy_stripe(r + f, buf[f][0]);
-        if ((f + 1) % G == 0) {
+        const uintptr_t sb = stripe_base<RUN>(g, r + uint32_t(f) + uint32_t(PF), junk) + uintptr_t(lane) * RUN;
 #pragma unroll
-          for (int q = f + 1 - G; q <= f; ++q) {
-            const uint32_t t = r + uint32_t(q) + uint32_t(PF);
-            const uintptr_t sb = (XF && t >= g.nstripes ? stripe_base<RUN>(*ng, 1u + uint32_t(q), junk)
-                                                         : stripe_base<RUN>(g, t, junk)) +
-                                 uintptr_t(lane) * RUN;
-#pragma unroll
-            for (int v = 0; v < kVec; ++v) buf[q][v] = ld128s<NT>(sb + 16u * v);
-          }
-        }
+        for (int v = 0; v < kVec; ++v) buf[f][v] = ld128s<NT>(sb + 16u * v);
       }
     }
-    // Remaining 0..PF-1 stripes are already in buf[0..].  XF: each slot then
-    // takes the next file's stripe -- after its last use here, or now if the
-    // main loop never ran (a slot past the end still holds `junk`; when the loop
-    // ran, its last pass refilled every slot past the end already).
-    const bool ran = r > 1u;
+    // Remaining 0..PF-1 stripes are already in buf[0..].
 #pragma unroll
-    for (int f = 0; f < PF; ++f) {
-      const bool use = f < PF - 1 && r + f < g.nstripes;  // at most PF - 1 stripes are left
-      if (use) {
+    for (int f = 0; f < PF - 1; ++f) {
+      if (r + f < g.nstripes) {
         const uint32_t c_old = c;
-        c = shift_stripe<S8>(T, c);
+        c = shift_stripe<LY>(T, c);
         if (f == 0) c ^= inj;
 #pragma unroll
         for (int v = 0; v < kVec; ++v) c = NOCRC ? c ^ buf[f][v].x : steps16(T, lb, c, buf[f][v]);
         c = (r + f == last && !lane_in_last) ? c_old : c;
         if (COPY && copy_on) copy_stripe(r + f, buf[f][0]);
       }
-      if (XF && (use || !ran)) {
-        const uintptr_t sb = stripe_base<RUN>(*ng, 1u + uint32_t(f), junk) + uintptr_t(lane) * RUN;
-#pragma unroll
-        for (int v = 0; v < kVec; ++v) buf[f][v] = ld128s<NT>(sb + 16u * v);
-      }
     }
-  } else if (XF) {  // one stripe: the ring (all junk) becomes the next file's
-    load_ring<RUN, PF, NT>(*ng, lane, buf, junk);
   }
   return c;
 }
 
 // Combine the lane chains into the file CRC and fold in the tail.
-template <int RUN, bool S8>
+template <int RUN, int LY>
 __device__ __forceinline__ uint32_t finish_file(const uint32_t* T, const LaneBase& lb, const FileGeo<RUN>& g,
                                                 const Head<RUN>& h, uint32_t c, int lane) {
   if (g.nstripes == 0) {  // tiny (< kMinParallelLen): the byte loop of func.cpp:429-433 in every lane
@@ -588,7 +552,7 @@ __device__ __forceinline__ uint32_t finish_file(const uint32_t* T, const LaneBas
   const uint32_t k = uint32_t(kWave - 1 - lane) - e_runs + (uint32_t(lane) < g.nvalid ? 0u : 64u);
 #pragma unroll
   for (int j = 0; j < kLevels; ++j) {
-    const uint32_t sh = shift_lds<S8>(T, LdsLayout<S8>::level_off + LdsLayout<S8>::stride * j, c);
+    const uint32_t sh = shift_lds<LdsLayout<LY>::level_s8>(T, LdsLayout<LY>::level_off + LdsLayout<LY>::stride * j, c);
     c = ((k >> j) & 1u) ? sh : c;
   }
 #pragma unroll
@@ -606,7 +570,7 @@ __device__ __forceinline__ uint32_t finish_file(const uint32_t* T, const LaneBas
 }
 
 // Single-file form (used by the block-verify kernel).
-template <int RUN, int PF, bool NT, bool S8>
+template <int RUN, int PF, bool NT, int LY>
 __device__ __forceinline__ uint32_t wave_crc(const uint32_t* T, const uint8_t* p, uint32_t len, uint32_t seed,
                                              int lane, uintptr_t junk) {
   const LaneBase lb = lane_base_of(lane);
@@ -614,16 +578,15 @@ __device__ __forceinline__ uint32_t wave_crc(const uint32_t* T, const uint8_t* p
   const Head<RUN> h = load_head<RUN>(g, lane);
   uint4 buf[PF][RUN / 16];
   load_ring<RUN, PF, NT>(g, lane, buf, junk);
-  const uint32_t c = g.nstripes ? lane_chain<RUN, PF, NT, S8>(T, lb, g, h, buf, lane, junk) : 0u;
-  return finish_file<RUN, S8>(T, lb, g, h, c, lane);
+  const uint32_t c = g.nstripes ? lane_chain<RUN, PF, NT, LY>(T, lb, g, h, buf, lane, junk) : 0u;
+  return finish_file<RUN, LY>(T, lb, g, h, c, lane);
 }
 
 constexpr int kRun = 16;  // product configuration (see DESIGN.md §4 for the sweep)
 constexpr int kPF = 5;
 constexpr bool kNT = true;
 constexpr bool kPAR = false;
-constexpr bool kDYN = true;
-constexpr bool kS8 = true;
+constexpr int kLY = 1;  // LDS table layout (LdsLayout): 32 slice-table copies, byte shift tables
 constexpr bool kIL = true;  // interleaved ticket groups (Tickets<IL>): +3 % Zipf, box-dependent +-3 % verify
 // Chunked tickets (FileCursor): 4 consecutive files per ticket, the last n/8 one
 // by one -- verify -2.8 to -3.8 %, Zipf -2.5 to -3.9 %, device block verify
@@ -643,9 +606,7 @@ constexpr int kTS = 3;
 // XCDs read one moving address window together; IL = false gives group g the
 // contiguous eighth [n*g/8, n*(g+1)/8) (eight windows 1/8 of the batch apart;
 // 2.5-3.7 % slower on Zipf, +-3 % box-dependent on uniform files; TFS_CRC_VARIANT=14).
-// W (measurement knob, IL only): W consecutive files per slot -- group g owns
-// files [8Wk + gW, 8Wk + gW + W) -- so fewer file-boundary lines are shared by two XCDs.
-template <bool IL = false, int W = 1>
+template <bool IL = false>
 struct Tickets {
   uint32_t* ctr;  // 8 zeroed counters for this launch, kSchedStride u32 apart (one per 256-byte line)
   uint32_t n, group;
@@ -661,16 +622,9 @@ struct Tickets {
   }
   __device__ __forceinline__ uint32_t gbegin(uint32_t g) const { return uint32_t((uint64_t(n) * g) >> 3); }
   __device__ __forceinline__ uint32_t gcount(uint32_t g) const {
-    if constexpr (IL && W > 1) {
-      const uint32_t rem = n % (8u * W), lo = g * W;
-      return (n / (8u * W)) * W + (rem > lo ? (rem - lo < uint32_t(W) ? rem - lo : uint32_t(W)) : 0u);
-    }
     return IL ? (n > g ? (n - g + 7u) >> 3 : 0u) : gbegin(g + 1) - gbegin(g);
   }
-  __device__ __forceinline__ uint32_t file_of(uint32_t g, uint32_t j) const {
-    if constexpr (IL && W > 1) return (j / W) * (8u * W) + g * W + j % W;
-    return IL ? j * 8u + g : gbegin(g) + j;
-  }
+  __device__ __forceinline__ uint32_t file_of(uint32_t g, uint32_t j) const { return IL ? j * 8u + g : gbegin(g) + j; }
   // Issue the atomic of the home group in lane 0; the result stays in lane 0's register.
   __device__ __forceinline__ uint32_t issue(int lane) {
     if (!dyn) {
@@ -716,9 +670,9 @@ struct Tickets {
 // out statically (wave w takes w, w+W, ...: one contiguous window, 16 consecutive
 // files per workgroup) and only the rest by single-file tickets, which even out the
 // waves' ends.
-template <bool IL, int W, int CF, int TS, int HS = 0>
+template <bool IL, int CF, int TS, int HS = 0>
 struct FileCursor {
-  Tickets<IL, W> tk;
+  Tickets<IL> tk;
   uint32_t n = 0, cf = 1, nA = 0, nt = 0, jv = 0, next = 0, end = 0;
   uint32_t hbase = 0, hnext = 0, hstride = 0;  // HS: the static phase covers files [0, hbase)
   bool done = false;
@@ -799,148 +753,92 @@ __device__ __forceinline__ void launch_exit(uint32_t* sched, uint32_t units, uin
 // `vseed`: 0 for files, TFS_PACKET_FLAG_V1 for packet bodies).
 // Files are software-pipelined per wave: the next file's stripe-0/tail words
 // and its first PF stripes are in flight while this file's lane chains are
-// combined, so HBM never waits on a file boundary.
-// BLK (measurement, with DYN = false): wave w takes the contiguous files
-// [w*per, (w+1)*per) instead of w, w+W, ... -- each CU's waves then walk a few
-// long sequential ranges (few address-translation misses) instead of files
-// spread over the whole moving window.
-// CF (measurement, with DYN): a ticket hands its wave CF consecutive files, so
-// each wave stays inside one address range for CF files (fewer translation
-// misses per CU) while all waves still read one moving window; the chunk
-// after this one is ticketed as soon as this one is taken.  TS > 0: the last
-// n >> TS files are ticketed one by one (chunks only while much work is left,
-// so a chunk of large files cannot become the launch's tail).
-template <int MODE, int RUN, int PF, bool NT, bool DYN, bool S8, int G = 1, bool HV = false, bool IL = false,
-          int W = 1, bool XF = false, bool BLK = false, int CF = 1, int TS = 0, int SPL = 0, int HS = 0>
+// combined, so HBM never waits on a file boundary.  Work goes by interleaved
+// dynamic tickets (Tickets, FileCursor): a ticket hands its wave CF consecutive
+// files (the product: kCF, the last n >> kTS files one by one, DESIGN §3.1;
+// measurement variant 50: one file per ticket).  With a split plan (SplitArgs)
+// the launch's units are its address-ordered SplitUnit list instead of desc.
+template <int MODE, int CF = kCF, int TS = kTS>
 __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __restrict__ base,
                                                            const Desc* __restrict__ desc, uint32_t n,
                                                            const Tables* __restrict__ tg, uint32_t* out_crc,
                                                            uint8_t* out_ok, uint32_t* n_bad, uint32_t* sched,
                                                            uint32_t vseed, uint32_t* done_flag, uint32_t seq,
                                                            SplitArgs sa) {
-  __shared__ uint32_t lds_tables[LdsLayout<S8>::bytes / 4];
-  load_tables<RUN, false, S8>(lds_tables, tg);
-  // Work units: the launch's files [0, nfiles), then the ext units of the split
-  // files (tfs_crc_device.h SplitArgs); a split file itself is skipped here.
+  constexpr int RUN = kRun, PF = kPF;
+  __shared__ uint32_t lds_tables[LdsLayout<kLY>::bytes / 4];
+  load_tables<RUN, false, kLY>(lds_tables, tg);
+  // Work units: the launch's files, or -- when the plan split some -- its unit
+  // list (whole files, heads and segments in address order).
   const uint32_t nfiles = n;
-  uint8_t* plan = nullptr;  // stays null when the plan split nothing: no per-file lookup
-  const SplitUnit* aou = nullptr;  // SPL 1: the address-ordered unit list (null: nothing split)
+  const SplitUnit* aou = nullptr;  // null: nothing split, the units are desc
   uint32_t* ucrc = nullptr;
   if (sa.plan) {
-    if constexpr (SPL == 1) {
-      const uint32_t* hdr = reinterpret_cast<const uint32_t*>(sa.plan);
-      if (hdr[1] == 0u) {
-        n = hdr[0];
-        aou = reinterpret_cast<const SplitUnit*>(sa.plan + ao_off_units(nfiles, sa.cap));
-        ucrc = reinterpret_cast<uint32_t*>(sa.plan + ao_off_ucrc(nfiles));
-      }
-    } else {
-      const unsigned long long used = *reinterpret_cast<const unsigned long long*>(sa.plan);
-      n = nfiles + uint32_t(used < sa.cap ? used : sa.cap);
-      if (used) plan = sa.plan;
+    const uint32_t* hdr = reinterpret_cast<const uint32_t*>(sa.plan);
+    if (hdr[1] == 0u) {
+      n = hdr[0];
+      aou = reinterpret_cast<const SplitUnit*>(sa.plan + ao_off_units(nfiles, sa.cap));
+      ucrc = reinterpret_cast<uint32_t*>(sa.plan + ao_off_ucrc(nfiles));
     }
   }
-  // kind: 0 a file, 1 an ext unit (a whole segment), 2 a split file's ragged head;
-  // fi: the file whose output a kind-0 unit writes
+  // kind: 0 a whole file, 1 a segment, 2 a split file's ragged head; fi: the file
+  // whose output a kind-0 unit writes
   auto unit = [&](uint32_t u, uint32_t& kind, uint32_t& fi) -> Desc {
     fi = u;
-    if constexpr (SPL == 1) {
-      kind = 0u;
-      if (!aou) return desc[u];
-      const SplitUnit U = aou[u];
-      kind = U.kind;
-      fi = U.file;
-      return Desc{U.offset, U.len, U.aux};
-    }
-    if (u >= nfiles) {
-      kind = 1u;
-      return reinterpret_cast<const Desc*>(plan + split_off_ext(nfiles, sa.cap))[u - nfiles];
-    }
-    Desc d = desc[u];
     kind = 0u;
-    if (plan && reinterpret_cast<const uint32_t*>(plan + split_off_base())[u] != kNoSplit) {
-      kind = 2u;
-      d.len -= ((d.len - 1u) / kSegBytes) * kSegBytes;
-    }
-    return d;
+    if (!aou) return desc[u];
+    const SplitUnit U = aou[u];
+    kind = U.kind;
+    fi = U.file;
+    return Desc{U.offset, U.len, U.aux};
   };
-  // ext units carry their own seed (a split file's seed on its head, 0 after)
+  // segments carry seed 0; a head keeps its file's seed (compute) or vseed (verify)
   auto seed_of = [&](const Desc& d, uint32_t kind) -> uint32_t { return (MODE == 0 || kind == 1u) ? d.aux : vseed; };
   const int lane = threadIdx.x & (kWave - 1);
   const LaneBase lb = lane_base_of(lane);
   const uint32_t wpb = kBlock / kWave;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const uint32_t stride = gridDim.x * wpb;
-  FileCursor<IL, W, CF, TS, HS> cur_files;  // HS (measurement, CF > 1): static chunks first (FileCursor)
-  Tickets<IL, W>& tk = cur_files.tk;
+  FileCursor<kIL, CF, TS> cur_files;
+  Tickets<kIL>& tk = cur_files.tk;
   cur_files.init(sched, n, blockIdx.x & 7u, stride, blockIdx.x * wpb + wave);
-  if (CF > 1 && DYN) cur_files.start(lane);
-  auto take = [&]() -> uint32_t { return cur_files.take(lane); };
+  if (CF > 1) cur_files.start(lane);
+  auto take = [&]() -> uint32_t { return CF > 1 ? cur_files.take(lane) : tk.resolve(tk.issue(lane), lane); };
   uint32_t bad = 0;
-  const uint32_t blk_per = (n + stride - 1u) / stride;
-  const uint32_t blk_end =
-      BLK ? uint32_t(min(uint64_t(n), (uint64_t(blockIdx.x) * wpb + wave + 1u) * uint64_t(blk_per))) : n;
   do {  // `break` = this wave has no (more) files; every wave reaches launch_exit
-  uint32_t f, fn;
-  if (DYN && CF > 1) {
-    f = take();
-    if (f >= n) break;
-    fn = take();
-  } else if (DYN) {
-    f = tk.resolve(tk.issue(lane), lane);
-    if (f >= n) break;
-    fn = tk.resolve(tk.issue(lane), lane);
-  } else if (BLK) {
-    const uint64_t f0 = (uint64_t(blockIdx.x) * wpb + wave) * uint64_t(blk_per);
-    if (f0 >= uint64_t(blk_end)) break;
-    f = uint32_t(f0);
-    fn = f + 1u < blk_end ? f + 1u : n;
-  } else {
-    f = blockIdx.x * wpb + wave;
-    if (f >= n) break;
-    fn = f + stride;
-  }
+  uint32_t f = take();
+  if (f >= n) break;
+  uint32_t fn = take();
   uint32_t kcur = 0, knxt = 0, ocur = 0, onxt = 0;
   Desc cur = unit(f, kcur, ocur);
   FileGeo<RUN> g = make_geo<RUN>(base + cur.offset, cur.len, seed_of(cur, kcur));
-  Head<RUN> h = load_head<RUN, HV>(g, lane);
+  Head<RUN> h = load_head<RUN>(g, lane);
   const uintptr_t junk = reinterpret_cast<uintptr_t>(tg->slice);
   uint4 buf[PF][RUN / 16];
-  load_ring<RUN, PF, NT>(g, lane, buf, junk);
+  load_ring<RUN, PF, kNT>(g, lane, buf, junk);
   Desc nxt = fn < n ? unit(fn, knxt, onxt) : Desc{0, 0, 0};
-  uint32_t jv = DYN && CF == 1 && fn < n ? tk.issue(lane) : 0u;  // ticket of the file after next, in flight
+  uint32_t jv = CF == 1 && fn < n ? tk.issue(lane) : 0u;  // ticket of the file after next, in flight
   for (;;) {
     const bool more = fn < n;
     const Desc ncur = nxt;
     const uint32_t kn = knxt, on = onxt;
-    // XF: the next file's geometry first -- this file's ring refills run into it.
-    FileGeo<RUN> ng = XF ? make_geo<RUN>(more ? base + ncur.offset : reinterpret_cast<const uint8_t*>(junk),
-                                         more ? ncur.len : 0u, seed_of(ncur, kn))
-                         : g;
-    const uint32_t c =
-        g.nstripes ? lane_chain<RUN, PF, NT, S8, false, G, false, 1, false, true, false, XF>(
-                         lds_tables, lb, g, h, buf, lane, junk, 0, false, &ng)
-                   : 0u;
+    const uint32_t c = g.nstripes ? lane_chain<RUN, PF, kNT, kLY>(lds_tables, lb, g, h, buf, lane, junk) : 0u;
     // Start the next file's loads before combining this one.
+    FileGeo<RUN> ng = g;
     Head<RUN> nh = h;
     uint32_t fnn = n;
     if (more) {
-      if (!XF) ng = make_geo<RUN>(base + ncur.offset, ncur.len, seed_of(ncur, kn));
-      nh = load_head<RUN, HV>(ng, lane);
-      if (!XF || !g.nstripes) load_ring<RUN, PF, NT>(ng, lane, buf, junk);
-      fnn = DYN ? (CF > 1 ? take() : tk.resolve(jv, lane))
-                : (BLK ? (fn + 1u < blk_end ? fn + 1u : n) : fn + stride);
+      ng = make_geo<RUN>(base + ncur.offset, ncur.len, seed_of(ncur, kn));
+      nh = load_head<RUN>(ng, lane);
+      load_ring<RUN, PF, kNT>(ng, lane, buf, junk);
+      fnn = CF > 1 ? cur_files.take(lane) : tk.resolve(jv, lane);
       if (fnn < n) nxt = unit(fnn, knxt, onxt);
-      if (DYN && CF == 1 && fnn < n) jv = tk.issue(lane);
+      if (CF == 1 && fnn < n) jv = tk.issue(lane);
     }
-    const uint32_t crc = finish_file<RUN, S8>(lds_tables, lb, g, h, c, lane);
+    const uint32_t crc = finish_file<RUN, kLY>(lds_tables, lb, g, h, c, lane);
     if (lane == 0) {
-      if (SPL == 1 && kcur != 0u) {
+      if (kcur != 0u) {
         ucrc[f] = crc;  // a head or a segment: the fold joins them
-      } else if (kcur == 1u) {
-        reinterpret_cast<uint32_t*>(plan + split_off_ext_crc(nfiles))[f - nfiles] = crc;
-      } else if (kcur == 2u) {
-        reinterpret_cast<uint32_t*>(plan + split_off_head(nfiles))[f] = crc;
       } else {
         if (out_crc) out_crc[ocur] = crc;
         if (MODE == 1) {
@@ -964,94 +862,6 @@ __global__ void __launch_bounds__(kBlock) crc_files_kernel(const uint8_t* __rest
   if (lane == 0) launch_exit(sched, gridDim.x * wpb, done_flag, seq);
 }
 
-// Split plan (tfs_crc_device.h SplitArgs): one thread per file.  A file longer
-// than kSplitMin keeps its ragged head (len - K*kSegBytes bytes, K = (len-1) /
-// kSegBytes, with its seed) as its own unit and gets K ext units for its whole
-// segments, reserved as one range per workgroup (one atomic per 256 files).  A
-// workgroup whose range would pass `cap` leaves its files whole (and writes
-// empty units into the part of its range below cap, so every unit the main
-// kernel takes is valid).
-#ifdef TFS_CRC_MEASURE
-template <int MODE>
-__global__ void __launch_bounds__(256) split_plan_kernel(const Desc* __restrict__ desc, uint32_t n, uint32_t vseed,
-                                                         SplitArgs sa) {
-  (void)vseed;  // the head keeps the file's seed: the main kernel checksums it in place
-  __shared__ uint32_t wsum[4];
-  __shared__ unsigned long long blk_base;
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  const int lane = threadIdx.x & (kWave - 1);
-  const uint32_t w = threadIdx.x / kWave;
-  Desc d{0, 0, 0};
-  if (i < n) d = desc[i];
-  const uint32_t K = (i < n && d.len > kSplitMin) ? (d.len - 1u) / kSegBytes : 0u;  // whole segments after the head
-  uint32_t x = K;  // inclusive scan over the wave
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o, kWave);
-    if (lane >= o) x += y;
-  }
-  if (lane == kWave - 1) wsum[w] = x;
-  __syncthreads();
-  uint32_t before = 0, total = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < 4; ++k) {
-    before += k < w ? wsum[k] : 0u;
-    total += wsum[k];
-  }
-  if (threadIdx.x == 0)
-    blk_base = total ? atomicAdd(reinterpret_cast<unsigned long long*>(sa.plan), (unsigned long long)total) : 0ull;
-  __syncthreads();
-  const unsigned long long b0 = blk_base;
-  const bool fits = b0 + total <= sa.cap;
-  const unsigned long long my = b0 + before + (x - K);
-  if (i < n) reinterpret_cast<uint32_t*>(sa.plan + split_off_base())[i] = (K && fits) ? uint32_t(my) : kNoSplit;
-  if (!K) return;
-  Desc* ext = reinterpret_cast<Desc*>(sa.plan + split_off_ext(n, sa.cap));
-  if (fits) {
-    const uint32_t head = d.len - K * kSegBytes;  // checksummed in the file's own place by the main kernel
-    for (uint32_t j = 0; j < K; ++j) ext[my + j] = Desc{d.offset + head + uint64_t(j) * kSegBytes, kSegBytes, 0u};
-  } else {
-    for (unsigned long long u = my; u < my + K && u < sa.cap; ++u) ext[u] = Desc{0, 0, 0};
-  }
-}
-
-// Split fold: each split file's CRC from its units' CRCs (seed-0 linearity,
-// crc(A||B) = shift(crc(A), |B|) ^ crc(B); the head carries the seed), then its
-// output and verdict as the main kernel writes them for whole files.
-template <int MODE>
-__global__ void __launch_bounds__(256) split_fold_kernel(const Desc* __restrict__ desc, uint32_t n,
-                                                         const Tables* __restrict__ tg, SplitArgs sa,
-                                                         uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad) {
-  __shared__ uint32_t T[uint32_t(kShiftChunks) * 32u];
-  if (*reinterpret_cast<const unsigned long long*>(sa.plan) == 0ull) return;  // nothing was split
-  const uint32_t* base = reinterpret_cast<const uint32_t*>(sa.plan + split_off_base());
-  const uint32_t* head_crc = reinterpret_cast<const uint32_t*>(sa.plan + split_off_head(n));
-  const uint32_t* ext_crc = reinterpret_cast<const uint32_t*>(sa.plan + split_off_ext_crc(n));
-  for (uint32_t k = threadIdx.x; k < uint32_t(kShiftChunks) * 32u; k += blockDim.x) T[k] = (&tg->seg_shift[0][0])[k];
-  __syncthreads();
-  uint32_t bad = 0;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint32_t b = base[i];
-    if (b == kNoSplit) continue;
-    const Desc d = desc[i];
-    const uint32_t K = (d.len - 1u) / kSegBytes;
-    uint32_t c = head_crc[i];
-    for (uint32_t j = 0; j < K; ++j) c = shift5(T, 0u, c) ^ ext_crc[b + j];
-    if (out_crc) out_crc[i] = c;
-    if (MODE == 1) {
-      const bool ok = c == d.aux;
-      if (out_ok) out_ok[i] = ok ? 1 : 0;
-      bad += ok ? 0u : 1u;
-    }
-  }
-  if (MODE == 1 && n_bad) {  // one atomic per wave
-#pragma unroll
-    for (int m = kWave / 2; m >= 1; m >>= 1) bad += __shfl_xor(bad, m, kWave);
-    if ((threadIdx.x & (kWave - 1)) == 0 && bad) atomicAdd(n_bad, bad);
-  }
-}
-#endif  // TFS_CRC_MEASURE
-
 // Address-ordered split plan (SplitUnit list, tfs_crc_device.h), step 1 of 3: the
 // number of whole segments of each block of kAoBlock files.
 __device__ __forceinline__ uint32_t ao_segments(const Desc& d) {
@@ -1074,15 +884,21 @@ __global__ void __launch_bounds__(kAoBlock) split_ao_count_kernel(const Desc* __
   }
 }
 
-// Step 2 (one workgroup): exclusive scan of the block counts in place; the
-// header gets the launch's unit count, or `nosplit` when nothing was split or the
-// segments would pass the plan's capacity (every file then stays whole).
-__global__ void __launch_bounds__(1024) split_ao_scan_kernel(uint32_t n, SplitArgs sa) {
+// Step 2 (one workgroup): exclusive scan of the block counts in place, and the
+// cut: when the segments of all files would pass the plan's room (cap - n ext
+// units), only the longest prefix of files whose segments fit is split (ADVICE
+// r4: one workgroup of the scan reads the 256 descriptors of the block the cut
+// falls in); the files from the cut on stay whole.  Header {units, nosplit,
+// ext, cut}: units = n + ext, ext = the segments of the files before `cut`.
+__global__ void __launch_bounds__(1024) split_ao_scan_kernel(const Desc* __restrict__ desc, uint32_t n, SplitArgs sa) {
   __shared__ uint32_t part[1024];
+  __shared__ uint32_t cut_blk, wsum[kAoBlock / kWave];
   uint32_t* blk = reinterpret_cast<uint32_t*>(sa.plan + ao_off_blk());
   const uint32_t nb = ao_nblk(n);
   const uint32_t per = (nb + 1023u) / 1024u;
   const uint32_t b0 = threadIdx.x * per, b1 = min(b0 + per, nb);
+  const uint64_t room = sa.cap > n ? uint64_t(sa.cap - n) : 0u;
+  if (threadIdx.x == 0) cut_blk = nb;
   uint32_t t = 0;
   for (uint32_t b = b0; b < b1; ++b) t += blk[b];
   part[threadIdx.x] = t;
@@ -1097,30 +913,65 @@ __global__ void __launch_bounds__(1024) split_ao_scan_kernel(uint32_t n, SplitAr
   for (uint32_t b = b0; b < b1; ++b) {
     const uint32_t v = blk[b];
     blk[b] = run;
+    if (uint64_t(run) + v > room) atomicMin(&cut_blk, b);  // the first block that does not fit
     run += v;
   }
+  __syncthreads();
+  const uint32_t cb = cut_blk;
+  uint32_t ext = part[1023], cut = n;
+  if (cb < nb) {  // split the files of block cb up to the last one whose segments still fit
+    const uint32_t base = blk[cb];
+    const uint32_t i = cb * kAoBlock + threadIdx.x;
+    const int lane = threadIdx.x & (kWave - 1);
+    uint32_t K = threadIdx.x < kAoBlock && i < n ? ao_segments(desc[i]) : 0u;
+    uint32_t x = K;  // inclusive scan over the wave, then over the block's waves
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, kWave);
+      if (lane >= o) x += y;
+    }
+    if (threadIdx.x < kAoBlock && lane == kWave - 1) wsum[threadIdx.x / kWave] = x;
+    __syncthreads();
+    if (threadIdx.x < kAoBlock)
+      for (uint32_t w = 0; w < threadIdx.x / kWave; ++w) x += wsum[w];
+    const bool fits = threadIdx.x < kAoBlock && i < n && uint64_t(base) + x <= room;
+    part[threadIdx.x] = fits ? 1u : 0u;  // the fitting files are a prefix of the block
+    __syncthreads();
+    if (fits && (threadIdx.x + 1u == kAoBlock || !part[threadIdx.x + 1u])) {  // the last fitting file
+      part[1023] = base + x;
+      part[1022] = i + 1u;
+    }
+    if (threadIdx.x == 0 && !fits) {  // not even the block's first file fits
+      part[1023] = base;
+      part[1022] = i;
+    }
+    __syncthreads();
+    ext = part[1023];
+    cut = part[1022];
+  }
   if (threadIdx.x == 1023u) {
-    const uint64_t ext = part[1023];
     uint32_t* hdr = reinterpret_cast<uint32_t*>(sa.plan);
-    const bool fits = ext > 0u && uint64_t(n) + ext <= uint64_t(sa.cap);
-    hdr[0] = fits ? uint32_t(n + ext) : n;
-    hdr[1] = fits ? 0u : 1u;
-    hdr[2] = uint32_t(ext);
+    hdr[0] = n + ext;
+    hdr[1] = ext ? 0u : 1u;
+    hdr[2] = ext;
+    hdr[3] = ext ? cut : 0u;
   }
 }
 
-// Step 3: every file's units at its place in address order: file i starts at
-// unit i + (segments of the files before it).
+// Step 3: every file's units at its place in address order: file i < cut starts
+// at unit i + (segments of the files before it), file i >= cut (whole) at i + ext.
 __global__ void __launch_bounds__(kAoBlock) split_ao_write_kernel(const Desc* __restrict__ desc, uint32_t n,
                                                                   SplitArgs sa) {
   __shared__ uint32_t wsum[kAoBlock / kWave];
-  if (reinterpret_cast<const uint32_t*>(sa.plan)[1] != 0u) return;  // nothing split: the kernel reads desc
+  const uint32_t* hdr = reinterpret_cast<const uint32_t*>(sa.plan);
+  if (hdr[1] != 0u) return;  // nothing split: the kernel reads desc
+  const uint32_t ext = hdr[2], cut = hdr[3];
   const uint32_t i = blockIdx.x * kAoBlock + threadIdx.x;
   const int lane = threadIdx.x & (kWave - 1);
   const uint32_t w = threadIdx.x / kWave;
   Desc d{0, 0, 0};
   if (i < n) d = desc[i];
-  const uint32_t K = i < n ? ao_segments(d) : 0u;
+  const uint32_t K = i < cut ? ao_segments(d) : 0u;
   uint32_t x = K;  // inclusive scan over the wave
 #pragma unroll
   for (int o = 1; o < kWave; o <<= 1) {
@@ -1132,7 +983,7 @@ __global__ void __launch_bounds__(kAoBlock) split_ao_write_kernel(const Desc* __
   if (i >= n) return;
   uint32_t before = reinterpret_cast<const uint32_t*>(sa.plan + ao_off_blk())[blockIdx.x] + (x - K);
   for (uint32_t k = 0; k < w; ++k) before += wsum[k];
-  const uint32_t base = i + before;
+  const uint32_t base = i + (i < cut ? before : ext);
   reinterpret_cast<uint32_t*>(sa.plan + ao_off_ubase(n))[i] = base;
   SplitUnit* U = reinterpret_cast<SplitUnit*>(sa.plan + ao_off_units(n, sa.cap));
   const uint32_t head = d.len - K * kSegBytes;
@@ -1151,10 +1002,11 @@ __global__ void __launch_bounds__(256) split_ao_fold_kernel(const Desc* __restri
   if (reinterpret_cast<const uint32_t*>(sa.plan)[1] != 0u) return;  // nothing was split
   const uint32_t* ubase = reinterpret_cast<const uint32_t*>(sa.plan + ao_off_ubase(n));
   const uint32_t* ucrc = reinterpret_cast<const uint32_t*>(sa.plan + ao_off_ucrc(n));
+  const uint32_t cut = reinterpret_cast<const uint32_t*>(sa.plan)[3];  // files from here on stayed whole
   for (uint32_t k = threadIdx.x; k < uint32_t(kShiftChunks) * 32u; k += blockDim.x) T[k] = (&tg->seg_shift[0][0])[k];
   __syncthreads();
   uint32_t bad = 0;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cut; i += gridDim.x * blockDim.x) {
     const Desc d = desc[i];
     const uint32_t K = ao_segments(d);
     if (K == 0u) continue;
@@ -1473,50 +1325,6 @@ __device__ __forceinline__ HdrFields read_hdr(const uint8_t* rec) {
   return h;
 }
 
-#ifdef TFS_CRC_MEASURE
-// ---------------------------------------------------------------------------
-// Measurement build only (libtfs_crc_measure.so, -DTFS_CRC_MEASURE): earlier
-// kernel forms kept as A/B baselines (TFS_CRC_VARIANT 7, 22, 24).  The product
-// library does not contain them and ignores TFS_CRC_VARIANT.
-// ---------------------------------------------------------------------------
-// Verify files stored in a block image (FileInfo header + payload per RawMeta):
-// the checks of sync_backup.cpp:345-435 / block_console.cpp:543-577.
-__global__ void __launch_bounds__(kBlock) block_verify_kernel(const uint8_t* __restrict__ image, uint64_t image_len,
-                                                              const RawMeta* __restrict__ metas, uint32_t n,
-                                                              const Tables* __restrict__ tg, uint32_t* out_crc,
-                                                              int32_t* out_status, uint32_t* n_bad) {
-  __shared__ uint32_t lds_tables[LdsLayout<kS8>::bytes / 4];
-  load_tables<kRun, kPAR, kS8>(lds_tables, tg);
-  const int lane = threadIdx.x & (kWave - 1);
-  const uint32_t wpb = kBlock / kWave;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  uint32_t bad = 0;
-  for (uint32_t f = blockIdx.x * wpb + wave; f < n; f += gridDim.x * wpb) {
-    const RawMeta m = metas[f];
-    int32_t status = kSuccess;
-    uint32_t c = 0;
-    if (m.size <= kFileInfoSize) {
-      status = kExitReadFileSizeError;
-    } else if (m.offset < 0 || uint64_t(m.offset) + uint64_t(m.size) > image_len) {
-      status = kExitParameterError;
-    } else {
-      const uint8_t* rec = image + m.offset;
-      const HdrFields h = read_hdr(rec);
-      c = wave_crc<kRun, kPF, kNT, kS8>(lds_tables, rec + kFileInfoSize, uint32_t(m.size - kFileInfoSize), 0u, lane,
-                                        reinterpret_cast<uintptr_t>(tg->slice));
-      if (h.id != m.file_id) status = kExitFileInfoError;
-      else if (h.size != m.size) status = kExitSyncFileError;
-      else if (c != h.crc) status = kExitCheckCrcError;
-    }
-    if (lane == 0) {
-      if (out_crc) out_crc[f] = c;
-      if (out_status) out_status[f] = status;
-      bad += status != kSuccess ? 1u : 0u;
-    }
-  }
-  if (lane == 0 && bad && n_bad) atomicAdd(n_bad, bad);
-}
-#endif  // TFS_CRC_MEASURE
 
 // ---------------------------------------------------------------------------
 // Packet CRC (BasePacket, src/common/base_packet.cpp).  A wire frame is the
@@ -1632,54 +1440,6 @@ __global__ void packet_finish_kernel(uint8_t* __restrict__ base, const PacketDes
 }
 
 #ifdef TFS_CRC_MEASURE
-// Compaction repack (task.cpp:753-798): copy each live record (FileInfo|payload)
-// to its new offset and rewrite offset_/size_/usize_/flag_.  One wave per record.
-// (Measurement build: the unfused A/B baseline, TFS_CRC_VARIANT=7.)
-__global__ void __launch_bounds__(kBlock) compact_copy_kernel(const uint8_t* __restrict__ src,
-                                                              const RawMeta* __restrict__ metas,
-                                                              const int32_t* __restrict__ flags,
-                                                              const int64_t* __restrict__ dest_off, uint32_t n,
-                                                              uint8_t* __restrict__ dst) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const uint32_t wpb = kBlock / kWave;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  for (uint32_t f = blockIdx.x * wpb + wave; f < n; f += gridDim.x * wpb) {
-    const int64_t doff = dest_off[f];
-    if (doff < 0) continue;
-    const RawMeta m = metas[f];
-    const uint8_t* s = src + m.offset;
-    uint8_t* d = dst + doff;
-    // Header: FileInfo with offset_(8) size_(12) usize_(16) flag_(28) rewritten,
-    // id_, times and crc_ copied (task.cpp:753-759).  Lanes 0..35 write one byte each.
-    if (lane < kFileInfoSize) {
-      uint8_t b = s[lane];
-      const int fld = lane >> 2, sh = 8 * (lane & 3);
-      if (fld == 2) b = uint8_t(uint32_t(int32_t(doff)) >> sh);
-      else if (fld == 3 || fld == 4) b = uint8_t(uint32_t(m.size) >> sh);
-      else if (fld == 7) b = uint8_t(uint32_t(flags[f]) >> sh);
-      d[lane] = b;
-    }
-    // Payload.
-    const uint8_t* sp = s + kFileInfoSize;
-    uint8_t* dp = d + kFileInfoSize;
-    const uint32_t size = uint32_t(m.size - kFileInfoSize);
-    const uintptr_t sa = reinterpret_cast<uintptr_t>(sp), da = reinterpret_cast<uintptr_t>(dp);
-    if (((sa ^ da) & 3u) == 0) {
-      // Same alignment mod 4: byte head, dword body, byte tail.
-      uint32_t head = uint32_t((4u - (da & 3u)) & 3u);
-      if (head > size) head = size;
-      for (uint32_t i = lane; i < head; i += kWave) dp[i] = sp[i];
-      const uint32_t nw = (size - head) / 4;
-      const uint32_t* s4 = reinterpret_cast<const uint32_t*>(sp + head);
-      uint32_t* d4 = reinterpret_cast<uint32_t*>(dp + head);
-      for (uint32_t i = lane; i < nw; i += kWave) d4[i] = s4[i];
-      for (uint32_t i = head + nw * 4 + lane; i < size; i += kWave) dp[i] = sp[i];
-    } else {
-      for (uint32_t i = lane; i < size; i += kWave) dp[i] = sp[i];
-    }
-  }
-}
-
 // Calibration (variants 65/66, measurement only): the record list of a device
 // compaction copied by the chunk copy's loop -- per job, bursts of 8 stripes of
 // 1 KiB (16 B per lane, nt loads and stores) over the 16-aligned body, the ragged
@@ -1730,102 +1490,6 @@ __global__ void __launch_bounds__(kBlock) compact_probe_copy_kernel(const uint8_
   if (lane == 0) launch_exit(sched, gridDim.x * wpb, nullptr, 0u);
 }
 
-// Fused compaction: one read of each live record computes its
-// payload CRC (the re-CRC verify) and, from the same registers, writes the
-// record to its new offset with offset_/size_/usize_/flag_ rewritten
-// (task.cpp:753-798).  Checks and statuses as block_verify_kernel.  Records
-// whose new offset is not congruent mod 4 with the old one take a byte copy
-// after the CRC (a second read of that record only).
-// WIDE: per-record CompactJob (64-bit offsets, many blocks per launch); else the
-// single-block form (RawMeta + flags + int64 dest offsets).
-template <bool WIDE>
-__global__ void __launch_bounds__(kBlock) compact_fused_kernel(const uint8_t* __restrict__ src, uint64_t src_len,
-                                                               const RawMeta* __restrict__ metas,
-                                                               const int32_t* __restrict__ flags,
-                                                               const int64_t* __restrict__ dest_off,
-                                                               const CompactJob* __restrict__ jobs, uint32_t n,
-                                                               uint8_t* __restrict__ dst, const Tables* __restrict__ tg,
-                                                               uint32_t* out_crc, int32_t* out_status,
-                                                               uint32_t* n_bad) {
-  __shared__ uint32_t lds_tables[LdsLayout<kS8>::bytes / 4];
-  load_tables<kRun, kPAR, kS8>(lds_tables, tg);
-  const int lane = threadIdx.x & (kWave - 1);
-  const LaneBase lb = lane_base_of(lane);
-  const uint32_t wpb = kBlock / kWave;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const uintptr_t junk = reinterpret_cast<uintptr_t>(tg->slice);
-  uint32_t bad = 0;
-  for (uint32_t f = blockIdx.x * wpb + wave; f < n; f += gridDim.x * wpb) {
-    uint64_t soff, doff, fid;
-    int32_t size, flag, new_off;
-    bool range_ok;
-    if (WIDE) {
-      const CompactJob j = jobs[f];
-      soff = j.src_offset, doff = j.dest_offset, fid = j.file_id;
-      size = j.size, flag = j.flag, new_off = j.new_offset;
-      range_ok = soff + uint64_t(size) <= src_len;
-    } else {
-      const RawMeta m = metas[f];
-      const int64_t d = dest_off[f];
-      soff = uint64_t(int64_t(m.offset)), doff = uint64_t(d), fid = m.file_id;
-      size = m.size, flag = flags[f], new_off = int32_t(d);
-      range_ok = m.offset >= 0 && d >= 0 && uint64_t(m.offset) + uint64_t(m.size) <= src_len;
-    }
-    int32_t status = kSuccess;
-    uint32_t c = 0;
-    if (size <= kFileInfoSize) {
-      status = kExitReadFileSizeError;
-    } else if (!range_ok) {
-      status = kExitParameterError;
-    } else {
-      const uint8_t* rec = src + soff;
-      uint8_t* drec = dst + doff;
-      const HdrFields hd = read_hdr(rec);
-      // header: FileInfo with offset_(8) size_(12) usize_(16) flag_(28) rewritten
-      if (lane < kFileInfoSize) {
-        uint8_t b = rec[lane];
-        const int fld = lane >> 2, sh = 8 * (lane & 3);
-        if (fld == 2) b = uint8_t(uint32_t(new_off) >> sh);
-        else if (fld == 3 || fld == 4) b = uint8_t(uint32_t(size) >> sh);
-        else if (fld == 7) b = uint8_t(uint32_t(flag) >> sh);
-        drec[lane] = b;
-      }
-      const uint8_t* p = rec + kFileInfoSize;
-      const uint32_t len = uint32_t(size - kFileInfoSize);
-      const intptr_t delta = intptr_t(drec) - intptr_t(rec);
-      const FileGeo<kRun> g = make_geo<kRun>(p, len, 0u);
-      const Head<kRun> h = load_head<kRun>(g, lane);
-      uint4 buf[kPF][kRun / 16];
-      load_ring<kRun, kPF, kNT>(g, lane, buf, junk);
-      const bool fused = (delta & 3) == 0;
-      c = g.nstripes ? lane_chain<kRun, kPF, kNT, kS8, true>(lds_tables, lb, g, h, buf, lane, junk, delta, fused)
-                     : 0u;
-      if (fused && g.nstripes) {
-        // tail [B16, end): dwords then bytes, from lane 0's registers
-        if (lane == 0) {
-          const uint32_t ntw = uint32_t((g.end & ~uintptr_t(3)) - g.B16) / 4u;
-          for (uint32_t i = 0; i < 3u; ++i)
-            if (i < ntw) st32(g.B16 + 4u * i + delta, h.tw[i]);
-          const uintptr_t B = g.end & ~uintptr_t(3);
-          for (uint32_t i = 0; i < 3u; ++i)
-            if (B + i < g.end) *reinterpret_cast<uint8_t*>(B + i + delta) = uint8_t(h.tb[i]);
-        }
-      } else {  // tiny file, or a destination not congruent mod 4: byte copy
-        for (uint32_t i = lane; i < len; i += kWave) drec[kFileInfoSize + i] = p[i];
-      }
-      c = finish_file<kRun, kS8>(lds_tables, lb, g, h, c, lane);
-      if (hd.id != fid) status = kExitFileInfoError;
-      else if (hd.size != size) status = kExitSyncFileError;
-      else if (c != hd.crc) status = kExitCheckCrcError;
-    }
-    if (lane == 0) {
-      if (out_crc) out_crc[f] = c;
-      if (out_status) out_status[f] = status;
-      bad += status != kSuccess ? 1u : 0u;
-    }
-  }
-  if (lane == 0 && bad && n_bad) atomicAdd(n_bad, bad);
-}
 #endif  // TFS_CRC_MEASURE
 
 // ---------------------------------------------------------------------------
@@ -1938,15 +1602,14 @@ __device__ __forceinline__ FileGeo<kRun> crec_geo(const CRec& r, const uint8_t* 
   return make_geo<kRun>(rec + kFileInfoSize, r.plen, 0u, aoff);
 }
 
-// HV (measurement): stripe 0 and the tail as one dwordx4 per lane each (load_head).
-template <bool DA, bool HV = false>
+template <bool DA>
 __device__ __forceinline__ CState issue_crec(const CRec& r, const uint8_t* src, uint64_t src_len, uint8_t* dst,
                                              int lane, uintptr_t junk) {
   CState s;
   s.g = crec_geo<DA>(r, src, src_len, dst, junk, s.delta);
   if (r.pre == kSuccess) {
     s.hb = lane < kFileInfoSize && r.kind != 1u ? uint32_t(src[r.soff + uint32_t(lane)]) : 0u;
-    s.h = load_head<kRun, HV>(s.g, lane);
+    s.h = load_head<kRun>(s.g, lane);
   } else {
     s.hb = 0u;
     s.h = Head<kRun>{};
@@ -1998,52 +1661,31 @@ __device__ __forceinline__ void copy_unaligned(const uint8_t* s, uint8_t* d, uin
 // temporal payload loads (with the destination-anchored grid a source line is
 // split between two stripes of the same wave; a temporal load keeps it in L2
 // for the second).  The product is both (kCompactDiag).  Measurement only: bit
-// 0 plain copy-through stores (variant 25), bit 1 no payload CRC steps (variant
-// 26, wrong CRCs and statuses); variant 27 = DIAG 0 (source-anchored grid,
-// non-temporal loads: the round-2 baseline), 29 = the anchored grid with
-// non-temporal loads, 30 = the product without the stripe-0, FileInfo and tail
-// stores (DIAG bit 4; wrong output), 31 = byte-shifted records copied after the
-// CRC by copy_unaligned instead of through the chain (DIAG bit 5), 32 = byte-
-// shifted records stored as each lane's 16 bytes at their byte address instead
-// of line-aligned alignbyte chunks (DIAG bit 6), 36 = sc1 copy-through stores
-// (DIAG bit 7), 60/61 = static record assignment r -> wave r mod W (DIAG bit 8),
-// with / without the payload CRC steps, 62-64 = the ring refilled in bursts of
-// CPF stripes (DIAG bit 9: CPF loads out together after CPF stripes are used,
-// as the chunk copy does; 64 also skips the CRC steps and the header/tail
-// stores).  CPF: stripes in flight per wave
-// (variants 33-35, 37: 6, 7, 8, 4).  Round 4, measurement: DIAG bit 10 the
-// cross-record ring (lane_chain XF: a ring slot freed past this record's last
-// stripe takes the next record's stripe, so the wave's loads stay in HBM across
-// the record boundary; variant 81), bit 11 stripe 0 and the tail loaded as one
-// dwordx4 per lane (load_head HV; 82), both (83); bit 12 no per-record combine
-// (finish_file skipped: wrong CRCs and statuses, timing only; 84, and 85 on the
-// copy-only form 64).
+// 1 no payload CRC steps (variant 26: wrong CRCs and statuses; the kernel's own
+// load/store schedule without the table lookups).
 constexpr int kCompactDiag = 4 | 8;
 // Record order of long device-compaction launches (FileCursor HS, round 4): the first
 // 3/4 of the records go statically (wave w: w, w+W, ...), the rest by tickets.  Against
 // one record per ticket, in one process on five boxes: -1.7, -1.7, 0.0, -1.8, -1.7 %
-// (measurement variant 88 before it became the product).
+// (DESIGN.md §4.1).
 constexpr int kCompactHS = 2;
-template <bool WIDE, bool DPPSH = true, bool VERIFY = false, int DIAG = kCompactDiag, int CPF = kPF, int CF = 1,
-          int TS = 0, bool SEG = false, int WW = 1, int HS = 0>
-__global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __restrict__ src, uint64_t src_len,
-                                                              const RawMeta* __restrict__ metas,
-                                                              const int32_t* __restrict__ flags,
-                                                              const int64_t* __restrict__ dest_off,
-                                                              const CompactJob* __restrict__ jobs, uint32_t n,
-                                                              uint8_t* __restrict__ dst, const Tables* __restrict__ tg,
-                                                              uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
-                                                              uint32_t* sched, CSegArgs cs) {
+// NW waves per workgroup, OCC workgroups per CU (LDS table layout LY must fit OCC
+// times in 160 KiB): the product is 16 waves, one workgroup, layout 1.
+template <bool WIDE, bool VERIFY = false, int DIAG = kCompactDiag, int CPF = kPF, int CF = 1, int TS = 0,
+          bool SEG = false, int HS = 0, int NW = kBlock / kWave, int OCC = 1, int LY = kLY>
+__global__ void __launch_bounds__(NW * kWave, OCC * NW / 4) compact_pipe_kernel(
+    const uint8_t* __restrict__ src, uint64_t src_len, const RawMeta* __restrict__ metas,
+    const int32_t* __restrict__ flags, const int64_t* __restrict__ dest_off, const CompactJob* __restrict__ jobs,
+    uint32_t n, uint8_t* __restrict__ dst, const Tables* __restrict__ tg, uint32_t* out_crc, int32_t* out_status,
+    uint32_t* n_bad, uint32_t* sched, CSegArgs cs) {
   constexpr bool DA = !VERIFY && (DIAG & 4) != 0;
   constexpr bool LNT = (DIAG & 8) && !VERIFY ? false : kNT;  // the verify form keeps the headline's loads
-  constexpr int SK = (DIAG & 1) ? 0 : ((DIAG & 128) ? 2 : 1);  // copy-through store kind (st128_kind)
-  constexpr bool XF = (DIAG & 1024) != 0 && !(DIAG & 512);
-  constexpr bool HV = (DIAG & 2048) != 0;
-  __shared__ uint32_t lds_tables[LdsLayout<kS8>::bytes / 4];
-  load_tables<kRun, kPAR, kS8>(lds_tables, tg);
+  static_assert(OCC * LdsLayout<LY>::bytes <= 160u * 1024u, "OCC workgroups per CU must fit the LDS");
+  __shared__ uint32_t lds_tables[LdsLayout<LY>::bytes / 4];
+  load_tables<kRun, kPAR, LY>(lds_tables, tg);
   const int lane = threadIdx.x & (kWave - 1);
-  const LaneBase lb = lane_base_of(lane);
-  const uint32_t wpb = kBlock / kWave;
+  const LaneBase lb = lane_base_for<LY>(lane);
+  const uint32_t wpb = NW;
   const uintptr_t junk = reinterpret_cast<uintptr_t>(tg->slice);
   // SEG: units are the jobs, then the ext segments of the split records (CSegArgs)
   const uint32_t njobs = n;
@@ -2057,14 +1699,12 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
     if constexpr (SEG) return load_cunit(u, njobs, src_len, jobs, plan, cs.cap, cs.lg);
     return load_crec<WIDE, VERIFY>(u, src_len, metas, flags, dest_off, jobs);
   };
-  // CF > 1: chunks of CF records per ticket; WW > 1: WW consecutive records per
-  // ticket-group slot, so an XCD's waves walk WW-record runs (measurement)
-  FileCursor<kIL, WW, CF, TS, HS> fc;
+  // CF > 1: chunks of CF records per ticket; HS: the static phase first
+  FileCursor<kIL, CF, TS, HS> fc;
   constexpr bool FC = CF > 1 || HS > 0;  // files come from the cursor (chunks / the static phase)
   auto& tk = fc.tk;
   fc.init(sched, n, blockIdx.x & 7u, gridDim.x * wpb,
           blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave));
-  if (DIAG & 256) tk.dyn = false;  // measurement: static record r -> wave r mod W (the chunk copy's order)
   if (FC) fc.start(lane);
   uint32_t bad = 0;
   do {
@@ -2072,31 +1712,23 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
     if (f >= n) break;
     uint32_t fn = FC ? fc.take(lane) : tk.resolve(tk.issue(lane), lane);
     CRec cur = unit(f);
-    CState st = issue_crec<DA, HV>(cur, src, src_len, dst, lane, junk);
+    CState st = issue_crec<DA>(cur, src, src_len, dst, lane, junk);
     uint4 buf[CPF][kRun / 16];
     load_ring<kRun, CPF, LNT>(st.g, lane, buf, junk);
     CRec nxt = fn < n ? unit(fn) : CRec{};
     uint32_t jv = !FC && fn < n ? tk.issue(lane) : 0u;
     for (;;) {
-      // DIAG bit 5 (variant 31, measurement): byte-shifted records copy after the CRC (copy_unaligned)
-      const bool chain_copy = !(DIAG & 32) || (st.delta & 3) == 0;
       const bool more = fn < n;
       const CRec ncur = nxt;
-      // XF: the next record's geometry first -- this record's ring refills run into it.
-      intptr_t ndelta = 0;
-      FileGeo<kRun> ng = st.g;
-      if constexpr (XF) ng = crec_geo<DA>(more ? ncur : CRec{0, 0, 0, 0, 0, 0, kExitParameterError, 0u, 0u}, src,
-                                         src_len, dst, junk, ndelta);
-      uint32_t c = st.g.nstripes ? lane_chain<kRun, CPF, LNT, kS8, !VERIFY, (DIAG & 512) ? CPF : 1, DPPSH, SK,
-                                            (DIAG & 2) != 0, !(DIAG & 16), (DIAG & 64) != 0, XF>(
-                                     lds_tables, lb, st.g, st.h, buf, lane, junk, st.delta, chain_copy, &ng)
+      uint32_t c = st.g.nstripes ? lane_chain<kRun, CPF, LNT, LY, !VERIFY, true, 1, (DIAG & 2) != 0>(
+                                       lds_tables, lb, st.g, st.h, buf, lane, junk, st.delta, true)
                                  : 0u;
       // The next record's loads go out before this one is finished.
       CState ns = st;
       uint32_t fnn = n;
       if (more) {
-        ns = issue_crec<DA, HV>(ncur, src, src_len, dst, lane, junk);
-        if (!XF || !st.g.nstripes) load_ring<kRun, CPF, LNT>(ns.g, lane, buf, junk);
+        ns = issue_crec<DA>(ncur, src, src_len, dst, lane, junk);
+        load_ring<kRun, CPF, LNT>(ns.g, lane, buf, junk);
         fnn = FC ? fc.take(lane) : tk.resolve(jv, lane);
         if (fnn < n) {
           nxt = unit(fnn);
@@ -2109,7 +1741,7 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
         uint8_t* drec = dst + cur.doff;
         const uint32_t len = cur.plen;
         // FileInfo with offset_(8) size_(12) usize_(16) flag_(28) rewritten, the rest copied (task.cpp:753-759)
-        if (!VERIFY && !(DIAG & 16) && lane < kFileInfoSize && cur.kind != 1u) {
+        if (!VERIFY && lane < kFileInfoSize && cur.kind != 1u) {
           const int fld = lane >> 2, sh = 8 * (lane & 3);
           uint32_t b = st.hb;
           if (fld == 2) b = uint32_t(cur.new_off) >> sh;
@@ -2118,8 +1750,8 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
           drec[lane] = uint8_t(b);
         }
         if (VERIFY) {
-        } else if (chain_copy && st.g.nstripes) {
-          if (lane == 0 && !(DIAG & 16)) {  // tail [B16, end) from lane 0's registers
+        } else if (st.g.nstripes) {
+          if (lane == 0) {  // tail [B16, end) from lane 0's registers
             const uint32_t ntw = uint32_t((st.g.end & ~uintptr_t(3)) - st.g.B16) / 4u;
             for (uint32_t i = 0; i < 3u; ++i)
               if (i < ntw) st32u(st.g.B16 + 4u * i + st.delta, st.h.tw[i]);
@@ -2127,10 +1759,10 @@ __global__ void __launch_bounds__(kBlock) compact_pipe_kernel(const uint8_t* __r
             for (uint32_t i = 0; i < 3u; ++i)
               if (B + i < st.g.end) *reinterpret_cast<uint8_t*>(B + i + st.delta) = uint8_t(st.h.tb[i]);
           }
-        } else {  // tiny payload, or a destination not congruent mod 4
+        } else {  // tiny payload
           copy_unaligned(rec + kFileInfoSize, drec + kFileInfoSize, len, lane);
         }
-        if (!(DIAG & 4096)) c = finish_file<kRun, kS8>(lds_tables, lb, st.g, st.h, c, lane);
+        c = finish_file<kRun, LY>(lds_tables, lb, st.g, st.h, c, lane);
         const uint64_t hid = uint64_t(hdr_dword(st.hb, 0)) | uint64_t(hdr_dword(st.hb, 1)) << 32;
         if (cur.kind == 1u) {
         } else if (hid != cur.fid) status = kExitFileInfoError;
@@ -2349,24 +1981,6 @@ __global__ void __launch_bounds__(kBlock) membench_kernel(const uint8_t* __restr
   if (acc == 0x9E3779B9u) out[0] = acc;  // keep the loads alive
 }
 
-// Calibration: streaming copy of nbytes (multiple of 16), 16 B per lane,
-// grid-stride; NT = non-temporal loads and stores.
-template <bool NT>
-__global__ void __launch_bounds__(kBlock) membench_copy_kernel(const uint8_t* __restrict__ src,
-                                                               uint8_t* __restrict__ dst, uint64_t nbytes) {
-  const uint64_t nv = nbytes / 16;
-  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-  const uintptr_t s = reinterpret_cast<uintptr_t>(src), d = reinterpret_cast<uintptr_t>(dst);
-  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nv; i += stride) {
-    const uint4 v = ld128s<NT>(s + 16 * i);
-    if (NT) {
-      st128_nt(d + 16 * i, v);
-    } else {
-      const u32x4 w = {v.x, v.y, v.z, v.w};
-      *reinterpret_cast<gu128wp>(d + 16 * i) = w;
-    }
-  }
-}
 
 // Calibration: copy with U 16-byte chunks per lane in flight per iteration
 // (U loads, then U stores); LNT = nt loads; SK = store kind (0 plain, 1 nt).
@@ -2418,122 +2032,13 @@ static unsigned grid_for(uint32_t nwork, unsigned cap = kMaxGrid) {
   if (g == 0) g = 1;
   return unsigned(g);
 }
-
-#ifdef TFS_CRC_MEASURE
-// Kernel variants (RUN bytes per lane per stripe, PF stripes in flight, ticket
-// forms).  Returns false for an id that is not a crc_files_kernel variant.
-template <int MODE>
-static bool launch_measure_variant(int variant, dim3 grid, dim3 block, const uint8_t* base, const Desc* desc,
-                                   uint32_t n, const Tables* tg, uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad,
-                                   uint32_t* sched, hipStream_t stream, uint32_t vseed, uint32_t* done_flag,
-                                   uint32_t seq, const SplitArgs& sa) {
-#define TFS_LAUNCH(R, P, N, D, S)                                                                          \
-  hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N, D, S>), grid, block, 0, stream, base, desc, n, tg, out_crc, \
-                     out_ok, n_bad, sched, vseed, done_flag, seq, sa)
-  switch (variant) {
-    case 1: TFS_LAUNCH(16, 5, true, false, true); break;
-    case 2: TFS_LAUNCH(16, 4, true, true, true); break;
-    case 3: TFS_LAUNCH(16, 6, true, true, true); break;
-    case 4: TFS_LAUNCH(16, 5, true, true, false); break;
-    case 5: TFS_LAUNCH(16, 8, true, true, true); break;
-    case 6: TFS_LAUNCH(16, 3, true, true, true); break;
-#undef TFS_LAUNCH
-#define TFS_LAUNCH_G(R, P, N, D, S, G)                                                                        \
-  hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N, D, S, G>), grid, block, 0, stream, base, desc, n, tg, out_crc, \
-                     out_ok, n_bad, sched, vseed, done_flag, seq, sa)
-    case 9: TFS_LAUNCH_G(16, 6, true, true, true, 2); break;
-    case 10: TFS_LAUNCH_G(16, 6, true, true, true, 3); break;
-    case 11: TFS_LAUNCH_G(16, 8, true, true, true, 4); break;
-    case 12: TFS_LAUNCH_G(16, 4, true, true, true, 2); break;
-#undef TFS_LAUNCH_G
-    case 13:
-      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, true>), grid, block, 0, stream, base,
-                         desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
-      break;
-    case 15:
-      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, true, 2>), grid, block, 0, stream,
-                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
-      break;
-    case 16:
-      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, true, 4>), grid, block, 0, stream,
-                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
-      break;
-    case 19:  // static contiguous ranges per wave (BLK)
-      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, false, kS8, 1, false, kIL, 1, false, true>), grid, block,
-                         0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
-      break;
-    case 17:  // cross-file ring (lane_chain XF): the next file's first stripes refill this file's freed slots
-      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, true>), grid, block, 0,
-                         stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
-      break;
-    case 18:  // cross-file ring, PF 6
-      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, 6, kNT, kDYN, kS8, 1, false, kIL, 1, true>), grid, block, 0,
-                         stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
-      break;
-    case 39:  // CF: 2 consecutive files per ticket
-      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, 2>), grid,
-                         block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
-      break;
-    case 40:  // CF: 4 consecutive files per ticket
-      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, 4>), grid,
-                         block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
-      break;
-    case 41:  // CF: 16 consecutive files per ticket
-      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, 16>), grid,
-                         block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
-      break;
-#define TFS_LAUNCH_CF(CF, TS)                                                                                         \
-  hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, CF, TS>), grid, \
-                     block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa)
-    case 42: TFS_LAUNCH_CF(4, 3); break;  // chunks of 4, the last n/8 files one by one (= the product)
-    case 47: TFS_LAUNCH_CF(4, 4); break;  // chunks of 4, the last n/16 one by one
-    case 48: TFS_LAUNCH_CF(4, 5); break;  // chunks of 4, the last n/32 one by one
-    case 43: TFS_LAUNCH_CF(4, 2); break;  // chunks of 4, the last n/4 one by one
-    case 44: TFS_LAUNCH_CF(2, 3); break;  // chunks of 2, the last n/8 one by one
-    case 45: TFS_LAUNCH_CF(3, 0); break;  // chunks of 3
-    case 46: TFS_LAUNCH_CF(3, 3); break;  // chunks of 3, the last n/8 one by one
-#undef TFS_LAUNCH_CF
-    case 14:  // contiguous ticket groups (the product before interleaving)
-      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, false>), grid, block, 0, stream,
-                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
-      break;
-#define TFS_LAUNCH(R, P, N, D, S)                                                                          \
-  hipLaunchKernelGGL((crc_files_kernel<MODE, R, P, N, D, S>), grid, block, 0, stream, base, desc, n, tg, out_crc, \
-                     out_ok, n_bad, sched, vseed, done_flag, seq, sa)
-#define TFS_LAUNCH_CX(P, IL_, CF, TS)                                                                                \
-  hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, P, kNT, kDYN, kS8, 1, false, IL_, 1, false, false, CF, TS>), grid,   \
-                     block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa)
-    case 51: TFS_LAUNCH_CX(kPF, false, kCF, kTS); break;  // chunked tickets over contiguous eighths
-    case 52: TFS_LAUNCH_CX(kPF, kIL, 8, kTS); break;      // chunks of 8
-    case 53: TFS_LAUNCH_CX(6, kIL, kCF, kTS); break;      // PF 6
-    case 54: TFS_LAUNCH_CX(4, kIL, kCF, kTS); break;      // PF 4
-    case 55: TFS_LAUNCH_CX(kPF, kIL, 6, kTS); break;      // chunks of 6
-#undef TFS_LAUNCH_CX
-#define TFS_LAUNCH_CW(WW)                                                                                           \
-  hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, WW, false, false, kCF, kTS>), \
-                     grid, block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa)
-#define TFS_LAUNCH_HS(HS_)                                                                                           \
-  hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, kCF, 0, 0, HS_>), \
-                     grid, block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa)
-    case 91: TFS_LAUNCH_HS(2); break;  // chunks of 4: the first 3/4 static (wave w: chunks w, w+W, ...), tickets after
-    case 92: TFS_LAUNCH_HS(1); break;  // the first 1/2 static
-    case 93: TFS_LAUNCH_HS(3); break;  // the first 7/8 static
-#undef TFS_LAUNCH_HS
-    case 56: TFS_LAUNCH_CW(2); break;  // chunked tickets, WW consecutive chunks per group slot (one XCD)
-    case 57: TFS_LAUNCH_CW(8); break;
-    case 58: TFS_LAUNCH_CW(4); break;
-#undef TFS_LAUNCH_CW
-    case 50:  // one file per ticket (the product before chunked tickets)
-      hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL>), grid, block, 0, stream,
-                         base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
-      break;
-    default:
-      return false;
-  }
-#undef TFS_LAUNCH
-  return true;
+// Workgroups of nw waves for nwork units, at most cap.
+static unsigned grid_waves(uint32_t nwork, uint32_t nw, unsigned cap) {
+  uint64_t g = (uint64_t(nwork) + nw - 1) / nw;
+  if (g > cap) g = cap;
+  if (g == 0) g = 1;
+  return unsigned(g);
 }
-#endif  // TFS_CRC_MEASURE
 
 template <int MODE>
 static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* desc, uint32_t n, const Tables* tg,
@@ -2541,63 +2046,39 @@ static hipError_t launch_variant(int variant, const uint8_t* base, const Desc* d
                                  hipStream_t stream, uint32_t vseed, uint32_t* done_flag, uint32_t seq, unsigned cap,
                                  const SplitArgs* split) {
   // Latency form for small batches (TFS_CRC_VARIANT 20 forces it for any n in
-  // the measurement build; the other measurement variants never use it).
-  if (variant == 20 || (variant == 0 && n <= kWgMaxFiles)) {
+  // the measurement build).
+  if (variant == 20 || n <= kWgMaxFiles) {
     const unsigned wg = n < kMaxGrid ? n : kMaxGrid;
     hipLaunchKernelGGL((crc_wg_kernel<MODE>), dim3(wg), dim3(kBlock), 0, stream, base, desc, n, tg, out_crc, out_ok,
                        n_bad, sched, vseed, done_flag, seq);
     return hipGetLastError();
   }
   if (!sched) return hipErrorInvalidValue;
-  // Split files (tfs_crc_device.h): the plan before the main kernel, the fold
-  // after it, all on `stream`; the completion-flag form (done_flag) never splits.
-  const SplitArgs sa = split && !done_flag ? *split : SplitArgs{nullptr, 0u, 0u};
-  // A split launch's work is its files plus the ext units the plan makes on the
-  // device (a few hundred 64 MiB files are ~150 k units), so it takes the whole
-  // capped grid; the tickets hand out any number of units.
+  // Split files (tfs_crc_device.h): the address-ordered plan (count, scan, write)
+  // before the main kernel, the fold after it, all on `stream`; the
+  // completion-flag form (done_flag) never splits.  A split launch's work is its
+  // files plus the segments the plan makes on the device (a few hundred 64 MiB
+  // files are ~150 k units), so it takes the whole capped grid.
+  const SplitArgs sa = split && !done_flag ? *split : SplitArgs{nullptr, 0u};
   const dim3 grid(sa.plan ? (cap < kMaxGrid ? cap : kMaxGrid) : grid_for(n, cap)), block(kBlock);
-  if (sa.plan && sa.ao) {
-    // Address-ordered split (the product, round 4): count, scan
-    // and write the unit list before the main kernel, the fold after it.
+  if (sa.plan) {
     const uint32_t nb = ao_nblk(n);
     hipLaunchKernelGGL(split_ao_count_kernel, dim3(nb), dim3(kAoBlock), 0, stream, desc, n, sa);
-    hipLaunchKernelGGL(split_ao_scan_kernel, dim3(1), dim3(1024), 0, stream, n, sa);
+    hipLaunchKernelGGL(split_ao_scan_kernel, dim3(1), dim3(1024), 0, stream, desc, n, sa);
     hipLaunchKernelGGL(split_ao_write_kernel, dim3(nb), dim3(kAoBlock), 0, stream, desc, n, sa);
     if (const hipError_t e = hipGetLastError()) return e;
   }
-  bool launched = false;
 #ifdef TFS_CRC_MEASURE
-  // Measurement build: round 3's appended split (segments after the files,
-  // tfs_crc32_set_split 2) and the kernel variants, which read that layout.
-  if (sa.plan && !sa.ao) {
-    hipLaunchKernelGGL((split_plan_kernel<MODE>), dim3((n + 255u) / 256u), dim3(256), 0, stream, desc, n, vseed, sa);
-    if (const hipError_t e = hipGetLastError()) return e;
-  }
-  launched = variant != 0 && launch_measure_variant<MODE>(variant, grid, block, base, desc, n, tg, out_crc, out_ok,
-                                                          n_bad, sched, stream, vseed, done_flag, seq, sa);
-  if (!launched && sa.plan && !sa.ao) {
-    hipLaunchKernelGGL((crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, kCF, kTS>),
-                       grid, block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq,
-                       sa);
-    launched = true;
-  }
-  if (launched && sa.plan && !sa.ao) {
-    if (const hipError_t e = hipGetLastError()) return e;
-    const uint32_t fg = (n + 255u) / 256u;
-    hipLaunchKernelGGL((split_fold_kernel<MODE>), dim3(fg < 1024u ? fg : 1024u), dim3(256), 0, stream, desc, n, tg, sa,
-                       out_crc, out_ok, n_bad);
-    return hipGetLastError();
-  }
+  if (variant == 50)  // one file per ticket (the product before chunked tickets)
+    hipLaunchKernelGGL((crc_files_kernel<MODE, 1, 0>), grid, block, 0, stream, base, desc, n, tg, out_crc, out_ok,
+                       n_bad, sched, vseed, done_flag, seq, sa);
+  else
 #endif
-  // The product: chunked interleaved tickets (kCF files per ticket, the last
-  // n >> kTS one by one), PF stripes in flight, the address-ordered unit list
-  // when the plan split files.
-  if (!launched)
-    hipLaunchKernelGGL(
-        (crc_files_kernel<MODE, kRun, kPF, kNT, kDYN, kS8, 1, false, kIL, 1, false, false, kCF, kTS, 1>), grid, block,
-        0, stream, base, desc, n, tg, out_crc, out_ok, n_bad, sched, vseed, done_flag, seq, sa);
+    hipLaunchKernelGGL((crc_files_kernel<MODE>), grid, block, 0, stream, base, desc, n, tg, out_crc, out_ok, n_bad,
+                       sched, vseed, done_flag, seq, sa);
+  (void)variant;
   if (const hipError_t e = hipGetLastError()) return e;
-  if (sa.plan && sa.ao) {
+  if (sa.plan) {
     const uint32_t fg = (n + 255u) / 256u;
     hipLaunchKernelGGL((split_ao_fold_kernel<MODE>), dim3(fg < 1024u ? fg : 1024u), dim3(256), 0, stream, desc, n, tg,
                        sa, out_crc, out_ok, n_bad);
@@ -2640,51 +2121,17 @@ hipError_t launch_packet_finish(uint8_t* base, const PacketDesc* pd, const Desc*
   return hipGetLastError();
 }
 
-#ifdef TFS_CRC_MEASURE
-hipError_t launch_block_verify(const uint8_t* image, uint64_t image_len, const RawMeta* metas, uint32_t n,
-                               const Tables* tg, uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad,
-                               hipStream_t stream) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(block_verify_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, image, image_len, metas, n, tg,
-                     out_crc, out_status, n_bad);
-  return hipGetLastError();
-}
-
-hipError_t launch_compact_copy(const uint8_t* src, const RawMeta* metas, const int32_t* flags, const int64_t* dest_off,
-                               uint32_t n, uint8_t* dst, hipStream_t stream) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(compact_copy_kernel, dim3(grid_for(n)), dim3(kBlock), 0, stream, src, metas, flags, dest_off, n,
-                     dst);
-  return hipGetLastError();
-}
-#endif  // TFS_CRC_MEASURE
 
 // Compaction of one block (RawMeta + flags + dest offsets): compact_pipe_kernel
-// (dynamic tickets on the stream's slot, next-record prefetch).  Measurement
-// build: 22 the unpipelined compact_fused_kernel, 23 ds_bpermute lane shifts,
-// 27 the source-anchored grid.
+// (dynamic tickets on the stream's slot, next-record prefetch).
 hipError_t launch_compact_fused(const uint8_t* src, uint64_t src_len, const RawMeta* metas, const int32_t* flags,
                                 const int64_t* dest_off, uint32_t n, uint8_t* dst, const Tables* tg, uint32_t* out_crc,
                                 int32_t* out_status, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
                                 int variant, unsigned cap) {
   if (n == 0) return hipSuccess;
   if (!sched) return hipErrorInvalidValue;
-  const dim3 grid(grid_for(n, cap));
-#ifdef TFS_CRC_MEASURE
-  if (variant == 22)
-    hipLaunchKernelGGL(compact_fused_kernel<false>, grid, dim3(kBlock), 0, stream, src, src_len, metas, flags,
-                       dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad);
-  else if (variant == 23)
-    hipLaunchKernelGGL((compact_pipe_kernel<false, false>), grid, dim3(kBlock), 0, stream, src, src_len, metas, flags,
-                       dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched, CSegArgs{nullptr, 0u, 0u});
-  else if (variant == 27)
-    hipLaunchKernelGGL((compact_pipe_kernel<false, true, false, 0>), grid, dim3(kBlock), 0, stream, src, src_len,
-                       metas, flags, dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched,
-                       CSegArgs{nullptr, 0u, 0u});
-  else
-#endif
-    hipLaunchKernelGGL(compact_pipe_kernel<false>, grid, dim3(kBlock), 0, stream, src, src_len, metas, flags,
-                       dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched, CSegArgs{nullptr, 0u, 0u});
+  hipLaunchKernelGGL(compact_pipe_kernel<false>, dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, src, src_len, metas,
+                     flags, dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched, CSegArgs{nullptr, 0u, 0u});
   (void)variant;
   return hipGetLastError();
 }
@@ -2695,97 +2142,55 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
                                uint32_t* sched, hipStream_t stream, int variant, unsigned cap, const CSegArgs* seg) {
   if (n == 0) return hipSuccess;
   if (!sched) return hipErrorInvalidValue;
+  const unsigned ccap = cap < kMaxGrid ? cap : kMaxGrid;
   if (seg && seg->plan) {
     // Segmented form: plan, the record kernel over jobs + segments (the whole
     // capped grid: the units are made on the device), fold -- all on `stream`.
     const CSegArgs cs = *seg;
     hipLaunchKernelGGL(compact_seg_plan_kernel, dim3((n + 255u) / 256u), dim3(256), 0, stream, jobs, n, src_len, cs);
     if (const hipError_t e = hipGetLastError()) return e;
-#ifdef TFS_CRC_MEASURE
-    if (variant == 90)  // segments with the hybrid unit order (static 3/4, tickets after; measurement)
-      hipLaunchKernelGGL((compact_pipe_kernel<true, true, false, kCompactDiag, kPF, 1, 0, true, 1, 2>),
-                         dim3(cap < kMaxGrid ? cap : kMaxGrid), dim3(kBlock), 0, stream, src, src_len, nullptr,
-                         nullptr, nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad, sched, cs);
-    else
-#endif
-    hipLaunchKernelGGL((compact_pipe_kernel<true, true, false, kCompactDiag, kPF, 1, 0, true>),
-                       dim3(cap < kMaxGrid ? cap : kMaxGrid), dim3(kBlock), 0, stream, src, src_len, nullptr, nullptr,
-                       nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad, sched, cs);
+    hipLaunchKernelGGL((compact_pipe_kernel<true, false, kCompactDiag, kPF, 1, 0, true>), dim3(ccap), dim3(kBlock), 0,
+                       stream, src, src_len, nullptr, nullptr, nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad,
+                       sched, cs);
     if (const hipError_t e = hipGetLastError()) return e;
     const uint32_t fg = (n + 255u) / 256u;
     hipLaunchKernelGGL(compact_seg_fold_kernel, dim3(fg < 1024u ? fg : 1024u), dim3(256), 0, stream, jobs, n, tg, cs,
                        out_crc, out_status, n_bad);
     return hipGetLastError();
   }
-  const dim3 grid(grid_for(n, cap));
-#define TFS_CJ(...)                                                                                                  \
-  hipLaunchKernelGGL((compact_pipe_kernel<__VA_ARGS__>), grid, dim3(kBlock), 0, stream, src, src_len, nullptr, nullptr, \
-                     nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad, sched, CSegArgs{nullptr, 0u, 0u})
+#define TFS_CJ(NW_, OCC_, LY_, PF_, DIAG_)                                                                           \
+  hipLaunchKernelGGL((compact_pipe_kernel<true, false, DIAG_, PF_, 1, 0, false, kCompactHS, NW_, OCC_, LY_>),        \
+                     dim3(grid_waves(n, NW_, ccap * OCC_)), dim3(NW_ * kWave), 0, stream, src, src_len, nullptr,       \
+                     nullptr, nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad, sched, CSegArgs{nullptr, 0u, 0u})
 #ifdef TFS_CRC_MEASURE
-  if (variant == 22)
-    hipLaunchKernelGGL(compact_fused_kernel<true>, grid, dim3(kBlock), 0, stream, src, src_len, nullptr, nullptr,
-                       nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad);
-  else if (variant == 23) TFS_CJ(true, false);
-  else if (variant == 25) TFS_CJ(true, true, false, kCompactDiag | 1);
-  else if (variant == 26) TFS_CJ(true, true, false, kCompactDiag | 2);
-  else if (variant == 27) TFS_CJ(true, true, false, 0);
-  else if (variant == 29) TFS_CJ(true, true, false, 4);
-  else if (variant == 30) TFS_CJ(true, true, false, kCompactDiag | 16);
-  else if (variant == 31) TFS_CJ(true, true, false, kCompactDiag | 32);
-  else if (variant == 32) TFS_CJ(true, true, false, kCompactDiag | 64);
-  else if (variant == 33) TFS_CJ(true, true, false, kCompactDiag, 6);
-  else if (variant == 34) TFS_CJ(true, true, false, kCompactDiag, 7);
-  else if (variant == 35) TFS_CJ(true, true, false, kCompactDiag, 8);
-  else if (variant == 36) TFS_CJ(true, true, false, kCompactDiag | 128);
-  else if (variant == 37) TFS_CJ(true, true, false, kCompactDiag, 4);
-  else if (variant == 75) TFS_CJ(true, true, false, kCompactDiag | 1, 8);  // plain stores, PF 8 (round 4)
-  else if (variant == 76) TFS_CJ(true, true, false, kCompactDiag | 1, 6);  // plain stores, PF 6
-  else if (variant == 79) TFS_CJ(true, true, false, 4 | 512 | 2 | 16, 8);        // 64 with non-temporal loads
-  else if (variant == 80) TFS_CJ(true, true, false, kCompactDiag | 512 | 2 | 16 | 256, 8);  // 64, static order
-  else if (variant == 86) TFS_CJ(true, true, false, kCompactDiag, kPF, 1, 0, false, 1, 3);  // static 7/8, tickets after
-  else if (variant == 87) TFS_CJ(true, true, false, kCompactDiag, kPF, 1, 0, false, 1, 5);  // static 31/32
-  else if (variant == 88) TFS_CJ(true, true, false, kCompactDiag, kPF, 1, 0, false, 1, 2);  // static 3/4
-  else if (variant == 89) TFS_CJ(true, true, false, kCompactDiag, kPF, 1, 0, false, 1, 1);  // static 1/2
-  else if (variant == 84) TFS_CJ(true, true, false, kCompactDiag | 4096);                  // no combine
-  else if (variant == 85) TFS_CJ(true, true, false, kCompactDiag | 512 | 2 | 16 | 4096, 8);  // 64, no combine
-  else if (variant == 81) TFS_CJ(true, true, false, kCompactDiag | 1024);         // cross-record ring
-  else if (variant == 82) TFS_CJ(true, true, false, kCompactDiag | 2048);         // stripe 0 / tail as dwordx4
-  else if (variant == 83) TFS_CJ(true, true, false, kCompactDiag | 1024 | 2048);  // both
-  else if (variant == 77) TFS_CJ(true, true, false, kCompactDiag, kPF, 1, 0, false, 4);   // 4 records per group slot
-  else if (variant == 78) TFS_CJ(true, true, false, kCompactDiag, kPF, 1, 0, false, 16);  // 16 records per group slot
-  else if (variant == 60) TFS_CJ(true, true, false, kCompactDiag | 256);      // static records, product otherwise
-  else if (variant == 61) TFS_CJ(true, true, false, kCompactDiag | 256 | 2);  // static, no payload CRC steps
-  else if (variant == 62) TFS_CJ(true, true, false, kCompactDiag | 512);      // ring refilled in bursts of CPF
-  else if (variant == 63) TFS_CJ(true, true, false, kCompactDiag | 512, 8);   // bursts of 8 (the chunk copy's)
-  else if (variant == 64) TFS_CJ(true, true, false, kCompactDiag | 512 | 2 | 16, 8);  // bursts of 8, copy only
-  else if (variant >= 65 && variant <= 68)  // the record list through the chunk copy's loop (calibration)
-    hipLaunchKernelGGL((variant == 65   ? compact_probe_copy_kernel<true>
-                        : variant == 66 ? compact_probe_copy_kernel<false>
-                        : variant == 67 ? compact_probe_copy_kernel<true, 128>
-                                        : compact_probe_copy_kernel<false, 128>),
-                       grid, dim3(kBlock), 0, stream, src, jobs, n, dst, sched);
-  else if (variant == 69 || variant == 70)  // 67 over 512 / 2,048 workgroups (two resident per CU, no LDS)
-    hipLaunchKernelGGL((compact_probe_copy_kernel<true, 128>), dim3(variant == 69 ? 512 : 2048), dim3(kBlock), 0,
-                       stream, src, jobs, n, dst, sched);
-  else if (variant == 71)  // 68 with one record per wave: n / 16 workgroups, each gone after one step
-    hipLaunchKernelGGL((compact_probe_copy_kernel<false, 128>), dim3((n + 15u) / 16u), dim3(kBlock), 0, stream, src,
-                       jobs, n, dst, sched);
-  else if (variant == 39) TFS_CJ(true, true, false, kCompactDiag, kPF, 2, 0);  // chunked tickets (as crc_files 39-45)
-  else if (variant == 40) TFS_CJ(true, true, false, kCompactDiag, kPF, 4, 0);
-  else if (variant == 42) TFS_CJ(true, true, false, kCompactDiag, kPF, 4, 3);
-  else if (variant == 43) TFS_CJ(true, true, false, kCompactDiag, kPF, 4, 2);
-  else if (variant == 45) TFS_CJ(true, true, false, kCompactDiag, kPF, 3, 0);
+  // Measurement forms: 26 the product without the payload CRC steps
+  // (its own load/store schedule; wrong CRCs); 67 / 68 the record list through the
+  // chunk copy's loop (dynamic / static order, calibration: no CRC, no headers).
+  // Round 5, two workgroups per CU: 74 KiB of LDS tables
+  // (LdsLayout<2>) and 12-wave (94-96: PF 5, 4, 3; 80 VGPRs), 10-wave (98: 96
+  // VGPRs) or 16-wave (99: 64 VGPRs) workgroups; 97 the 74 KiB tables at one
+  // 16-wave workgroup per CU (control).
+  if (variant == 26) TFS_CJ(16, 1, kLY, kPF, kCompactDiag | 2);
+  else if (variant == 67 || variant == 68)
+    hipLaunchKernelGGL((variant == 67 ? compact_probe_copy_kernel<true, 128> : compact_probe_copy_kernel<false, 128>),
+                       dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, src, jobs, n, dst, sched);
+  else if (variant == 94) TFS_CJ(12, 2, 2, kPF, kCompactDiag);
+  else if (variant == 95) TFS_CJ(12, 2, 2, 4, kCompactDiag);
+  else if (variant == 96) TFS_CJ(12, 2, 2, 3, kCompactDiag);
+  else if (variant == 97) TFS_CJ(16, 1, 2, kPF, kCompactDiag);
+  else if (variant == 98) TFS_CJ(10, 2, 2, kPF, kCompactDiag);
+  else if (variant == 99) TFS_CJ(16, 2, 2, 3, kCompactDiag);
   else
 #endif
-    TFS_CJ(true, true, false, kCompactDiag, kPF, 1, 0, false, 1, kCompactHS);
+    TFS_CJ(16, 1, kLY, kPF, kCompactDiag);
 #undef TFS_CJ
   (void)variant;
   return hipGetLastError();
 }
 
 // Verify-on-read of block records: the verify form of the record kernel
-// (chunked tickets like the file kernel).  Measurement build: round 1's static
-// grid-stride block_verify_kernel (24), other ticket forms (39-50).
+// (chunked tickets like the file kernel).  Measurement build: one record per
+// ticket (50).
 hipError_t launch_block_verify_pipe(const uint8_t* image, uint64_t image_len, const RawMeta* metas,
                                     const CompactJob* jobs, uint32_t n, const Tables* tg, uint32_t* out_crc,
                                     int32_t* out_status, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
@@ -2793,34 +2198,17 @@ hipError_t launch_block_verify_pipe(const uint8_t* image, uint64_t image_len, co
   if (n == 0) return hipSuccess;
   if (!sched) return hipErrorInvalidValue;
   const dim3 grid(grid_for(n, cap));
-#define TFS_BV(...)                                                                                                  \
-  hipLaunchKernelGGL((compact_pipe_kernel<true, true, true, kCompactDiag, kPF, __VA_ARGS__>), grid, dim3(kBlock), 0, \
-                     stream, image, image_len, nullptr, nullptr, nullptr, jobs, n, nullptr, tg, out_crc, out_status,   \
-                     n_bad, sched, CSegArgs{nullptr, 0u, 0u})
+#define TFS_BV(WIDE_, CF_, TS_)                                                                                     \
+  hipLaunchKernelGGL((compact_pipe_kernel<WIDE_, true, kCompactDiag, kPF, CF_, TS_>), grid, dim3(kBlock), 0, stream, \
+                     image, image_len, metas, nullptr, nullptr, jobs, n, nullptr, tg, out_crc, out_status, n_bad, sched, \
+                     CSegArgs{nullptr, 0u, 0u})
 #ifdef TFS_CRC_MEASURE
-  if (jobs && variant == 39) TFS_BV(2, 0);
-  else if (jobs && variant == 40) TFS_BV(4, 0);
-  else if (jobs && variant == 42) TFS_BV(4, 3);
-  else if (jobs && variant == 43) TFS_BV(4, 2);
-  else if (jobs && variant == 45) TFS_BV(3, 0);
-  else if (jobs && variant == 47) TFS_BV(4, 4);
-  else if (jobs && variant == 48) TFS_BV(4, 5);
-  else if (jobs && variant == 50) TFS_BV(1, 0);  // one record per ticket (the product before chunked tickets)
-  else if (!jobs && variant == 24)
-    hipLaunchKernelGGL(block_verify_kernel, grid, dim3(kBlock), 0, stream, image, image_len, metas, n, tg, out_crc,
-                       out_status, n_bad);
-  else if (!jobs && variant == 50)
-    hipLaunchKernelGGL((compact_pipe_kernel<false, true, true>), grid, dim3(kBlock), 0, stream, image, image_len, metas,
-                       nullptr, nullptr, nullptr, n, nullptr, tg, out_crc, out_status, n_bad, sched,
-                       CSegArgs{nullptr, 0u, 0u});
+  if (variant == 50 && jobs) TFS_BV(true, 1, 0);
+  else if (variant == 50) TFS_BV(false, 1, 0);
   else
 #endif
-  if (jobs)
-    TFS_BV(kCF, kTS);
-  else
-    hipLaunchKernelGGL((compact_pipe_kernel<false, true, true, kCompactDiag, kPF, kCF, kTS>), grid, dim3(kBlock), 0,
-                       stream, image, image_len, metas, nullptr, nullptr, nullptr, n, nullptr, tg, out_crc, out_status,
-                       n_bad, sched, CSegArgs{nullptr, 0u, 0u});
+  if (jobs) TFS_BV(true, kCF, kTS);
+  else TFS_BV(false, kCF, kTS);
 #undef TFS_BV
   (void)variant;
   return hipGetLastError();
@@ -2879,122 +2267,11 @@ __global__ void __launch_bounds__(kBlock) membench_copy_chunk_kernel(const uint8
   }
 }
 
-// Calibration: read-only form of the chunked copy (nt loads, XOR into a register):
-// the chunked-ticket verify kernel's access shape without its arithmetic.
-template <int PF>
-__global__ void __launch_bounds__(kBlock) membench_read_chunk_kernel(const uint8_t* __restrict__ src, uint64_t nbytes,
-                                                                     uint64_t ch, uint32_t* out) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const uint64_t wave = uint64_t(blockIdx.x) * (kBlock / kWave) + __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const uint64_t nw = uint64_t(gridDim.x) * (kBlock / kWave);
-  const uint64_t nch = nbytes / ch;
-  const uintptr_t s = reinterpret_cast<uintptr_t>(src);
-  uint32_t acc = 0;
-  for (uint64_t c = wave; c < nch; c += nw) {
-    const uint64_t b = c * ch + 16u * uint64_t(lane);
-    for (uint64_t o = 0; o < ch; o += 1024u * PF) {
-      uint4 v[PF];
-#pragma unroll
-      for (int k = 0; k < PF; ++k) v[k] = ld128s<true>(s + b + o + 1024u * k);
-#pragma unroll
-      for (int k = 0; k < PF; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
-    }
-  }
-  if (acc == 0x9E3779B9u) out[0] = acc;  // keep the loads alive
-}
 
-// Calibration: workgroup-contiguous chunks -- chunk c (ch bytes) to workgroup
-// c mod G, and inside a chunk wave w reads 1 KiB stripes w, w+16, ... (the
-// latency form's access shape, crc_wg_kernel): at any moment a CU's 16 waves read
-// one contiguous run of 16 stripes.  PF stripes per wave in flight.
-template <int PF>
-__global__ void __launch_bounds__(kBlock) membench_wg_chunk_kernel(const uint8_t* __restrict__ src, uint64_t nbytes,
-                                                                   uint64_t ch, uint32_t* out) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const uint64_t nch = nbytes / ch;
-  const uint64_t nst = ch / 1024u;
-  const uintptr_t s = reinterpret_cast<uintptr_t>(src);
-  uint32_t acc = 0;
-  for (uint64_t c = blockIdx.x; c < nch; c += gridDim.x) {
-    const uint64_t b = c * ch + 16u * uint64_t(lane);
-    for (uint64_t st = wave; st < nst; st += 16u * PF) {
-      uint4 v[PF];
-#pragma unroll
-      for (int k = 0; k < PF; ++k) {
-        const uint64_t sk = st + 16u * uint64_t(k);
-        v[k] = ld128s<true>(s + b + 1024u * (sk < nst ? sk : st));
-      }
-#pragma unroll
-      for (int k = 0; k < PF; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
-    }
-  }
-  if (acc == 0x9E3779B9u) out[0] = acc;  // keep the loads alive
-}
 
-// Calibration: copy form of the workgroup-contiguous chunks (the access shape a
-// workgroup-per-record compaction would have): chunk c to workgroup c mod G; wave
-// w copies 1 KiB stripes w, w+16, ... of it, PF in flight, nt loads and stores.
-template <int PF>
-__global__ void __launch_bounds__(kBlock) membench_wg_copy_kernel(const uint8_t* __restrict__ src,
-                                                                  uint8_t* __restrict__ dst, uint64_t nbytes,
-                                                                  uint64_t ch) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  const uint64_t nch = nbytes / ch;
-  const uint64_t nst = ch / 1024u;
-  const uintptr_t s = reinterpret_cast<uintptr_t>(src), d = reinterpret_cast<uintptr_t>(dst);
-  for (uint64_t c = blockIdx.x; c < nch; c += gridDim.x) {
-    const uint64_t b = c * ch + 16u * uint64_t(lane);
-    for (uint64_t st = wave; st < nst; st += 16u * PF) {
-      uint4 v[PF];
-#pragma unroll
-      for (int k = 0; k < PF; ++k) {
-        const uint64_t sk = st + 16u * uint64_t(k);
-        if (sk < nst) v[k] = ld128s<true>(s + b + 1024u * sk);
-      }
-#pragma unroll
-      for (int k = 0; k < PF; ++k) {
-        const uint64_t sk = st + 16u * uint64_t(k);
-        if (sk < nst) st128_nt(d + b + 1024u * sk, v[k]);
-      }
-    }
-  }
-}
 
 hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, uint32_t n, uint64_t nbytes,
                            uint32_t* out, unsigned grid, hipStream_t stream) {
-  if (pattern >= 57000 && pattern < 58000) {
-    // 57PCC: workgroup-contiguous chunk copy into `out`, CC = chunk in 16 KiB units, P = stripes in flight per wave
-    const int P = (pattern / 100) % 10, CC = pattern % 100;
-    const uint64_t ch = uint64_t(CC ? CC : 4) * 16384u;
-    const dim3 g(grid ? grid : kMaxGrid);
-    const uint64_t nb = nbytes / ch * ch;
-    uint8_t* d = reinterpret_cast<uint8_t*>(out);
-    if (P <= 2) hipLaunchKernelGGL(membench_wg_copy_kernel<2>, g, dim3(kBlock), 0, stream, base, d, nb, ch);
-    else if (P <= 4) hipLaunchKernelGGL(membench_wg_copy_kernel<4>, g, dim3(kBlock), 0, stream, base, d, nb, ch);
-    else hipLaunchKernelGGL(membench_wg_copy_kernel<8>, g, dim3(kBlock), 0, stream, base, d, nb, ch);
-    return hipGetLastError();
-  }
-  if (pattern >= 55000 && pattern < 56000) {
-    // 55PCC: workgroup-contiguous chunks, CC = chunk in 16 KiB units, P = stripes in flight per wave (1-8)
-    const int P = (pattern / 100) % 10, CC = pattern % 100;
-    const uint64_t ch = uint64_t(CC ? CC : 4) * 16384u;
-    const dim3 g(grid ? grid : kMaxGrid);
-    const uint64_t nb = nbytes / ch * ch;
-    if (P <= 2) hipLaunchKernelGGL(membench_wg_chunk_kernel<2>, g, dim3(kBlock), 0, stream, base, nb, ch, out);
-    else if (P <= 4) hipLaunchKernelGGL(membench_wg_chunk_kernel<4>, g, dim3(kBlock), 0, stream, base, nb, ch, out);
-    else hipLaunchKernelGGL(membench_wg_chunk_kernel<8>, g, dim3(kBlock), 0, stream, base, nb, ch, out);
-    return hipGetLastError();
-  }
-  if (pattern >= 54000 && pattern < 55000) {
-    // 540CC: chunked read, CC = chunk in 16 KiB units; PF 8, 256 workgroups
-    const int CC = pattern % 100;
-    const uint64_t ch = uint64_t(CC ? CC : 4) * 16384u;
-    const dim3 g(grid ? grid : kMaxGrid);
-    hipLaunchKernelGGL(membench_read_chunk_kernel<8>, g, dim3(kBlock), 0, stream, base, nbytes / ch * ch, ch, out);
-    return hipGetLastError();
-  }
   if (pattern >= 53000 && pattern < 54000) {
     // 53SCC: chunked copy, S = store kind (0 plain, 1 nt), CC = chunk in 16 KiB units; PF 8, 256 workgroups
     const int S = (pattern / 100) % 10, CC = pattern % 100;
@@ -3015,8 +2292,7 @@ hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, u
     return hipGetLastError();
   }
   // pattern: 0 = coalesced, 16 = stripe pattern (run 16); +1000 = non-temporal loads;
-  // +10000 = stripes anchored at 128-byte boundaries (else 16);
-  // 50000 / 51000 = streaming copy of nbytes into `out` (default / non-temporal)
+  // +10000 = stripes anchored at 128-byte boundaries (else 16)
   if (pattern >= 52000 && pattern < 53000) {
     // 52LSU: L = nt loads (0/1), S = store kind (0 plain, 1 nt), U = chunks in flight (1, 4, 8)
     const int L = (pattern / 100) % 10, S = (pattern / 10) % 10, U = pattern % 10;
@@ -3027,16 +2303,6 @@ hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, u
     TFS_COPY2(0, 0, 1); TFS_COPY2(0, 0, 4); TFS_COPY2(0, 0, 8); TFS_COPY2(1, 0, 4); TFS_COPY2(1, 1, 4);
     TFS_COPY2(0, 1, 4); TFS_COPY2(1, 1, 8); TFS_COPY2(1, 0, 8);
 #undef TFS_COPY2
-    return hipGetLastError();
-  }
-  if (pattern == 50000 || pattern == 51000) {
-    const dim3 g(grid ? grid : 2048u);
-    if (pattern == 51000)
-      hipLaunchKernelGGL(membench_copy_kernel<true>, g, dim3(kBlock), 0, stream, base,
-                         reinterpret_cast<uint8_t*>(out), nbytes);
-    else
-      hipLaunchKernelGGL(membench_copy_kernel<false>, g, dim3(kBlock), 0, stream, base,
-                         reinterpret_cast<uint8_t*>(out), nbytes);
     return hipGetLastError();
   }
   const uint32_t align = pattern >= 10000 ? 128u : 16u;

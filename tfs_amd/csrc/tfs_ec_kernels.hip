@@ -35,12 +35,7 @@ __device__ __forceinline__ uint32_t xand(uint32_t acc, uint32_t in, uint32_t m) 
   return __builtin_amdgcn_bitop3_b32(acc, in, m, 0x78);
 }
 
-// MATH = false (measurement build, TFS_EC_VARIANT 7): the same loads, stores and
-// schedule with one XOR per output row instead of the bitmatrix product -- the
-// kernel's memory shape without its VALU work (wrong parity: timing only).
-// PREF = false (measurement, TFS_EC_VARIANT 11): no next-member prefetch -- fewer
-// VGPRs (more waves per SIMD) for fewer bytes in flight per wave.
-template <int OG, bool MATH = true, bool PREF = true>
+template <int OG>
 __device__ __forceinline__ void ec_apply_body(const EcArgs& a, const uint32_t* __restrict__ masks) {
   const int lane = threadIdx.x & 63;
   const uint32_t u = uint32_t(lane) >> 4;
@@ -65,22 +60,12 @@ __device__ __forceinline__ void ec_apply_body(const EcArgs& a, const uint32_t* _
       u32x2 nx[8];
       const bool more = s + 1 < a.S;
       const uint8_t* np = a.src[more ? s + 1 : s];
-      if constexpr (PREF) {
 #pragma unroll
-        for (int c = 0; c < 8; ++c) nx[c] = (ok && more) ? ld64nt(np + base + 128u * c) : u32x2{0u, 0u};
-      } else if (s > 0) {
-#pragma unroll
-        for (int c = 0; c < 8; ++c) in[c] = ok ? ld64nt(a.src[s] + base + 128u * c) : u32x2{0u, 0u};
-      }
+      for (int c = 0; c < 8; ++c) nx[c] = (ok && more) ? ld64nt(np + base + 128u * c) : u32x2{0u, 0u};
 #pragma unroll
       for (int o = 0; o < OG; ++o)
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-          if constexpr (!MATH) {
-            acc[o][r].x ^= in[r].x;
-            acc[o][r].y ^= in[r].y;
-            continue;
-          }
           const uint32_t* m = masks + ((uint32_t(o) * 8u + uint32_t(r)) * a.S + s) * 8u;
 #pragma unroll
           for (int c = 0; c < 8; ++c) {
@@ -89,10 +74,8 @@ __device__ __forceinline__ void ec_apply_body(const EcArgs& a, const uint32_t* _
             acc[o][r].y = xand(acc[o][r].y, in[c].y, mk);
           }
         }
-      if constexpr (PREF) {
 #pragma unroll
-        for (int c = 0; c < 8; ++c) in[c] = nx[c];
-      }
+      for (int c = 0; c < 8; ++c) in[c] = nx[c];
     }
     if (ok) {
 #pragma unroll
@@ -103,144 +86,11 @@ __device__ __forceinline__ void ec_apply_body(const EcArgs& a, const uint32_t* _
   }
 }
 
-template <int OG, bool MATH = true>
+template <int OG>
 __global__ void __launch_bounds__(256) ec_apply_kernel(EcArgs a, const uint32_t* __restrict__ masks) {
-  ec_apply_body<OG, MATH>(a, masks);
+  ec_apply_body<OG>(a, masks);
 }
 
-#ifdef TFS_CRC_MEASURE
-// Narrow form (measurement, TFS_EC_VARIANT 9, round 4): 4 bytes per lane, so lane
-// l owns bytes 4*(l & 31) of packet c of unit (l >> 5) and a wave step covers 2
-// units: twice the memory instructions of the product for the same bytes, at
-// about half its VGPRs (more waves per SIMD) -- the other side of the wide form.
-typedef const __attribute__((address_space(1))) uint32_t* gu32p;
-typedef __attribute__((address_space(1))) uint32_t* gu32wp;
-template <int OG>
-__global__ void __launch_bounds__(256) ec_apply_narrow_kernel(EcArgs a, const uint32_t* __restrict__ masks) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t u = uint32_t(lane) >> 5;
-  const uint32_t off = 4u * uint32_t(lane & 31);
-  const uint64_t ntiles = (a.units + 1) / 2;
-  const uint64_t wave = uint64_t(blockIdx.x) * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t nwaves = uint64_t(gridDim.x) * (blockDim.x / 64);
-  for (uint64_t t = wave; t < ntiles; t += nwaves) {
-    const uint64_t unit = t * 2 + u;
-    const bool ok = unit < a.units;
-    const uint64_t base = unit * 1024u + off;
-    uint32_t acc[OG][8];
-#pragma unroll
-    for (int o = 0; o < OG; ++o)
-#pragma unroll
-      for (int r = 0; r < 8; ++r) acc[o][r] = 0u;
-    auto ld = [&](const uint8_t* p) -> uint32_t {
-      return __builtin_nontemporal_load(reinterpret_cast<gu32p>(reinterpret_cast<uintptr_t>(p)));
-    };
-    uint32_t in[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) in[c] = ok ? ld(a.src[0] + base + 128u * c) : 0u;
-    for (uint32_t s = 0; s < a.S; ++s) {
-      uint32_t nx[8];
-      const bool more = s + 1 < a.S;
-      const uint8_t* np = a.src[more ? s + 1 : s];
-#pragma unroll
-      for (int c = 0; c < 8; ++c) nx[c] = (ok && more) ? ld(np + base + 128u * c) : 0u;
-#pragma unroll
-      for (int o = 0; o < OG; ++o)
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const uint32_t* m = masks + ((uint32_t(o) * 8u + uint32_t(r)) * a.S + s) * 8u;
-#pragma unroll
-          for (int c = 0; c < 8; ++c) acc[o][r] = xand(acc[o][r], in[c], m[c]);
-        }
-#pragma unroll
-      for (int c = 0; c < 8; ++c) in[c] = nx[c];
-    }
-    if (ok) {
-#pragma unroll
-      for (int o = 0; o < OG; ++o)
-#pragma unroll
-        for (int r = 0; r < 8; ++r)
-          __builtin_nontemporal_store(acc[o][r],
-                                      reinterpret_cast<gu32wp>(reinterpret_cast<uintptr_t>(a.dst[o] + base + 128u * r)));
-    }
-  }
-}
-
-// The product body held to 6 waves per SIMD (measurement, TFS_EC_VARIANT 10: 80 VGPRs,
-// 36 bytes of scratch spills per lane), and without the next-member prefetch (11).
-template <int OG>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) ec_apply_w6_kernel(
-    EcArgs a, const uint32_t* __restrict__ masks) {
-  ec_apply_body<OG, true>(a, masks);
-}
-template <int OG>
-__global__ void __launch_bounds__(256) ec_apply_w7_kernel(EcArgs a, const uint32_t* __restrict__ masks) {
-  ec_apply_body<OG, true, false>(a, masks);
-}
-
-typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
-typedef const __attribute__((address_space(1))) u32x4v* gu128p;
-typedef __attribute__((address_space(1))) u32x4v* gu128wp;
-
-// Wide form (measurement, TFS_EC_VARIANT 8, round 4): 16 bytes per lane, so
-// lane l owns bytes 16*(l & 7) of packet c of unit (l >> 3) and a wave step
-// covers 8 units (8 KiB of every member): half the memory instructions of the
-// product for the same bytes, at more VGPRs (fewer waves per SIMD).
-template <int OG>
-__global__ void __launch_bounds__(256) ec_apply_wide_kernel(EcArgs a, const uint32_t* __restrict__ masks) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t u = uint32_t(lane) >> 3;
-  const uint32_t off = 16u * uint32_t(lane & 7);
-  const uint64_t ntiles = (a.units + 7) / 8;
-  const uint64_t wave = uint64_t(blockIdx.x) * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t nwaves = uint64_t(gridDim.x) * (blockDim.x / 64);
-  for (uint64_t t = wave; t < ntiles; t += nwaves) {
-    const uint64_t unit = t * 8 + u;
-    const bool ok = unit < a.units;
-    const uint64_t base = unit * 1024u + off;
-    u32x4v acc[OG][8];
-#pragma unroll
-    for (int o = 0; o < OG; ++o)
-#pragma unroll
-      for (int r = 0; r < 8; ++r) acc[o][r] = u32x4v{0u, 0u, 0u, 0u};
-    u32x4v in[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c)
-      in[c] = ok ? __builtin_nontemporal_load(reinterpret_cast<gu128p>(reinterpret_cast<uintptr_t>(a.src[0] + base + 128u * c)))
-                 : u32x4v{0u, 0u, 0u, 0u};
-    for (uint32_t s = 0; s < a.S; ++s) {
-      u32x4v nx[8];
-      const bool more = s + 1 < a.S;
-      const uint8_t* np = a.src[more ? s + 1 : s];
-#pragma unroll
-      for (int c = 0; c < 8; ++c)
-        nx[c] = (ok && more) ? __builtin_nontemporal_load(reinterpret_cast<gu128p>(reinterpret_cast<uintptr_t>(np + base + 128u * c)))
-                             : u32x4v{0u, 0u, 0u, 0u};
-#pragma unroll
-      for (int o = 0; o < OG; ++o)
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const uint32_t* m = masks + ((uint32_t(o) * 8u + uint32_t(r)) * a.S + s) * 8u;
-#pragma unroll
-          for (int c = 0; c < 8; ++c) {
-            const uint32_t mk = m[c];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) acc[o][r][q] = xand(acc[o][r][q], in[c][q], mk);
-          }
-        }
-#pragma unroll
-      for (int c = 0; c < 8; ++c) in[c] = nx[c];
-    }
-    if (ok) {
-#pragma unroll
-      for (int o = 0; o < OG; ++o)
-#pragma unroll
-        for (int r = 0; r < 8; ++r)
-          __builtin_nontemporal_store(acc[o][r], reinterpret_cast<gu128wp>(reinterpret_cast<uintptr_t>(a.dst[o] + base + 128u * r)));
-    }
-  }
-}
-#endif  // TFS_CRC_MEASURE
 
 // Chunked form (K > 1): a wave takes K consecutive tiles (4K KiB of every
 // member) per step of its grid stride, and the next tile's first member is
@@ -324,7 +174,7 @@ static void launch_chunk(const EcArgs& a, int og, dim3 g, dim3 b, hipStream_t st
 // The product: the grid-stride tile kernel.  Measurement build (TFS_EC_VARIANT
 // 1, 2, 3): the chunked form with K = 2, 4, 8 tiles per wave step; 4, 6: the
 // product's kernel over 8,192 / 2,048 workgroups striding (the product launches
-// one grid step per wave); 7: the product's shape without the bitmatrix product.
+// one grid step per wave).
 hipError_t launch_ec_apply(const EcArgs& a, int og, int variant, hipStream_t stream) {
   if (a.units == 0) return hipSuccess;
   const uint64_t ntiles = (a.units + 3) / 4;
@@ -354,50 +204,6 @@ hipError_t launch_ec_apply(const EcArgs& a, int og, int variant, hipStream_t str
   if (blocks > cap) blocks = cap;
   const dim3 g(static_cast<unsigned>(blocks)), b(256);
 #ifdef TFS_CRC_MEASURE
-  if (variant == 8) {  // measurement: 16 bytes per lane, 8 units per wave step
-    const uint64_t t8 = (a.units + 7) / 8;
-    const dim3 g8(static_cast<unsigned>((t8 + 3) / 4)), b8(256);
-    switch (og) {
-      case 1: hipLaunchKernelGGL(ec_apply_wide_kernel<1>, g8, b8, 0, stream, a, a.masks); break;
-      case 2: hipLaunchKernelGGL(ec_apply_wide_kernel<2>, g8, b8, 0, stream, a, a.masks); break;
-      case 3: hipLaunchKernelGGL(ec_apply_wide_kernel<3>, g8, b8, 0, stream, a, a.masks); break;
-      default: hipLaunchKernelGGL(ec_apply_wide_kernel<4>, g8, b8, 0, stream, a, a.masks); break;
-    }
-    return hipGetLastError();
-  }
-  if (variant == 10 || variant == 11) {  // measurement: the product body at 6 / 7 waves per SIMD
-#define TFS_EC_W(K)                                                                            \
-  if (variant == 10) hipLaunchKernelGGL(ec_apply_w6_kernel<K>, g, b, 0, stream, a, a.masks); \
-  else hipLaunchKernelGGL(ec_apply_w7_kernel<K>, g, b, 0, stream, a, a.masks)
-    switch (og) {
-      case 1: TFS_EC_W(1); break;
-      case 2: TFS_EC_W(2); break;
-      case 3: TFS_EC_W(3); break;
-      default: TFS_EC_W(4); break;
-    }
-#undef TFS_EC_W
-    return hipGetLastError();
-  }
-  if (variant == 9) {  // measurement: 4 bytes per lane, 2 units per wave step
-    const uint64_t t2 = (a.units + 1) / 2;
-    const dim3 g2(static_cast<unsigned>((t2 + 3) / 4)), b2(256);
-    switch (og) {
-      case 1: hipLaunchKernelGGL(ec_apply_narrow_kernel<1>, g2, b2, 0, stream, a, a.masks); break;
-      case 2: hipLaunchKernelGGL(ec_apply_narrow_kernel<2>, g2, b2, 0, stream, a, a.masks); break;
-      case 3: hipLaunchKernelGGL(ec_apply_narrow_kernel<3>, g2, b2, 0, stream, a, a.masks); break;
-      default: hipLaunchKernelGGL(ec_apply_narrow_kernel<4>, g2, b2, 0, stream, a, a.masks); break;
-    }
-    return hipGetLastError();
-  }
-  if (variant == 7) {  // measurement: the memory shape without the bitmatrix product
-    switch (og) {
-      case 1: hipLaunchKernelGGL((ec_apply_kernel<1, false>), g, b, 0, stream, a, a.masks); break;
-      case 2: hipLaunchKernelGGL((ec_apply_kernel<2, false>), g, b, 0, stream, a, a.masks); break;
-      case 3: hipLaunchKernelGGL((ec_apply_kernel<3, false>), g, b, 0, stream, a, a.masks); break;
-      default: hipLaunchKernelGGL((ec_apply_kernel<4, false>), g, b, 0, stream, a, a.masks); break;
-    }
-    return hipGetLastError();
-  }
 #endif
   switch (og) {
     case 1: hipLaunchKernelGGL(ec_apply_kernel<1>, g, b, 0, stream, a, a.masks); break;

@@ -4,21 +4,16 @@ only).  Builds bench.py's compact_device workload once (1,024 resident blocks,
 341 of every 1,024 records live, one job per live record), then interleaves, round
 by round, launches of
 
-  * kernel variants on the packed destination (product 0: stripe grid anchored
-    on destination lines, temporal payload loads; 27 the source-anchored grid
-    with non-temporal loads (the earlier product); 29 the anchored grid with
-    non-temporal loads; 25 plain copy-through stores; 26 no payload CRC steps
-    -- the kernel's own load/store schedule; 30 no stripe-0/FileInfo/tail
-    stores; 31 byte-shifted records copied after the CRC; 32 byte-shifted
-    records stored unaligned, lane by lane), and
-  * the product kernel on destinations congruent to the source mod 16 (no lane
-    shift) and mod 128 (whole destination lines per stripe), and on
-    destinations one byte off (every record takes the unaligned copy),
+  * kernel variants on the packed destination (AB_VARIANTS: 26 the product
+    without its payload CRC steps; 67 / 68 the record list through the chunk
+    copy's loop, dynamic / static order; 94-99 the round-5 occupancy forms), and
+  * the product kernel on destinations congruent to the source mod 128 (whole
+    destination lines per stripe),
 
-each timed with HIP events on its own context's stream.  With chunked-ticket
-variants (39-45) in AB_VARIANTS, verify-on-read of every resident record
-(tfs_blocks_verify_device) is timed for them and the product too.  The streaming-copy
-ceiling of the same bytes (membench pattern 52114) is timed in the same rounds.
+each timed with HIP events on its own context's stream.  The streaming-copy
+ceilings of the same bytes (membench 52114 grid-stride, 53104/53116/53004/53016
+wave-contiguous chunks) are timed in the same rounds.  Verify-on-read of every
+resident record (tfs_blocks_verify_device) is timed for the product.
 
   python tools/ab_compact.py [ROUNDS] [NBLOCKS]
 """
@@ -75,14 +70,7 @@ def main():
     # record list (src = dest = j * 65,536, size 65,536) -- the dense copy's own layout
     # through the record kernel (timing only: the FileInfo checks fail)
     dsts = {"packed": k * rec,                                   # the product workload (contiguous new blocks)
-            "dst16": k * 65584 + (soff & np.uint64(15)),         # delta == 0 mod 16: no lane shift
-            "dst128": k * 65664 + (soff & np.uint64(127)),       # delta == 0 mod 128: whole lines per stripe
-            "shift1": k * rec + np.uint64(1)}                    # delta == 1 mod 4: the unaligned copy
-    # AB_SPLIT=S[,S...] (probe for a segmented record kernel): every live record cut
-    # into consecutive pieces of about S bytes, each run as its own job -- the
-    # kernel's cost per piece and the tighter address window of S-byte units, no
-    # fold (the pieces' FileInfo checks fail: timing only)
-    splits = [int(x) for x in os.environ.get("AB_SPLIT", "").split(",") if x]
+            "dst128": k * 65664 + (soff & np.uint64(127))}       # delta == 0 mod 128: whole lines per stripe
     d_dst = crc.DeviceBuffer(ctx, int(k.size) * 65664 + 256)
     d_bad = crc.DeviceBuffer(ctx, 4)
     jobsets = {}
@@ -98,35 +86,17 @@ def main():
         j["src_offset"] = j["dest_offset"] = k * np.uint64(65536)
         j["file_id"], j["size"] = 1, 65536
         jobsets["aligned64k"] = crc.DeviceBuffer(ctx, j.nbytes).upload(j)
-    for S in splits:
-        npc = (rec + S - 1) // S
-        psz = (rec + npc - 1) // npc
-        sizes = np.full(npc, psz, np.int64)
-        sizes[-1] = rec - psz * (npc - 1)
-        po = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
-        j = np.zeros(k.size * npc, crc.COMPACT_JOB_DTYPE)
-        j["src_offset"] = (soff[:, None] + po[None, :]).reshape(-1)
-        j["dest_offset"] = (dsts["packed"][:, None] + po[None, :]).reshape(-1)
-        j["file_id"] = 1
-        j["size"] = np.tile(sizes, k.size)
-        j["new_offset"] = (j["dest_offset"] % np.uint64(1 << 31)).astype(np.int32)
-        jobsets["split%d" % S] = crc.DeviceBuffer(ctx, j.nbytes).upload(j)
-        jobsets["split%d" % S].njobs = int(j.size)
-    want = [int(x) for x in os.environ.get("AB_VARIANTS", "27,25,26,29,30,31,32").split(",") if x]
+    want = [int(x) for x in os.environ.get("AB_VARIANTS", "26,68").split(",") if x]
     ctxs = {0: ctx}
     for v in want:
         ctxs[v] = ctx_for(v)
-    # 65/66: the record list through the chunk copy's loop -- destinations congruent mod 16 only
-    cases = ([(0, "packed")] + [(v, "packed") for v in want if v not in (31, 32, 65, 66, 67, 68, 69, 70, 71)] + [(0, "dst128")] +
-             [(v, "dst128") for v in want if v in (65, 66, 67, 68, 69, 70, 71)])
-    if 31 in want or 32 in want:
-        cases += [(0, "shift1")] + [(v, "shift1") for v in want if v in (31, 32)]
-    cases += [(0, "split%d" % S) for S in splits]
+    # 67/68: the record list through the chunk copy's loop -- destinations congruent mod 128 only
+    cases = ([(0, "packed")] + [(v, "packed") for v in want if v not in (67, 68)] + [(0, "dst128")] +
+             [(v, "dst128") for v in want if v in (67, 68)])
     if os.environ.get("AB_ALIGNED"):
-        # every requested variant on the dense layout too (the probe copies 65-71
-        # and the kernel reduced to a copy, 64, included): where the 8 % between
-        # the kernel and the chunk copy of the same layout goes
-        cases += [(0, "aligned64k")] + [(v, "aligned64k") for v in want if v not in (31, 32)]
+        # every requested variant on the dense layout too: where the kernel trails
+        # the chunk copy of the same layout
+        cases += [(0, "aligned64k")] + [(v, "aligned64k") for v in want]
     # AB_SEG=S[,S...]: the segmented compaction (tfs_crc32_set_compact_segment) on the
     # product context itself, toggled around its rounds (no second context's placement);
     # the other cases run it with whole records (set_compact_segment 0)
@@ -138,7 +108,7 @@ def main():
     allj["src_offset"], allj["file_id"], allj["size"] = rec_off, 1 + np.arange(n, dtype=np.uint64), rec
     d_allj = crc.DeviceBuffer(ctx, allj.nbytes).upload(allj)
     d_vst = crc.DeviceBuffer(ctx, 4 * n)
-    vcases = [0] + [v for v in want if v in (39, 40, 42, 43, 45, 47, 48, 50)]
+    vcases = [0] + [v for v in want if v == 50]
     nj = int(k.size)
     live_bytes = float(nj) * rec
     algo = 2 * live_bytes + nj * (40 + 4)
@@ -152,7 +122,7 @@ def main():
         return ctxs[v]
 
     for v, js in cases:
-        if v in (26, 30, 61, 64, 65, 66, 67, 68, 69, 70, 71, 79, 80, 84, 85) or js.startswith("split") or js == "aligned64k":
+        if v in (26, 67, 68) or js == "aligned64k":
             continue
         d_bad.zero()
         c = ctx_of(v)
