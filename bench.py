@@ -51,6 +51,7 @@ WORKLOADS = {
     "block_verify_device": ("benchlines.block_verify", "bench_block_verify_device"),
     "compact_files": ("benchlines.compact_files", "bench_compact_files"),     # a11 + f2
     "mixed": ("benchlines.mixed", "bench_mixed"),                   # closes beside throughput launches
+    "small_bodies": ("benchlines.small_bodies", "bench_small_bodies"),  # latency of lone RPC bodies
 }
 
 
@@ -236,6 +237,7 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
+    elapsed_local = elapsed
     kern_ms = [a.elapsed_ms(b) for a, b in ev]
     nbad = int(d_bad.download(np.uint32)[0])
     if nbad:
@@ -267,6 +269,12 @@ def main():
     # Every rank's mean kernel time (HIP events on its own launch stream); the
     # roofline is priced at the slowest GPU's, with the spread beside it.
     rank_kms = _gather_floats(dist, world, float(np.mean(kern_ms)))
+    # Each rank's own device-resident rate (its own wall time between the barriers,
+    # before the max) and where it runs, so a curve below linear names its rank.
+    rank_dev = per_rank(dist, world, elapsed_local, float(args.steps) * nfiles * FILE_SIZE)
+    rank_where = {"local_rank": [int(x) for x in _gather_floats(dist, world, int(os.environ.get("LOCAL_RANK", 0)))],
+                  "device": [int(x) for x in _gather_floats(dist, world, local)],
+                  "numa_node": [int(x) for x in _gather_floats(dist, world, _NUMA.get("node", -1))]}
     avg_kern_s = max(rank_kms) / 1e3
     achieved = nfiles * ALGO_BYTES_PER_FILE / avg_kern_s / 1e9
 
@@ -299,6 +307,7 @@ def main():
             "partition_check": partition,
             "host_numa": dict(_NUMA),
         },
+        "per_rank": dict(rank_where, device_GiBs=rank_dev),
         "parity": {"files_checked": checked, "mismatches": mism, "verdicts_all_ok": all_ok,
                    "method": "every %d-th resident block of every rank: all 1,024 CRCs recomputed by the oracle "
                              "(pthreads) over the device's bytes; 48 files' bytes vs the host generator; every "
@@ -341,12 +350,13 @@ def main():
     if args.e2e_blocks > 0:
         # configs[4] asks for device-resident AND end-to-end at every N: the same
         # job's PCIe-inclusive rate, reported beside `value` (never as `value`).
-        gibs, pcie, el = e2e_blocks(ctx, dist, world, rank, args.e2e_blocks)
+        gibs, pcie, el, e2e_ranks = e2e_blocks(ctx, dist, world, rank, args.e2e_blocks)
         ceil = pcie_ceiling(ctx, dist=dist)
         result["end_to_end"] = {
             "value": gibs, "unit": "GiB/s", "pcie_GBs": pcie, "ms_per_block": el / args.e2e_blocks * 1e3,
             "workload": "%d pinned host 64 MiB block images per GPU -> H2D -> verify -> verdicts back, "
                         "3 in flight, max over ranks" % args.e2e_blocks,
+            "per_rank": e2e_ranks,
             "roofline": {"bound": "pcie", "achieved": pcie / world, "peak": ceil["h2d_GBs"], "unit": "GB/s (per GPU)",
                          "frac": pcie / world / ceil["h2d_GBs"], "peak_source": ceil["source"],
                          "traffic": "whole block images host->device (64 MiB + 36 B headers per 1,024 files)"}}

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-__all__ = ['ROOT', 'emit', 'DATA_SEED', 'FILE_SIZE', 'FILES_PER_BLOCK', 'FILEINFO', 'HBM_PEAK_GBS', 'ALGO_BYTES_PER_FILE', 'rank_blocks', '_init_gloo', 'TRAFFIC_NOTE', 'HEADLINE_KERNEL', 'PACKET_PIPELINE', '_pmc_traffic', 'cpu_baseline', '_dist_init', '_NUMA', '_bind_numa', '_gather_floats', '_max_over_ranks', 'BLOCK_DATA', 'zipf_sizes', '_fragmented_flags', 'live_bytes_total', '_ref_crc_fn', '_PCIE', 'pcie_ceiling', '_pcie_measure', '_cpu_budget', '_allcore_threads', '_cpu_model', 'e2e_blocks', '_compact_allcore']
+__all__ = ['ROOT', 'emit', 'DATA_SEED', 'FILE_SIZE', 'FILES_PER_BLOCK', 'FILEINFO', 'HBM_PEAK_GBS', 'ALGO_BYTES_PER_FILE', 'rank_blocks', '_init_gloo', 'TRAFFIC_NOTE', 'HEADLINE_KERNEL', 'PACKET_PIPELINE', '_pmc_traffic', 'cpu_baseline', '_dist_init', '_NUMA', '_bind_numa', '_gather_floats', 'per_rank', '_max_over_ranks', 'BLOCK_DATA', 'zipf_sizes', '_fragmented_flags', 'live_bytes_total', '_ref_crc_fn', '_PCIE', 'pcie_ceiling', '_pcie_measure', '_cpu_budget', '_allcore_threads', '_cpu_model', 'e2e_blocks', '_compact_allcore']
 
 
 FILE_SIZE = 65536
@@ -205,6 +205,19 @@ def _gather_floats(dist, world, v):
     out = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
     dist.all_gather(out, torch.tensor([float(v)], dtype=torch.float64))
     return [float(t.item()) for t in out]
+
+
+def per_rank(dist, world, elapsed_s, nbytes, div=2**30):
+    """Every rank's own rate over its own elapsed time (taken before the
+    max-over-ranks), so an N > 1 line can say which rank -- which GPU and link --
+    fell short: {values: [rank 0, rank 1, ...], elapsed_s, min, max, mean,
+    slowest_rank, fastest_rank, min_over_max}.  div: 2**30 for GiB/s, 1e9 for GB/s."""
+    els = _gather_floats(dist, world, elapsed_s)
+    vals = [float(nbytes) / e / div if e > 0 else 0.0 for e in els]
+    lo, hi = min(vals), max(vals)
+    return {"values": vals, "elapsed_s": els, "min": lo, "max": hi, "mean": sum(vals) / len(vals),
+            "slowest_rank": vals.index(lo), "fastest_rank": vals.index(hi),
+            "min_over_max": lo / hi if hi > 0 else 0.0}
 
 
 def _max_over_ranks(dist, v):
@@ -409,7 +422,7 @@ def e2e_blocks(ctx, dist, world, rank, nsub, inflight=3, cpu=None):
     """configs[4] end-to-end leg: pinned host block images -> H2D -> verify ->
     verdicts back, `inflight` blocks in flight (submit/wait), timed between
     barriers, max over ranks.  Returns (payload GiB/s over all ranks, PCIe GB/s,
-    elapsed s)."""
+    elapsed s, per-rank {payload GiB/s, PCIe GB/s} (per_rank))."""
     import tfs_amd.crc as crc
     nfiles, rec = FILES_PER_BLOCK, FILEINFO + FILE_SIZE
     blk_bytes = nfiles * rec
@@ -448,7 +461,10 @@ def e2e_blocks(ctx, dist, world, rank, nsub, inflight=3, cpu=None):
         hs.append(ctx.submit_verify(srcs[i % ndistinct].array, offs, lens, exps[i % ndistinct]))
     while hs:
         bad += ctx.wait(hs.pop(0))[2]
-    el = _max_over_ranks(dist, time.perf_counter() - t0)
+    el_local = time.perf_counter() - t0
+    el = _max_over_ranks(dist, el_local)
+    ranks = {"payload_GiBs": per_rank(dist, world, el_local, float(nsub) * nfiles * FILE_SIZE),
+             "pcie_GBs": per_rank(dist, world, el_local, float(nsub) * blk_bytes, 1e9)}
     if bad:
         raise SystemExit("e2e: mismatches on clean data")
     if cpu is not None:
@@ -458,7 +474,7 @@ def e2e_blocks(ctx, dist, world, rank, nsub, inflight=3, cpu=None):
     for b in (d_img, d_desc, d_crc):
         b.free()
     payload = float(world) * nsub * nfiles * FILE_SIZE
-    return payload / el / 2**30, float(world) * nsub * blk_bytes / el / 1e9, el
+    return payload / el / 2**30, float(world) * nsub * blk_bytes / el / 1e9, el, ranks
 
 
 def _compact_allcore(ora, src_ptrs, mo, ms, flags, nfiles, dest_cap, expect_len, live_bytes, blk_bytes, seconds):

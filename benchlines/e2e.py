@@ -23,8 +23,8 @@ def bench_e2e(args):
         # the same verify of one page-locked block image on the host CPU
         cpu_res["v"] = cpu_baseline(arr, offs, lens, exp, args.cpu_seconds,
                                     "64 KiB payloads of a page-locked block image")
-    gibs, pcie, el = e2e_blocks(ctx, dist, world, rank, nsub, inflight,
-                                cpu if rank == 0 and not args.no_cpu else None)
+    gibs, pcie, el, ranks = e2e_blocks(ctx, dist, world, rank, nsub, inflight,
+                                       cpu if rank == 0 and not args.no_cpu else None)
     res = {
         "metric": "GiB/s CRC32 verify end-to-end from pinned host block images (H2D included)",
         "value": gibs, "unit": "GiB/s", "n_gpus": world, "steps": nsub, "warmup": 2,
@@ -32,6 +32,7 @@ def bench_e2e(args):
         "dtype": "u8", "data": "synthetic 64 KiB files, 1024 per 64 MiB block",
         "config": {"workload": "pinned host blocks -> GPU verify, %d in flight, %d blocks" % (inflight, nsub)},
         "pcie_GBs": pcie,
+        "per_rank": ranks,
     }
     ceil = pcie_ceiling(ctx, dist=dist)
     res["roofline"] = {"bound": "pcie", "achieved": pcie / world, "peak": ceil["h2d_GBs"], "unit": "GB/s (per GPU)",

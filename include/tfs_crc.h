@@ -243,7 +243,11 @@ int tfs_block_compact_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_l
 /* The same data pass over many device-resident blocks in one launch (64-bit
  * offsets; one entry per live record, any order).  Writes FileInfo{offset_ =
  * new_offset, size_ = usize_ = size, flag_ = flag} | payload at d_dest +
- * dest_offset after checking id/size/crc as above. */
+ * dest_offset after checking id/size/crc as above.  `reserved`: 0, or
+ * TFS_COMPACT_JOB_EDGE when fewer than 128 readable bytes follow the record (the
+ * kernel then reads no byte past it; with 0 it may read up to 112 bytes past a
+ * record that ends at least 128 bytes before src_len, to write whole lines). */
+#define TFS_COMPACT_JOB_EDGE 1
 typedef struct tfs_compact_job {
   uint64_t src_offset;
   uint64_t dest_offset;

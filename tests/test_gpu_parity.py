@@ -486,6 +486,76 @@ def test_blocks_compact_pipelined_matches_oracle(gpu_ctx, oracle):
             k[0].free()
 
 
+def test_blocks_compact_zero_copy_groups(gpu_ctx, oracle):
+    """tfs_blocks_compact sends runs of up to 16 page-locked blocks to the GPU as one
+    multi-block record launch (round 5): 37 blocks in separate
+    page-locked allocations, a pageable block in the middle (the run breaks there
+    and it takes the per-block path), a block with every record deleted, records of
+    every size class and destination shift, records ending exactly at their image's
+    end (TFS_COMPACT_JOB_EDGE: no read past them), corrupted records in two blocks.
+    Every block's bytes, new RawMeta list, crc_ok, status, dest_len and n_live equal
+    the oracle's real_compact; run twice on the same context."""
+    import tfs_amd.crc as crc
+    rng = np.random.default_rng(4501)
+    nblk = 37
+    bufs, keep = [], []
+    try:
+        for b in range(nblk):
+            if b % 5 == 0:
+                sizes = [65536] * 30
+            else:
+                sizes = [int(x) for x in rng.choice([1, 3, 33, 100, 1023, 4096, 5001, 65536, 70001], 25)]
+            img, metas = _block_image(oracle, sizes, seed=4600 + b)
+            img = img[:int(metas["size"].astype(np.int64).sum())].copy()  # the last record ends the image
+            flags = np.zeros(len(sizes), np.int32)
+            flags[(b + 1) % 3::3] |= 1
+            if b == 9:
+                flags[:] = 1                                               # nothing live
+            if b in (5, 30):
+                live = np.nonzero(flags == 0)[0]
+                k = int(live[len(live) // 2])
+                img[int(metas[k]["offset"]) + 36 + int(metas[k]["size"]) // 3 - 12] ^= 0x40
+            if b == 17:
+                src_ptr, src_arr, srcbuf = img.ctypes.data, img, None      # pageable: breaks the run
+            else:
+                srcbuf = crc.PinnedBuffer(gpu_ctx, img.size)
+                srcbuf.array[:] = img
+                bufs.append(srcbuf)
+                src_ptr, src_arr = srcbuf.ptr, srcbuf.array
+            cap = int(metas["size"].astype(np.int64).sum()) + 64
+            dst = crc.PinnedBuffer(gpu_ctx, cap)
+            bufs.append(dst)
+            odest, doff, ook = _oracle_compact(oracle, img, metas, flags)
+            keep.append((src_ptr, img, metas, flags, dst, cap, odest, doff, ook))
+        for rep in range(2):
+            jobs = (crc.BlockJob * nblk)()
+            outs = []
+            for b, (src_ptr, img, metas, flags, dst, cap, odest, doff, ook) in enumerate(keep):
+                dst.array[:] = 0
+                ok = np.full(len(metas), 7, np.uint8)
+                dm = np.zeros(len(metas), crc.META_DTYPE)
+                outs.append((ok, dm))
+                j = jobs[b]
+                j.src_image, j.src_len, j.metas, j.flags, j.n = src_ptr, img.size, metas.ctypes.data, \
+                    flags.ctypes.data, len(metas)
+                j.dest_image, j.dest_cap, j.dest_metas, j.crc_ok = dst.ptr, cap, dm.ctypes.data, ok.ctypes.data
+            assert gpu_ctx.blocks_compact(jobs) == -1010
+            for b, (src_ptr, img, metas, flags, dst, cap, odest, doff, ook) in enumerate(keep):
+                ok, dm = outs[b]
+                live = np.nonzero((flags & 3) == 0)[0]
+                w = int(jobs[b].dest_len)
+                assert w == odest.size and jobs[b].n_live == live.size, (rep, b)
+                assert (dst.array[:w] == odest).all(), (rep, b)
+                assert (ok == ook).all(), (rep, b)
+                assert jobs[b].status == (-1010 if b in (5, 30) else 0), (rep, b)
+                assert (dm["file_id"][:live.size] == metas["file_id"][live]).all(), (rep, b)
+                assert (dm["offset"][:live.size] == doff[live]).all(), (rep, b)
+                assert (dm["size"][:live.size] == metas["size"][live]).all(), (rep, b)
+    finally:
+        for p in bufs:
+            p.free()
+
+
 def test_blocks_compact_zero_copy_matches_oracle(gpu_ctx, oracle, monkeypatch):
     """Page-locked source and destination images: the fused kernel reads the live
     records over PCIe and writes the new block in place (no whole-block DMA).

@@ -208,3 +208,12 @@ def test_bench_gpus_2_self_launched(tmp_path):
     kr = res["roofline"]["kernel_ms_per_rank"]
     assert len(kr["ms"]) == 2 and kr["min"] <= kr["max"] and res["roofline"]["kernel_ms_avg"] == kr["max"]
     assert "in turn" in res["end_to_end"]["roofline"]["peak_source"]
+    # each rank's own rates, so a shortfall names its rank
+    pr = res["per_rank"]
+    assert pr["local_rank"] == [0, 1] and pr["device"] == [0, 0] and len(pr["numa_node"]) == 2  # one shared GPU
+    dv = pr["device_GiBs"]
+    assert len(dv["values"]) == 2 and 0 < dv["min"] <= dv["max"] and dv["slowest_rank"] in (0, 1)
+    # the line's value is the max-over-ranks time, so it is at most world x the slowest rank's rate
+    assert res["value"] <= 2 * dv["min"] * 1.0001
+    er = res["end_to_end"]["per_rank"]
+    assert len(er["payload_GiBs"]["values"]) == 2 and er["pcie_GBs"]["min"] > 0

@@ -24,6 +24,14 @@ t = bench._max_over_ranks(dist, 1.0 + rank)
 assert t == float(world), t
 g = bench._gather_floats(dist, world, 10.0 + rank)  # per-rank kernel times of the roofline
 assert g == [10.0 + r for r in range(world)], g
+# per-rank rates of the N > 1 line (device-resident and end-to-end legs): rank r
+# "takes" 1 + r seconds for 2 GiB, so rank world-1 is the slowest and named as such
+pr = bench.per_rank(dist, world, 1.0 + rank, 2 * 2**30)
+assert len(pr["values"]) == world and pr["values"][0] == 2.0 and abs(pr["min"] - 2.0 / world) < 1e-12, pr
+assert pr["slowest_rank"] == world - 1 and pr["fastest_rank"] == 0 and pr["elapsed_s"][rank] == 1.0 + rank
+assert abs(pr["min_over_max"] - 1.0 / world) < 1e-12
+for k in ("values", "elapsed_s", "min", "max", "mean", "slowest_rank", "fastest_rank", "min_over_max"):
+    assert k in pr, k
 import torch
 allb = [None] * world
 dist.all_gather_object(allb, mine.tolist())

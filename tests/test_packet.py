@@ -174,10 +174,20 @@ def test_gpu_packet_seal_then_verify(gpu_ctx, oracle):
 
 
 @pytest.mark.gpu
-def test_gpu_packet_device_resident(gpu_ctx, oracle):
+@pytest.mark.parametrize("n_ok,form", [(200, "small"), (600, "one_pass"), (600, "three")])
+def test_gpu_packet_device_resident(gpu_ctx, oracle, n_ok, form, monkeypatch):
+    """Device-resident verify then seal of a stream with every status kind, at both
+    launch sizes: <= 256 frames (parse, latency form, finish) and more (round 5's
+    one-pass packet_files_kernel; `three`: the measurement build's three-launch
+    form of the same launch, TFS_CRC_VARIANT=51).  Statuses, CRCs, n_bad and the
+    sealed bytes equal the oracle's."""
     import tfs_amd.crc as crc_mod
+    if form == "three":
+        monkeypatch.setenv("TFS_CRC_VARIANT", "51")
+        gpu_ctx = crc_mod.Context(0)
+        monkeypatch.setenv("TFS_CRC_VARIANT", "0")
     rng = np.random.default_rng(13)
-    buf, frames, kinds = build_stream(rng, n=200)
+    buf, frames, kinds = build_stream(rng, n=n_ok)
     n = len(frames)
     d = np.zeros(n, crc_mod.PACKET_DESC_DTYPE)
     d["offset"] = [f[0] for f in frames]
@@ -200,6 +210,8 @@ def test_gpu_packet_device_resident(gpu_ctx, oracle):
     gpu_ctx.sync()
     ob, _, _ = o_seal(oracle, buf, frames)
     assert np.array_equal(d_base.download(np.uint8, len(b)), ob)
+    if form == "three":
+        gpu_ctx.close()
 
 
 @pytest.mark.gpu

@@ -34,6 +34,9 @@ hipError_t launch_crc_files(int mode, const uint8_t* base, const Desc* desc, uin
                             const SplitArgs* split);
 hipError_t launch_packet_parse(const uint8_t* base, const PacketDesc* pd, uint32_t n, int mode, Desc* desc,
                                int32_t* pre, hipStream_t stream);
+hipError_t launch_packet_files(uint8_t* base, const PacketDesc* pd, uint32_t n, int mode, const Tables* tg,
+                               uint32_t* crc, int32_t* status, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
+                               unsigned cap);
 hipError_t launch_packet_finish(uint8_t* base, const PacketDesc* pd, const Desc* desc, uint32_t n, int mode,
                                 const int32_t* pre, const uint8_t* ok, uint32_t* crc, int32_t* status,
                                 uint32_t* n_bad, hipStream_t stream);
@@ -211,6 +214,11 @@ struct CompactSlot {
   PinBuf h_aux, h_status, h_stage;
   std::vector<uint32_t> live_idx;
   tfs_block_job* job = nullptr;
+  // A zero-copy group (compact_enqueue_group): its jobs and, per job, where its
+  // records start in live_idx / the status array.
+  std::vector<tfs_block_job*> gjobs;
+  std::vector<uint32_t> gstart;
+  std::vector<CompactJob> gjob_list;
   bool busy = false;
   void release() {
     d_src.release(); d_dst.release(); d_aux.release();
@@ -270,6 +278,7 @@ struct tfs_crc_ctx {
   uint32_t foreign_next = 0;
   uint64_t foreign_launches = 0;
   int compact_slots = 8;  // blocks in flight in tfs_blocks_compact (TFS_CRC_COMPACT_SLOTS, 1..8)
+  uint32_t compact_group = 16;  // page-locked blocks per launch in tfs_blocks_compact (TFS_CRC_COMPACT_GROUP, 1..64)
 #ifdef TFS_CRC_MEASURE
   int variant = 0;  // kernel variant (TFS_CRC_VARIANT; measurement build only)
 #else
@@ -1152,6 +1161,7 @@ int tfs_crc32_ctx_create(int device, tfs_crc_ctx** out) {
   if (const char* v = getenv("TFS_CRC_VARIANT")) ctx->variant = atoi(v);
 #endif
   if (const char* v = getenv("TFS_CRC_COMPACT_SLOTS")) ctx->compact_slots = std::min(std::max(atoi(v), 1), kCompactSlots);
+  if (const char* v = getenv("TFS_CRC_COMPACT_GROUP")) ctx->compact_group = uint32_t(std::min(std::max(atoi(v), 1), 64));
   if (const char* v = getenv("TFS_CRC_RESIDENT")) ctx->resident = atoi(v) != 0;
   if (const char* v = getenv("TFS_CRC_RESIDENT_WGS")) ctx->res_grid = unsigned(std::min(std::max(atoi(v), 1), 256));
   if (const char* v = getenv("TFS_CRC_RESIDENT_IDLE_US")) ctx->res_idle_us = uint32_t(std::min(std::max(atoi(v), 1), 1000000));
@@ -1610,10 +1620,127 @@ static int compact_dma(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job, ui
   return TFS_SUCCESS;
 }
 
+// Zero-copy groups (round 5).  Blocks whose source and
+// destination images are both page-locked go to the GPU compact_group (16) at a time
+// as ONE multi-block record launch (tfs_compact_jobs_device's kernel, offsets
+// taken from the lowest image address of the group), instead of one launch per
+// block: a block is only ~341 live records, so per-block launches kept at most
+// 8 x 341 waves (176 workgroups) reading over PCIe, with a copy-engine hop
+// before and after each kernel.  One launch over 16 blocks fills the grid.
+// Measured against per-block launches (profiles/r05/host_compact_direction/):
+// the link then runs at 0.94 of its measured duplex rate instead of 0.88.
+
+bool zc_eligible(const tfs_crc_ctx* ctx, const tfs_block_job& job) {
+  return job.n && ctx->variant != kVariantDmaCompact && job.src_image && job.dest_image && job.metas && job.flags &&
+         is_pinned_host(job.src_image) && is_pinned_host(job.dest_image);
+}
+
+static int compact_enqueue_group(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* jobs, uint32_t count) {
+  cs.job = nullptr;
+  cs.gjobs.clear();
+  cs.gstart.clear();
+  cs.live_idx.clear();
+  struct Span {
+    uintptr_t src, dst;
+  };
+  std::vector<Span> sp(count);
+  uintptr_t sbase = UINTPTR_MAX, send = 0, dbase = UINTPTR_MAX;
+  for (uint32_t k = 0; k < count; ++k) {
+    tfs_block_job* job = &jobs[k];
+    job->status = TFS_SUCCESS;
+    job->dest_len = 0;
+    job->n_live = 0;
+    if (const int f = injected_fault(ctx)) {
+      job->status = f;
+      return f;
+    }
+    void *zs = nullptr, *zd = nullptr;
+    if (!host_dev_ptr(job->src_image, &zs) || !host_dev_ptr(job->dest_image, &zd))
+      return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "page-locked image without a device address");
+    sp[k] = Span{reinterpret_cast<uintptr_t>(zs), reinterpret_cast<uintptr_t>(zd)};
+    sbase = std::min(sbase, sp[k].src);
+    send = std::max<uintptr_t>(send, sp[k].src + job->src_len);
+    dbase = std::min(dbase, sp[k].dst);
+  }
+  // Host: each block's new offsets in iteration order (task.cpp:753-768), its
+  // RawMeta list, and one CompactJob per live record with group-relative offsets.
+  std::vector<CompactJob>& cj = cs.gjob_list;
+  cj.clear();
+  for (uint32_t k = 0; k < count; ++k) {
+    tfs_block_job* job = &jobs[k];
+    cs.gjobs.push_back(job);
+    cs.gstart.push_back(uint32_t(cs.live_idx.size()));
+    int64_t w = 0;
+    for (uint32_t i = 0; i < job->n; ++i) {
+      const tfs_raw_meta& m = job->metas[i];
+      if (m.size < TFS_FILEINFO_SIZE || m.offset < 0 || uint64_t(m.offset) + uint64_t(m.size) > job->src_len) {
+        job->status = TFS_EXIT_PARAMETER_ERROR;
+        return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "meta %u out of range", i);
+      }
+      if (job->flags[i] & (TFS_FI_DELETED | TFS_FI_INVALID)) continue;
+      if (uint64_t(w) + uint64_t(m.size) > job->dest_cap) {
+        job->status = TFS_EXIT_PARAMETER_ERROR;
+        return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "dest_cap %llu too small", (unsigned long long)job->dest_cap);
+      }
+      if (job->dest_metas) job->dest_metas[cs.live_idx.size() - cs.gstart.back()] =
+          tfs_raw_meta{m.file_id, int32_t(w), m.size};
+      const bool edge = uint64_t(m.offset) + uint64_t(m.size) + 128u > job->src_len;
+      cj.push_back(CompactJob{sp[k].src - sbase + uint64_t(m.offset), sp[k].dst - dbase + uint64_t(w), m.file_id,
+                              m.size, job->flags[i], int32_t(w), edge ? TFS_COMPACT_JOB_EDGE : 0});
+      cs.live_idx.push_back(i);
+      w += m.size;
+    }
+    job->dest_len = uint64_t(w);
+    job->n_live = uint32_t(cs.live_idx.size()) - cs.gstart.back();
+  }
+  const uint32_t nl = uint32_t(cj.size());
+  const size_t jb = size_t(nl) * sizeof(CompactJob), fb = size_t(nl) * 4;
+  HIP_TRY(ctx, cs.h_aux.reserve(jb + 64));
+  HIP_TRY(ctx, cs.d_aux.reserve(jb + 2 * fb + 128));
+  HIP_TRY(ctx, cs.h_status.reserve(fb + 4));
+  if (nl) {
+    memcpy(cs.h_aux.p, cj.data(), jb);
+    uint8_t* da = static_cast<uint8_t*>(cs.d_aux.p);
+    const CompactJob* d_jobs = reinterpret_cast<const CompactJob*>(da);
+    uint32_t* d_crc = reinterpret_cast<uint32_t*>(da + ((jb + 63) & ~size_t(63)));
+    int32_t* d_status = reinterpret_cast<int32_t*>(d_crc + nl);
+    HIP_TRY(ctx, hipMemcpyAsync(da, cs.h_aux.p, jb, hipMemcpyHostToDevice, cs.stream));
+    SCHED_LAUNCH(ctx, cs.stream, "compact_group",
+                 launch_compact_jobs(reinterpret_cast<const uint8_t*>(sbase), uint64_t(send - sbase), d_jobs, nl,
+                                     reinterpret_cast<uint8_t*>(dbase), ctx->d_tables, d_crc, d_status, nullptr, sched,
+                                     cs.stream, ctx->variant, throughput_cap(ctx), nullptr));
+    HIP_TRY(ctx, hipMemcpyAsync(cs.h_status.p, d_status, fb, hipMemcpyDeviceToHost, cs.stream));
+  }
+  if (!cs.done) HIP_TRY(ctx, hipEventCreateWithFlags(&cs.done, hipEventDisableTiming));
+  HIP_TRY(ctx, hipEventRecord(cs.done, cs.stream));
+  cs.busy = true;
+  return TFS_SUCCESS;
+}
+
 static int compact_finish(tfs_crc_ctx* ctx, CompactSlot& cs) {
   if (!cs.busy) return TFS_SUCCESS;
   cs.busy = false;
   HIP_TRY(ctx, hipEventSynchronize(cs.done));
+  if (!cs.gjobs.empty()) {  // a zero-copy group: statuses per job
+    const int32_t* st = static_cast<const int32_t*>(cs.h_status.p);
+    int worst = TFS_SUCCESS;
+    for (size_t k = 0; k < cs.gjobs.size(); ++k) {
+      tfs_block_job* job = cs.gjobs[k];
+      const uint32_t a = cs.gstart[k], e = k + 1 < cs.gjobs.size() ? cs.gstart[k + 1] : uint32_t(cs.live_idx.size());
+      if (job->crc_ok)
+        for (uint32_t i = 0; i < job->n; ++i) job->crc_ok[i] = 2;  // skipped unless live
+      uint32_t bad = 0;
+      for (uint32_t q = a; q < e; ++q) {
+        const bool ok = st[q] == TFS_SUCCESS;
+        bad += ok ? 0u : 1u;
+        if (job->crc_ok) job->crc_ok[cs.live_idx[q]] = ok ? 1 : 0;
+      }
+      job->status = bad ? TFS_EXIT_CHECK_CRC_ERROR : TFS_SUCCESS;
+      if (bad) worst = TFS_EXIT_CHECK_CRC_ERROR;
+    }
+    cs.gjobs.clear();
+    return worst;
+  }
   tfs_block_job* job = cs.job;
   const int32_t* st = static_cast<const int32_t*>(cs.h_status.p);
   if (job->crc_ok)
@@ -1641,15 +1768,33 @@ int tfs_blocks_compact(tfs_crc_ctx* ctx, tfs_block_job* jobs, uint32_t njobs) {
   auto note = [&](int rc) {
     if (rc != TFS_SUCCESS && (worst == TFS_SUCCESS || worst == TFS_EXIT_CHECK_CRC_ERROR)) worst = rc;
   };
-  for (uint32_t j = 0; j < njobs; ++j) {
-    CompactSlot& cs = ctx->cslots[j % uint32_t(ctx->compact_slots)];
+  uint32_t slot = 0;
+  for (uint32_t j = 0; j < njobs;) {
+    CompactSlot& cs = ctx->cslots[slot++ % uint32_t(ctx->compact_slots)];
     note(compact_finish(ctx, cs));
-    const int rc = compact_enqueue(ctx, cs, &jobs[j]);
+    // a run of up to kGroupBlocks zero-copy blocks goes as one launch
+    uint32_t g = 0;
+    while (g < ctx->compact_group && j + g < njobs && zc_eligible(ctx, jobs[j + g])) ++g;
+    const int rc = g >= 2 ? compact_enqueue_group(ctx, cs, &jobs[j], g) : compact_enqueue(ctx, cs, &jobs[j]);
+    const uint32_t took = g >= 2 ? g : 1u;
     if (rc != TFS_SUCCESS) {
-      jobs[j].status = rc;
+      if (took == 1) jobs[j].status = rc;
       note(rc);
       if (rc != TFS_EXIT_PARAMETER_ERROR) break;  // device error: stop issuing
+      if (took > 1) {  // a bad job inside a group: run the group's jobs one by one instead
+        for (uint32_t q = 0; q < took; ++q) {
+          CompactSlot& c1 = ctx->cslots[slot++ % uint32_t(ctx->compact_slots)];
+          note(compact_finish(ctx, c1));
+          const int r1 = compact_enqueue(ctx, c1, &jobs[j + q]);
+          if (r1 != TFS_SUCCESS) {
+            jobs[j + q].status = r1;
+            note(r1);
+            if (r1 != TFS_EXIT_PARAMETER_ERROR) return worst;
+          }
+        }
+      }
     }
+    j += took;
   }
   for (auto& cs : ctx->cslots) note(compact_finish(ctx, cs));
   return worst;
@@ -1727,10 +1872,15 @@ int tfs_block_compact(tfs_crc_ctx* ctx, const void* src_image, uint64_t src_len,
 }
 
 // ---- packet CRC ------------------------------------------------------------
-// parse (frame -> body descriptor + pre-status) -> CRC kernel over the bodies
-// (verify: seed TFS_PACKET_FLAG_V1 vs the header crc; seal: compute) ->
-// finish (statuses, seal writes the header crc).  `scratch` holds n Desc, n
-// pre-status and n ok bytes.
+// Throughput launches (more than kWgMaxFiles frames): one pass,
+// packet_files_kernel (round 5).  Smaller launches, and the measurement build's
+// TFS_CRC_VARIANT=51: parse (frame -> body descriptor + pre-status) -> CRC kernel
+// over the bodies (verify: seed TFS_PACKET_FLAG_V1 vs the header crc; seal:
+// compute) -> finish (statuses, seal writes the header crc).  `scratch` holds n
+// Desc, n pre-status and n ok bytes.
+#ifdef TFS_CRC_MEASURE
+constexpr int kVariantPacket3 = 51;  // the three-launch packet form for throughput launches (A/B)
+#endif
 
 static size_t packet_scratch_bytes(uint32_t n) { return size_t(n) * (sizeof(Desc) + 4 + 4 + 1) + 64; }
 
@@ -1742,6 +1892,16 @@ static int packet_enqueue(tfs_crc_ctx* ctx, int mode, const PacketDesc* d_pd, ui
   uint32_t* d_tmp_crc = reinterpret_cast<uint32_t*>(sp + size_t(n) * (sizeof(Desc) + 4));
   uint8_t* d_ok = sp + size_t(n) * (sizeof(Desc) + 8);
   uint32_t* crc = d_crc ? d_crc : d_tmp_crc;
+  bool one_pass = n > kWgMaxFiles;
+#ifdef TFS_CRC_MEASURE
+  if (ctx->variant == kVariantPacket3) one_pass = false;
+#endif
+  if (one_pass) {
+    SCHED_LAUNCH(ctx, st, "packet_files",
+                 launch_packet_files(d_base, d_pd, n, mode, ctx->d_tables, d_crc, d_status, d_n_bad, sched, st,
+                                     throughput_cap(ctx)));
+    return TFS_SUCCESS;
+  }
   HIP_TRY(ctx, launch_packet_parse(d_base, d_pd, n, mode, d_desc, d_pre, st));
   if (const int rc = files_launch(ctx, st, mode, d_base, d_desc, n, crc, mode == 1 ? d_ok : nullptr, nullptr,
                                   kPacketFlagV1))

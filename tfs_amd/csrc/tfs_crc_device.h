@@ -129,7 +129,7 @@ struct CompactJob {
   int32_t size;          // record size incl. the 36-byte FileInfo
   int32_t flag;          // FileInfo.flag_ to write
   int32_t new_offset;    // FileInfo.offset_ to write (offset inside the new block)
-  int32_t reserved;
+  int32_t reserved;      // bit 0 (TFS_COMPACT_JOB_EDGE): read no byte past the record
 };
 
 // Packet frames (BasePacket / BasePacketStreamer, src/common/base_packet*.{h,cpp}).

@@ -1336,9 +1336,12 @@ __device__ __forceinline__ HdrFields read_hdr(const uint8_t* rec) {
 // Func::crc(TFS_PACKET_FLAG_V1, body) == header crc; the send side
 // (BasePacket::copy/reply, base_packet.cpp:74,208) computes it.
 //
-// packet_parse_kernel turns frames into CRC descriptors (one thread per
-// frame); crc_files_kernel computes the bodies; packet_finish_kernel folds in
-// the verdicts (verify) or writes the CRC into the header (seal).
+// Throughput launches (more than kWgMaxFiles frames) run packet_files_kernel
+// below: one pass, the header parsed by the wave that checksums the body.  Small
+// launches keep three steps: packet_parse_kernel turns frames into CRC
+// descriptors (one thread per frame), the latency form computes the bodies, and
+// packet_finish_kernel folds in the verdicts (verify) or writes the CRC into the
+// header (seal).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t ld_le32(const uint8_t* p) {
   return uint32_t(p[0]) | uint32_t(p[1]) << 8 | uint32_t(p[2]) << 16 | uint32_t(p[3]) << 24;
@@ -1355,52 +1358,59 @@ __device__ __forceinline__ uint32_t ld32u(const uint8_t* p) {
   return *reinterpret_cast<gu32ucp>(reinterpret_cast<uintptr_t>(p));
 }
 
-// mode 1 = verify (desc.aux = stored crc), 0 = seal (desc.aux = seed).
+// One frame's header by the rules of getPacketInfo (base_packet_streamer.cpp:
+// 43-124) and the version decode() sees (base_packet.cpp:100-141): h = the first
+// 24 header bytes as little-endian dwords (only bytes inside `avail` are ever
+// used); d = the body to checksum (len 0 when there is none).  Returns the
+// frame's status, or kPacketPending when its body CRC decides it.
+// mode 1 = verify (d.aux = stored crc), 0 = seal (d.aux = seed).
+__device__ __forceinline__ int32_t parse_frame(const uint32_t (&h)[6], uint32_t avail, uint64_t off, int mode,
+                                               Desc& d) {
+  d = Desc{off, 0u, kPacketFlagV1};  // len 0: Func::crc returns the seed
+  if (avail < uint32_t(kPacketHeaderV0Size)) return kPacketIncomplete;  // getPacketInfo:49
+  const uint32_t flag = h[0];
+  const int32_t length = int32_t(h[1]);
+  const int32_t type = int16_t(uint16_t(h[2])), check = int16_t(uint16_t(h[2] >> 16));
+  const bool v1 = flag == kPacketFlagV1;
+  if (v1 && avail < uint32_t(kPacketHeaderV0Size + kPacketHeaderDiffSize))
+    return kPacketIncomplete;  // :65-69, the V1 header's last 12 bytes are not there yet
+  if ((flag != kPacketFlagV0 && !v1) || length <= 0 || length > kPacketMaxDataLen)
+    return kTfsError;  // :78-87 "stream error": broken
+  // _dataLen (:73,93) and the version decode() sees: _pcode = type (sign-extended)
+  // | check << 16 for V1 (:89), version = (_pcode >> 16) & 0xFFFF (base_packet.cpp:104).
+  const int64_t data_len = int64_t(length) + (v1 ? kPacketHeaderDiffSize : 0);
+  const uint32_t version = ((type < 0) ? 0xFFFFu : 0u) | (v1 ? uint32_t(uint16_t(check)) : 0u);
+  if (uint64_t(kPacketHeaderV0Size) + uint64_t(data_len) > avail) return kPacketIncomplete;
+  if (version < 1u) return kSuccess;  // decoded without a CRC check
+  if (data_len < kPacketHeaderDiffSize) return kTfsError;  // id/crc would be read past the packet
+  // decode: id (8) and crc (4) follow the V0 header, the body after them (:117-141).
+  d.offset = off + kPacketHeaderV0Size + kPacketHeaderDiffSize;
+  d.len = uint32_t(data_len - kPacketHeaderDiffSize);
+  d.aux = mode == 1 ? h[5] : kPacketFlagV1;  // avail >= 24 here
+  return kPacketPending;
+}
+
+// Small launches (<= kWgMaxFiles frames, the latency form) and the measurement
+// build's three-launch form: one thread per frame turns frames into CRC
+// descriptors and pre-statuses.
 __global__ void packet_parse_kernel(const uint8_t* __restrict__ base, const PacketDesc* __restrict__ pd, uint32_t n,
                                     int mode, Desc* __restrict__ desc, int32_t* __restrict__ pre) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const PacketDesc f = pd[i];
-  Desc d{f.offset, 0u, kPacketFlagV1};  // len 0: Func::crc returns the seed, which then "matches"
-  int32_t st = kSuccess;
   const uint8_t* p = base + f.offset;
-  if (f.len < uint32_t(kPacketHeaderV0Size)) {
-    st = kPacketIncomplete;  // getPacketInfo:49
-  } else {
-    // A frame of at least 24 bytes (every frame whose crc field is read) takes its
-    // header as one 16-byte and one 4-byte load; shorter ones byte by byte.
-    const bool wide = f.len >= uint32_t(kPacketHeaderV0Size + kPacketHeaderDiffSize);
-    const u32x4 h = wide ? ld128u(p) : u32x4{ld_le32(p), ld_le32(p + 4), ld_le32(p + 8), 0u};
-    const uint32_t flag = h.x;
-    const int32_t length = int32_t(h.y);
-    const int32_t type = int16_t(uint16_t(h.z)), check = int16_t(uint16_t(h.z >> 16));
-    const bool v1 = flag == kPacketFlagV1;
-    if (v1 && f.len < uint32_t(kPacketHeaderV0Size + kPacketHeaderDiffSize)) {
-      st = kPacketIncomplete;  // :65-69, the V1 header's last 12 bytes are not there yet
-    } else if ((flag != kPacketFlagV0 && !v1) || length <= 0 || length > kPacketMaxDataLen) {
-      st = kTfsError;  // :78-87 "stream error": broken
-    } else {
-      // _dataLen (:73,93) and the version decode() sees: _pcode = type (sign-
-      // extended) | check << 16 for V1 (:89), version = (_pcode >> 16) & 0xFFFF (base_packet.cpp:104).
-      const int64_t data_len = int64_t(length) + (v1 ? kPacketHeaderDiffSize : 0);
-      const uint32_t version = ((type < 0) ? 0xFFFFu : 0u) | (v1 ? uint32_t(uint16_t(check)) : 0u);
-      if (uint64_t(kPacketHeaderV0Size) + uint64_t(data_len) > f.len) {
-        st = kPacketIncomplete;
-      } else if (version >= 1u) {
-        if (data_len < kPacketHeaderDiffSize) {
-          st = kTfsError;  // id/crc would be read past the packet
-        } else {
-          // decode: id (8) and crc (4) follow the V0 header, the body after them (:117-141).
-          d.offset = f.offset + kPacketHeaderV0Size + kPacketHeaderDiffSize;
-          d.len = uint32_t(data_len - kPacketHeaderDiffSize);
-          d.aux = mode == 1 ? ld32u(p + kPacketHeaderV0Size + 8) : kPacketFlagV1;  // f.len >= 24 here
-          st = kPacketPending;
-        }
-      }
-    }
+  // A frame of at least 24 bytes takes its header as one 16-byte and two 4-byte
+  // loads; shorter ones byte by byte (never a byte past `avail`).
+  uint32_t h[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+  if (f.len >= uint32_t(kPacketHeaderV0Size + kPacketHeaderDiffSize)) {
+    const u32x4 v = ld128u(p);
+    h[0] = v.x, h[1] = v.y, h[2] = v.z, h[3] = v.w, h[4] = ld32u(p + 16), h[5] = ld32u(p + 20);
+  } else if (f.len >= uint32_t(kPacketHeaderV0Size)) {
+    h[0] = ld_le32(p), h[1] = ld_le32(p + 4), h[2] = ld_le32(p + 8);
   }
+  Desc d;
+  pre[i] = parse_frame(h, f.len, f.offset, mode, d);
   desc[i] = d;
-  pre[i] = st;
 }
 
 __global__ void packet_finish_kernel(uint8_t* __restrict__ base, const PacketDesc* __restrict__ pd,
@@ -1511,6 +1521,7 @@ struct CRec {
   int32_t pre;  // kSuccess, or the status decided before reading (size / range)
   uint32_t plen;  // payload bytes this unit covers (size - 36 for a whole record)
   uint32_t kind;  // 0 a whole record, 1 a payload segment of a split record, 2 a split record's head
+  uint32_t edge;  // 1: no byte past the record may be read (CompactJob.reserved bit 0)
 };
 
 template <bool WIDE, bool VERIFY = false>
@@ -1518,6 +1529,7 @@ __device__ __forceinline__ CRec load_crec(uint32_t f, uint64_t src_len, const Ra
                                           const int32_t* __restrict__ flags, const int64_t* __restrict__ dest_off,
                                           const CompactJob* __restrict__ jobs) {
   CRec r;
+  r.edge = 0u;
   bool range_ok;
   if (VERIFY && !WIDE) {
     const RawMeta m = metas[f];
@@ -1528,6 +1540,7 @@ __device__ __forceinline__ CRec load_crec(uint32_t f, uint64_t src_len, const Ra
     const CompactJob j = jobs[f];
     r.soff = j.src_offset, r.doff = j.dest_offset, r.fid = j.file_id;
     r.size = j.size, r.flag = j.flag, r.new_off = j.new_offset;
+    r.edge = uint32_t(j.reserved) & 1u;
     range_ok = r.soff + uint64_t(uint32_t(r.size)) <= src_len;
   } else {
     const RawMeta m = metas[f];
@@ -1570,6 +1583,7 @@ __device__ __forceinline__ CRec load_cunit(uint32_t f, uint32_t njobs, uint64_t 
   r.pre = kSuccess;
   r.plen = u.len;
   r.kind = 1u;
+  r.edge = 0u;
   return r;
 }
 
@@ -1597,7 +1611,7 @@ __device__ __forceinline__ FileGeo<kRun> crec_geo(const CRec& r, const uint8_t* 
   const uint8_t* rec = src + r.soff;
   delta = intptr_t(dst + r.doff) - intptr_t(rec);
   uint32_t aoff = 0u;
-  if (DA && r.soff + kFileInfoSize + uint64_t(r.plen) + 128u <= src_len)
+  if (DA && !r.edge && r.soff + kFileInfoSize + uint64_t(r.plen) + 128u <= src_len)
     aoff = uint32_t(-(delta & ~intptr_t(15))) & 127u;
   return make_geo<kRun>(rec + kFileInfoSize, r.plen, 0u, aoff);
 }
@@ -1889,6 +1903,113 @@ __global__ void __launch_bounds__(256) compact_seg_fold_kernel(const CompactJob*
   }
 }
 
+// Packet frames in one pass (round 5): the throughput form of
+// BasePacket::decode (verify, MODE 1) and BasePacket::copy + encode (seal, MODE 0)
+// over n frames.  A wave takes frames by the file kernel's chunked tickets; it
+// loads a frame's 24 header bytes (lanes 0..23, one byte each, only bytes inside
+// the frame's `avail`) a frame ahead, parses them by getPacketInfo + decode's
+// rules (parse_frame) when that frame comes up, checksums the body with seed
+// TFS_PACKET_FLAG_V1 and writes the frame's final status and CRC itself (verify:
+// against the header's crc_; seal: the CRC stored into the V1 header at +20).  No
+// parse or finish launch and no descriptor scratch.  Bodies stay whole: a
+// WriteDataMessage carries at most one 2 MiB segment (MAX_SEGMENT_SIZE,
+// internal.h:157), so no body makes a launch's tail the way a 64 MiB file can.
+template <int MODE>
+__global__ void __launch_bounds__(kBlock) packet_files_kernel(uint8_t* __restrict__ base,
+                                                              const PacketDesc* __restrict__ pd, uint32_t n,
+                                                              const Tables* __restrict__ tg, uint32_t* out_crc,
+                                                              int32_t* out_status, uint32_t* n_bad, uint32_t* sched) {
+  constexpr int RUN = kRun, PF = kPF;
+  __shared__ uint32_t lds_tables[LdsLayout<kLY>::bytes / 4];
+  load_tables<RUN, false, kLY>(lds_tables, tg);
+  const int lane = threadIdx.x & (kWave - 1);
+  const LaneBase lb = lane_base_of(lane);
+  const uint32_t wpb = kBlock / kWave;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const uintptr_t junk = reinterpret_cast<uintptr_t>(tg->slice);
+  FileCursor<kIL, kCF, kTS> frames;
+  frames.init(sched, n, blockIdx.x & 7u, gridDim.x * wpb, blockIdx.x * wpb + wave);
+  frames.start(lane);
+  struct Issued {  // a frame whose header bytes are in flight
+    uint64_t off;
+    uint32_t avail, hb;  // hb: this lane's header byte (lanes 0..23)
+  };
+  struct Frame {
+    Desc d;
+    int32_t pre;
+    uint32_t flag;
+  };
+  auto issue = [&](uint32_t u) -> Issued {
+    const PacketDesc f = pd[u];
+    Issued x{f.offset, f.len, 0u};
+    if (uint32_t(lane) < 24u && uint32_t(lane) < f.len) x.hb = ld8(reinterpret_cast<uintptr_t>(base + f.offset) + lane);
+    return x;
+  };
+  auto parse = [&](const Issued& x) -> Frame {
+    uint32_t h[6];
+#pragma unroll
+    for (uint32_t k = 0; k < 6u; ++k) h[k] = hdr_dword(x.hb, k);
+    Frame r;
+    r.flag = h[0];
+    r.pre = parse_frame(h, x.avail, x.off, MODE, r.d);
+    return r;
+  };
+  uint32_t bad = 0;
+  do {  // `break` = this wave has no (more) frames; every wave reaches launch_exit
+    uint32_t f = frames.take(lane);
+    if (f >= n) break;
+    uint32_t fn = frames.take(lane);
+    Frame cur = parse(issue(f));
+    FileGeo<RUN> g = make_geo<RUN>(base + cur.d.offset, cur.d.len, kPacketFlagV1);
+    Head<RUN> h = load_head<RUN>(g, lane);
+    uint4 buf[PF][RUN / 16];
+    load_ring<RUN, PF, kNT>(g, lane, buf, junk);
+    Issued nx = fn < n ? issue(fn) : Issued{0, 0u, 0u};
+    for (;;) {
+      const bool more = fn < n;
+      const uint32_t c = g.nstripes ? lane_chain<RUN, PF, kNT, kLY>(lds_tables, lb, g, h, buf, lane, junk) : 0u;
+      // The next frame's header is in; its body loads go out before this one is finished.
+      Frame ncur = cur;
+      FileGeo<RUN> ng = g;
+      Head<RUN> nh = h;
+      uint32_t fnn = n;
+      if (more) {
+        ncur = parse(nx);
+        ng = make_geo<RUN>(base + ncur.d.offset, ncur.d.len, kPacketFlagV1);
+        nh = load_head<RUN>(ng, lane);
+        load_ring<RUN, PF, kNT>(ng, lane, buf, junk);
+        fnn = frames.take(lane);
+        if (fnn < n) nx = issue(fnn);
+      }
+      const uint32_t crc = finish_file<RUN, kLY>(lds_tables, lb, g, h, c, lane);
+      if (lane == 0) {
+        int32_t st = cur.pre;
+        uint32_t co = 0u;
+        if (st == kPacketPending) {
+          co = crc;
+          if (MODE == 1) {
+            st = crc == cur.d.aux ? kSuccess : kExitCheckCrcError;  // decode returns false (:142-148)
+          } else {
+            st = kSuccess;  // seal: only V1 headers carry a crc (base_packet_streamer.cpp:166-175)
+            if (cur.flag == kPacketFlagV1) st32u(reinterpret_cast<uintptr_t>(base + cur.d.offset) - 4u, crc);
+          }
+        }
+        if (out_crc) out_crc[f] = co;
+        out_status[f] = st;
+        bad += st != kSuccess ? 1u : 0u;
+      }
+      if (!more) break;
+      f = fn;
+      fn = fnn;
+      cur = ncur;
+      g = ng;
+      h = nh;
+    }
+  } while (false);
+  if (lane == 0 && bad && n_bad) atomicAdd(n_bad, bad);
+  if (lane == 0) launch_exit(sched, gridDim.x * wpb, nullptr, 0u);
+}
+
 // Synthetic payload bytes: word i = splitmix64(seed + (first_word + i + 1) * GOLDEN)
 // (same stream as tfs_amd/synth.py).
 __global__ void synth_fill_kernel(uint64_t* __restrict__ dst, uint64_t nwords, uint64_t seed, uint64_t first_word) {
@@ -2109,6 +2230,20 @@ hipError_t launch_packet_parse(const uint8_t* base, const PacketDesc* pd, uint32
                                int32_t* pre, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(packet_parse_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, base, pd, n, mode, desc, pre);
+  return hipGetLastError();
+}
+
+hipError_t launch_packet_files(uint8_t* base, const PacketDesc* pd, uint32_t n, int mode, const Tables* tg,
+                               uint32_t* crc, int32_t* status, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
+                               unsigned cap) {
+  if (n == 0) return hipSuccess;
+  if (!sched) return hipErrorInvalidValue;
+  if (mode == 1)
+    hipLaunchKernelGGL(packet_files_kernel<1>, dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, base, pd, n, tg, crc,
+                       status, n_bad, sched);
+  else
+    hipLaunchKernelGGL(packet_files_kernel<0>, dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, base, pd, n, tg, crc,
+                       status, n_bad, sched);
   return hipGetLastError();
 }
 
