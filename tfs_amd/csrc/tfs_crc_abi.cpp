@@ -2052,7 +2052,7 @@ static int packet_host(tfs_crc_ctx* ctx, int mode, const tfs_packet_desc* d, uin
   HIP_TRY(ctx, s->d_ok.reserve(size_t(n) * 4));  // statuses
   HIP_TRY(ctx, s->d_bad.reserve(4));
   HIP_TRY(ctx, s->h_crc.reserve(size_t(n) * 4));
-  HIP_TRY(ctx, s->h_ok.reserve(size_t(n) * 8));  // statuses, then (seal) the parse pre-statuses
+  HIP_TRY(ctx, s->h_ok.reserve(size_t(n) * 4));  // statuses
   HIP_TRY(ctx, s->h_bad.reserve(4));
   HIP_TRY(ctx, hipMemcpyAsync(s->d_desc.p, d, size_t(n) * sizeof(PacketDesc), hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(ctx, hipMemsetAsync(s->d_bad.p, 0, 4, ctx->stream));
@@ -2062,10 +2062,6 @@ static int packet_host(tfs_crc_ctx* ctx, int mode, const tfs_packet_desc* d, uin
   if (rc) return rc;
   HIP_TRY(ctx, hipMemcpyAsync(s->h_crc.p, s->d_crc.p, size_t(n) * 4, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipMemcpyAsync(s->h_ok.p, s->d_ok.p, size_t(n) * 4, hipMemcpyDeviceToHost, ctx->stream));
-  if (mode == 0)
-    HIP_TRY(ctx, hipMemcpyAsync(static_cast<int32_t*>(s->h_ok.p) + n,
-                                static_cast<uint8_t*>(s->d_aux.p) + size_t(n) * sizeof(Desc), size_t(n) * 4,
-                                hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipMemcpyAsync(s->h_bad.p, s->d_bad.p, 4, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   const uint32_t* hc = static_cast<const uint32_t*>(s->h_crc.p);
@@ -2076,11 +2072,14 @@ static int packet_host(tfs_crc_ctx* ctx, int mode, const tfs_packet_desc* d, uin
   if (n_bad) *n_bad = bad;
   if (mode == 0) {
     // Seal: the device wrote the crc into its copy of each checked V1 header;
-    // store the same four bytes into the caller's frames.
-    const int32_t* pre = hs + n;
+    // store the same four bytes into the caller's frames (the frames it checked:
+    // the same header rules on the host bytes, packet_parse_host).
     uint8_t* hb = static_cast<uint8_t*>(base);
     for (uint32_t i = 0; i < n; ++i) {
-      if (pre[i] != kPacketPending) continue;
+      Desc x;
+      int32_t pre;
+      packet_parse_host(hb, d[i], mode, &x, &pre);
+      if (pre != kPacketPending) continue;
       uint8_t* p = hb + d[i].offset;
       const uint32_t flag = uint32_t(p[0]) | uint32_t(p[1]) << 8 | uint32_t(p[2]) << 16 | uint32_t(p[3]) << 24;
       if (flag != TFS_PACKET_FLAG_V1) continue;

@@ -9,7 +9,7 @@ interleaves, round by round:
   three      the same call through the three-launch form (TFS_CRC_VARIANT=51:
              parse, crc_files_kernel, finish)
   verify     tfs_crc32_verify_device over the same frames' bodies (descriptors
-             built on the host, expected = the sealed CRCs): the headline kernel
+             built on the host, expected = the bodies' seed-0 CRCs): the headline kernel
              on exactly these bytes, no packet work at all
 
 each timed with HIP events around REPS launches on its own context's stream.
@@ -57,9 +57,16 @@ def main():
     ctx.packet_seal_device(d_pd, n, img, d_crc, d_st)
     ctx.sync()
     sealed = d_crc.download(np.uint32, n)
+    # verify checks Func::crc(0, body) (seed 0, as for a FileInfo payload): its
+    # expected values are the bodies' zero-seeded CRCs, computed on the device
     vd = np.zeros(n, crc.DESC_DTYPE)
-    vd["offset"], vd["len"], vd["aux"] = off + 24, body, sealed
+    vd["offset"], vd["len"] = off + 24, body
     d_vd = crc.DeviceBuffer(ctx, vd.nbytes).upload(vd)
+    d_z = crc.DeviceBuffer(ctx, 4 * n)
+    ctx.batch_device(d_vd, n, img, d_z)
+    ctx.sync()
+    vd["aux"] = d_z.download(np.uint32, n)
+    d_vd.upload(vd)
     d_ok = crc.DeviceBuffer(ctx, n)
     # every form agrees before timing: no bad frame, the same CRCs
     for name, c in (("one_pass", ctx), ("three", c3)):
