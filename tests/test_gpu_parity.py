@@ -486,16 +486,21 @@ def test_blocks_compact_pipelined_matches_oracle(gpu_ctx, oracle):
             k[0].free()
 
 
-def test_blocks_compact_zero_copy_groups(gpu_ctx, oracle):
-    """tfs_blocks_compact sends runs of up to 16 page-locked blocks to the GPU as one
+def test_blocks_compact_zero_copy_groups(gpu_ctx, oracle, monkeypatch):
+    """tfs_blocks_compact sends runs of up to 64 page-locked blocks to the GPU as one
     multi-block record launch (round 5): 37 blocks in separate
     page-locked allocations, a pageable block in the middle (the run breaks there
     and it takes the per-block path), a block with every record deleted, records of
     every size class and destination shift, records ending exactly at their image's
     end (TFS_COMPACT_JOB_EDGE: no read past them), corrupted records in two blocks.
     Every block's bytes, new RawMeta list, crc_ok, status, dest_len and n_live equal
-    the oracle's real_compact; run twice on the same context."""
+    the oracle's real_compact; run twice on the same context, and once more on a
+    context of 8 blocks per launch (TFS_CRC_COMPACT_GROUP), where runs are cut by
+    the group size too."""
     import tfs_amd.crc as crc
+    monkeypatch.setenv("TFS_CRC_COMPACT_GROUP", "8")
+    ctx8 = crc.Context(0)
+    monkeypatch.delenv("TFS_CRC_COMPACT_GROUP")
     rng = np.random.default_rng(4501)
     nblk = 37
     bufs, keep = [], []
@@ -527,7 +532,7 @@ def test_blocks_compact_zero_copy_groups(gpu_ctx, oracle):
             bufs.append(dst)
             odest, doff, ook = _oracle_compact(oracle, img, metas, flags)
             keep.append((src_ptr, img, metas, flags, dst, cap, odest, doff, ook))
-        for rep in range(2):
+        for rep, ctx in enumerate((gpu_ctx, gpu_ctx, ctx8)):
             jobs = (crc.BlockJob * nblk)()
             outs = []
             for b, (src_ptr, img, metas, flags, dst, cap, odest, doff, ook) in enumerate(keep):
@@ -539,7 +544,7 @@ def test_blocks_compact_zero_copy_groups(gpu_ctx, oracle):
                 j.src_image, j.src_len, j.metas, j.flags, j.n = src_ptr, img.size, metas.ctypes.data, \
                     flags.ctypes.data, len(metas)
                 j.dest_image, j.dest_cap, j.dest_metas, j.crc_ok = dst.ptr, cap, dm.ctypes.data, ok.ctypes.data
-            assert gpu_ctx.blocks_compact(jobs) == -1010
+            assert ctx.blocks_compact(jobs) == -1010
             for b, (src_ptr, img, metas, flags, dst, cap, odest, doff, ook) in enumerate(keep):
                 ok, dm = outs[b]
                 live = np.nonzero((flags & 3) == 0)[0]
@@ -554,6 +559,7 @@ def test_blocks_compact_zero_copy_groups(gpu_ctx, oracle):
     finally:
         for p in bufs:
             p.free()
+        ctx8.close()
 
 
 def test_blocks_compact_zero_copy_matches_oracle(gpu_ctx, oracle, monkeypatch):

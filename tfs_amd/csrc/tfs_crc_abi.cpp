@@ -278,7 +278,7 @@ struct tfs_crc_ctx {
   uint32_t foreign_next = 0;
   uint64_t foreign_launches = 0;
   int compact_slots = 8;  // blocks in flight in tfs_blocks_compact (TFS_CRC_COMPACT_SLOTS, 1..8)
-  uint32_t compact_group = 16;  // page-locked blocks per launch in tfs_blocks_compact (TFS_CRC_COMPACT_GROUP, 1..64)
+  uint32_t compact_group = 64;  // page-locked blocks per launch in tfs_blocks_compact (TFS_CRC_COMPACT_GROUP, 1..256)
 #ifdef TFS_CRC_MEASURE
   int variant = 0;  // kernel variant (TFS_CRC_VARIANT; measurement build only)
 #else
@@ -1161,7 +1161,7 @@ int tfs_crc32_ctx_create(int device, tfs_crc_ctx** out) {
   if (const char* v = getenv("TFS_CRC_VARIANT")) ctx->variant = atoi(v);
 #endif
   if (const char* v = getenv("TFS_CRC_COMPACT_SLOTS")) ctx->compact_slots = std::min(std::max(atoi(v), 1), kCompactSlots);
-  if (const char* v = getenv("TFS_CRC_COMPACT_GROUP")) ctx->compact_group = uint32_t(std::min(std::max(atoi(v), 1), 64));
+  if (const char* v = getenv("TFS_CRC_COMPACT_GROUP")) ctx->compact_group = uint32_t(std::min(std::max(atoi(v), 1), 256));
   if (const char* v = getenv("TFS_CRC_RESIDENT")) ctx->resident = atoi(v) != 0;
   if (const char* v = getenv("TFS_CRC_RESIDENT_WGS")) ctx->res_grid = unsigned(std::min(std::max(atoi(v), 1), 256));
   if (const char* v = getenv("TFS_CRC_RESIDENT_IDLE_US")) ctx->res_idle_us = uint32_t(std::min(std::max(atoi(v), 1), 1000000));
@@ -1621,14 +1621,14 @@ static int compact_dma(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job, ui
 }
 
 // Zero-copy groups (round 5).  Blocks whose source and
-// destination images are both page-locked go to the GPU compact_group (16) at a time
+// destination images are both page-locked go to the GPU compact_group (64) at a time
 // as ONE multi-block record launch (tfs_compact_jobs_device's kernel, offsets
 // taken from the lowest image address of the group), instead of one launch per
 // block: a block is only ~341 live records, so per-block launches kept at most
 // 8 x 341 waves (176 workgroups) reading over PCIe, with a copy-engine hop
-// before and after each kernel.  One launch over 16 blocks fills the grid.
-// Measured against per-block launches (profiles/r05/host_compact_direction/):
-// the link then runs at 0.94 of its measured duplex rate instead of 0.88.
+// before and after each kernel.  Blocks per launch, measured in one process
+// (tools/compact_group_probe.py, profiles/r05/host_compact_groups/): 1 -> 0.88 of
+// the link's measured duplex rate, 8 -> 0.93, 16 -> 0.94, 32 -> 0.95, 64 -> 0.96.
 
 bool zc_eligible(const tfs_crc_ctx* ctx, const tfs_block_job& job) {
   return job.n && ctx->variant != kVariantDmaCompact && job.src_image && job.dest_image && job.metas && job.flags &&
@@ -1772,7 +1772,7 @@ int tfs_blocks_compact(tfs_crc_ctx* ctx, tfs_block_job* jobs, uint32_t njobs) {
   for (uint32_t j = 0; j < njobs;) {
     CompactSlot& cs = ctx->cslots[slot++ % uint32_t(ctx->compact_slots)];
     note(compact_finish(ctx, cs));
-    // a run of up to kGroupBlocks zero-copy blocks goes as one launch
+    // a run of up to compact_group zero-copy blocks goes as one launch
     uint32_t g = 0;
     while (g < ctx->compact_group && j + g < njobs && zc_eligible(ctx, jobs[j + g])) ++g;
     const int rc = g >= 2 ? compact_enqueue_group(ctx, cs, &jobs[j], g) : compact_enqueue(ctx, cs, &jobs[j]);
