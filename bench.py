@@ -59,7 +59,7 @@ def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=16)
-    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--blocks", type=int, default=1024, help="resident blocks per GPU (1024 = 1 M files)")
     p.add_argument("--compact-blocks", type=int, default=4096, help="blocks per GPU for --workload compact/e2e")
     p.add_argument("--file-blocks", type=int, default=32, help="blocks on disk per GPU for --workload compact_files")

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-__all__ = ['ROOT', 'emit', 'DATA_SEED', 'FILE_SIZE', 'FILES_PER_BLOCK', 'FILEINFO', 'HBM_PEAK_GBS', 'ALGO_BYTES_PER_FILE', 'rank_blocks', '_init_gloo', 'TRAFFIC_NOTE', 'HEADLINE_KERNEL', 'PACKET_PIPELINE', '_pmc_traffic', 'cpu_baseline', '_dist_init', '_NUMA', '_bind_numa', '_gather_floats', 'per_rank', '_max_over_ranks', 'BLOCK_DATA', 'zipf_sizes', '_fragmented_flags', 'live_bytes_total', '_ref_crc_fn', '_PCIE', 'pcie_ceiling', '_pcie_measure', '_cpu_budget', '_allcore_threads', '_cpu_model', 'e2e_blocks', '_compact_allcore']
+__all__ = ['ROOT', 'emit', 'DATA_SEED', 'FILE_SIZE', 'FILES_PER_BLOCK', 'FILEINFO', 'HBM_PEAK_GBS', 'ALGO_BYTES_PER_FILE', 'rank_blocks', '_init_gloo', 'TRAFFIC_NOTE', 'HEADLINE_KERNEL', 'PACKET_KERNEL', '_pmc_traffic', 'cpu_baseline', '_dist_init', '_NUMA', '_bind_numa', '_gather_floats', 'per_rank', '_max_over_ranks', 'BLOCK_DATA', 'zipf_sizes', '_fragmented_flags', 'live_bytes_total', '_ref_crc_fn', '_PCIE', 'pcie_ceiling', '_pcie_measure', '_cpu_budget', '_allcore_threads', '_cpu_model', 'e2e_blocks', '_compact_allcore']
 
 
 FILE_SIZE = 65536
@@ -57,11 +57,10 @@ TRAFFIC_NOTE = ("quoted: HBM bytes per launch from the committed rocprofv3 PMC p
                 "run; null when this run is not the profiled configuration")
 
 
-HEADLINE_KERNEL = "crc_files_kernel<1, 16, 5, true, true, true, 1, false, true, 1, false, false, 4, 3, 1"
+HEADLINE_KERNEL = "crc_files_kernel<1, 4, 3>"
 
 
-PACKET_PIPELINE = ("packet pipeline: packet_parse_kernel + crc_files_kernel<1, ..., 4, 3, 1> + "
-                   "packet_finish_kernel")
+PACKET_KERNEL = "packet_files_kernel<1>"
 
 
 def _pmc_traffic(rel, kernel, applies):

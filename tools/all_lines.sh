@@ -12,5 +12,5 @@ run default && run zipf --workload zipf && run packet --workload packet && run c
   && run block_verify_device --workload block_verify_device && run compact --workload compact \
   && run block_verify --workload block_verify && run e2e --workload e2e && run ec --workload ec \
   && run compact_files --workload compact_files \
-  && run loopback --workload loopback
+  && run loopback --workload loopback && run small_bodies --workload small_bodies
 echo "all_lines done"

@@ -34,7 +34,7 @@ def kernel_stats(path, kernel):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kernel", default="crc_files_kernel<1, 16, 5, true, true, true, 1, false, true, 1, false, false, 4, 3")
+    ap.add_argument("--kernel", default="crc_files_kernel<1, 4, 3>")
     ap.add_argument("--tag", required=True)
     ap.add_argument("--algo-bytes", type=float, default=1048576.0 * 65557)
     ap.add_argument("--stats", required=True, help="kernel_stats.csv of rocprofv3 --stats on the same command")
