@@ -7,8 +7,7 @@ import sys
 
 from conftest import ROOT
 
-KERNEL = ("void tfscrc::crc_files_kernel<1, 16, 5, true, true, true, 1, false, true, 1, false, false, 4, 3>"
-          "(unsigned char const*)")
+KERNEL = "void tfscrc::crc_files_kernel<1, 4, 3>(unsigned char const*)"
 HDR = ('"Correlation_Id","Dispatch_Id","Agent_Id","Queue_Id","Process_Id","Thread_Id","Grid_Size","Kernel_Id",'
        '"Kernel_Name","Workgroup_Size","LDS_Block_Size","Scratch_Size","VGPR_Count","Accum_VGPR_Count","SGPR_Count",'
        '"Counter_Name","Counter_Value","Start_Timestamp","End_Timestamp"')
