@@ -2,6 +2,8 @@
 # Round 5, run 7: host compaction at 64 blocks per launch (the group test at 64 and 8),
 # blocks per launch 16..256, then the PMC passes of every device-resident line
 # on the pruned kernel set (profiles/r05/cmds/pmc.sh).
+# (As run: bash ignores an assignment to GROUPS, so the probe ran its default
+# list 1..64; the probe now reads CG_GROUPS.)
 set -u
 O=gpurun_out/r05/run7
 mkdir -p $O

@@ -6,7 +6,9 @@ BASELINE configs[3]'s job list (fragmented 64 MiB blocks of 64 KiB records, 341
 of every 1,024 live, 8 distinct page-locked images cycled) compacted by contexts
 created with 1 (per-block launches, the round-4 product) to 256 blocks per launch, interleaved in one process, wall time per call.
 
-  python tools/compact_group_probe.py [NBLOCKS] [ROUNDS]
+  CG_GROUPS=1,8,16,32,64 python tools/compact_group_probe.py [NBLOCKS] [ROUNDS]
+
+(bash reserves GROUPS, so the list is CG_GROUPS.)
 """
 import json
 import os
@@ -26,7 +28,7 @@ from benchlines.common import pcie_ceiling  # noqa: E402
 def main():
     nb = int(sys.argv[1]) if len(sys.argv) > 1 else 512
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-    groups = [int(x) for x in os.environ.get("GROUPS", "1,8,16,32,64").split(",")]
+    groups = [int(x) for x in os.environ.get("CG_GROUPS", "1,8,16,32,64").split(",")]
     ctxs = {}
     for g in groups:
         os.environ["TFS_CRC_COMPACT_GROUP"] = str(g)
