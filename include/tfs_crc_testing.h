@@ -101,12 +101,13 @@ int tfs_crc32_sched_stats(tfs_crc_ctx* ctx, uint32_t* owned_streams, uint64_t* f
 int tfs_crc32_plan_stats(tfs_crc_ctx* ctx, uint32_t* plans, uint64_t* bytes);
 /* The latest split throughput launch of ctx (debug/test hook; call it with no
  * other launch of ctx in flight): split launches so far, ext units its plan
- * reserved (`used`: segments of files > 128 KiB; files past `cap` stayed whole),
+ * reserved (`used`: segments of files > 128 KiB; when they do not all fit, the
+ * files of the address-ordered prefix that fits in `cap` are split and the rest stay whole),
  * its files, the plan's capacity and the workgroups it ran on.  The launch's
  * work units are files + min(used, cap); it takes dynamic chunked tickets when
  * those units come to >= 16 tickets per wave.  Waits for that
- * launch.  Each scheduler slot (stream) has its own plan, so split launches on
- * different streams overlap. */
+ * launch.  Each owned stream has its own plan, so split launches on different
+ * owned streams overlap; launches on foreign streams share one plan. */
 int tfs_crc32_split_stats(tfs_crc_ctx* ctx, uint64_t* launches, uint64_t* used, uint32_t* files, uint32_t* cap,
                           uint32_t* grid);
 

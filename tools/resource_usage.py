@@ -2,7 +2,7 @@
 """Per-kernel register / LDS / scratch / occupancy table of a gfx950 build
 (hipcc -Rpass-analysis=kernel-resource-usage), demangled names shortened.
 
-  python tools/resource_usage.py [-DTFS_CRC_MEASURE] [FILTER]
+  python tools/resource_usage.py [-DTFS_CRC_MEASURE] [--src=tfs_amd/csrc/tfs_ec_kernels.hip] [FILTER]
 """
 import re
 import subprocess
@@ -13,8 +13,9 @@ SRC = "tfs_amd/csrc/tfs_crc_kernels.hip"
 
 def main():
     defs = [a for a in sys.argv[1:] if a.startswith("-D")]
-    filt = [a for a in sys.argv[1:] if not a.startswith("-D")]
-    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-c", SRC, "-o", "/tmp/ru_k.o",
+    srcs = [a[6:] for a in sys.argv[1:] if a.startswith("--src=")]
+    filt = [a for a in sys.argv[1:] if not a.startswith("-D") and not a.startswith("--src=")]
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-c", srcs[0] if srcs else SRC, "-o", "/tmp/ru_k.o",
            "-Rpass-analysis=kernel-resource-usage", *defs]
     out = subprocess.run(cmd, capture_output=True, text=True).stderr
     rows, cur = [], None
@@ -32,7 +33,7 @@ def main():
     names = subprocess.run(["c++filt"], input="\n".join(r["name"] for r in rows), capture_output=True,
                            text=True).stdout.splitlines()
     for r, n in zip(rows, names):
-        n = re.sub(r"\(.*\)$", "", n).replace("tfscrc::", "")
+        n = re.sub(r"\(.*\)$", "", n).replace("tfscrc::", "").replace("tfsec::", "")
         if filt and not any(f in n for f in filt):
             continue
         print("%4s v %3s a %4s s %5s scr %6s lds occ %2s  %s" % (r.get("VGPRs"), r.get("AGPRs"), r.get("TotalSGPRs"),
