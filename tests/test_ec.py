@@ -177,12 +177,11 @@ def test_gpu_statuses_and_device_form(gpu_ctx, ec_oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 6, 7])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 6])
 def test_gpu_kernel_forms_ragged_sizes(gpu_ctx, ec_oracle, variant, monkeypatch):
     """Every kernel form (TFS_EC_VARIANT 0: one grid step of tiles per wave; 1-3:
     chunks of 2, 4, 8 tiles per wave step with the cross-tile prefetch; 4, 6: the
-    tile kernel striding over 8,192 / 2,048 workgroups; 7: every source member's
-    loads in flight before any is combined) on unit counts that leave
+    tile kernel striding over 8,192 / 2,048 workgroups) on unit counts that leave
     partial tiles, partial chunks and a grid stride larger than the work:
     encode and a 3-member decode byte-exact against the oracle.  The forms live
     in the measurement build (the product library never

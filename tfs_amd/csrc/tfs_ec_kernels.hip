@@ -159,59 +159,6 @@ __global__ void __launch_bounds__(256) ec_apply_chunk_kernel(EcArgs a, const uin
 }
 
 #ifdef TFS_CRC_MEASURE
-// All members in flight (measurement, TFS_EC_VARIANT=7): the product's tile and
-// lane mapping, but every source member's 4 KiB of the tile is loaded before any
-// is combined (SM x 8 dwordx2 loads per lane, 2.5x the bytes in flight per wave
-// of the product's one-member-ahead pipeline, fewer waves per SIMD).  Says
-// whether the product's memory shape is limited by its bytes in flight.
-template <int OG, int SM>
-__global__ void __launch_bounds__(256) ec_apply_all_kernel(EcArgs a, const uint32_t* __restrict__ masks) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t u = uint32_t(lane) >> 4;
-  const uint32_t off = 8u * uint32_t(lane & 15);
-  const uint64_t ntiles = (a.units + 3) / 4;
-  const uint64_t wave = uint64_t(blockIdx.x) * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t nwaves = uint64_t(gridDim.x) * (blockDim.x / 64);
-  for (uint64_t t = wave; t < ntiles; t += nwaves) {
-    const uint64_t unit = t * 4 + u;
-    const bool ok = unit < a.units;
-    const uint64_t base = unit * 1024u + off;
-    u32x2 in[SM][8];
-#pragma unroll
-    for (int s = 0; s < SM; ++s)
-#pragma unroll
-      for (int c = 0; c < 8; ++c)
-        in[s][c] = (ok && uint32_t(s) < a.S) ? ld64nt(a.src[s] + base + 128u * c) : u32x2{0u, 0u};
-    u32x2 acc[OG][8];
-#pragma unroll
-    for (int o = 0; o < OG; ++o)
-#pragma unroll
-      for (int r = 0; r < 8; ++r) acc[o][r] = u32x2{0u, 0u};
-#pragma unroll
-    for (int s = 0; s < SM; ++s) {
-      if (uint32_t(s) >= a.S) break;
-#pragma unroll
-      for (int o = 0; o < OG; ++o)
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const uint32_t* m = masks + ((uint32_t(o) * 8u + uint32_t(r)) * a.S + uint32_t(s)) * 8u;
-#pragma unroll
-          for (int c = 0; c < 8; ++c) {
-            const uint32_t mk = m[c];
-            acc[o][r].x = xand(acc[o][r].x, in[s][c].x, mk);
-            acc[o][r].y = xand(acc[o][r].y, in[s][c].y, mk);
-          }
-        }
-    }
-    if (ok) {
-#pragma unroll
-      for (int o = 0; o < OG; ++o)
-#pragma unroll
-        for (int r = 0; r < 8; ++r) st64nt(a.dst[o] + base + 128u * r, acc[o][r]);
-    }
-  }
-}
-
 template <int K>
 static void launch_chunk(const EcArgs& a, int og, dim3 g, dim3 b, hipStream_t stream) {
   switch (og) {
@@ -227,7 +174,7 @@ static void launch_chunk(const EcArgs& a, int og, dim3 g, dim3 b, hipStream_t st
 // The product: the grid-stride tile kernel.  Measurement build (TFS_EC_VARIANT
 // 1, 2, 3): the chunked form with K = 2, 4, 8 tiles per wave step; 4, 6: the
 // product's kernel over 8,192 / 2,048 workgroups striding (the product launches
-// one grid step per wave); 7: every source member in flight at once (S <= 5).
+// one grid step per wave).
 hipError_t launch_ec_apply(const EcArgs& a, int og, int variant, hipStream_t stream) {
   if (a.units == 0) return hipSuccess;
   const uint64_t ntiles = (a.units + 3) / 4;
@@ -240,16 +187,6 @@ hipError_t launch_ec_apply(const EcArgs& a, int og, int variant, hipStream_t str
     if (K == 2) launch_chunk<2>(a, og, g, b, stream);
     else if (K == 4) launch_chunk<4>(a, og, g, b, stream);
     else launch_chunk<8>(a, og, g, b, stream);
-    return hipGetLastError();
-  }
-  if (variant == 7 && a.S <= 5) {
-    const dim3 g(static_cast<unsigned>((ntiles + 3) / 4)), b(256);
-    switch (og) {
-      case 1: hipLaunchKernelGGL((ec_apply_all_kernel<1, 5>), g, b, 0, stream, a, a.masks); break;
-      case 2: hipLaunchKernelGGL((ec_apply_all_kernel<2, 5>), g, b, 0, stream, a, a.masks); break;
-      case 3: hipLaunchKernelGGL((ec_apply_all_kernel<3, 5>), g, b, 0, stream, a, a.masks); break;
-      default: hipLaunchKernelGGL((ec_apply_all_kernel<4, 5>), g, b, 0, stream, a, a.masks); break;
-    }
     return hipGetLastError();
   }
 #else

@@ -4,10 +4,11 @@
 Builds the ec line's members (k = 5 data + m = 3 parity of 1,536 MiB, device
 resident), then interleaves, round by round, encodes through the product
 library and through measurement-build forms selected by TFS_EC_VARIANT
-(tfs_ec_kernels.hip: 1-3 chunked tiles, 4 / 6 striding grids, 7 every source
-member's loads in flight at once), each timed with HIP events.
+(tfs_ec_kernels.hip: 1-3 chunked tiles, 4 / 6 striding grids), each timed with
+HIP events.  (Round 5's form 7, every source member's loads in flight at once, was
+measured and deleted: DESIGN.md §4.2.)
 
-  python tools/ab_ec.py VARIANTS [ROUNDS] [MIB]     e.g. python tools/ab_ec.py 7 8
+  python tools/ab_ec.py VARIANTS [ROUNDS] [MIB]     e.g. python tools/ab_ec.py 1,4 8
 """
 import json
 import os
