@@ -650,8 +650,68 @@ def test_block_verify_zero_copy_pinned_image(gpu_ctx, oracle):
         for i in range(len(live)):
             o, sz = int(live[i]["offset"]), int(live[i]["size"])
             assert int(c1[i]) == ocrc(oracle, 0, img[o + 36:o + sz].tobytes())
+        # the same slot again with another meta list (metas, CRCs and statuses go
+        # through its page-locked words: nothing of the previous call may remain)
+        m2 = np.ascontiguousarray(live[::-2])
+        c3, s3, n3, r3 = gpu_ctx.block_verify(pin.array, m2)
+        c4, s4, n4, r4 = gpu_ctx.block_verify(img.copy(), m2)
+        assert (c3 == c4).all() and (s3 == s4).all() and n3 == n4 and r3 == r4
     finally:
         pin.free()
+
+
+def test_wide_pinned_batches_read_in_place(gpu_ctx, oracle, monkeypatch):
+    """A page-locked batch wider than 8 MiB with more than 256 files (a block image
+    read back for verify) runs as one throughput launch that reads the files, its
+    descriptors and writes its verdicts in host memory (round 5): tfs_crc32_verify,
+    tfs_crc32_batch and three submissions in flight give the oracle's CRCs and the
+    same verdicts as the pageable path and as the staged form (TFS_CRC_VARIANT=52);
+    files over 128 KiB take the split plan over host-resident descriptors."""
+    import tfs_amd.crc as crc
+    rng = np.random.default_rng(5252)
+    n = 700
+    lens = rng.integers(0, 60000, n).astype(np.uint32)
+    lens[:6] = [0, 1, 3, 4, 65536, 300 * 1024 + 5]                    # one file to split
+    lens[n // 2] = 1 << 20
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + rng.integers(0, 9, n - 1).astype(np.uint64))
+    size = int(offs[-1] + lens[-1]) + 64
+    assert size > 8 << 20
+    data = rng.integers(0, 256, size, dtype=np.uint8)
+    exp = np.array([ocrc(oracle, 0, data[int(o):int(o) + int(l)].tobytes()) for o, l in zip(offs, lens)], np.uint32)
+    bad = np.array([5, 77, n // 2, n - 1])
+    expected = exp.copy()
+    expected[bad] ^= 0x10
+    seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    monkeypatch.setenv("TFS_CRC_VARIANT", "52")
+    staged = crc.Context(0, measure=True)
+    monkeypatch.setenv("TFS_CRC_VARIANT", "0")
+    pin = crc.PinnedBuffer(gpu_ctx, size)
+    try:
+        pin.array[:] = data
+        for rep in range(2):
+            c1, ok1, nb1, rc1 = gpu_ctx.verify(pin.array, offs, lens, expected)
+            c2, ok2, nb2, rc2 = gpu_ctx.verify(data.copy(), offs, lens, expected)
+            c3, ok3, nb3, rc3 = staged.verify(pin.array, offs, lens, expected)
+            assert (c1 == exp).all() and (c2 == exp).all() and (c3 == exp).all(), rep
+            assert (ok1 == ok2).all() and (ok1 == ok3).all() and nb1 == nb2 == nb3 == len(bad), rep
+            assert rc1 == rc2 == rc3 == -1010 and (ok1[bad] == 0).all(), rep
+            c4, ok4, nb4, rc4 = gpu_ctx.verify(pin.array, offs, lens, exp)
+            assert nb4 == 0 and rc4 == 0 and ok4.all() and (c4 == exp).all(), rep
+        s1 = gpu_ctx.batch(pin.array, offs, lens, seeds)
+        s2 = gpu_ctx.batch(data.copy(), offs, lens, seeds)
+        assert (s1 == s2).all()
+        for i in (0, 1, 4, 5, n // 2, n - 1):
+            assert int(s1[i]) == ocrc(oracle, int(seeds[i]), data[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes())
+        # three submissions in flight over the same page-locked image, each wide
+        parts = [np.arange(k, n, 3) for k in range(3)]
+        hs = [gpu_ctx.submit_verify(pin.array, offs[p], lens[p], expected[p]) for p in parts]
+        for p, h in zip(parts, hs):
+            c, ok, nb, rc = gpu_ctx.wait(h)
+            assert (c == exp[p]).all() and nb == int((ok == 0).sum()) == int(np.isin(p, bad).sum())
+    finally:
+        pin.free()
+        staged.close()
 
 
 def test_small_pinned_batches_read_in_place(gpu_ctx, oracle):

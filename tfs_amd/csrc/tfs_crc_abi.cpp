@@ -235,6 +235,11 @@ constexpr uint32_t kForeignSlots = 64;    // the last 64 scheduler slots: launch
 constexpr uint32_t kOwnedSlots = kSchedSlots - kForeignSlots;
 // Measurement build only (TFS_CRC_VARIANT; the product's ctx->variant is a constant 0):
 constexpr int kVariantDmaCompact = 8;      // DMA staging for host compaction / block verify / small batches
+#ifdef TFS_CRC_MEASURE
+constexpr int kVariantStagedWide = 52;     // wide page-locked host batches staged by DMA (the round-4 form; A/B)
+#else
+constexpr int kVariantStagedWide = -1;
+#endif
 // A context that posted a close batch this recently keeps the resident kernel's
 // CUs out of its device's throughput launches even while the kernel is between
 // lifetimes.
@@ -694,7 +699,7 @@ int split_prepare(tfs_crc_ctx* ctx, hipStream_t st, uint32_t k, uint32_t n, Spli
 // (n > kWgMaxFiles) get a scheduler slot, that slot's split plan and the CU cap
 // of their device; batches of at most kWgMaxFiles files take the latency form.
 int files_launch(tfs_crc_ctx* ctx, hipStream_t st, int mode, const uint8_t* base, const Desc* desc, uint32_t n,
-                 uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t vseed) {
+                 uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad, uint32_t vseed, bool may_split = true) {
   SchedLease lease;
   if (const int r = sched_acquire(ctx, st, &lease)) return r;
   const uint32_t k = plan_index(lease, slot_index(ctx, lease));
@@ -702,7 +707,7 @@ int files_launch(tfs_crc_ctx* ctx, hipStream_t st, int mode, const uint8_t* base
   SplitArgs sa{nullptr, 0u};
   const SplitArgs* split = nullptr;
   int rc = TFS_SUCCESS;
-  if (n > kWgMaxFiles && ctx->split_files.load(std::memory_order_relaxed) != 0) {
+  if (may_split && n > kWgMaxFiles && ctx->split_files.load(std::memory_order_relaxed) != 0) {
     lk.lock();
     rc = plan_order(ctx, st, lease, k);
     if (rc == TFS_SUCCESS) rc = split_prepare(ctx, st, k, n, &sa);
@@ -991,11 +996,38 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
     }
     (void)hipGetLastError();  // not mappable: stage it
   }
+  // No file over kSplitMin (a block image of 64 KiB files): no split plan, so no
+  // plan kernels ahead of the CRC launch (their descriptors are on the host here).
+  uint32_t max_len = 0;
+  for (uint32_t i = 0; i < n; ++i) max_len = std::max(max_len, dd[i].len);
+  const bool may_split = max_len > kSplitMin;
   s.count_bad = false;
   // On the context stream.  (A stream per slot, so that one block's launch overlaps
   // the next block's copy, measured 0.8 % faster on one box but halved the
   // context stream's copies on another -- 30 against 57 GB/s)
   hipStream_t st = ctx->stream;
+  // A wide page-locked batch (a 64 MiB block image read back for verify, configs[4]'s
+  // end-to-end leg): the throughput kernel reads the files in place over PCIe, its
+  // descriptors from the slot's page-locked words, and writes its verdicts there --
+  // one launch per batch, no copy-engine work at all.  A zero-copy read of a whole
+  // block image runs at the link's DMA rate (58.1 against 57.5 GB/s).
+  // Measurement build: TFS_CRC_VARIANT=52 stages it as before (A/B).
+  if (wide && n <= kZeroCopyOutFiles && ctx->variant != kVariantDmaCompact && ctx->variant != kVariantStagedWide &&
+      is_pinned_host(base)) {
+    void* zb = nullptr;
+    HIP_TRY(ctx, s.h_desc.reserve(size_t(n) * sizeof(Desc)));
+    if (host_dev_ptr(static_cast<const uint8_t*>(base) + lo, &zb) && s.h_desc.dev && s.h_crc.dev && s.h_ok.dev) {
+      memcpy(s.h_desc.p, d, size_t(n) * sizeof(Desc));
+      s.count_bad = true;
+      if (const int rc2 = files_launch(ctx, st, mode, static_cast<const uint8_t*>(zb) - lo,
+                                       static_cast<const Desc*>(s.h_desc.dev), n, static_cast<uint32_t*>(s.h_crc.dev),
+                                       static_cast<uint8_t*>(s.h_ok.dev), nullptr, 0u, may_split))
+        return rc2;
+      HIP_TRY(ctx, hipEventRecord(s.done, st));
+      return TFS_SUCCESS;
+    }
+    (void)hipGetLastError();
+  }
   const uint8_t* d_base = nullptr;
   int rc = stage_span(ctx, s, base, lo, hi, &d_base, st);
   if (rc) return rc;
@@ -1010,7 +1042,7 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
   if (n <= kZeroCopyOutFiles && zcrc && zok) {
     s.count_bad = true;
     if (const int rc2 = files_launch(ctx, st, mode, d_base, static_cast<const Desc*>(s.d_desc.p), n,
-                                     static_cast<uint32_t*>(zcrc), static_cast<uint8_t*>(zok), nullptr, 0u))
+                                     static_cast<uint32_t*>(zcrc), static_cast<uint8_t*>(zok), nullptr, 0u, may_split))
       return rc2;
     HIP_TRY(ctx, hipEventRecord(s.done, st));
     return TFS_SUCCESS;
@@ -1021,7 +1053,7 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
   HIP_TRY(ctx, hipMemsetAsync(s.d_bad.p, 0, 4, st));
   if (const int rc2 = files_launch(ctx, st, mode, d_base, static_cast<const Desc*>(s.d_desc.p), n,
                                    static_cast<uint32_t*>(s.d_crc.p), static_cast<uint8_t*>(s.d_ok.p),
-                                   static_cast<uint32_t*>(s.d_bad.p), 0u))
+                                   static_cast<uint32_t*>(s.d_bad.p), 0u, may_split))
     return rc2;
   HIP_TRY(ctx, hipMemcpyAsync(s.h_crc.p, s.d_crc.p, size_t(n) * 4, hipMemcpyDeviceToHost, st));
   if (mode == 1) {
@@ -1472,6 +1504,28 @@ int tfs_block_verify(tfs_crc_ctx* ctx, const void* image, uint64_t image_len, co
   void* zc = nullptr;
   if (ctx->variant != kVariantDmaCompact && is_pinned_host(image) && host_dev_ptr(image, &zc)) {
     d_base = static_cast<const uint8_t*>(zc);
+    // Metas, CRCs and statuses through the slot's page-locked words too: one launch
+    // and a stream sync per block, no copy-engine work (five DMA set-ups less behind
+    // every ~0.4 ms block).  n_bad is counted from the statuses.
+    HIP_TRY(ctx, s->h_desc.reserve(size_t(n) * sizeof(RawMeta)));
+    HIP_TRY(ctx, s->h_crc.reserve(size_t(n) * 4));
+    HIP_TRY(ctx, s->h_ok.reserve(size_t(n) * 4));
+    if (ctx->variant != kVariantStagedWide && s->h_desc.dev && s->h_crc.dev && s->h_ok.dev) {
+      memcpy(s->h_desc.p, metas, size_t(n) * sizeof(RawMeta));
+      SCHED_LAUNCH(ctx, ctx->stream, "block_verify_pipe",
+                   launch_block_verify_pipe(d_base, image_len, static_cast<const RawMeta*>(s->h_desc.dev), nullptr, n,
+                                            ctx->d_tables, static_cast<uint32_t*>(s->h_crc.dev),
+                                            static_cast<int32_t*>(s->h_ok.dev), nullptr, sched, ctx->stream,
+                                            ctx->variant, throughput_cap(ctx)));
+      HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+      const int32_t* st = static_cast<const int32_t*>(s->h_ok.p);
+      uint32_t bad = 0;
+      for (uint32_t i = 0; i < n; ++i) bad += st[i] != TFS_SUCCESS ? 1u : 0u;
+      if (out_crc) memcpy(out_crc, s->h_crc.p, size_t(n) * 4);
+      if (out_status) memcpy(out_status, st, size_t(n) * 4);
+      if (n_bad) *n_bad = bad;
+      return bad ? TFS_EXIT_CHECK_CRC_ERROR : TFS_SUCCESS;
+    }
   } else {
     (void)hipGetLastError();
     const int rc = stage_span(ctx, *s, image, 0, image_len, &d_base);
