@@ -43,7 +43,7 @@ hipError_t launch_packet_finish(uint8_t* base, const PacketDesc* pd, const Desc*
 hipError_t launch_block_verify_pipe(const uint8_t* image, uint64_t image_len, const RawMeta* metas,
                                     const CompactJob* jobs, uint32_t n, const Tables* tg, uint32_t* out_crc,
                                     int32_t* out_status, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
-                                    int variant, unsigned cap, uint32_t* done_flag = nullptr, uint32_t seq = 0u);
+                                    int variant, unsigned cap);
 hipError_t launch_compact_fused(const uint8_t* src, uint64_t src_len, const RawMeta* metas, const int32_t* flags,
                                 const int64_t* dest_off, uint32_t n, uint8_t* dst, const Tables* tg, uint32_t* out_crc,
                                 int32_t* out_status, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
@@ -1510,22 +1510,14 @@ int tfs_block_verify(tfs_crc_ctx* ctx, const void* image, uint64_t image_len, co
     HIP_TRY(ctx, s->h_desc.reserve(size_t(n) * sizeof(RawMeta)));
     HIP_TRY(ctx, s->h_crc.reserve(size_t(n) * 4));
     HIP_TRY(ctx, s->h_ok.reserve(size_t(n) * 4));
-    HIP_TRY(ctx, s->h_flag.reserve(64));
-    if (!s->done) HIP_TRY(ctx, hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
-    if (ctx->variant != kVariantStagedWide && s->h_desc.dev && s->h_crc.dev && s->h_ok.dev && s->h_flag.dev) {
+    if (ctx->variant != kVariantStagedWide && s->h_desc.dev && s->h_crc.dev && s->h_ok.dev) {
       memcpy(s->h_desc.p, metas, size_t(n) * sizeof(RawMeta));
-      // completion: the launch's last workgroup stores seq into the slot's flag word
-      // (launch_exit), which the host spins on (wait_flag), as for small batches
-      s->seq = g_flag_seq.fetch_add(1) + 1u;
-      if (s->seq == 0) s->seq = g_flag_seq.fetch_add(1) + 1u;
       SCHED_LAUNCH(ctx, ctx->stream, "block_verify_pipe",
                    launch_block_verify_pipe(d_base, image_len, static_cast<const RawMeta*>(s->h_desc.dev), nullptr, n,
                                             ctx->d_tables, static_cast<uint32_t*>(s->h_crc.dev),
                                             static_cast<int32_t*>(s->h_ok.dev), nullptr, sched, ctx->stream,
-                                            ctx->variant, throughput_cap(ctx), static_cast<uint32_t*>(s->h_flag.dev),
-                                            s->seq));
-      HIP_TRY(ctx, hipEventRecord(s->done, ctx->stream));
-      if (const int wr = wait_flag(ctx, *s)) return wr;
+                                            ctx->variant, throughput_cap(ctx)));
+      HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
       const int32_t* st = static_cast<const int32_t*>(s->h_ok.p);
       uint32_t bad = 0;
       for (uint32_t i = 0; i < n; ++i) bad += st[i] != TFS_SUCCESS ? 1u : 0u;

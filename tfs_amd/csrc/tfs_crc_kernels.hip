@@ -1691,7 +1691,7 @@ __global__ void __launch_bounds__(NW * kWave, OCC * NW / 4) compact_pipe_kernel(
     const uint8_t* __restrict__ src, uint64_t src_len, const RawMeta* __restrict__ metas,
     const int32_t* __restrict__ flags, const int64_t* __restrict__ dest_off, const CompactJob* __restrict__ jobs,
     uint32_t n, uint8_t* __restrict__ dst, const Tables* __restrict__ tg, uint32_t* out_crc, int32_t* out_status,
-    uint32_t* n_bad, uint32_t* sched, CSegArgs cs, uint32_t* done_flag, uint32_t seq) {
+    uint32_t* n_bad, uint32_t* sched, CSegArgs cs) {
   constexpr bool DA = !VERIFY && (DIAG & 4) != 0;
   constexpr bool LNT = (DIAG & 8) && !VERIFY ? false : kNT;  // the verify form keeps the headline's loads
   static_assert(OCC * LdsLayout<LY>::bytes <= 160u * 1024u, "OCC workgroups per CU must fit the LDS");
@@ -1807,7 +1807,7 @@ __global__ void __launch_bounds__(NW * kWave, OCC * NW / 4) compact_pipe_kernel(
     }
   } while (false);
   if (lane == 0 && bad && n_bad) atomicAdd(n_bad, bad);
-  if (lane == 0) launch_exit(sched, gridDim.x * wpb, done_flag, seq);
+  if (lane == 0) launch_exit(sched, gridDim.x * wpb, nullptr, 0u);
 }
 
 // Segmented compaction plan (CSegArgs): one thread per job.  A live record whose
@@ -2266,8 +2266,7 @@ hipError_t launch_compact_fused(const uint8_t* src, uint64_t src_len, const RawM
   if (n == 0) return hipSuccess;
   if (!sched) return hipErrorInvalidValue;
   hipLaunchKernelGGL(compact_pipe_kernel<false>, dim3(grid_for(n, cap)), dim3(kBlock), 0, stream, src, src_len, metas,
-                     flags, dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched, CSegArgs{nullptr, 0u, 0u},
-                     nullptr, 0u);
+                     flags, dest_off, nullptr, n, dst, tg, out_crc, out_status, n_bad, sched, CSegArgs{nullptr, 0u, 0u});
   (void)variant;
   return hipGetLastError();
 }
@@ -2287,7 +2286,7 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
     if (const hipError_t e = hipGetLastError()) return e;
     hipLaunchKernelGGL((compact_pipe_kernel<true, false, kCompactDiag, kPF, 1, 0, true>), dim3(ccap), dim3(kBlock), 0,
                        stream, src, src_len, nullptr, nullptr, nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad,
-                       sched, cs, nullptr, 0u);
+                       sched, cs);
     if (const hipError_t e = hipGetLastError()) return e;
     const uint32_t fg = (n + 255u) / 256u;
     hipLaunchKernelGGL(compact_seg_fold_kernel, dim3(fg < 1024u ? fg : 1024u), dim3(256), 0, stream, jobs, n, tg, cs,
@@ -2297,8 +2296,7 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
 #define TFS_CJ(NW_, OCC_, LY_, PF_, DIAG_)                                                                           \
   hipLaunchKernelGGL((compact_pipe_kernel<true, false, DIAG_, PF_, 1, 0, false, kCompactHS, NW_, OCC_, LY_>),        \
                      dim3(grid_waves(n, NW_, ccap * OCC_)), dim3(NW_ * kWave), 0, stream, src, src_len, nullptr,       \
-                     nullptr, nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad, sched, CSegArgs{nullptr, 0u, 0u}, \
-                     nullptr, 0u)
+                     nullptr, nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad, sched, CSegArgs{nullptr, 0u, 0u})
 #ifdef TFS_CRC_MEASURE
   // Measurement forms: 26 the product without the payload CRC steps
   // (its own load/store schedule; wrong CRCs); 67 / 68 the record list through the
@@ -2331,14 +2329,14 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
 hipError_t launch_block_verify_pipe(const uint8_t* image, uint64_t image_len, const RawMeta* metas,
                                     const CompactJob* jobs, uint32_t n, const Tables* tg, uint32_t* out_crc,
                                     int32_t* out_status, uint32_t* n_bad, uint32_t* sched, hipStream_t stream,
-                                    int variant, unsigned cap, uint32_t* done_flag, uint32_t seq) {
+                                    int variant, unsigned cap) {
   if (n == 0) return hipSuccess;
   if (!sched) return hipErrorInvalidValue;
   const dim3 grid(grid_for(n, cap));
 #define TFS_BV(WIDE_, CF_, TS_)                                                                                     \
   hipLaunchKernelGGL((compact_pipe_kernel<WIDE_, true, kCompactDiag, kPF, CF_, TS_>), grid, dim3(kBlock), 0, stream, \
                      image, image_len, metas, nullptr, nullptr, jobs, n, nullptr, tg, out_crc, out_status, n_bad, sched, \
-                     CSegArgs{nullptr, 0u, 0u}, done_flag, seq)
+                     CSegArgs{nullptr, 0u, 0u})
 #ifdef TFS_CRC_MEASURE
   if (variant == 50 && jobs) TFS_BV(true, 1, 0);
   else if (variant == 50) TFS_BV(false, 1, 0);
