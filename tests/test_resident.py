@@ -69,46 +69,6 @@ def test_resident_batches_match_oracle(monkeypatch, oracle):
         ctx.close()
 
 
-@pytest.mark.parametrize("seg_kib", [16, 4, 0])
-def test_resident_segmented_units(monkeypatch, oracle, seg_kib):
-    """Files longer than the resident segment (default 16 KiB) go to the ring as a
-    ragged head with the seed and whole seed-0 segments, one unit each, folded back
-    on the host (round 5): lengths at every segment boundary, compute with seeds and
-    verify with mismatches, pageable and page-locked; 4 KiB segments take the
-    general shift, 0 keeps files whole; a batch that would pass 1,024 units goes as
-    whole files.  Every CRC against the oracle."""
-    import tfs_amd.crc as crc
-    ctx = _ctx(monkeypatch, TFS_CRC_RESIDENT=1, TFS_CRC_RESIDENT_SEG_KIB=seg_kib)
-    try:
-        rng = np.random.default_rng(1600 + seg_kib)
-        S = 16384
-        base = [0, 1, 4095, 4096, 4097, S - 1, S, S + 1, 2 * S, 2 * S + 3, 65536, 65537, 100000, 300001]
-        for lens in (np.array(base, np.uint32), np.full(20, 300 * 1024 + 7, np.uint32)):
-            n = len(lens)
-            offs = np.cumsum(np.concatenate([[0], lens[:-1]]).astype(np.uint64) + rng.integers(0, 9, n).astype(np.uint64))
-            buf = synth_bytes(1700 + n, int(offs[-1] + lens[-1]) + 64)
-            seeds = rng.integers(0, 2**32, n).astype(np.uint32)
-            exp = _oracle_batch(oracle, buf, offs, lens, seeds)
-            zexp = _oracle_batch(oracle, buf, offs, lens, np.zeros(n, np.uint32))
-            want = zexp.copy()
-            want[[2, n - 1]] ^= 0x100
-            before = ctx.resident_stats()[1]
-            assert (ctx.batch(buf, offs, lens, seeds) == exp).all(), seg_kib
-            c, ok, nbad, rc = ctx.verify(buf, offs, lens, want)
-            assert (c == zexp).all() and nbad == 2 and rc == -1010 and not ok[2] and not ok[n - 1], seg_kib
-            pin = crc.PinnedBuffer(ctx, buf.size)
-            try:
-                pin.array[:] = buf
-                assert (ctx.batch(pin.array, offs, lens, seeds) == exp).all(), seg_kib
-                c2, ok2, nbad2, _ = ctx.verify(pin.array, offs, lens, zexp)
-                assert (c2 == zexp).all() and nbad2 == 0 and ok2.all(), seg_kib
-            finally:
-                pin.free()
-            assert ctx.resident_stats()[1] == before + 4 * n  # all four calls through the ring
-    finally:
-        ctx.close()
-
-
 def test_resident_idle_exit_and_relaunch(monkeypatch, oracle):
     """The kernel leaves after its idle time; the next batch relaunches it."""
     ctx = _ctx(monkeypatch, TFS_CRC_RESIDENT=1, TFS_CRC_RESIDENT_IDLE_US=50)

@@ -182,9 +182,7 @@ struct Slot {
   bool count_bad = false;  // zero-copy launch: n_bad is counted from h_ok
   bool spin = false;       // zero-copy launch: completion = h_flag reaching `seq`
   bool resident = false;   // posted to the resident kernel's ring (no launch, no s.done)
-  uint32_t res_first = 0;  // ... as units [res_first, res_first + res_units)
-  uint32_t res_units = 0;  // units of the posted batch (files cut into segments: more than files)
-  std::vector<uint32_t> res_k;  // units of each file of the posted batch
+  uint32_t res_first = 0;  // ... as units [res_first, res_first + n)
   uint32_t seq = 0;
   Slot() { h_crc.coherent = h_ok.coherent = h_bad.coherent = h_flag.coherent = h_res.coherent = true; }
   // user outputs for the async path
@@ -317,7 +315,6 @@ struct tfs_crc_ctx {
   // cursor/counters, its own stream.  All fields under `mu`.
   bool resident = true;  // TFS_CRC_RESIDENT=0 launches every batch instead
   unsigned res_grid = 16;  // workgroups of the resident kernel (TFS_CRC_RESIDENT_WGS)
-  uint32_t res_seg = kResSegDefault;  // resident units: files cut into segments of this many bytes (0: whole)
   uint32_t res_idle_us = 200, res_life_us = 10000;  // TFS_CRC_RESIDENT_IDLE_US / _LIFE_US
   ResHost* res_host = nullptr;
   ResHost* res_host_d = nullptr;  // its device-visible address
@@ -794,67 +791,31 @@ int resident_ensure_running(tfs_crc_ctx* ctx, bool post = false) {
   return TFS_SUCCESS;
 }
 
-// shift(c, seg) of the resident segments: byte tables for the default segment
-// (built once), the GF(2) product for any other (TFS_CRC_RESIDENT_SEG_KIB).
-uint32_t res_shift(uint32_t seg, uint32_t c) {
-  struct T {
-    uint32_t t[4][256];
-    T() { make_shift_table(t, kResSegDefault); }
-  };
-  static const T tab;
-  if (seg == kResSegDefault)
-    return tab.t[0][c & 255u] ^ tab.t[1][(c >> 8) & 255u] ^ tab.t[2][(c >> 16) & 255u] ^ tab.t[3][c >> 24];
-  return shift_bytes(c, seg);
-}
-
 // (Caller holds ctx->mu.)  Post a zero-copy batch (device-visible base `zb`)
-// as units [P, P + units), each with its result word in s.h_res; then
-// `published`; the kernel is (re)launched if gone.  A file longer than
-// ctx->res_seg goes as a ragged head (its seed, its first len - (k-1)*res_seg
-// bytes) and k-1 whole segments (seed 0), one unit each, so that k workgroups
-// read it at once; wait_resident folds their CRCs back into the file's
-// (crc(A||B) = shift(crc(A), |B|) ^ crc(0, B), crc_math.h).  Returns 1 (nothing
-// posted) when the ring has no room: a unit of a batch still outstanding would
-// be rewritten.
+// as units [P, P + n), one per file, each with its result word in s.h_res; then
+// `published`; the kernel is (re)launched if gone.  Returns 1 (nothing posted)
+// when the ring has no room: a unit of a batch still outstanding would be
+// rewritten.
 int resident_post(tfs_crc_ctx* ctx, Slot& s, int mode, const uint8_t* zb, const Desc* d, uint32_t n) {
   if (const int rc = resident_setup(ctx)) return rc;
   ResHost* H = ctx->res_host;
   const uint32_t P = ctx->res_published;
-  const uint32_t seg = ctx->res_seg;
-  s.res_k.assign(n, 1u);
-  uint32_t nu = 0;
-  for (uint32_t i = 0; i < n; ++i) {
-    if (seg && d[i].len > seg) s.res_k[i] = (d[i].len + seg - 1u) / seg;
-    nu += s.res_k[i];
-  }
-  if (nu > kResMaxBatchUnits) {  // a batch of long files: whole files (one unit each)
-    s.res_k.assign(n, 1u);
-    nu = n;
-  }
   for (const Slot& x : ctx->sync_slots)
-    if (&x != &s && x.busy && x.resident && int32_t(P + nu - kResUnits - x.res_first) > 0) return 1;
-  HIP_TRY(ctx, s.h_res.reserve(size_t(nu) * 8));
+    if (&x != &s && x.busy && x.resident && int32_t(P + n - kResUnits - x.res_first) > 0) return 1;
+  HIP_TRY(ctx, s.h_res.reserve(size_t(n) * 8));
   void* zres = s.h_res.dev;
   if (!zres) return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "resident result words are not mapped");
-  uint32_t q = 0;
   for (uint32_t i = 0; i < n; ++i) {
-    const uint32_t k = s.res_k[i];
-    uint64_t a = uint64_t(reinterpret_cast<uintptr_t>(zb + d[i].offset));
-    for (uint32_t j = 0; j < k; ++j, ++q) {
-      const uint32_t len = k == 1 ? d[i].len : (j == 0 ? d[i].len - (k - 1u) * seg : seg);
-      ResUnit& u = H->units[(P + q) % kResUnits];
-      u.addr = a;
-      u.out = uint64_t(reinterpret_cast<uintptr_t>(zres)) + 8u * q;
-      u.len = len;
-      u.seed = mode == 0 && j == 0 ? d[i].aux : 0u;
-      u.seq = s.seq;
-      u.reserved = 0;
-      a += len;
-    }
+    ResUnit& u = H->units[(P + i) % kResUnits];
+    u.addr = uint64_t(reinterpret_cast<uintptr_t>(zb + d[i].offset));
+    u.out = uint64_t(reinterpret_cast<uintptr_t>(zres)) + 8u * i;
+    u.len = d[i].len;
+    u.seed = mode == 0 ? d[i].aux : 0u;
+    u.seq = s.seq;
+    u.reserved = 0;
   }
   s.res_first = P;
-  s.res_units = nu;
-  ctx->res_published = P + nu;
+  ctx->res_published = P + n;
   ctx->res_files += n;
   ctx->res_last_post_ns.store(now_ns(), std::memory_order_relaxed);
   __atomic_store_n(&H->published, uint64_t(ctx->res_published), __ATOMIC_RELEASE);
@@ -881,12 +842,11 @@ int wait_resident(tfs_crc_ctx* ctx, Slot& s, int mode, uint32_t n) {
   // one before it can leave, so relaunches without a new result of this batch
   // are bounded by the units queued ahead of it; past kResMaxIdleRelaunches in a
   // row the wait ends with a device error.
-  const uint32_t nu = s.res_units;
   uint32_t i = 0, relaunches = 0;
   for (uint32_t spins = 1;; ++spins) {
     const uint32_t i0 = i;
-    while (i < nu && uint32_t(res[i] >> 32) == s.seq) ++i;
-    if (i == nu) break;
+    while (i < n && uint32_t(res[i] >> 32) == s.seq) ++i;
+    if (i == n) break;
     if (i != i0) relaunches = 0;
     __builtin_ia32_pause();
     if ((spins & 255u) == 0) {
@@ -915,11 +875,8 @@ int wait_resident(tfs_crc_ctx* ctx, Slot& s, int mode, uint32_t n) {
   uint32_t* crc = static_cast<uint32_t*>(s.h_crc.p);
   uint8_t* ok = static_cast<uint8_t*>(s.h_ok.p);
   const Desc* d = static_cast<const Desc*>(s.h_desc.p);
-  uint32_t q = 0;
   for (uint32_t k = 0; k < n; ++k) {
-    uint32_t c = uint32_t(res[q++]);
-    for (uint32_t j = 1; j < s.res_k[k]; ++j) c = res_shift(ctx->res_seg, c) ^ uint32_t(res[q++]);
-    crc[k] = c;
+    crc[k] = uint32_t(res[k]);
     if (mode == 1) ok[k] = crc[k] == d[k].aux ? 1 : 0;
   }
   return TFS_SUCCESS;
@@ -1239,7 +1196,6 @@ int tfs_crc32_ctx_create(int device, tfs_crc_ctx** out) {
   if (const char* v = getenv("TFS_CRC_COMPACT_GROUP")) ctx->compact_group = uint32_t(std::min(std::max(atoi(v), 1), 256));
   if (const char* v = getenv("TFS_CRC_RESIDENT")) ctx->resident = atoi(v) != 0;
   if (const char* v = getenv("TFS_CRC_RESIDENT_WGS")) ctx->res_grid = unsigned(std::min(std::max(atoi(v), 1), 256));
-  if (const char* v = getenv("TFS_CRC_RESIDENT_SEG_KIB")) ctx->res_seg = uint32_t(std::min(std::max(atoi(v), 0), 1024)) << 10;
   if (const char* v = getenv("TFS_CRC_RESIDENT_IDLE_US")) ctx->res_idle_us = uint32_t(std::min(std::max(atoi(v), 1), 1000000));
   if (const char* v = getenv("TFS_CRC_RESIDENT_LIFE_US")) ctx->res_life_us = uint32_t(std::min(std::max(atoi(v), 1), 10000000));
   int rc = TFS_SUCCESS;

@@ -76,8 +76,6 @@ constexpr uint32_t kWgLdsBytes = kWgLevelOff + uint32_t(kWgLevels) * 1024u;  // 
 // P + n - kResUnits <= the first unit of every batch still outstanding
 // (tfs_crc_abi.cpp resident_post), otherwise it launches instead.
 constexpr uint32_t kResUnits = 4096;            // ring of units
-constexpr uint32_t kResSegDefault = 16u << 10;  // resident units: files cut into 16 KiB segments (host side)
-constexpr uint32_t kResMaxBatchUnits = 1024;    // ... while a batch comes to at most this many units
 constexpr uint32_t kResMaxGrid = 256;           // workgroups of the resident kernel, at most
 constexpr uint32_t kResExitLine = kResMaxGrid * kSchedStride;  // dstate: generation of the launch that is leaving
 constexpr uint32_t kResLeftLine = kResExitLine + kSchedStride;  // dstate: workgroups of this launch that have left
