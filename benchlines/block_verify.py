@@ -2,9 +2,7 @@
 block images (sync_backup.cpp:345-435, block_console.cpp:543-577 checks), from
 page-locked host memory and device-resident."""
 import ctypes
-import json
 import os
-import sys
 import time
 
 import numpy as np

@@ -2,9 +2,7 @@
 block images held in page-locked host memory (CompactTask::real_compact,
 src/dataserver/task.cpp:713-836, with the re-CRC), PCIe included."""
 import ctypes
-import json
 import os
-import sys
 import time
 
 import numpy as np

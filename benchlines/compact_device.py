@@ -2,9 +2,7 @@
 (CompactTask::real_compact, src/dataserver/task.cpp:713-836) fused with the
 re-CRC on device-resident blocks."""
 import ctypes
-import json
 import os
-import sys
 import time
 
 import numpy as np

@@ -1,8 +1,6 @@
 """bench.py --workload compact_files."""
 import ctypes
-import json
 import os
-import sys
 import time
 
 import numpy as np

@@ -1,11 +1,5 @@
 """bench.py --workload e2e."""
-import ctypes
-import json
-import os
-import sys
-import time
 
-import numpy as np
 
 from benchlines.common import *  # noqa: F401,F403
 

@@ -1,8 +1,6 @@
 """bench.py --workload ec."""
 import ctypes
-import json
 import os
-import sys
 import time
 
 import numpy as np

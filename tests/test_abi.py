@@ -1,12 +1,10 @@
 """CPU-side checks of the drop-in boundary: the C-ABI library loads and exports
 every symbol include/tfs_crc.h declares; the ABI structs have the reference
 layouts; without a GPU the library fails loudly instead of computing on the CPU."""
-import ctypes
 import os
 import re
 import subprocess
 
-import numpy as np
 import pytest
 
 from conftest import ROOT

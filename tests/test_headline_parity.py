@@ -16,7 +16,6 @@ PF-stripe ring and the cross-file prefetch run under chunked tickets.
 References: Func::crc src/common/func.cpp:426-435; verify sync_backup.cpp:345-435;
 real_compact src/dataserver/task.cpp:753-798.
 """
-import ctypes
 
 import numpy as np
 import pytest

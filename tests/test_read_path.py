@@ -3,7 +3,6 @@ as the harness restates it -- truncation, offset and meta errors, the FileInfo
 checks on the first fragment with the real flag -- and the verify-on-read hook
 the build adds behind DataManagement::read_data (data_management.cpp:238-268;
 the reference hands FileInfo.crc_ to the client unchecked, dataservice.cpp:1557)."""
-import numpy as np
 import pytest
 
 from conftest import ocrc

@@ -6,7 +6,6 @@ region work runs in libtfs_crc.so's gfx950 kernels; no CPU fallback.
 """
 import ctypes
 
-import numpy as np
 
 from . import crc as _crc
 
