@@ -70,7 +70,10 @@ def headline_image(gpu_ctx):
 def test_headline_launch_takes_the_chunked_path(gpu_ctx, headline_image):
     img, nblocks, n, total, desc, expected = headline_image
     waves = gpu_ctx.throughput_grid() * 16
-    assert waves == 4096 and n // waves >= 16  # kDynMinPerWave: chunked tickets (FileCursor::init)
+    # the whole chip (256 CUs x 16 waves), or the chip less the 16 CUs of a resident
+    # kernel that ran in this process within the last few ms (throughput_cap)
+    assert waves in (4096, 4096 - 16 * 16), waves
+    assert n // waves >= 16  # kDynMinPerWave: chunked tickets (FileCursor::init)
 
 
 def test_headline_verify_wrong_expectations_and_oracle_blocks(gpu_ctx, oracle, headline_image):
