@@ -83,7 +83,11 @@ def bench_small_bodies(args):
             oc, os_, ob = np.zeros(nfr, np.uint32), np.zeros(nfr, np.int32), np.zeros(1, np.uint32)
             args = (ctx.handle, pd.ctypes.data, nfr, buf.ctypes.data, buf.size, oc.ctypes.data, os_.ctypes.data,
                     ob.ctypes.data)
-            return (lambda: L.tfs_packet_verify(*args)), os_, ob
+            keep = (pd, oc, os_, ob, buf)  # the arrays the pointers name stay alive with the call
+
+            def call(keep=keep):
+                return L.tfs_packet_verify(*args)
+            return call, os_, ob
         fcall, fst, fbad = verify_call(frame, 1)
         fus = []
         for _ in range(20):
