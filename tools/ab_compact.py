@@ -81,6 +81,13 @@ def main():
         j["size"] = rec
         j["new_offset"] = (do % np.uint64(1 << 31)).astype(np.int32)
         jobsets[name] = crc.DeviceBuffer(ctx, j.nbytes).upload(j)
+    # AB_PARTS=1: the product on the first half and the first quarter of the packed job
+    # list too (same buffers, one launch each): a fixed per-launch cost shows as a
+    # higher time per record in the shorter launches
+    parts = {}
+    if os.environ.get("AB_PARTS"):
+        for nm, den in (("half", 2), ("quarter", 4)):
+            parts[nm] = int(k.size) // den
     if os.environ.get("AB_ALIGNED"):
         j = np.zeros(k.size, crc.COMPACT_JOB_DTYPE)
         j["src_offset"] = j["dest_offset"] = k * np.uint64(65536)
@@ -97,6 +104,7 @@ def main():
         # every requested variant on the dense layout too: where the kernel trails
         # the chunk copy of the same layout
         cases += [(0, "aligned64k")] + [(v, "aligned64k") for v in want]
+    cases += [(0, nm) for nm in parts]
     # AB_SEG=S[,S...]: the segmented compaction (tfs_crc32_set_compact_segment) on the
     # product context itself, toggled around its rounds (no second context's placement);
     # the other cases run it with whole records (set_compact_segment 0)
@@ -122,7 +130,7 @@ def main():
         return ctxs[v]
 
     for v, js in cases:
-        if v in (26, 67, 68) or js == "aligned64k":
+        if v in (26, 67, 68) or js == "aligned64k" or js in parts:
             continue
         d_bad.zero()
         c = ctx_of(v)
@@ -159,11 +167,12 @@ def main():
         for v, js in cases:
             c = ctx_of(v)
             e0, e1 = crc.Event(c), crc.Event(c)
-            nn = getattr(jobsets[js], "njobs", nj)
-            c.compact_jobs_device(img, total, jobsets[js], nn, d_dst, None, d_st, d_bad)
+            nn = parts.get(js, getattr(jobsets.get(js), "njobs", nj))
+            jb = jobsets["packed"] if js in parts else jobsets[js]
+            c.compact_jobs_device(img, total, jb, nn, d_dst, None, d_st, d_bad)
             e0.record()
             for _ in range(reps):
-                c.compact_jobs_device(img, total, jobsets[js], nn, d_dst, None, d_st, d_bad)
+                c.compact_jobs_device(img, total, jb, nn, d_dst, None, d_st, d_bad)
             e1.record()
             c.sync()
             times["%s_%s" % (v, js)].append(e0.elapsed_ms(e1) / reps)
@@ -202,6 +211,9 @@ def main():
         v = sorted(v)
         med = v[len(v) // 2]
         by = 2.0 * cb if name.startswith("copy") else (n * (rec + 40 + 8) if name.startswith("verify") else algo)
+        for nm, cnt in parts.items():
+            if name == "0_" + nm:
+                by = algo * cnt / nj
         res[name] = {"median_ms": med, "min_ms": v[0], "max_ms": v[-1], "GBs": by / (med / 1e3) / 1e9,
                      "frac_8TBs": by / (med / 1e3) / 1e9 / 8000.0}
     print(json.dumps({"tool": "ab_compact", "rounds": rounds, "nblocks": nblocks, "records": nj,
