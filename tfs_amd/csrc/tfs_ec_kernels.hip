@@ -30,40 +30,12 @@ __device__ __forceinline__ u32x2 ld64nt(const uint8_t* p) {
 __device__ __forceinline__ void st64nt(uint8_t* p, u32x2 v) {
   __builtin_nontemporal_store(v, reinterpret_cast<gu64wp>(reinterpret_cast<uintptr_t>(p)));
 }
-__device__ __forceinline__ u32x2 ld64(const uint8_t* p, bool nt) {
-  return nt ? ld64nt(p) : *reinterpret_cast<const u32x2*>(p);
-}
-__device__ __forceinline__ void st64(uint8_t* p, u32x2 v, bool nt) {
-  if (nt) st64nt(p, v);
-  else *reinterpret_cast<u32x2*>(p) = v;
-}
 __device__ __forceinline__ uint32_t xand(uint32_t acc, uint32_t in, uint32_t m) {
   // truth table indexed (src0 << 2) | (src1 << 1) | src2: acc ^ (in & m) = 0x78
   return __builtin_amdgcn_bitop3_b32(acc, in, m, 0x78);
 }
 
-// acc[o][r] ^= AND of member s's packets with row r's bit mask (one bitop3 per dword).
 template <int OG>
-__device__ __forceinline__ void combine(u32x2 (&acc)[OG][8], const u32x2 (&in)[8], const uint32_t* __restrict__ masks,
-                                        uint32_t S, uint32_t s) {
-#pragma unroll
-  for (int o = 0; o < OG; ++o)
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const uint32_t* m = masks + ((uint32_t(o) * 8u + uint32_t(r)) * S + s) * 8u;
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const uint32_t mk = m[c];
-        acc[o][r].x = xand(acc[o][r].x, in[c].x, mk);
-        acc[o][r].y = xand(acc[o][r].y, in[c].y, mk);
-      }
-    }
-}
-
-// NTL / NTS: non-temporal member loads / parity stores (the product: both).  PD:
-// source members in flight ahead of the one being combined (the product: 1).
-// Measurement build (TFS_EC_VARIANT 8, 9, 10): plain stores, plain loads, PD 2.
-template <int OG, bool NTL = true, bool NTS = true, int PD = 1>
 __device__ __forceinline__ void ec_apply_body(const EcArgs& a, const uint32_t* __restrict__ masks) {
   const int lane = threadIdx.x & 63;
   const uint32_t u = uint32_t(lane) >> 4;
@@ -81,51 +53,42 @@ __device__ __forceinline__ void ec_apply_body(const EcArgs& a, const uint32_t* _
     for (int o = 0; o < OG; ++o)
 #pragma unroll
       for (int r = 0; r < 8; ++r) acc[o][r] = u32x2{0u, 0u};
-    if constexpr (PD == 1) {  // the product: the next member in flight while one is combined
-      u32x2 in[8];
+    u32x2 in[8];
 #pragma unroll
-      for (int c = 0; c < 8; ++c) in[c] = ok ? ld64(a.src[0] + base + 128u * c, NTL) : u32x2{0u, 0u};
-      for (uint32_t s = 0; s < a.S; ++s) {
-        u32x2 nx[8];
-        const bool more = s + 1 < a.S;
-        const uint8_t* np = a.src[more ? s + 1 : s];
+    for (int c = 0; c < 8; ++c) in[c] = ok ? ld64nt(a.src[0] + base + 128u * c) : u32x2{0u, 0u};
+    for (uint32_t s = 0; s < a.S; ++s) {
+      u32x2 nx[8];
+      const bool more = s + 1 < a.S;
+      const uint8_t* np = a.src[more ? s + 1 : s];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) nx[c] = (ok && more) ? ld64(np + base + 128u * c, NTL) : u32x2{0u, 0u};
-        combine<OG>(acc, in, masks, a.S, s);
+      for (int c = 0; c < 8; ++c) nx[c] = (ok && more) ? ld64nt(np + base + 128u * c) : u32x2{0u, 0u};
 #pragma unroll
-        for (int c = 0; c < 8; ++c) in[c] = nx[c];
-      }
-    } else {  // ring of PD + 1 members: ring[0] is combined while ring[1..PD] are in flight
-      u32x2 ring[PD + 1][8];
+      for (int o = 0; o < OG; ++o)
 #pragma unroll
-      for (int q = 0; q <= PD; ++q)
+        for (int r = 0; r < 8; ++r) {
+          const uint32_t* m = masks + ((uint32_t(o) * 8u + uint32_t(r)) * a.S + s) * 8u;
 #pragma unroll
-        for (int c = 0; c < 8; ++c)
-          ring[q][c] = (ok && uint32_t(q) < a.S) ? ld64(a.src[q] + base + 128u * c, NTL) : u32x2{0u, 0u};
-      for (uint32_t s = 0; s < a.S; ++s) {
-        combine<OG>(acc, ring[0], masks, a.S, s);
+          for (int c = 0; c < 8; ++c) {
+            const uint32_t mk = m[c];
+            acc[o][r].x = xand(acc[o][r].x, in[c].x, mk);
+            acc[o][r].y = xand(acc[o][r].y, in[c].y, mk);
+          }
+        }
 #pragma unroll
-        for (int q = 0; q < PD; ++q)
-#pragma unroll
-          for (int c = 0; c < 8; ++c) ring[q][c] = ring[q + 1][c];
-        const uint32_t nxt = s + 1u + uint32_t(PD);
-#pragma unroll
-        for (int c = 0; c < 8; ++c)
-          ring[PD][c] = (ok && nxt < a.S) ? ld64(a.src[nxt < a.S ? nxt : 0u] + base + 128u * c, NTL) : u32x2{0u, 0u};
-      }
+      for (int c = 0; c < 8; ++c) in[c] = nx[c];
     }
     if (ok) {
 #pragma unroll
       for (int o = 0; o < OG; ++o)
 #pragma unroll
-        for (int r = 0; r < 8; ++r) st64(a.dst[o] + base + 128u * r, acc[o][r], NTS);
+        for (int r = 0; r < 8; ++r) st64nt(a.dst[o] + base + 128u * r, acc[o][r]);
     }
   }
 }
 
-template <int OG, bool NTL = true, bool NTS = true, int PD = 1>
+template <int OG>
 __global__ void __launch_bounds__(256) ec_apply_kernel(EcArgs a, const uint32_t* __restrict__ masks) {
-  ec_apply_body<OG, NTL, NTS, PD>(a, masks);
+  ec_apply_body<OG>(a, masks);
 }
 
 
@@ -241,18 +204,6 @@ hipError_t launch_ec_apply(const EcArgs& a, int og, int variant, hipStream_t str
   if (blocks > cap) blocks = cap;
   const dim3 g(static_cast<unsigned>(blocks)), b(256);
 #ifdef TFS_CRC_MEASURE
-#define TFS_EC_FORM(NTL_, NTS_, PD_)                                                                            \
-  switch (og) {                                                                                                \
-    case 1: hipLaunchKernelGGL((ec_apply_kernel<1, NTL_, NTS_, PD_>), g, b, 0, stream, a, a.masks); break;      \
-    case 2: hipLaunchKernelGGL((ec_apply_kernel<2, NTL_, NTS_, PD_>), g, b, 0, stream, a, a.masks); break;      \
-    case 3: hipLaunchKernelGGL((ec_apply_kernel<3, NTL_, NTS_, PD_>), g, b, 0, stream, a, a.masks); break;      \
-    default: hipLaunchKernelGGL((ec_apply_kernel<4, NTL_, NTS_, PD_>), g, b, 0, stream, a, a.masks); break;     \
-  }                                                                                                            \
-  return hipGetLastError()
-  if (variant == 8) { TFS_EC_FORM(true, false, 1); }
-  if (variant == 9) { TFS_EC_FORM(false, true, 1); }
-  if (variant == 10) { TFS_EC_FORM(true, true, 2); }
-#undef TFS_EC_FORM
 #endif
   switch (og) {
     case 1: hipLaunchKernelGGL(ec_apply_kernel<1>, g, b, 0, stream, a, a.masks); break;
