@@ -332,6 +332,7 @@ def test_closes_beside_throughput_launches(oracle):
         d_st = crc.DeviceBuffer(ctx, 4 * jobs.size)
         d_ok = crc.DeviceBuffer(ctx, n)
         d_nb = crc.DeviceBuffer(ctx, 4)
+        time.sleep(0.1)  # no resident kernel of an earlier test alive or posted within 50 ms
         assert ctx.throughput_grid() == 256
         for reserve in (True, False):
             ctx.set_cu_reserve(reserve)
