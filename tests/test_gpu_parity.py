@@ -714,6 +714,54 @@ def test_wide_pinned_batches_read_in_place(gpu_ctx, oracle, monkeypatch):
         staged.close()
 
 
+def test_wide_pinned_batches_from_several_threads(gpu_ctx, oracle):
+    """Four threads verify and compute over their own wide page-locked images (16 MiB,
+    300 files each: the in-place throughput launch) on one context at once, 6 calls
+    each, a mismatch planted per image: every result equals the oracle's."""
+    import threading
+    import tfs_amd.crc as crc
+    rng = np.random.default_rng(9191)
+    n = 300
+    jobs = []
+    for t in range(4):
+        lens = rng.integers(20000, 90000, n).astype(np.uint32)
+        offs = np.zeros(n, np.uint64)
+        offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + 3)
+        size = int(offs[-1] + lens[-1]) + 64
+        data = synth_bytes(9200 + t, size)
+        exp = np.array([ocrc(oracle, 0, data[int(o):int(o) + int(l)].tobytes()) for o, l in zip(offs, lens)],
+                       np.uint32)
+        want = exp.copy()
+        want[t * 7] ^= 1
+        pin = crc.PinnedBuffer(gpu_ctx, size)
+        pin.array[:] = data
+        jobs.append((pin, offs, lens, exp, want))
+    errors = []
+
+    def work(t):
+        pin, offs, lens, exp, want = jobs[t]
+        try:
+            for it in range(6):
+                c, ok, nb, rc = gpu_ctx.verify(pin.array, offs, lens, want)
+                if not ((c == exp).all() and nb == 1 and rc == -1010 and not ok[t * 7]):
+                    errors.append((t, it, "verify"))
+                s = gpu_ctx.batch(pin.array, offs, lens, np.zeros(len(offs), np.uint32))
+                if not (s == exp).all():
+                    errors.append((t, it, "batch"))
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append((t, repr(e)))
+    try:
+        ths = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        assert not errors, errors
+    finally:
+        for j in jobs:
+            j[0].free()
+
+
 def test_small_pinned_batches_read_in_place(gpu_ctx, oracle):
     """tfs_crc32_verify / tfs_crc32_batch / submit+wait on a page-locked buffer whose
     span is <= 8 MiB run as one zero-copy launch (payloads, descriptors and verdicts in
