@@ -149,8 +149,10 @@ int tfs_datafile_get_crc(tfs_crc_ctx* ctx, const char* data, int32_t length, uin
 /* ---- batch, host memory ----------------------------------------------- */
 
 /* Batched Func::crc over `n` files of a host buffer [base, base+base_len):
- * out_crc[i] = Func::crc(d[i].seed, base + d[i].offset, d[i].len).  The
- * touched bytes are staged through pinned memory (hipMemcpyAsync) to the GPU.
+ * out_crc[i] = Func::crc(d[i].seed, base + d[i].offset, d[i].len).  A
+ * page-locked `base` (tfs_crc32_host_malloc_pinned / hipHostMalloc) is read in
+ * place by the kernel (zero-copy, up to 65,536 files); pageable bytes are staged
+ * through pinned memory (hipMemcpyAsync) to the GPU.
  * Call sites: data_file.cpp:190 via data_management.cpp:197 (write), batched
  * across concurrent leases. */
 int tfs_crc32_batch(tfs_crc_ctx* ctx, const tfs_crc_desc* d, uint32_t n, const void* base, uint64_t base_len,
@@ -204,7 +206,8 @@ int tfs_crc32_wait(tfs_crc_ctx* ctx, tfs_crc_ticket ticket);
  * meta id), TFS_EXIT_READ_FILE_SIZE_ERROR (meta.size <= 36),
  * TFS_EXIT_SYNC_FILE_ERROR (FileInfo.size_ != meta.size), TFS_EXIT_CHECK_CRC_ERROR}
  * -- the checks of sync_backup.cpp:345-435 / block_console.cpp:543-577 in that
- * order.  d_* variants take device pointers; the host variant copies the image. */
+ * order.  d_* variants take device pointers; the host variant reads a page-locked
+ * image in place (only the named records cross PCIe) and copies a pageable one. */
 int tfs_block_verify(tfs_crc_ctx* ctx, const void* image, uint64_t image_len, const tfs_raw_meta* metas, uint32_t n,
                      uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad);
 int tfs_block_verify_device(tfs_crc_ctx* ctx, const void* d_image, uint64_t image_len, const tfs_raw_meta* d_metas,
