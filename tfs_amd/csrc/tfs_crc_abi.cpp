@@ -237,10 +237,8 @@ constexpr uint32_t kOwnedSlots = kSchedSlots - kForeignSlots;
 constexpr int kVariantDmaCompact = 8;      // DMA staging for host compaction / block verify / small batches
 #ifdef TFS_CRC_MEASURE
 constexpr int kVariantStagedWide = 52;     // wide page-locked host batches staged by DMA (the round-4 form; A/B)
-constexpr int kVariantWideTwoStreams = 53; // wide page-locked batches alternate between two streams (A/B)
 #else
 constexpr int kVariantStagedWide = -1;
-constexpr int kVariantWideTwoStreams = -1;
 #endif
 // A context that posted a close batch this recently keeps the resident kernel's
 // CUs out of its device's throughput launches even while the kernel is between
@@ -255,7 +253,6 @@ struct tfs_crc_ctx {
   int device = -1;
   uint64_t id = 0;  // process-unique (live-context registry)
   hipStream_t stream = nullptr;
-  hipStream_t wide_stream = nullptr;  // measurement form 53: every other wide page-locked batch
   // The latency path's streams (zero-copy small batches; the resident kernel's
   // res_stream) have the device's greatest priority: they never queue behind
   // a throughput launch on `stream`, and their workgroups are dispatched first.
@@ -1014,20 +1011,9 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
   // descriptors from the slot's page-locked words, and writes its verdicts there --
   // one launch per batch, no copy-engine work at all.  A zero-copy read of a whole
   // block image runs at the link's DMA rate (58.1 against 57.5 GB/s).
-  // Measurement build: TFS_CRC_VARIANT=52 stages it as before, 53 puts every other
-  // slot's launch on a second stream so one block's launch can start while the
-  // previous one drains (A/B).
+  // Measurement build: TFS_CRC_VARIANT=52 stages it as before (A/B).
   if (wide && n <= kZeroCopyOutFiles && ctx->variant != kVariantDmaCompact && ctx->variant != kVariantStagedWide &&
       is_pinned_host(base)) {
-    const uintptr_t sa = reinterpret_cast<uintptr_t>(&s), s0 = reinterpret_cast<uintptr_t>(&ctx->slots[0]);
-    const bool odd_async_slot = sa >= s0 && sa < s0 + sizeof(ctx->slots) && (((sa - s0) / sizeof(Slot)) & 1u);
-    if (ctx->variant == kVariantWideTwoStreams && odd_async_slot) {
-      if (!ctx->wide_stream) {
-        HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->wide_stream, hipStreamNonBlocking));
-        HIP_TRY(ctx, bind_owned_stream(ctx, ctx->wide_stream));
-      }
-      st = ctx->wide_stream;
-    }
     void* zb = nullptr;
     HIP_TRY(ctx, s.h_desc.reserve(size_t(n) * sizeof(Desc)));
     if (host_dev_ptr(static_cast<const uint8_t*>(base) + lo, &zb) && s.h_desc.dev && s.h_crc.dev && s.h_ok.dev) {
@@ -1265,7 +1251,6 @@ int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx) {
   resident_teardown(ctx);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->lat_stream) (void)hipStreamSynchronize(ctx->lat_stream);
-  if (ctx->wide_stream) (void)hipStreamSynchronize(ctx->wide_stream);
   for (auto& s : ctx->slots) s.release();
   for (auto& s : ctx->sync_slots) s.release();
   for (auto& cs : ctx->cslots) {
@@ -1289,7 +1274,6 @@ int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx) {
   if (ctx->d_sched) (void)hipFree(ctx->d_sched);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->lat_stream) (void)hipStreamDestroy(ctx->lat_stream);
-  if (ctx->wide_stream) (void)hipStreamDestroy(ctx->wide_stream);
   delete ctx;
   return TFS_SUCCESS;
 }

@@ -9,9 +9,8 @@
 each through the product context (wide page-locked batches read in place by the
 throughput kernel; block verify with metas and verdicts in page-locked words) and a
 measurement context with TFS_CRC_VARIANT=52 (the round-4 forms: the block image
-staged by DMA; block verify with its metas and verdicts copied), and for e2e one
-with 53 (every other in-flight block launched on a second stream), interleaved
-round by round.
+staged by DMA; block verify with its metas and verdicts copied), interleaved round
+by round.
 
   python tools/ab_host_paths.py [ROUNDS] [BLOCKS]
 """
@@ -36,8 +35,6 @@ def main():
     ctx = crc.Context(0)
     os.environ["TFS_CRC_VARIANT"] = "52"
     staged = crc.Context(0, measure=True)
-    os.environ["TFS_CRC_VARIANT"] = "53"
-    two = crc.Context(0, measure=True)
     os.environ["TFS_CRC_VARIANT"] = "0"
     nfiles, rec = bench.FILES_PER_BLOCK, bench.FILEINFO + bench.FILE_SIZE
     blk = nfiles * rec
@@ -87,7 +84,7 @@ def main():
                 raise SystemExit("ab_host_paths: block verify mismatches")
         return (time.perf_counter() - t0) / nblk * 1e3
 
-    cases = {"e2e_product": (e2e, ctx), "e2e_staged": (e2e, staged), "e2e_two_streams": (e2e, two),
+    cases = {"e2e_product": (e2e, ctx), "e2e_staged": (e2e, staged),
              "blockv_product": (blockv, ctx), "blockv_staged": (blockv, staged)}
     for fn, c in cases.values():  # warm every slot and path
         for _ in range(2):
