@@ -2211,78 +2211,10 @@ int tfs_crc32_membench_device(tfs_crc_ctx* ctx, int pattern, const void* d_base,
 #endif
 }
 
-// TFS_CRC_DEV_VMM=<MiB> (measurement): large device buffers built from physical
-// chunks of that size (hipMemCreate), mapped back to back into one reserved range
-// aligned to the chunk, so that each chunk can be mapped with the largest page-table
-// fragments.  Kept in a registry for tfs_crc32_dev_free.
-struct VmmAlloc {
-  size_t total = 0, chunk = 0;
-  std::vector<hipMemGenericAllocationHandle_t> handles;
-};
-std::mutex g_vmm_mu;
-std::map<uintptr_t, VmmAlloc> g_vmm;
-
-void vmm_release(void* va, VmmAlloc& a) {
-  for (size_t k = 0; k < a.handles.size(); ++k) {
-    (void)hipMemUnmap(static_cast<char*>(va) + k * a.chunk, a.chunk);
-    (void)hipMemRelease(a.handles[k]);
-  }
-  (void)hipMemAddressFree(va, a.total);
-}
-
-hipError_t vmm_alloc(int device, uint64_t bytes, uint64_t chunk, void** out) {
-  hipMemAllocationProp prop = {};
-  prop.type = hipMemAllocationTypePinned;
-  prop.location.type = hipMemLocationTypeDevice;
-  prop.location.id = device;
-  size_t gran = 0;
-  hipError_t e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended);
-  if (e != hipSuccess) return e;
-  if (gran == 0) gran = 2u << 20;
-  chunk = (chunk + gran - 1) / gran * gran;
-  VmmAlloc a;
-  a.chunk = size_t(chunk);
-  a.total = size_t((bytes + chunk - 1) / chunk * chunk);
-  void* va = nullptr;
-  if ((e = hipMemAddressReserve(&va, a.total, a.chunk, nullptr, 0)) != hipSuccess) return e;
-  for (size_t off = 0; off < a.total; off += a.chunk) {
-    hipMemGenericAllocationHandle_t h;
-    if ((e = hipMemCreate(&h, a.chunk, &prop, 0)) != hipSuccess) break;
-    if ((e = hipMemMap(static_cast<char*>(va) + off, a.chunk, 0, h, 0)) != hipSuccess) {
-      (void)hipMemRelease(h);
-      break;
-    }
-    a.handles.push_back(h);
-  }
-  if (e == hipSuccess) {
-    hipMemAccessDesc acc = {};
-    acc.location = prop.location;
-    acc.flags = hipMemAccessFlagsProtReadWrite;
-    e = hipMemSetAccess(va, a.total, &acc, 1);
-  }
-  if (e != hipSuccess) {
-    vmm_release(va, a);
-    return e;
-  }
-  std::lock_guard<std::mutex> g(g_vmm_mu);
-  g_vmm[reinterpret_cast<uintptr_t>(va)] = std::move(a);
-  *out = va;
-  return hipSuccess;
-}
-
 int tfs_crc32_dev_malloc(tfs_crc_ctx* ctx, uint64_t bytes, void** d_ptr) {
   if (!ctx || !d_ptr) return TFS_EXIT_PARAMETER_ERROR;
   *d_ptr = nullptr;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
-  static const uint64_t vmm_chunk = [] {
-    const char* v = getenv("TFS_CRC_DEV_VMM");
-    return v ? uint64_t(std::min(std::max(atoi(v), 0), 65536)) << 20 : 0ull;
-  }();
-  if (vmm_chunk && bytes >= vmm_chunk) {
-    if (vmm_alloc(ctx->device, bytes, vmm_chunk, d_ptr) == hipSuccess) return TFS_SUCCESS;
-    (void)hipGetLastError();
-    *d_ptr = nullptr;
-  }
   // TFS_CRC_DEV_CONTIG=1 (measurement): physically contiguous memory, so the
   // page tables can map it with the largest fragments (fewer address-translation
   // misses for a scan over tens of GiB); ordinary memory when that fails.
@@ -2303,24 +2235,6 @@ int tfs_crc32_dev_free(tfs_crc_ctx* ctx, void* d_ptr) {
   if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
   if (!d_ptr) return TFS_SUCCESS;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
-  {
-    VmmAlloc a;
-    bool vmm = false;
-    {
-      std::lock_guard<std::mutex> g(g_vmm_mu);
-      auto it = g_vmm.find(reinterpret_cast<uintptr_t>(d_ptr));
-      if (it != g_vmm.end()) {
-        a = std::move(it->second);
-        g_vmm.erase(it);
-        vmm = true;
-      }
-    }
-    if (vmm) {
-      HIP_TRY(ctx, hipDeviceSynchronize());  // no launch may still read it
-      vmm_release(d_ptr, a);
-      return TFS_SUCCESS;
-    }
-  }
   HIP_TRY(ctx, hipFree(d_ptr));
   return TFS_SUCCESS;
 }
