@@ -12,9 +12,9 @@ drops out.
 Two more entries: "product_nosplit" is the product library's SAME context with
 file splitting switched off (tfs_crc32_set_split 0) for its rounds, so split on
 vs off shares one stream and one scratch set and the per-context placement
-noise (up to +-2 % between two contexts of one library) drops out of that pair;
-"appended" is a measurement-build context in round 3's split form (segments
-after all files, set_split 2).  OTHER_SO "-" compares only those.
+noise (up to +-2 % between two contexts of one library) drops out of that pair.
+(Round 3's "appended" split form was deleted in round 5.)  OTHER_SO "-" compares
+only those.
 AB_VARIANTS=v[,v...] adds measurement-build contexts running kernel variant v
 (TFS_CRC_VARIANT) as entries "v<v>".
 """
@@ -54,9 +54,7 @@ def main():
     ctx = crc.Context(0)
     prod = bind(crc.LIB_PATH)
     prod[0].tfs_crc32_set_split.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    meas = bind(os.path.join(os.path.dirname(crc.LIB_PATH), "libtfs_crc_measure.so"))
-    meas[0].tfs_crc32_set_split.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    libs = {"product": prod, "product_nosplit": prod, "appended": meas}
+    libs = {"product": prod, "product_nosplit": prod}
     for i, o in enumerate(x for x in other.split(",") if x and x != "-"):
         libs["other%d" % i] = bind(os.path.abspath(o))
     if mode == "zipf":
@@ -105,8 +103,8 @@ def main():
     times = {k: [] for k in libs}
     for r in range(rounds):
         for name, (L, h) in libs.items():
-            if name in ("product", "product_nosplit", "appended"):  # split forms (tfs_crc32_set_split)
-                assert L.tfs_crc32_set_split(h, {"product": 1, "product_nosplit": 0, "appended": 2}[name]) == 0
+            if name in ("product", "product_nosplit"):  # split on / off (tfs_crc32_set_split)
+                assert L.tfs_crc32_set_split(h, {"product": 1, "product_nosplit": 0}[name]) == 0
             e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
             L.tfs_crc32_event_create(h, ctypes.byref(e0))
             L.tfs_crc32_event_create(h, ctypes.byref(e1))
