@@ -2440,10 +2440,13 @@ hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, u
 #undef TFS_COPY2
     return hipGetLastError();
   }
+  if (pattern < 0 || pattern >= 20000) return hipErrorInvalidValue;  // no other shape is built
   const uint32_t align = pattern >= 10000 ? 128u : 16u;
   pattern %= 10000;
   const bool nt = pattern >= 1000;
   const uint32_t run = uint32_t(pattern % 1000);
+  // a stripe is 64 lanes x 16 B = 64 * run bytes: run 0 (grid-stride) or a multiple of 16
+  if ((run != 0 && run % 16 != 0) || pattern >= 2000) return hipErrorInvalidValue;
   const dim3 g(grid ? grid : (run ? grid_for(n) : 2048u));
   if (nt)
     hipLaunchKernelGGL(membench_kernel<true>, g, dim3(kBlock), 0, stream, base, desc, n, nbytes, run, out, align);

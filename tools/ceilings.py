@@ -4,9 +4,8 @@
 Builds bench.py's configs[1] resident set (or benchlines.zipf's configs[2]
 image), times the product kernel on it, then the calibration kernels of the
 measurement build (libtfs_crc_measure.so, membench_kernel) over the same bytes:
-the kernel's own access pattern without the CRC arithmetic, wave- and
-workgroup-contiguous chunks, and the grid-stride stream -- the ceilings the
-kernel is held to.  One JSON line on stdout.
+the kernel's own access pattern without the CRC arithmetic and the grid-stride
+stream -- the ceilings the kernel is held to.  One JSON line on stdout.
 
   python tools/ceilings.py verify|zipf [ROUNDS]
 """
@@ -24,9 +23,9 @@ import tfs_amd.crc as crc  # noqa: E402
 from benchlines import zipf as zl  # noqa: E402
 
 # pattern ids of launch_membench (tfs_crc_kernels.hip): 1000 grid-stride; 11016 the
-# kernel's 1 KiB stripes with 128-byte anchors; 54xxx wave-contiguous and 55xxx
-# workgroup-contiguous chunks of (xx) x 16 KiB
-VERIFY_PATTERNS = [(1000, 0), (1000, 1024), (11016, 0), (54004, 0), (54016, 0), (55404, 0), (55404, 512)]
+# kernel's 1 KiB stripes with 128-byte anchors.  (The wave- and workgroup-contiguous
+# chunk reads, 54xxx / 55xxx, were deleted in round 5; DESIGN §4 keeps what they read.)
+VERIFY_PATTERNS = [(1000, 0), (1000, 1024), (11016, 0)]
 ZIPF_PATTERNS = [(11016, 0), (1000, 0), (1000, 1024)]
 
 
@@ -68,10 +67,7 @@ def main():
         kernel = (lambda: ctx.verify_device(d_desc, n, img, None, d_ok, None))
         pats = []
         for p, g in VERIFY_PATTERNS:
-            if p >= 54000:
-                ch = (p % 100) * 16384
-                nb = total // ch * ch
-            elif p % 1000 == 0:
+            if p % 1000 == 0:
                 nb = total
             else:
                 run = p % 1000

@@ -34,7 +34,7 @@ for grid in (256, 1024, 2048, 4096):
         s = t(lambda: ctx.membench_device(pat, h.ptr, None, 0, N, out, grid=grid))
         res["zc_read_p%d_g%d_GBs" % (pat, grid)] = N / s / 1e9
 for grid in (256, 2048):
-    for pat in (50000, 51000):
+    for pat in (52004, 52114):  # grid-stride copies: plain, and nt loads + stores
         s = t(lambda: ctx.membench_device(pat, h.ptr, None, 0, N // 2, h2.ptr, grid=grid))
         res["zc_host2host_copy_p%d_g%d_GBs_each_way" % (pat, grid)] = (N // 2) / s / 1e9
         s = t(lambda: ctx.membench_device(pat, d.ptr, None, 0, N, h2.ptr, grid=grid))
