@@ -354,8 +354,9 @@ def main():
         ceil = pcie_ceiling(ctx, dist=dist)
         result["end_to_end"] = {
             "value": gibs, "unit": "GiB/s", "pcie_GBs": pcie, "ms_per_block": el / args.e2e_blocks * 1e3,
-            "workload": "%d pinned host 64 MiB block images per GPU -> H2D -> verify -> verdicts back, "
-                        "3 in flight, max over ranks" % args.e2e_blocks,
+            "workload": "%d pinned host 64 MiB block images per GPU, verified by the GPU reading each image "
+                        "over PCIe in place (zero-copy; verdicts back in page-locked words), 3 in flight, max "
+                        "over ranks" % args.e2e_blocks,
             "per_rank": e2e_ranks,
             "roofline": {"bound": "pcie", "achieved": pcie / world, "peak": ceil["h2d_GBs"], "unit": "GB/s (per GPU)",
                          "frac": pcie / world / ceil["h2d_GBs"], "peak_source": ceil["source"],

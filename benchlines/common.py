@@ -418,7 +418,7 @@ def _cpu_model():
 
 
 def e2e_blocks(ctx, dist, world, rank, nsub, inflight=3, cpu=None):
-    """configs[4] end-to-end leg: pinned host block images -> H2D -> verify ->
+    """configs[4] end-to-end leg: pinned host block images -> (read over PCIe in place) verify ->
     verdicts back, `inflight` blocks in flight (submit/wait), timed between
     barriers, max over ranks.  Returns (payload GiB/s over all ranks, PCIe GB/s,
     elapsed s, per-rank {payload GiB/s, PCIe GB/s} (per_rank))."""

@@ -5,7 +5,7 @@ from benchlines.common import *  # noqa: F401,F403
 
 
 def bench_e2e(args):
-    """Verify-on-read starting in host memory: pinned block images -> H2D ->
+    """Verify-on-read starting in host memory: pinned block images -> (read over PCIe in place) ->
     verify -> verdicts back, several blocks in flight (submit/wait)."""
     import tfs_amd.crc as crc
     world, rank, local, dist = _dist_init()
