@@ -714,6 +714,41 @@ def test_wide_pinned_batches_read_in_place(gpu_ctx, oracle, monkeypatch):
         staged.close()
 
 
+@pytest.mark.parametrize("n", [65536, 65537])
+def test_wide_pinned_batch_file_limit(gpu_ctx, oracle, n):
+    """The in-place path for wide page-locked batches takes up to 65,536 files (the
+    slot's page-locked verdict words); one file more goes the staged way.  Both
+    sides of the limit: ragged small files with seeds (compute) and with planted
+    mismatches (verify), every CRC against the oracle."""
+    import tfs_amd.crc as crc
+    rng = np.random.default_rng(n)
+    lens = rng.integers(0, 300, n).astype(np.uint32)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + rng.integers(0, 5, n - 1).astype(np.uint64))
+    size = int(offs[-1] + lens[-1]) + 64
+    assert size > 8 << 20
+    data = synth_bytes(7300 + n, size)
+    seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    d = np.zeros(n, crc.DESC_DTYPE)
+    d["offset"], d["len"], d["aux"] = offs, lens, seeds
+    exp_s = np.zeros(n, np.uint32)
+    oracle.oracle_crc_batch(d.ctypes.data, n, data.ctypes.data, exp_s.ctypes.data)
+    d["aux"] = 0
+    exp0 = np.zeros(n, np.uint32)
+    oracle.oracle_crc_batch(d.ctypes.data, n, data.ctypes.data, exp0.ctypes.data)
+    want = exp0.copy()
+    bad = np.array([0, n // 2, n - 1])
+    want[bad] ^= 0x40
+    pin = crc.PinnedBuffer(gpu_ctx, size)
+    try:
+        pin.array[:] = data
+        assert (gpu_ctx.batch(pin.array, offs, lens, seeds) == exp_s).all()
+        c, ok, nb, rc = gpu_ctx.verify(pin.array, offs, lens, want)
+        assert (c == exp0).all() and nb == 3 and rc == -1010 and not ok[bad].any() and ok.sum() == n - 3
+    finally:
+        pin.free()
+
+
 def test_wide_pinned_batches_from_several_threads(gpu_ctx, oracle):
     """Four threads verify and compute over their own wide page-locked images (16 MiB,
     300 files each: the in-place throughput launch) on one context at once, 6 calls
