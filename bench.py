@@ -41,6 +41,7 @@ from benchlines.common import *  # noqa: E402,F401,F403
 
 WORKLOADS = {
     "zipf": ("benchlines.zipf", "bench_zipf"),                      # BASELINE configs[2]
+    "zipf_e2e": ("benchlines.zipf_e2e", "bench_zipf_e2e"),          # configs[2] from host receive buffers
     "compact": ("benchlines.compact", "bench_compact"),             # configs[3]
     "e2e": ("benchlines.e2e", "bench_e2e"),                         # configs[4] end-to-end
     "loopback": ("benchlines.loopback", "bench_loopback"),          # configs[0]
@@ -68,7 +69,8 @@ def parse(argv=None):
                    help="every K-th resident block is checked in full against the oracle (outside the timed region)")
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--e2e-blocks", type=int, default=128,
-                   help="blocks per GPU for the end-to-end (H2D-inclusive) leg of the default line; 0 = off")
+                   help="blocks (receive buffers for zipf/zipf_e2e) per GPU for the end-to-end (H2D-inclusive) leg "
+                        "of the default and zipf lines; 0 = off")
     p.add_argument("--ec-mib", type=int, default=1536,
                    help="member size in MiB for --workload ec (< 2048: ErasureCode sizes are int)")
     p.add_argument("--workload", default="verify", choices=["verify"] + sorted(WORKLOADS),

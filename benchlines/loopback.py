@@ -8,6 +8,29 @@ import numpy as np
 from benchlines.common import *  # noqa: F401,F403
 
 
+def close_tail(us, ph):
+    """Where the slowest closes' time went: the mean of each
+    CloseTiming phase over the closes at or above p99 against those at or below p50,
+    and how many of each saw a resident-kernel relaunch or a ring-full launch during
+    their batch's verify."""
+    import tfs_amd.dataserver as ds
+    p50, p99 = np.percentile(us, 50), np.percentile(us, 99)
+    out = {}
+    for name, sel in (("at_or_above_p99", us >= p99), ("at_or_below_p50", us <= p50)):
+        sub = ph[sel]
+        d = {k: float(sub[:, i].mean()) for i, k in enumerate(ds.CLOSE_PHASES[:6])}
+        d["total_us"] = float(us[sel].mean())
+        d["closes"] = int(sel.sum())
+        d["with_relaunch"] = int((sub[:, 8] > 0).sum())
+        d["with_ring_full"] = int((sub[:, 9] > 0).sum())
+        out[name] = d
+    out["note"] = ("phases of a close (ds_harness.h CloseTiming): claim = batch slot, copy = payload into the gather "
+                   "buffer, wait = until the verdicts are in (a leader's wait is its own verify call: lead_wait + "
+                   "verify), append = FileInfo|payload persist; with_relaunch = closes whose batch verify spanned a "
+                   "resident kernel launch")
+    return out
+
+
 def bench_loopback(args):
     """BASELINE configs[0]: src/dataserver write + verify over one 64 MiB block of
     1024 x 64 KiB synthetic payloads, single-process loopback (no nameserver).
@@ -136,11 +159,15 @@ def bench_loopback(args):
     sl = ds.scalar_latency(300)
     lat["scalar_tfs_crc32_64KiB"] = {"p50_us": float(np.percentile(sl, 50)), "p99_us": float(np.percentile(sl, 99)),
                                      "calls": int(sl.size)}
+    st0 = ctx.stats()
     for nl, it in ((1, 300), (8, 64), (64, 8)):
-        cl = ds.close_latency(ctx, nl, it)
+        cl, ph = ds.close_latency(ctx, nl, it, phases=True)
         lat["close_%d_leases" % nl] = {"p50_us": float(np.percentile(cl, 50)), "p99_us": float(np.percentile(cl, 99)),
-                                       "closes": int(cl.size)}
+                                       "closes": int(cl.size), "tail": close_tail(cl, ph)}
+    st1 = ctx.stats()
     res["latency"] = lat
+    res["latency_counters"] = {k: st1[k] - st0[k] for k in ("resident_launches", "resident_files",
+                                                            "resident_ring_full", "lone_calls", "host_calls")}
     # resident kernel over this whole line: launches (first + relaunches after
     # idle or lifetime exits) against the files it took
     launches, rfiles = ctx.resident_stats()

@@ -133,6 +133,11 @@ def bench_zipf(args):
                                            "Zipf-sized payloads (evenly spaced files of the batch)")
     if dist and not args.no_cpu:
         dist.barrier()
+    if args.e2e_blocks > 0:
+        # north_star: the write path starts in host memory (the receive buffer), so
+        # the PCIe-inclusive rate of the same Zipf files rides beside `value`
+        from benchlines.zipf_e2e import zipf_e2e_leg
+        res["end_to_end"] = zipf_e2e_leg(ctx, dist, world, rank, args.e2e_blocks)
     emit(rank, res)
     del ev
     for b in (img, d_desc, d_out):

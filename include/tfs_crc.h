@@ -140,6 +140,26 @@ int tfs_crc32_bind_thread(tfs_crc_ctx* ctx);
  * NULL when none can be made. */
 tfs_crc_ctx* tfs_crc32_default_ctx(void);
 
+/* Per-context call counters, monotonic from the context's creation, so an
+ * integration can see callers that should batch.  A lone host call (one body)
+ * shorter than TFS_CRC_LONE_CROSSOVER bytes costs one GPU round trip over PCIe
+ * (~9 us), longer than the reference's host loop takes on
+ * it (1.6 ns/byte): such a caller -- a small RPC body checked alone,
+ * base_packet.cpp:141 -- should gather its bodies into one tfs_crc32_batch /
+ * tfs_packet_verify call.  Scalar calls count on the context they run on. */
+#define TFS_CRC_LONE_CROSSOVER 5660
+typedef struct tfs_crc_stats {
+  uint64_t host_calls;         /* synchronous host-memory calls: scalar, get_crc, batch, verify, small packet sets */
+  uint64_t host_files;         /* bodies they carried */
+  uint64_t lone_calls;         /* of host_calls, those carrying exactly one body */
+  uint64_t lone_small_calls;   /* of lone_calls, bodies shorter than TFS_CRC_LONE_CROSSOVER bytes */
+  uint64_t lone_small_bytes;   /* the bytes of those bodies */
+  uint64_t resident_launches;  /* resident kernel launches (the first and every relaunch) */
+  uint64_t resident_files;     /* bodies the resident kernel took */
+  uint64_t resident_ring_full; /* batches launched because the resident ring had no room */
+} tfs_crc_stats;
+int tfs_crc32_stats(tfs_crc_ctx* ctx, tfs_crc_stats* out);
+
 /* Replaces DataFile::get_crc() (src/dataserver/data_file.cpp:168-194):
  * Func::crc(0, data, length).  The reference re-reads payloads > 2 MiB in
  * 2 MiB chunks with a running seed (:183-186); that equals one pass over the

@@ -63,6 +63,16 @@ int tfs_crc32_debug_poison_resident(tfs_crc_ctx* ctx, uint32_t done);
  * Stats: kernel launches made and files taken through the ring so far. */
 int tfs_crc32_set_resident(tfs_crc_ctx* ctx, int on);
 int tfs_crc32_resident_stats(tfs_crc_ctx* ctx, uint64_t* launches, uint64_t* files);
+/* Resident-path stamps (measurement build only, libtfs_crc_measure.so; the product
+ * returns TFS_EXIT_PARAMETER_ERROR).  tfs_crc32_res_trace, before the context's
+ * first resident call: `pinned` (page-locked, 4096 units x 4 u64) receives, per
+ * ring unit, the GPU's 100 MHz wall-clock stamps of the poll issue that found the
+ * unit published, that poll's return, the unit's words back and its CRC done.
+ * tfs_crc32_res_trace_last: the last synchronous call's host stamps (steady clock
+ * ns) {enter, posted, result seen, return}, its first ring unit, whether it went
+ * through the ring, and the wall-clock rate in kHz (tools/floor_probe.cpp). */
+int tfs_crc32_res_trace(tfs_crc_ctx* ctx, void* pinned);
+int tfs_crc32_res_trace_last(tfs_crc_ctx* ctx, uint64_t* out8);
 /* Throughput launches (the *_device calls and large host batches: one
  * persistent workgroup per CU) leave the CUs of every resident kernel of their
  * device free while it lives or has had a batch in the last 50 ms, so a close

@@ -45,7 +45,7 @@ PRODUCT_API = {
     "tfs_crc32_ctx_create", "tfs_crc32_ctx_destroy", "tfs_crc32_last_error", "tfs_crc32_device_count",
     "tfs_crc32_device_numa_node",
     "tfs_crc32", "tfs_crc32_e", "tfs_crc32_error_count", "tfs_crc32_set_default_ctx", "tfs_crc32_bind_thread",
-    "tfs_crc32_default_ctx", "tfs_datafile_get_crc",
+    "tfs_crc32_default_ctx", "tfs_datafile_get_crc", "tfs_crc32_stats",
     "tfs_crc32_batch", "tfs_crc32_verify", "tfs_crc32_batch_device", "tfs_crc32_verify_device",
     "tfs_crc32_submit_verify", "tfs_crc32_wait",
     "tfs_block_verify", "tfs_block_verify_device", "tfs_block_compact", "tfs_block_compact_device",

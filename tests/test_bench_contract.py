@@ -48,9 +48,18 @@ def test_default_line_contract_small():
 
 @pytest.mark.gpu
 def test_zipf_and_compact_lines_carry_cpu_baseline():
-    z = _run(["--workload", "zipf", "--blocks", "8", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0.3"])
+    z = _run(["--workload", "zipf", "--blocks", "8", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0.3",
+              "--e2e-blocks", "20"])
     assert z["roofline"]["bound"] == "hbm" and z["cpu_baseline"]["value"] > 0
     assert z["parity"]["files_checked"] > 100 and z["parity"]["mismatches"] == 0
+    # configs[2] from host memory: the receive-buffer leg beside the device-resident value
+    e = z["end_to_end"]
+    assert 0 < e["value"] < z["value"] and e["pcie_GBs"] > 0 and e["n_buffers"] == 20 and e["inflight"] == 3
+    assert e["roofline"]["bound"] == "pcie" and 0 < e["roofline"]["frac"] < 1.2
+    assert e["parity"]["mismatches"] == 0 and e["parity"]["files_checked"] > 20 * 100
+    assert e["per_rank"]["pcie_GBs"]
+    s = _run(["--workload", "zipf_e2e", "--e2e-blocks", "8"])
+    assert s["value"] > 0 and s["roofline"]["bound"] == "pcie" and s["parity"]["mismatches"] == 0
     c = _run(["--workload", "compact", "--compact-blocks", "16", "--cpu-seconds", "0.3"])
     assert c["value"] > 0 and c["cpu_baseline"]["kind"] == "port"
     assert c["unit"] == "GiB/s of live payload" and c["source_block_GiBs"] > c["value"]

@@ -143,13 +143,16 @@ def test_product_segmented_compaction_toggle(gpu_ctx, oracle, seg):
     gpu_ctx.set_compact_segment(seg)
     try:
         _jobs_statuses_case(gpu_ctx, oracle)
+        # every record flagged TFS_COMPACT_JOB_EDGE (the bit rides on a
+        # split record's last segment): the same bytes, CRCs and statuses
+        _jobs_statuses_case(gpu_ctx, oracle, edge=True)
     finally:
         gpu_ctx.set_compact_segment(1)  # the default again (whole records)
     with pytest.raises(Exception):
         gpu_ctx.set_compact_segment(12345)
 
 
-def _jobs_statuses_case(vctx, oracle):
+def _jobs_statuses_case(vctx, oracle, edge=False):
     """tfs_compact_jobs_device over records of every size class (many longer than
     the 8 / 16 / 32 KiB segments of the segmented form, including exact
     multiples and one byte past them), with rejected records on both short and
@@ -169,6 +172,8 @@ def _jobs_statuses_case(vctx, oracle):
     j = np.zeros(n, crc.COMPACT_JOB_DTYPE)
     j["src_offset"], j["dest_offset"] = metas["offset"], doff
     j["file_id"], j["size"], j["new_offset"] = metas["file_id"], metas["size"], doff
+    if edge:
+        j["reserved"] = 1   # TFS_COMPACT_JOB_EDGE: no byte past any record is read
     big = [k for k in range(n) if sizes[k] > 40000]
     bad = {}
     img2 = img.copy()

@@ -562,6 +562,120 @@ def test_blocks_compact_zero_copy_groups(gpu_ctx, oracle, monkeypatch):
         ctx8.close()
 
 
+def _pinned_group_blocks(gpu_ctx, oracle, nblk, seed, bufs):
+    """nblk page-locked source/destination block pairs with their oracle results."""
+    import tfs_amd.crc as crc
+    rng = np.random.default_rng(seed)
+    keep = []
+    for b in range(nblk):
+        sizes = [int(x) for x in rng.choice([1, 33, 1023, 4096, 65536, 70001], 20)]
+        img, metas = _block_image(oracle, sizes, seed=seed + b)
+        img = img[:int(metas["size"].astype(np.int64).sum())].copy()
+        flags = np.zeros(len(sizes), np.int32)
+        flags[b % 3::3] |= 1
+        src = crc.PinnedBuffer(gpu_ctx, img.size)
+        src.array[:] = img
+        cap = int(metas["size"].astype(np.int64).sum()) + 64
+        dst = crc.PinnedBuffer(gpu_ctx, cap)
+        bufs += [src, dst]
+        keep.append([src, img, metas, flags, dst, cap])
+    return keep
+
+
+def _group_jobs(keep):
+    import tfs_amd.crc as crc
+    jobs = (crc.BlockJob * len(keep))()
+    outs = []
+    for b, (src, img, metas, flags, dst, cap) in enumerate(keep):
+        dst.array[:] = 0
+        ok = np.full(len(metas), 7, np.uint8)
+        dm = np.zeros(len(metas), crc.META_DTYPE)
+        outs.append((ok, dm))
+        j = jobs[b]
+        j.src_image, j.src_len, j.metas, j.flags, j.n = src.ptr, img.size, metas.ctypes.data, flags.ctypes.data, \
+            len(metas)
+        j.dest_image, j.dest_cap, j.dest_metas, j.crc_ok = dst.ptr, cap, dm.ctypes.data, ok.ctypes.data
+        j.status = 12345
+    return jobs, outs
+
+
+def _check_group_block(oracle, keep_b, job, out, tag):
+    src, img, metas, flags, dst, cap = keep_b
+    odest, doff, ook = _oracle_compact(oracle, src.array.copy(), metas, flags)
+    ok, dm = out
+    live = np.nonzero((flags & 3) == 0)[0]
+    w = int(job.dest_len)
+    assert w == odest.size and job.n_live == live.size, tag
+    assert (dst.array[:w] == odest).all(), tag
+    assert (ok == ook).all(), tag
+    assert job.status == (0 if (ook[live] == 1).all() else -1010), tag
+    assert (dm["offset"][:live.size] == doff[live]).all(), tag
+
+
+def test_blocks_compact_group_failures(gpu_ctx, oracle):
+    """the failure paths of a zero-copy group.  A pinned run of 12 blocks
+    (more than the 8 compaction slots, so the per-job fallback reuses the slot the
+    failed group held) with an out-of-range meta in block 4 and a too-small
+    dest_cap in block 7: those two report TFS_EXIT_PARAMETER_ERROR with nothing
+    written, every other block (one with a corrupted record) equals the oracle.
+    Then a device error injected in the middle of the fallback: the blocks issued
+    before it finish, it and every later block carry the device error, and the
+    call returns it.  After each, a clean call on the same context is exact and
+    leaves the earlier call's job array untouched (no stale slot state)."""
+    import ctypes
+    bufs = []
+    try:
+        keep = _pinned_group_blocks(gpu_ctx, oracle, 12, 7100, bufs)
+        live10 = np.nonzero((keep[10][3] & 3) == 0)[0]
+        k = int(live10[0])
+        keep[10][0].array[int(keep[10][2][k]["offset"]) + 36 + int(keep[10][2][k]["size"]) // 2 - 20] ^= 0x08
+
+        def run(jobs):
+            return gpu_ctx.L.tfs_blocks_compact(gpu_ctx.handle, ctypes.cast(jobs, ctypes.c_void_p), len(jobs))
+
+        # (1) parameter errors inside the group
+        bad_metas = keep[4][2].copy()
+        bad_metas[3]["offset"] = keep[4][1].size  # past the image
+        jobs1, outs1 = _group_jobs(keep)
+        jobs1[4].metas = bad_metas.ctypes.data
+        jobs1[7].dest_cap = 100
+        assert run(jobs1) == -1016
+        for b in range(12):
+            if b in (4, 7):
+                assert jobs1[b].status == -1016 and jobs1[b].dest_len == 0 and jobs1[b].n_live == 0, b
+            else:
+                _check_group_block(oracle, keep[b], jobs1[b], outs1[b], ("param", b))
+        snap1 = [(j.status, j.dest_len, j.n_live) for j in jobs1]
+
+        jobs2, outs2 = _group_jobs(keep)
+        assert run(jobs2) == -1010
+        for b in range(12):
+            _check_group_block(oracle, keep[b], jobs2[b], outs2[b], ("clean", b))
+        assert [(j.status, j.dest_len, j.n_live) for j in jobs1] == snap1
+
+        # (2) a device error in the per-job fallback: the group consults the fault
+        # hook for jobs 0..4 before rejecting job 4, the fallback once per job.
+        jobs3, outs3 = _group_jobs(keep)
+        jobs3[4].metas = bad_metas.ctypes.data
+        gpu_ctx.inject_device_error(5 + 3, 1)
+        assert run(jobs3) == -20001
+        for b in range(3):
+            _check_group_block(oracle, keep[b], jobs3[b], outs3[b], ("dev", b))
+        for b in range(3, 12):
+            assert jobs3[b].status == -20001 and jobs3[b].dest_len == 0 and jobs3[b].n_live == 0, b
+        snap3 = [(j.status, j.dest_len, j.n_live) for j in jobs3]
+
+        jobs4, outs4 = _group_jobs(keep)
+        assert run(jobs4) == -1010
+        for b in range(12):
+            _check_group_block(oracle, keep[b], jobs4[b], outs4[b], ("after", b))
+        assert [(j.status, j.dest_len, j.n_live) for j in jobs3] == snap3
+    finally:
+        gpu_ctx.inject_device_error(0, 0)
+        for p in bufs:
+            p.free()
+
+
 def test_blocks_compact_zero_copy_matches_oracle(gpu_ctx, oracle, monkeypatch):
     """Page-locked source and destination images: the fused kernel reads the live
     records over PCIe and writes the new block in place (no whole-block DMA).

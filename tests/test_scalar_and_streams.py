@@ -338,3 +338,39 @@ def test_owned_streams_keep_their_slots(gpu_ctx, oracle):
     finally:
         for b in (out, ok, bad, img, dd):
             b.free()
+
+
+def test_stats_count_lone_small_calls(oracle):
+    """tfs_crc32_stats: every synchronous host call is counted,
+    and the lone ones (one body) under TFS_CRC_LONE_CROSSOVER bytes -- the calls
+    an integration should batch -- separately with their bytes, the scalar
+    drop-in's included (on the context it runs on); the results stay exact."""
+    import tfs_amd.crc as crc
+    L = crc.lib()
+    ctx = crc.Context(0)
+    try:
+        buf = synth_bytes(77, 3 * crc.LONE_CROSSOVER)
+        raw = buf.tobytes()
+        s0 = ctx.stats()
+        assert all(v == 0 for v in s0.values()), s0
+        assert ctx.batch(buf, [5], [100])[0] == ocrc(oracle, 0, raw[5:105])              # lone, small
+        n = crc.LONE_CROSSOVER
+        assert ctx.batch(buf, [0], [n])[0] == ocrc(oracle, 0, raw[:n])                  # lone, at the crossover
+        assert ctx.batch(buf, [0], [n - 1])[0] == ocrc(oracle, 0, raw[:n - 1])          # lone, just under
+        got = ctx.batch(buf, [0, 300, 900], [10, 20, 30])                               # three bodies
+        assert [int(x) for x in got] == [ocrc(oracle, 0, raw[o:o + k]) for o, k in ((0, 10), (300, 20), (900, 30))]
+        exp = ocrc(oracle, 0, raw[7:7 + 64])
+        _, ok, nbad, rc = ctx.verify(buf, [7], [64], [exp])                            # lone verify, small
+        assert nbad == 0 and ok[0] == 1
+        assert L.tfs_crc32_bind_thread(ctx.handle) == 0
+        try:
+            assert L.tfs_crc32(0, raw[:33], 33) == ocrc(oracle, 0, raw[:33])            # scalar, small
+        finally:
+            L.tfs_crc32_bind_thread(None)
+        s1 = ctx.stats()
+        assert s1["host_calls"] == 6 and s1["host_files"] == 8, s1
+        assert s1["lone_calls"] == 5, s1
+        assert s1["lone_small_calls"] == 4 and s1["lone_small_bytes"] == 100 + (n - 1) + 64 + 33, s1
+        assert s1["resident_files"] >= 0 and s1["resident_ring_full"] == 0
+    finally:
+        ctx.close()

@@ -70,7 +70,7 @@ EXPORTED = [
     "tfs_crc32_event_elapsed_ms", "tfs_crc32_event_destroy",
     "tfs_crc32_stream", "tfs_crc32_sync", "tfs_crc32_stream_create", "tfs_crc32_stream_sync",
     "tfs_crc32_stream_destroy", "tfs_crc32_inject_device_error", "tfs_crc32_set_resident",
-    "tfs_crc32_resident_stats", "tfs_crc32_error_count", "tfs_crc32_set_default_ctx", "tfs_crc32_bind_thread",
+    "tfs_crc32_resident_stats", "tfs_crc32_stats", "tfs_crc32_res_trace", "tfs_crc32_res_trace_last", "tfs_crc32_error_count", "tfs_crc32_set_default_ctx", "tfs_crc32_bind_thread",
     "tfs_crc32_default_ctx", "tfs_crc32_set_cu_reserve", "tfs_crc32_throughput_grid", "tfs_crc32_sched_stats", "tfs_crc32_plan_stats",
     "tfs_crc32_debug_state", "tfs_crc32_debug_poison_resident",
     "tfs_crc32_set_split", "tfs_crc32_split_stats", "tfs_crc32_set_compact_segment",
@@ -89,6 +89,16 @@ class BlockJob(ctypes.Structure):
                 ("flags", ctypes.c_void_p), ("n", ctypes.c_uint32), ("dest_image", ctypes.c_void_p),
                 ("dest_cap", ctypes.c_uint64), ("dest_metas", ctypes.c_void_p), ("crc_ok", ctypes.c_void_p),
                 ("dest_len", ctypes.c_uint64), ("n_live", ctypes.c_uint32), ("status", ctypes.c_int)]
+
+
+class CrcStats(ctypes.Structure):
+    """tfs_crc_stats (include/tfs_crc.h)."""
+    _fields_ = [(k, ctypes.c_uint64) for k in (
+        "host_calls", "host_files", "lone_calls", "lone_small_calls", "lone_small_bytes", "resident_launches",
+        "resident_files", "resident_ring_full")]
+
+
+LONE_CROSSOVER = 5660  # TFS_CRC_LONE_CROSSOVER
 
 
 class TfsCrcError(RuntimeError):
@@ -160,6 +170,9 @@ def lib(measure=False):
             "tfs_crc32_set_resident": (ctypes.c_int, [vp, ctypes.c_int]),
             "tfs_crc32_resident_stats": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64),
                                                         ctypes.POINTER(ctypes.c_uint64)]),
+            "tfs_crc32_stats": (ctypes.c_int, [vp, vp]),
+            "tfs_crc32_res_trace": (ctypes.c_int, [vp, vp]),
+            "tfs_crc32_res_trace_last": (ctypes.c_int, [vp, vp]),
             "tfs_crc32_error_count": (ctypes.c_uint64, []),
             "tfs_crc32_set_default_ctx": (ctypes.c_int, [vp]),
             "tfs_crc32_bind_thread": (ctypes.c_int, [vp]),
@@ -302,6 +315,13 @@ class Context:
         a, b = ctypes.c_uint64(), ctypes.c_uint64()
         self._check(self.L.tfs_crc32_resident_stats(self.handle, ctypes.byref(a), ctypes.byref(b)), "resident_stats")
         return a.value, b.value
+
+    def stats(self):
+        """tfs_crc32_stats as a dict: host calls, lone (one-body) calls and those under
+        TFS_CRC_LONE_CROSSOVER, resident kernel launches / files / ring-full launches."""
+        st = CrcStats()
+        self._check(self.L.tfs_crc32_stats(self.handle, ctypes.byref(st)), "stats")
+        return {k: getattr(st, k) for k, _ in CrcStats._fields_}
 
     def set_cu_reserve(self, on):
         """Leave live resident kernels' CUs out of throughput launches (on, the default) or not."""

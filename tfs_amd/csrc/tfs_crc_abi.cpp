@@ -61,7 +61,7 @@ hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, u
                            uint32_t* out, unsigned grid, hipStream_t stream);
 #endif
 hipError_t launch_resident(const Tables* tg, const ResHost* hs, uint32_t* dstate, unsigned grid, uint32_t idle_ticks,
-                           uint32_t life_ticks, uint32_t gen, hipStream_t stream);
+                           uint32_t life_ticks, uint32_t gen, hipStream_t stream, uint64_t* trace);
 }  // namespace tfscrc
 
 namespace tfscrc {
@@ -104,6 +104,7 @@ bool pin_lookup(const void* p, void** dev) {
 static_assert(sizeof(tfs_crc_desc) == 16 && sizeof(tfs_crc_vdesc) == 16, "descriptor ABI");
 static_assert(sizeof(tfs_raw_meta) == sizeof(tfscrc::RawMeta), "RawMeta ABI");
 static_assert(sizeof(tfs_file_info) == 36, "FileInfo ABI");
+static_assert(sizeof(tfs_crc_stats) == 64, "stats ABI");
 static_assert(sizeof(tfs_packet_desc) == sizeof(tfscrc::PacketDesc), "packet descriptor ABI");
 static_assert(sizeof(tfs_compact_job) == sizeof(tfscrc::CompactJob) && sizeof(tfs_compact_job) == 40, "compact job ABI");
 
@@ -325,6 +326,17 @@ struct tfs_crc_ctx {
   uint32_t res_published = 0;
   uint32_t res_idle_ticks = 0, res_life_ticks = 0;
   uint64_t res_launches = 0, res_files = 0;
+  uint64_t res_ring_full = 0;  // batches launched because the ring had no room (tfs_crc32_stats)
+  uint64_t* res_trace_dev = nullptr;  // measurement build: per-unit stamps (tfs_crc32_res_trace); null in the product
+#ifdef TFS_CRC_MEASURE
+  // tfs_crc32_res_trace_last: host stamps (steady clock ns) of the last synchronous call
+  std::atomic<int64_t> tr_enter{0}, tr_posted{0}, tr_seen{0}, tr_done{0};
+  std::atomic<uint32_t> tr_first{0}, tr_resident{0};
+  int tr_khz = 0;
+#endif
+  // tfs_crc32_stats: synchronous host calls, their bodies, lone calls, lone calls
+  // under TFS_CRC_LONE_CROSSOVER and their bytes
+  std::atomic<uint64_t> st_calls{0}, st_files{0}, st_lone{0}, st_lone_small{0}, st_lone_small_bytes{0};
   // Read without ctx->mu by other contexts' throughput launches (throughput_cap):
   std::atomic<uint32_t> res_gen{0};           // generation of the latest resident launch
   std::atomic<int64_t> res_last_post_ns{0};   // steady-clock time of the latest post
@@ -677,6 +689,20 @@ int plan_order(tfs_crc_ctx* ctx, hipStream_t st, const SchedLease& L, uint32_t p
   return TFS_SUCCESS;
 }
 
+// (Caller holds plan_mu[k], right after a launch on st that reads plan k.)  Record
+// plan_done[k] behind it.  When the event cannot be created or recorded, the
+// next user of a shared plan would not wait for this launch, so the launch is
+// drained here, under the lock, instead.
+int plan_mark(tfs_crc_ctx* ctx, hipStream_t st, uint32_t k) {
+  hipEvent_t& ev = ctx->plan_done[k];
+  if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ev = nullptr;
+  if (ev && hipEventRecord(ev, st) == hipSuccess) return TFS_SUCCESS;
+  if (ev) (void)hipEventDestroy(ev);
+  ev = nullptr;
+  HIP_TRY(ctx, hipStreamSynchronize(st));
+  return TFS_SUCCESS;
+}
+
 // (Caller holds plan_mu[k].)  Slot k's split plan for a throughput crc_files
 // launch of n files on st (tfs_crc_device.h: one allocation, up to cap ext
 // units).  The earlier launches using this plan are ordered before st's: they
@@ -718,12 +744,7 @@ int files_launch(tfs_crc_ctx* ctx, hipStream_t st, int mode, const uint8_t* base
                                                              lease.slot, st, ctx->variant, vseed, nullptr, 0u, cap, split)
                                           : hipSuccess;
   if (split && le == hipSuccess) {
-    hipEvent_t& ev = ctx->plan_done[k];
-    if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ev = nullptr;
-    if (ev && hipEventRecord(ev, st) != hipSuccess) {
-      (void)hipEventDestroy(ev);
-      ev = nullptr;
-    }
+    rc = plan_mark(ctx, st, k);
     std::lock_guard<std::mutex> g(ctx->last_split_mu);
     ctx->last_split_slot = int(k);
     ctx->last_split_n = n;
@@ -783,7 +804,7 @@ int resident_ensure_running(tfs_crc_ctx* ctx, bool post = false) {
   }
   const uint32_t gen = uint32_t(ctx->res_launches + 1u);
   HIP_TRY(ctx, launch_resident(ctx->d_tables, ctx->res_host_d, ctx->res_state, ctx->res_grid, ctx->res_idle_ticks,
-                               ctx->res_life_ticks, gen, ctx->res_stream));
+                               ctx->res_life_ticks, gen, ctx->res_stream, ctx->res_trace_dev));
   HIP_TRY(ctx, hipEventRecord(ctx->res_event, ctx->res_stream));
   ctx->res_running = true;
   ++ctx->res_launches;
@@ -846,7 +867,12 @@ int wait_resident(tfs_crc_ctx* ctx, Slot& s, int mode, uint32_t n) {
   for (uint32_t spins = 1;; ++spins) {
     const uint32_t i0 = i;
     while (i < n && uint32_t(res[i] >> 32) == s.seq) ++i;
-    if (i == n) break;
+    if (i == n) {
+#ifdef TFS_CRC_MEASURE
+      ctx->tr_seen.store(now_ns(), std::memory_order_relaxed);
+#endif
+      break;
+    }
     if (i != i0) relaunches = 0;
     __builtin_ia32_pause();
     if ((spins & 255u) == 0) {
@@ -981,7 +1007,7 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
           s.resident = true;
           return TFS_SUCCESS;
         }
-        // no room in the ring: launch this batch
+        ++ctx->res_ring_full;  // no room in the ring: launch this batch
       }
       // n_bad is counted from the verdicts on the host (no atomics on host memory)
       SCHED_LAUNCH(ctx, ctx->lat_stream, "crc_files",
@@ -1308,6 +1334,18 @@ tfs_crc_ctx* tfs_crc32_default_ctx(void) { return scalar_ctx(nullptr); }
 
 namespace {
 
+// tfs_crc32_stats: every synchronous host call, and the lone ones under the crossover.
+void count_host_call(tfs_crc_ctx* ctx, const Desc* d, uint32_t n) {
+  ctx->st_calls.fetch_add(1, std::memory_order_relaxed);
+  ctx->st_files.fetch_add(n, std::memory_order_relaxed);
+  if (n != 1) return;
+  ctx->st_lone.fetch_add(1, std::memory_order_relaxed);
+  if (d[0].len < TFS_CRC_LONE_CROSSOVER) {
+    ctx->st_lone_small.fetch_add(1, std::memory_order_relaxed);
+    ctx->st_lone_small_bytes.fetch_add(d[0].len, std::memory_order_relaxed);
+  }
+}
+
 // A synchronous host call: its slot is taken and its launch queued under
 // ctx->mu, and the wait for the result (the completion-flag spin of a
 // zero-copy batch) runs outside it, so calls from several threads -- the
@@ -1315,6 +1353,10 @@ namespace {
 // to back on the ctx stream.
 int sync_host_call(tfs_crc_ctx* ctx, int mode, const void* d, uint32_t n, const void* base, uint64_t base_len,
                    uint32_t* out_crc, uint8_t* out_ok, uint32_t* n_bad) {
+  count_host_call(ctx, static_cast<const Desc*>(d), n);
+#ifdef TFS_CRC_MEASURE
+  ctx->tr_enter.store(now_ns(), std::memory_order_relaxed);
+#endif
   Slot* s = nullptr;
   {
     std::unique_lock<std::mutex> lk(ctx->mu);
@@ -1335,8 +1377,16 @@ int sync_host_call(tfs_crc_ctx* ctx, int mode, const void* d, uint32_t n, const 
       ctx->sync_cv.notify_one();
       return rc;
     }
+#ifdef TFS_CRC_MEASURE
+    ctx->tr_posted.store(now_ns(), std::memory_order_relaxed);
+    ctx->tr_first.store(s->res_first, std::memory_order_relaxed);
+    ctx->tr_resident.store(s->resident ? 1u : 0u, std::memory_order_relaxed);
+#endif
   }
   const int rc = finish_slot(ctx, *s, mode, n, out_crc, out_ok, n_bad);
+#ifdef TFS_CRC_MEASURE
+  ctx->tr_done.store(now_ns(), std::memory_order_relaxed);
+#endif
   {
     std::lock_guard<std::mutex> g(ctx->mu);
     s->busy = false;
@@ -1568,6 +1618,9 @@ static int compact_dma(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job, ui
 static int compact_enqueue(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* job) {
   const uint32_t n = job->n;
   cs.job = job;
+  // A slot that last carried a group must not finish this block as one.
+  cs.gjobs.clear();
+  cs.gstart.clear();
   cs.live_idx.clear();
   job->status = TFS_SUCCESS;
   job->dest_len = 0;
@@ -1689,7 +1742,23 @@ bool zc_eligible(const tfs_crc_ctx* ctx, const tfs_block_job& job) {
          is_pinned_host(job.src_image) && is_pinned_host(job.dest_image);
 }
 
+static int compact_enqueue_group_body(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* jobs, uint32_t count);
+
+// Any failure leaves the slot idle and empty: no job pointer of this call may
+// survive into a later compact_finish of the same slot.
 static int compact_enqueue_group(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* jobs, uint32_t count) {
+  const int rc = compact_enqueue_group_body(ctx, cs, jobs, count);
+  if (rc != TFS_SUCCESS) {
+    cs.busy = false;
+    cs.job = nullptr;
+    cs.gjobs.clear();
+    cs.gstart.clear();
+    cs.live_idx.clear();
+  }
+  return rc;
+}
+
+static int compact_enqueue_group_body(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_job* jobs, uint32_t count) {
   cs.job = nullptr;
   cs.gjobs.clear();
   cs.gstart.clear();
@@ -1707,6 +1776,21 @@ static int compact_enqueue_group(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_jo
     if (const int f = injected_fault(ctx)) {
       job->status = f;
       return f;
+    }
+    // Validate the whole job before anything of the group is recorded.
+    int64_t w = 0;
+    for (uint32_t i = 0; i < job->n; ++i) {
+      const tfs_raw_meta& m = job->metas[i];
+      if (m.size < TFS_FILEINFO_SIZE || m.offset < 0 || uint64_t(m.offset) + uint64_t(m.size) > job->src_len) {
+        job->status = TFS_EXIT_PARAMETER_ERROR;
+        return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "meta %u out of range", i);
+      }
+      if (job->flags[i] & (TFS_FI_DELETED | TFS_FI_INVALID)) continue;
+      w += m.size;
+    }
+    if (uint64_t(w) > job->dest_cap) {
+      job->status = TFS_EXIT_PARAMETER_ERROR;
+      return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "dest_cap %llu too small", (unsigned long long)job->dest_cap);
     }
     void *zs = nullptr, *zd = nullptr;
     if (!host_dev_ptr(job->src_image, &zs) || !host_dev_ptr(job->dest_image, &zd))
@@ -1726,16 +1810,8 @@ static int compact_enqueue_group(tfs_crc_ctx* ctx, CompactSlot& cs, tfs_block_jo
     cs.gstart.push_back(uint32_t(cs.live_idx.size()));
     int64_t w = 0;
     for (uint32_t i = 0; i < job->n; ++i) {
-      const tfs_raw_meta& m = job->metas[i];
-      if (m.size < TFS_FILEINFO_SIZE || m.offset < 0 || uint64_t(m.offset) + uint64_t(m.size) > job->src_len) {
-        job->status = TFS_EXIT_PARAMETER_ERROR;
-        return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "meta %u out of range", i);
-      }
+      const tfs_raw_meta& m = job->metas[i];  // validated above
       if (job->flags[i] & (TFS_FI_DELETED | TFS_FI_INVALID)) continue;
-      if (uint64_t(w) + uint64_t(m.size) > job->dest_cap) {
-        job->status = TFS_EXIT_PARAMETER_ERROR;
-        return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "dest_cap %llu too small", (unsigned long long)job->dest_cap);
-      }
       if (job->dest_metas) job->dest_metas[cs.live_idx.size() - cs.gstart.back()] =
           tfs_raw_meta{m.file_id, int32_t(w), m.size};
       const bool edge = uint64_t(m.offset) + uint64_t(m.size) + 128u > job->src_len;
@@ -1823,7 +1899,8 @@ int tfs_blocks_compact(tfs_crc_ctx* ctx, tfs_block_job* jobs, uint32_t njobs) {
     if (rc != TFS_SUCCESS && (worst == TFS_SUCCESS || worst == TFS_EXIT_CHECK_CRC_ERROR)) worst = rc;
   };
   uint32_t slot = 0;
-  for (uint32_t j = 0; j < njobs;) {
+  uint32_t unissued = njobs;  // first job never enqueued after a device error
+  for (uint32_t j = 0; j < njobs && unissued == njobs;) {
     CompactSlot& cs = ctx->cslots[slot++ % uint32_t(ctx->compact_slots)];
     note(compact_finish(ctx, cs));
     // a run of up to compact_group zero-copy blocks goes as one launch
@@ -1834,7 +1911,10 @@ int tfs_blocks_compact(tfs_crc_ctx* ctx, tfs_block_job* jobs, uint32_t njobs) {
     if (rc != TFS_SUCCESS) {
       if (took == 1) jobs[j].status = rc;
       note(rc);
-      if (rc != TFS_EXIT_PARAMETER_ERROR) break;  // device error: stop issuing
+      if (rc != TFS_EXIT_PARAMETER_ERROR) {  // device error: stop issuing, drain below
+        unissued = j;
+        break;
+      }
       if (took > 1) {  // a bad job inside a group: run the group's jobs one by one instead
         for (uint32_t q = 0; q < took; ++q) {
           CompactSlot& c1 = ctx->cslots[slot++ % uint32_t(ctx->compact_slots)];
@@ -1843,12 +1923,21 @@ int tfs_blocks_compact(tfs_crc_ctx* ctx, tfs_block_job* jobs, uint32_t njobs) {
           if (r1 != TFS_SUCCESS) {
             jobs[j + q].status = r1;
             note(r1);
-            if (r1 != TFS_EXIT_PARAMETER_ERROR) return worst;
+            if (r1 != TFS_EXIT_PARAMETER_ERROR) {
+              unissued = j + q;
+              break;
+            }
           }
         }
       }
     }
     j += took;
+  }
+  // Jobs never issued carry the error that stopped the call, not a stale status.
+  for (uint32_t j = unissued; j < njobs; ++j) {
+    if (j > unissued || jobs[j].status == TFS_SUCCESS) jobs[j].status = worst;
+    jobs[j].dest_len = 0;
+    jobs[j].n_live = 0;
   }
   for (auto& cs : ctx->cslots) note(compact_finish(ctx, cs));
   return worst;
@@ -1894,12 +1983,7 @@ int tfs_compact_jobs_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_le
                                               cs.plan ? &cs : nullptr)
                         : hipSuccess;
   if (cs.plan && le == hipSuccess) {
-    hipEvent_t& ev = ctx->plan_done[k];
-    if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ev = nullptr;
-    if (ev && hipEventRecord(ev, st) != hipSuccess) {
-      (void)hipEventDestroy(ev);
-      ev = nullptr;
-    }
+    rc = plan_mark(ctx, st, k);
   }
   const int r2 = sched_release(ctx, st, lease, le, "compact_jobs");
   return rc != TFS_SUCCESS ? rc : r2;
@@ -2454,6 +2538,54 @@ int tfs_crc32_sched_stats(tfs_crc_ctx* ctx, uint32_t* owned_streams, uint64_t* f
   for (hipStream_t st : ctx->sched_streams) k += st ? 1u : 0u;
   if (owned_streams) *owned_streams = k;
   if (foreign_launches) *foreign_launches = ctx->foreign_launches;
+  return TFS_SUCCESS;
+}
+
+int tfs_crc32_res_trace(tfs_crc_ctx* ctx, void* pinned) {
+  if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
+#ifdef TFS_CRC_MEASURE
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (ctx->res_running) return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "res_trace: set it before the first resident call");
+  void* dev = nullptr;
+  if (pinned && !host_dev_ptr(pinned, &dev)) return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "res_trace: not page-locked");
+  ctx->res_trace_dev = static_cast<uint64_t*>(dev);
+  HIP_TRY(ctx, hipDeviceGetAttribute(&ctx->tr_khz, hipDeviceAttributeWallClockRate, ctx->device));
+  return TFS_SUCCESS;
+#else
+  (void)pinned;
+  return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "res_trace: measurement build only (libtfs_crc_measure.so)");
+#endif
+}
+
+int tfs_crc32_res_trace_last(tfs_crc_ctx* ctx, uint64_t* out) {
+  if (!ctx || !out) return TFS_EXIT_PARAMETER_ERROR;
+#ifdef TFS_CRC_MEASURE
+  out[0] = uint64_t(ctx->tr_enter.load());
+  out[1] = uint64_t(ctx->tr_posted.load());
+  out[2] = uint64_t(ctx->tr_seen.load());
+  out[3] = uint64_t(ctx->tr_done.load());
+  out[4] = ctx->tr_first.load();
+  out[5] = ctx->tr_resident.load();
+  out[6] = uint64_t(ctx->tr_khz);
+  out[7] = 0;
+  return TFS_SUCCESS;
+#else
+  return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "res_trace_last: measurement build only (libtfs_crc_measure.so)");
+#endif
+}
+
+int tfs_crc32_stats(tfs_crc_ctx* ctx, tfs_crc_stats* out) {
+  if (!ctx || !out) return TFS_EXIT_PARAMETER_ERROR;
+  memset(out, 0, sizeof *out);
+  out->host_calls = ctx->st_calls.load(std::memory_order_relaxed);
+  out->host_files = ctx->st_files.load(std::memory_order_relaxed);
+  out->lone_calls = ctx->st_lone.load(std::memory_order_relaxed);
+  out->lone_small_calls = ctx->st_lone_small.load(std::memory_order_relaxed);
+  out->lone_small_bytes = ctx->st_lone_small_bytes.load(std::memory_order_relaxed);
+  std::lock_guard<std::mutex> g(ctx->mu);
+  out->resident_launches = ctx->res_launches;
+  out->resident_files = ctx->res_files;
+  out->resident_ring_full = ctx->res_ring_full;
   return TFS_SUCCESS;
 }
 

@@ -221,7 +221,7 @@ struct CSegArgs {
 struct CSegUnit {  // one whole payload segment of a split record
   uint64_t src, dst;  // payload byte offsets in the source / destination images
   uint32_t len, job;
-  uint64_t pad;
+  uint64_t pad;  // bit 0: the record's TFS_COMPACT_JOB_EDGE, on its last segment only
 };
 static_assert(sizeof(CSegUnit) == 32, "segment unit layout");
 constexpr uint32_t kCSegLgMin = 3, kCSegLgMax = 5;

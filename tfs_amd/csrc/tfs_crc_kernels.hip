@@ -1225,9 +1225,13 @@ __device__ __forceinline__ uint64_t ld_sys64(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// trace (measurement build only, tfs_crc32_res_trace; always null in the product):
+// per ring unit, four 100 MHz wall-clock stamps of the workgroup that took it --
+// the issue of the poll that found it published, that poll's return, the unit's
+// words back, its CRC done (just before the result store).
 __global__ void __launch_bounds__(kBlock) crc_resident_kernel(const Tables* __restrict__ tg, const ResHost* hs,
                                                               uint32_t* dstate, uint32_t idle_ticks,
-                                                              uint32_t life_ticks, uint32_t gen) {
+                                                              uint32_t life_ticks, uint32_t gen, uint64_t* trace) {
   __shared__ uint32_t lds_tables[kWgLdsBytes / 4];
   __shared__ uint32_t part[kWgWaves];
   __shared__ uint64_t claim[4];  // go, then the unit's addr, out, len | seed << 32 (seq kept by thread 0)
@@ -1243,16 +1247,33 @@ __global__ void __launch_bounds__(kBlock) crc_resident_kernel(const Tables* __re
   uint64_t last = t0;
   uint32_t seen = 0;  // thread 0: `published` when last looked
   if (threadIdx.x == 0) seen = uint32_t(ld_sys64(&hs->published));
+#ifdef TFS_CRC_MEASURE
+  uint64_t t_issue = 0, t_go = 0, t_unit = 0;
+  uint32_t t_want = 0;
+#else
+  (void)trace;
+#endif
   for (;;) {
     if (threadIdx.x == 0) {
       const uint32_t want = blockIdx.x + done * gridDim.x;  // this workgroup's next unit
       uint32_t go = 0;
       for (uint32_t it = 0;; ++it) {
+#ifdef TFS_CRC_MEASURE
+        const uint64_t ti = trace ? wall_clock64() : 0u;
+#endif
         // Both loads in flight together: one PCIe round trip per poll.
         const uint64_t ps = ld_sys64(&hs->published);  // published | stop << 32
         const uint32_t ex = __hip_atomic_load(&dstate[kResExitLine], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (int32_t(uint32_t(ps) - want) > 0) {
           go = 1;
+#ifdef TFS_CRC_MEASURE
+          if (trace) {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            t_issue = ti;
+            t_go = wall_clock64();
+            t_want = want;
+          }
+#endif
           break;
         }
         if (ex == gen) break;
@@ -1277,6 +1298,12 @@ __global__ void __launch_bounds__(kBlock) crc_resident_kernel(const Tables* __re
         claim[3] = w2;
         seq = uint32_t(w3);
         ++done;
+#ifdef TFS_CRC_MEASURE
+        if (trace) {  // after the unit's words are back
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          t_unit = wall_clock64();
+        }
+#endif
       }
       claim[0] = go;
     }
@@ -1291,6 +1318,17 @@ __global__ void __launch_bounds__(kBlock) crc_resident_kernel(const Tables* __re
     uint4 buf[kWgPF];
     wg_issue(g, h, buf, wave, lane, junk);
     const uint32_t crc = wg_file_crc(lds_tables, part, lb, g, h, buf, wave, lane, junk);
+#ifdef TFS_CRC_MEASURE
+    if (trace && threadIdx.x == 0) {  // vector stores to page-locked host memory
+      uint64_t* tr = trace + 4u * (t_want % kResUnits);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      const uint64_t t_crc = wall_clock64();
+      __hip_atomic_store(tr + 0, t_issue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(tr + 1, t_go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(tr + 2, t_unit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(tr + 3, t_crc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+#endif
     if (threadIdx.x == 0)
       __hip_atomic_store(reinterpret_cast<uint64_t*>(uintptr_t(claim[2])), uint64_t(crc) | uint64_t(seq) << 32,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1583,7 +1621,7 @@ __device__ __forceinline__ CRec load_cunit(uint32_t f, uint32_t njobs, uint64_t 
   r.pre = kSuccess;
   r.plen = u.len;
   r.kind = 1u;
-  r.edge = 0u;
+  r.edge = uint32_t(u.pad) & 1u;
   return r;
 }
 
@@ -1859,7 +1897,11 @@ __global__ void __launch_bounds__(256) compact_seg_plan_kernel(const CompactJob*
   if (fits) {
     const uint64_t head = uint64_t(uint32_t(j.size - kFileInfoSize)) - uint64_t(K) * seg;
     const uint64_t s0 = j.src_offset + kFileInfoSize + head, d0 = j.dest_offset + kFileInfoSize + head;
-    for (uint32_t k = 0; k < K; ++k) ext[my + k] = CSegUnit{s0 + uint64_t(k) * seg, d0 + uint64_t(k) * seg, seg, i, 0u};
+    // The record's edge bit rides on its last segment (the only one that ends
+    // where the record ends): that unit never reads past the record either.
+    const uint64_t edge = uint64_t(j.reserved) & 1u;
+    for (uint32_t k = 0; k < K; ++k)
+      ext[my + k] = CSegUnit{s0 + uint64_t(k) * seg, d0 + uint64_t(k) * seg, seg, i, k + 1 == K ? edge : 0u};
   } else {
     for (unsigned long long u = my; u < my + K && u < cs.cap; ++u) ext[u] = CSegUnit{0, 0, 0, 0, 0};
   }
@@ -2220,9 +2262,9 @@ hipError_t launch_crc_files(int mode, const uint8_t* base, const Desc* desc, uin
 }
 
 hipError_t launch_resident(const Tables* tg, const ResHost* hs, uint32_t* dstate, unsigned grid, uint32_t idle_ticks,
-                           uint32_t life_ticks, uint32_t gen, hipStream_t stream) {
+                           uint32_t life_ticks, uint32_t gen, hipStream_t stream, uint64_t* trace) {
   hipLaunchKernelGGL(crc_resident_kernel, dim3(grid), dim3(kBlock), 0, stream, tg, hs, dstate, idle_ticks, life_ticks,
-                     gen);
+                     gen, trace);
   return hipGetLastError();
 }
 

@@ -159,6 +159,73 @@ __global__ void __launch_bounds__(256) ec_apply_chunk_kernel(EcArgs a, const uin
 }
 
 #ifdef TFS_CRC_MEASURE
+// The ceiling of f4's memory shape: the product's tile walk,
+// grid and non-temporal loads and stores over the same members, with the
+// bitmatrix combine replaced by one XOR per dword -- every output is the XOR of
+// the S sources' same packet.  Not an erasure code (measurement only):
+// AHEAD = 1 loads one member ahead as the product does; AHEAD = 0 issues every
+// member's loads of a tile before the first XOR (a plain streaming 5:3 copy).
+constexpr uint32_t kEcMaxSrc = 5;  // AHEAD = 0: the k = 5 encode of the ec line (sources past 5 are not read)
+template <int OG, bool AHEAD>
+__global__ void __launch_bounds__(256) ec_copy_kernel(EcArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t u = uint32_t(lane) >> 4;
+  const uint32_t off = 8u * uint32_t(lane & 15);
+  const uint64_t ntiles = (a.units + 3) / 4;
+  const uint64_t wave = uint64_t(blockIdx.x) * (blockDim.x / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t nwaves = uint64_t(gridDim.x) * (blockDim.x / 64);
+  for (uint64_t t = wave; t < ntiles; t += nwaves) {
+    const uint64_t unit = t * 4 + u;
+    const bool ok = unit < a.units;
+    const uint64_t base = unit * 1024u + off;
+    u32x2 acc[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[c] = u32x2{0u, 0u};
+    if (AHEAD) {
+      u32x2 in[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) in[c] = ok ? ld64nt(a.src[0] + base + 128u * c) : u32x2{0u, 0u};
+      for (uint32_t s = 0; s < a.S; ++s) {
+        u32x2 nx[8];
+        const bool more = s + 1 < a.S;
+        const uint8_t* np = a.src[more ? s + 1 : s];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) nx[c] = (ok && more) ? ld64nt(np + base + 128u * c) : u32x2{0u, 0u};
+#pragma unroll
+        for (int c = 0; c < 8; ++c) acc[c] ^= in[c];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) in[c] = nx[c];
+      }
+    } else {
+      u32x2 in[kEcMaxSrc][8];
+#pragma unroll
+      for (uint32_t s = 0; s < kEcMaxSrc; ++s)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) in[s][c] = (ok && s < a.S) ? ld64nt(a.src[s] + base + 128u * c) : u32x2{0u, 0u};
+#pragma unroll
+      for (uint32_t s = 0; s < kEcMaxSrc; ++s)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) acc[c] ^= in[s][c];
+    }
+    if (ok) {
+#pragma unroll
+      for (int o = 0; o < OG; ++o)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) st64nt(a.dst[o] + base + 128u * r, acc[r]);
+    }
+  }
+}
+
+template <bool AHEAD>
+static void launch_copy(const EcArgs& a, int og, dim3 g, dim3 b, hipStream_t stream) {
+  switch (og) {
+    case 1: hipLaunchKernelGGL((ec_copy_kernel<1, AHEAD>), g, b, 0, stream, a); break;
+    case 2: hipLaunchKernelGGL((ec_copy_kernel<2, AHEAD>), g, b, 0, stream, a); break;
+    case 3: hipLaunchKernelGGL((ec_copy_kernel<3, AHEAD>), g, b, 0, stream, a); break;
+    default: hipLaunchKernelGGL((ec_copy_kernel<4, AHEAD>), g, b, 0, stream, a); break;
+  }
+}
+
 template <int K>
 static void launch_chunk(const EcArgs& a, int og, dim3 g, dim3 b, hipStream_t stream) {
   switch (og) {
@@ -204,6 +271,11 @@ hipError_t launch_ec_apply(const EcArgs& a, int og, int variant, hipStream_t str
   if (blocks > cap) blocks = cap;
   const dim3 g(static_cast<unsigned>(blocks)), b(256);
 #ifdef TFS_CRC_MEASURE
+  if (variant == 20 || variant == 21) {  // measurement: the 5:3 copy ceiling (ec_copy_kernel)
+    if (variant == 20) launch_copy<true>(a, og, g, b, stream);
+    else launch_copy<false>(a, og, g, b, stream);
+    return hipGetLastError();
+  }
 #endif
   switch (og) {
     case 1: hipLaunchKernelGGL(ec_apply_kernel<1>, g, b, 0, stream, a, a.masks); break;

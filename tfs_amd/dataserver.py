@@ -105,6 +105,7 @@ def lib():
             "tfs_ds_decode": (ctypes.c_int, [vp, vp, i64, vp, vp, vp, u32, ctypes.POINTER(u32),
                                              ctypes.POINTER(i64)]),
             "tfs_ds_close_latency": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, i32, vp]),
+            "tfs_ds_close_latency_phases": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, i32, vp, vp]),
             "tfs_ds_scalar_latency": (ctypes.c_int, [ctypes.c_int, i32, vp]),
             "tfs_ds_close_stream": (ctypes.c_int, [vp, ctypes.c_int, i32, vp, vp, u64, ctypes.POINTER(u64)]),
             "tfs_ds_service_new": (vp, [vp, u32, ctypes.c_int]),
@@ -551,13 +552,23 @@ def loopback_block(ctx, payloads, n, length, client_crc, nthreads, block, batche
                                             c.ctypes.data, nthreads, block.h)
 
 
-def close_latency(ctx, nleases, iters, length=65536):
-    """Microseconds per CloseBatcher close with `nleases` leases closing concurrently."""
+CLOSE_PHASES = ("claim_us", "copy_us", "wait_us", "append_us", "lead_wait_us", "verify_us", "leader", "batch_n",
+                "relaunches", "ring_full")
+
+
+def close_latency(ctx, nleases, iters, length=65536, phases=False):
+    """Microseconds per CloseBatcher close with `nleases` leases closing concurrently.
+    phases: also each close's CloseTiming (ds_harness.h), a (closes, 10) array in
+    CLOSE_PHASES order; returns (us, phases)."""
     out = np.zeros(nleases * iters, np.float64)
-    rc = lib().tfs_ds_close_latency(_ctx(ctx), nleases, iters, length, out.ctypes.data)
+    if phases:
+        ph = np.zeros((nleases * iters, len(CLOSE_PHASES)), np.float64)
+        rc = lib().tfs_ds_close_latency_phases(_ctx(ctx), nleases, iters, length, out.ctypes.data, ph.ctypes.data)
+    else:
+        rc = lib().tfs_ds_close_latency(_ctx(ctx), nleases, iters, length, out.ctypes.data)
     if rc != 0:
         raise _crc.TfsCrcError(rc, "close_latency")
-    return out
+    return (out, ph) if phases else out
 
 
 class CloseStream:

@@ -235,7 +235,12 @@ int tfs_ds_loopback_block_with(tfs_crc_ctx* ctx, void* batcher, const char* payl
 // `nleases` worker threads (concurrent leases) each close `iters` files of `len`
 // bytes; a close is timed from the call to its return (GPU check of the client
 // CRC + FileInfo|payload append).  out_us receives nleases*iters microseconds.
-int tfs_ds_close_latency(tfs_crc_ctx* ctx, int nleases, int iters, int32_t len, double* out_us) {
+// out_phase (may be NULL): kClosePhases doubles per close, in out_us's order --
+// CloseTiming's claim, copy, wait, append, lead_wait, verify (us), leader,
+// batch_n, relaunches, ring_full.
+constexpr int kClosePhases = 10;
+int tfs_ds_close_latency_phases(tfs_crc_ctx* ctx, int nleases, int iters, int32_t len, double* out_us,
+                                double* out_phase) {
   if (!ctx || nleases < 1 || iters < 1 || len < 0 || !out_us) return TFS_EXIT_PARAMETER_ERROR;
   std::vector<char> payload(size_t(len) + 1);
   for (int32_t i = 0; i < len; ++i) payload[size_t(i)] = char((i * 2654435761u) >> 11);
@@ -261,17 +266,28 @@ int tfs_ds_close_latency(tfs_crc_ctx* ctx, int nleases, int iters, int32_t len, 
           info.block_id_ = 1;
           info.file_id_ = fid;
           info.crc_ = client;
+          CloseTiming ph;
           const auto t0 = std::chrono::steady_clock::now();
-          const int r = batcher.close(info, df, blk);
+          const int r = batcher.close(info, df, blk, out_phase ? &ph : nullptr);
           const auto t1 = std::chrono::steady_clock::now();
-          if (k >= 0)
-            out_us[size_t(t) * size_t(iters) + size_t(k)] = std::chrono::duration<double, std::micro>(t1 - t0).count();
+          const size_t at = size_t(t) * size_t(iters) + size_t(k);
+          if (k >= 0) out_us[at] = std::chrono::duration<double, std::micro>(t1 - t0).count();
+          if (k >= 0 && out_phase) {
+            double* o = out_phase + at * kClosePhases;
+            o[0] = ph.claim_us, o[1] = ph.copy_us, o[2] = ph.wait_us, o[3] = ph.append_us;
+            o[4] = ph.lead_wait_us, o[5] = ph.verify_us, o[6] = ph.leader, o[7] = ph.batch_n;
+            o[8] = ph.relaunches, o[9] = ph.ring_full;
+          }
           if (r != TFS_SUCCESS) err = r;
         }
       });
     for (auto& w : workers) w.join();
   }
   return err.load();
+}
+
+int tfs_ds_close_latency(tfs_crc_ctx* ctx, int nleases, int iters, int32_t len, double* out_us) {
+  return tfs_ds_close_latency_phases(ctx, nleases, iters, len, out_us, nullptr);
 }
 
 // A stream of closes (DataManagement::close_write_file, data_management.cpp:

@@ -435,6 +435,8 @@ void CloseBatcher::lead(Batch* b) {
     n = b->n;
   }
   spin_until([&] { return b->ready.load(std::memory_order_acquire) == n; });
+  tfs_crc_stats s0{};
+  if (b->timed) tfs_crc32_stats(ctx_, &s0);
   const auto t0 = std::chrono::steady_clock::now();
   if (trace_) t_lead_wait_ += std::chrono::duration_cast<std::chrono::microseconds>(t0 - b->opened).count();
   uint32_t nbad = 0;
@@ -442,12 +444,21 @@ void CloseBatcher::lead(Batch* b) {
   b->rc = pool_ ? tfs_crc32_verify(ctx_, b->desc.data(), n, pool_->base(), pool_->bytes(), b->crc.data(),
                                    b->ok.data(), &nbad)
                 : tfs_crc32_verify(ctx_, b->desc.data(), n, b->gather, b->bytes, b->crc.data(), b->ok.data(), &nbad);
-  verify_us_ += std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+  const auto t1 = std::chrono::steady_clock::now();
+  verify_us_ += std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count();
+  if (b->timed) {
+    tfs_crc_stats s1{};
+    tfs_crc32_stats(ctx_, &s1);
+    b->lead_wait_us = std::chrono::duration<double, std::micro>(t0 - b->opened).count();
+    b->verify_us = std::chrono::duration<double, std::micro>(t1 - t0).count();
+    b->relaunches = uint32_t(s1.resident_launches - s0.resident_launches);
+    b->ring_full = uint32_t(s1.resident_ring_full - s0.resident_ring_full);
+  }
   ++batches_;
   b->done.store(1, std::memory_order_release);
 }
 
-int CloseBatcher::close(const CloseFileInfo& info, DataFile& df, LogicBlockImage& block) {
+int CloseBatcher::close(const CloseFileInfo& info, DataFile& df, LogicBlockImage& block, CloseTiming* t) {
   const int32_t len = df.get_length();
   const char* own = df.in_memory_payload();
   const bool pooled = pool_ && own && pool_->owns(own);
@@ -457,7 +468,8 @@ int CloseBatcher::close(const CloseFileInfo& info, DataFile& df, LogicBlockImage
   auto us = [](clk::time_point a, clk::time_point b2) {
     return int64_t(std::chrono::duration_cast<std::chrono::microseconds>(b2 - a).count());
   };
-  const auto c0 = trace_ ? clk::now() : clk::time_point();
+  const bool timed = trace_ || t;
+  const auto c0 = timed ? clk::now() : clk::time_point();
   Batch* b;
   uint32_t slot;
   uint64_t off;
@@ -470,6 +482,7 @@ int CloseBatcher::close(const CloseFileInfo& info, DataFile& df, LogicBlockImage
     if (!cur_) cur_ = take_batch(lk);
     b = cur_;
     slot = b->n++;
+    if (slot == 0) b->timed = t != nullptr;
     off = b->bytes;
     b->bytes += uint64_t(len);
     b->left.fetch_add(1);
@@ -478,7 +491,7 @@ int CloseBatcher::close(const CloseFileInfo& info, DataFile& df, LogicBlockImage
       cur_ = nullptr;
     }
   }
-  const auto c1 = trace_ ? clk::now() : clk::time_point();
+  const auto c1 = timed ? clk::now() : clk::time_point();
   // This lease's payload into the batch's gather buffer (data_file.cpp:115-166),
   // or, from a lease pool, read where it is.
   int32_t got = 0;
@@ -496,14 +509,30 @@ int CloseBatcher::close(const CloseFileInfo& info, DataFile& df, LogicBlockImage
   const bool readable = got == len;
   b->desc[slot] = tfs_crc_vdesc{off, readable ? uint32_t(len) : 0u, info.crc_};
   b->ready.fetch_add(1, std::memory_order_release);
-  const auto c2 = trace_ ? clk::now() : clk::time_point();
+  const auto c2 = timed ? clk::now() : clk::time_point();
   if (slot == 0) lead(b);
   else spin_until([&] { return b->done.load(std::memory_order_acquire) != 0; });
-  if (trace_) {
+  if (timed) {
     const auto c3 = clk::now();
-    t_claim_ += us(c0, c1);
-    t_copy_ += us(c1, c2);
-    t_wait_ += us(c2, c3);
+    if (trace_) {
+      t_claim_ += us(c0, c1);
+      t_copy_ += us(c1, c2);
+      t_wait_ += us(c2, c3);
+    }
+    if (t) {
+      auto fus = [](clk::time_point a, clk::time_point b2) { return std::chrono::duration<double, std::micro>(b2 - a).count(); };
+      t->claim_us = fus(c0, c1);
+      t->copy_us = fus(c1, c2);
+      t->wait_us = fus(c2, c3);
+      t->leader = slot == 0;
+      t->batch_n = b->n;
+      if (b->timed) {
+        t->lead_wait_us = b->lead_wait_us;
+        t->verify_us = b->verify_us;
+        t->relaunches = b->relaunches;
+        t->ring_full = b->ring_full;
+      }
+    }
   }
   int status;
   uint32_t crc = 0;
@@ -525,9 +554,13 @@ int CloseBatcher::close(const CloseFileInfo& info, DataFile& df, LogicBlockImage
   if (status != kAppend) return status;
   // Checked: persist from this thread (LogicBlock::close_write_file runs on the
   // worker, logic_block.cpp:156-372), so the appends of a batch run side by side.
-  const auto c4 = trace_ ? clk::now() : clk::time_point();
+  const auto c4 = timed ? clk::now() : clk::time_point();
   const int rc = block.close_write_file(info.file_id_, df, crc);
-  if (trace_) t_append_ += us(c4, clk::now());
+  if (timed) {
+    const auto c5 = clk::now();
+    if (trace_) t_append_ += us(c4, c5);
+    if (t) t->append_us = std::chrono::duration<double, std::micro>(c5 - c4).count();
+  }
   return rc;
 }
 

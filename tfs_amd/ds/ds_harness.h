@@ -233,6 +233,20 @@ int close_write_file(const CloseFileInfo& info, DataFile& df, LogicBlockImage& b
 // at once, so the next batch forms while one is on the GPU.  Each member then gets the status
 // close_write_file would have returned and persists its own record.  Payloads
 // larger than kMaxBatched take the unbatched close.
+// One close's phases (CloseBatcher::close with a CloseTiming): where its time went.
+struct CloseTiming {
+  double claim_us = 0;      // taking a batch slot (the batcher's lock, a free batch)
+  double copy_us = 0;       // the lease's payload into the gather buffer
+  double wait_us = 0;       // until the batch's verdicts are in (the leader: its verify)
+  double append_us = 0;     // the FileInfo|payload append
+  double lead_wait_us = 0;  // the batch's leader: from the batch's opening to its verify call
+  double verify_us = 0;     // the batch's tfs_crc32_verify call
+  uint32_t leader = 0;      // this close led its batch
+  uint32_t batch_n = 0;     // members of its batch
+  uint32_t relaunches = 0;  // resident kernel launches during the batch's verify call
+  uint32_t ring_full = 0;   // ring-full launches during it
+};
+
 class CloseBatcher {
  public:
   // pool: closes of DataFiles whose buffers are in it are checked in place (no
@@ -241,7 +255,9 @@ class CloseBatcher {
                LeaseBufferPool* pool = nullptr);
   ~CloseBatcher();
   // Blocks until this close has been checked (and persisted on success).
-  int close(const CloseFileInfo& info, DataFile& df, LogicBlockImage& block);
+  // With `t`, the close's phases go there (the leader also reads the context's
+  // counters around its verify call: tfs_crc32_stats).
+  int close(const CloseFileInfo& info, DataFile& df, LogicBlockImage& block, CloseTiming* t = nullptr);
   uint64_t batches() const { return batches_.load(); }
   LeaseBufferPool* pool() const { return pool_; }
 
@@ -271,6 +287,9 @@ class CloseBatcher {
     std::atomic<int> done{0};
     int rc = TFS_SUCCESS;
     std::chrono::steady_clock::time_point opened;
+    bool timed = false;  // the leader asked for timing: the fields below are filled
+    double lead_wait_us = 0, verify_us = 0;
+    uint32_t relaunches = 0, ring_full = 0;
   };
   static constexpr int kAppend = 1;  // checked, the closing thread persists it
   Batch* take_batch(std::unique_lock<std::mutex>& lk);

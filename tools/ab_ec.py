@@ -4,8 +4,10 @@
 Builds the ec line's members (k = 5 data + m = 3 parity of 1,536 MiB, device
 resident), then interleaves, round by round, encodes through the product
 library and through measurement-build forms selected by TFS_EC_VARIANT
-(tfs_ec_kernels.hip: 1-3 chunked tiles, 4 / 6 striding grids), each timed with
-HIP events.  (Round 5's form 7, every source member's loads in flight at once, was
+(tfs_ec_kernels.hip: 1-3 chunked tiles, 4 / 6 striding grids; 20 / 21 the
+5-read : 3-write copy ceiling of the same tile walk -- one member ahead as the
+product, or all five members' loads in flight -- with one XOR per dword instead
+of the bitmatrix, not an erasure code), each timed with HIP events.  (Round 5's form 7, every source member's loads in flight at once, was
 measured and deleted: DESIGN.md §4.2.)
 
   python tools/ab_ec.py VARIANTS [ROUNDS] [MIB]     e.g. python tools/ab_ec.py 1,4 8

@@ -1,0 +1,139 @@
+// floor_probe.cpp -- where the ~9 us of one lone small call goes.
+// Measurement build only: links libtfs_crc_measure.so, whose resident kernel stamps
+// each ring unit with the GPU's 100 MHz wall clock (tfs_crc32_res_trace) and whose
+// synchronous path stamps the host side (tfs_crc32_res_trace_last).
+//   (no HIP headers needed)
+//   g++ -O2 -std=c++17 tools/floor_probe.cpp -Ltfs_amd -ltfs_crc_measure -Wl,-rpath,$PWD/tfs_amd -o tools/floor_probe
+//   tools/floor_probe [iters]   -> one JSON object on stdout
+// Per call (a lone body through tfs_crc32_batch from page-locked memory, and the
+// scalar drop-in tfs_crc32 from pageable memory) it splits the host's wall time into
+//   host_pre     call entry -> the unit published (lock, slot, descriptor, staging copy)
+//   post_to_go   published -> the GPU's poll returns with it   (needs the clock offset)
+//   poll_rtt     the issue of that poll -> its return        (GPU clock: one PCIe read)
+//   unit_rtt     the unit's four words back                   (GPU clock: one PCIe read)
+//   body         payload read + CRC                           (GPU clock)
+//   crc_to_seen  result store -> the host sees it             (needs the clock offset)
+//   host_post    result seen -> the call returns
+// post_to_go + crc_to_seen is measured without any offset ((seen - posted) - (crc - go));
+// its split uses the offset estimate min(a) - min(b) over the calls, halved
+// (a = go - posted, b = seen - crc: the fastest up and down legs taken as equal).
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../include/tfs_crc.h"
+#include "../include/tfs_crc_testing.h"
+
+static double pct(std::vector<double> v, double p) {
+  if (v.empty()) return 0;
+  std::sort(v.begin(), v.end());
+  return v[std::min(v.size() - 1, size_t(p * double(v.size())))];
+}
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? atoi(argv[1]) : 400;
+  tfs_crc_ctx* ctx = nullptr;
+  if (tfs_crc32_ctx_create(0, &ctx) != TFS_SUCCESS) {
+    fprintf(stderr, "ctx: %s\n", ctx ? tfs_crc32_last_error(ctx) : "?");
+    return 1;
+  }
+  void* trace = nullptr;
+  if (tfs_crc32_host_malloc_pinned(ctx, 4096 * 32, &trace) != TFS_SUCCESS) return 1;
+  memset(trace, 0, 4096 * 32);
+  if (tfs_crc32_res_trace(ctx, trace) != TFS_SUCCESS) {
+    fprintf(stderr, "res_trace: %s\n", tfs_crc32_last_error(ctx));
+    return 1;
+  }
+  tfs_crc32_bind_thread(ctx);
+  const size_t kBuf = 1 << 20;
+  void* pinned = nullptr;
+  tfs_crc32_host_malloc_pinned(ctx, kBuf, &pinned);
+  std::vector<char> pageable(kBuf);
+  for (size_t i = 0; i < kBuf; ++i) pageable[i] = char(i * 2654435761u >> 13);
+  memcpy(pinned, pageable.data(), kBuf);
+  volatile uint64_t* tr = static_cast<volatile uint64_t*>(trace);
+  std::string out = "{\"tool\": \"floor_probe\", \"iters\": " + std::to_string(iters);
+  for (int form = 0; form < 2; ++form) {
+    for (uint32_t len : {32u, 1024u, 4096u}) {
+      struct Rec {
+        double total, host_pre, host_post, poll_rtt, unit_rtt, body, legs, a, b;
+      };
+      std::vector<Rec> recs;
+      int resident = 0, lost = 0;
+      for (int it = -50; it < iters; ++it) {
+        const uint64_t off = (uint64_t(it + 50) * 4099u) % (kBuf - len);
+        uint32_t crc = 0;
+        if (form == 0) {
+          tfs_crc_desc d{off, len, 0u};
+          if (tfs_crc32_batch(ctx, &d, 1, static_cast<char*>(pinned), kBuf, &crc) != TFS_SUCCESS) return 2;
+        } else {
+          int err = 0;
+          crc = tfs_crc32_e(0, pageable.data() + off, int32_t(len), &err);
+          if (err) return 2;
+        }
+        uint64_t h[8];
+        tfs_crc32_res_trace_last(ctx, h);
+        if (it < 0) continue;
+        if (!h[5]) continue;  // launched, not through the ring
+        ++resident;
+        volatile uint64_t* u = tr + 4u * (h[4] % 4096u);
+        // the stamps are stored just before the result: give them a moment to land
+        for (int spin = 0; spin < 100000 && u[3] == 0; ++spin) std::this_thread::yield();
+        if (u[3] == 0) {
+          ++lost;
+          continue;
+        }
+        const double tick = 1e6 / double(h[6] ? h[6] : 100000);  // ns per wall-clock tick
+        const double gi = double(u[0]) * tick, gg = double(u[1]) * tick, gu = double(u[2]) * tick,
+                     gc = double(u[3]) * tick;
+        const double enter = double(h[0]), posted = double(h[1]), seen = double(h[2]), done = double(h[3]);
+        Rec r;
+        r.total = (done - enter) / 1e3;
+        r.host_pre = (posted - enter) / 1e3;
+        r.host_post = (done - seen) / 1e3;
+        r.poll_rtt = (gg - gi) / 1e3;
+        r.unit_rtt = (gu - gg) / 1e3;
+        r.body = (gc - gu) / 1e3;
+        r.legs = ((seen - posted) - (gc - gg)) / 1e3;
+        r.a = (gg - posted) / 1e3;  // offset + up leg
+        r.b = (seen - gc) / 1e3;    // down leg - offset
+        recs.push_back(r);
+        u[0] = u[1] = u[2] = u[3] = 0;
+      }
+      double amin = 1e300, bmin = 1e300;
+      for (auto& r : recs) amin = std::min(amin, r.a), bmin = std::min(bmin, r.b);
+      const double off_us = (amin - bmin) / 2;  // the fastest up and down legs taken as equal
+      auto col = [&](auto f) {
+        std::vector<double> v;
+        for (auto& r : recs) v.push_back(f(r));
+        return v;
+      };
+      char b[1024];
+      snprintf(b, sizeof b,
+               ", \"%s_%u\": {\"calls\": %zu, \"resident\": %d, \"stamps_lost\": %d, \"p50_us\": {\"total\": %.2f, "
+               "\"host_pre\": %.2f, \"post_to_go\": %.2f, \"poll_rtt\": %.2f, \"unit_rtt\": %.2f, \"body\": %.2f, "
+               "\"crc_to_seen\": %.2f, \"host_post\": %.2f, \"legs_offset_free\": %.2f}, \"p99_total_us\": %.2f, "
+               "\"min_legs_us\": %.2f}",
+               form == 0 ? "batch_pinned" : "scalar_pageable", len, recs.size(), resident, lost,
+               pct(col([](const Rec& r) { return r.total; }), 0.5), pct(col([](const Rec& r) { return r.host_pre; }), 0.5),
+               pct(col([&](const Rec& r) { return r.a - off_us; }), 0.5),
+               pct(col([](const Rec& r) { return r.poll_rtt; }), 0.5), pct(col([](const Rec& r) { return r.unit_rtt; }), 0.5),
+               pct(col([](const Rec& r) { return r.body; }), 0.5), pct(col([&](const Rec& r) { return r.b + off_us; }), 0.5),
+               pct(col([](const Rec& r) { return r.host_post; }), 0.5), pct(col([](const Rec& r) { return r.legs; }), 0.5),
+               pct(col([](const Rec& r) { return r.total; }), 0.99), pct(col([](const Rec& r) { return r.legs; }), 0.0));
+      out += b;
+    }
+  }
+  tfs_crc32_bind_thread(nullptr);
+  out += "}";
+  printf("%s\n", out.c_str());
+  // no unit is outstanding: the idle resident kernel writes no more stamps
+  tfs_crc32_host_free_pinned(ctx, pinned);
+  tfs_crc32_host_free_pinned(ctx, trace);
+  tfs_crc32_ctx_destroy(ctx);
+  return 0;
+}
