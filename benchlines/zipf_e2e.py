@@ -131,7 +131,7 @@ def zipf_e2e_leg(ctx, dist, world, rank, nsub, inflight=3, ndistinct=16, seed=42
                     "payloads (%d files in the %d distinct buffers, mean %.1f KiB, %d files > 128 KiB holding "
                     "%.0f%% of the bytes) at arbitrary byte offsets (U[0,%d) gaps); one tfs_crc32_batch per "
                     "buffer (wide in-place path: payloads read over PCIe where they lie), %d caller threads" % (
-                        nsub, ndistinct, nfiles, sum(b[2] for b in bufs) / nfiles / 1024, big,
+                        nsub, ndistinct, nfiles, ndistinct, sum(b[2] for b in bufs) / nfiles / 1024, big,
                         100.0 * big_bytes / sum(b[2] for b in bufs), RECV_GAP, inflight),
         "distinct_note": "%d distinct buffers (%d MiB of page-locked host memory per GPU) are cycled: every byte "
                          "still crosses PCIe on every call (the GPU holds no copy of a receive buffer), and the "

@@ -20,7 +20,7 @@ def ocrc_payload(oracle, img, meta):
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=[0, 94, 95, 96, 97, 98, 99])
+@pytest.fixture(params=[0, 94, 95, 96, 97, 98, 99, 120, 121])
 def vctx(request, monkeypatch):
     import tfs_amd.crc as crc
     monkeypatch.setenv("TFS_CRC_VARIANT", str(request.param))

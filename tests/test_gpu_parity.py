@@ -654,11 +654,13 @@ def test_blocks_compact_group_failures(gpu_ctx, oracle):
         assert [(j.status, j.dest_len, j.n_live) for j in jobs1] == snap1
 
         # (2) a device error in the per-job fallback: the group consults the fault
-        # hook for jobs 0..4 before rejecting job 4, the fallback once per job.
+        # hook for jobs 0..4 before rejecting job 4, the fallback once per job.  The
+        # call returns its first non-CRC error (the group's parameter error); every
+        # job from the failed one on carries the device error.
         jobs3, outs3 = _group_jobs(keep)
         jobs3[4].metas = bad_metas.ctypes.data
         gpu_ctx.inject_device_error(5 + 3, 1)
-        assert run(jobs3) == -20001
+        assert run(jobs3) == -1016
         for b in range(3):
             _check_group_block(oracle, keep[b], jobs3[b], outs3[b], ("dev", b))
         for b in range(3, 12):

@@ -1900,6 +1900,7 @@ int tfs_blocks_compact(tfs_crc_ctx* ctx, tfs_block_job* jobs, uint32_t njobs) {
   };
   uint32_t slot = 0;
   uint32_t unissued = njobs;  // first job never enqueued after a device error
+  int stop_rc = TFS_SUCCESS;  // that device error
   for (uint32_t j = 0; j < njobs && unissued == njobs;) {
     CompactSlot& cs = ctx->cslots[slot++ % uint32_t(ctx->compact_slots)];
     note(compact_finish(ctx, cs));
@@ -1913,6 +1914,7 @@ int tfs_blocks_compact(tfs_crc_ctx* ctx, tfs_block_job* jobs, uint32_t njobs) {
       note(rc);
       if (rc != TFS_EXIT_PARAMETER_ERROR) {  // device error: stop issuing, drain below
         unissued = j;
+        stop_rc = rc;
         break;
       }
       if (took > 1) {  // a bad job inside a group: run the group's jobs one by one instead
@@ -1925,6 +1927,7 @@ int tfs_blocks_compact(tfs_crc_ctx* ctx, tfs_block_job* jobs, uint32_t njobs) {
             note(r1);
             if (r1 != TFS_EXIT_PARAMETER_ERROR) {
               unissued = j + q;
+              stop_rc = r1;
               break;
             }
           }
@@ -1935,7 +1938,7 @@ int tfs_blocks_compact(tfs_crc_ctx* ctx, tfs_block_job* jobs, uint32_t njobs) {
   }
   // Jobs never issued carry the error that stopped the call, not a stale status.
   for (uint32_t j = unissued; j < njobs; ++j) {
-    if (j > unissued || jobs[j].status == TFS_SUCCESS) jobs[j].status = worst;
+    if (j > unissued || jobs[j].status == TFS_SUCCESS) jobs[j].status = stop_rc;
     jobs[j].dest_len = 0;
     jobs[j].n_live = 0;
   }

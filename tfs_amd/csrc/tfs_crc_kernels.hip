@@ -28,6 +28,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "tfs_crc_device.h"
 
 namespace tfscrc {
@@ -279,6 +281,63 @@ __device__ __forceinline__ void load_ring(const FileGeo<RUN>& g, int lane, uint4
   }
 }
 
+// LDS-DMA ring (measurement build; TFS_CRC_VARIANT 120-121):
+// the PF stripes in flight live in LDS instead of VGPRs.  Each refill is one
+// global_load_lds_dwordx4 (lane l's 16 bytes land at the wave's slot base + 16 l,
+// exactly the stripe's lane order); a stripe is read back with ds_read_b128 in
+// inline asm behind an explicit s_waitcnt vmcnt(N): hipcc does not order its own
+// ds_reads after a pending LDS-DMA to the same array (it waits vmcnt(0) or moves
+// the read past the next refill), so the waits are counted here.  N counts only
+// the younger LDS-DMAs (PF - 1 in the steady state): loads, stores and LDS-DMAs
+// retire in issue order (MI355X_MICROARCH.md), so ignoring the younger stores
+// only waits longer, never too little.
+typedef __attribute__((address_space(3))) void* lds_vp;
+typedef const __attribute__((address_space(1))) void* glb_vp;
+__device__ __forceinline__ void glds16(uintptr_t gsrc, uint4* lds_slot) {
+  __builtin_amdgcn_global_load_lds(reinterpret_cast<glb_vp>(gsrc), (lds_vp)(lds_slot), 16, 0, 0);
+}
+template <int N>
+__device__ __forceinline__ uint4 ring_rd(uint32_t lds_addr) {
+  u32x4 v;
+  asm volatile("s_waitcnt vmcnt(%1)\n\tds_read_b128 %0, %2\n\ts_waitcnt lgkmcnt(0)"
+               : "=v"(v) : "i"(N), "v"(lds_addr) : "memory");
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+// Slot f of the wave's ring: `base` (generic) / `addr` (LDS byte address) of slot 0,
+// slots `stride` uint4 apart.
+struct LdsRing {
+  uint4* base;
+  uint32_t addr;
+  uint32_t stride;
+};
+template <int RUN, int PF>
+__device__ __forceinline__ void load_ring_lds(const FileGeo<RUN>& g, int lane, const LdsRing& rg, uintptr_t junk) {
+  static_assert(RUN == 16, "one 16-byte run per lane");
+#pragma unroll
+  for (int f = 0; f < PF; ++f) glds16(stripe_base<RUN>(g, 1u + f, junk) + uintptr_t(lane) * RUN, rg.base + f * rg.stride);
+}
+template <int PF>
+__device__ __forceinline__ uint4 ring_slot(const LdsRing& rg, int lane, int f, int younger) {
+  const uint32_t a = rg.addr + uint32_t(f) * rg.stride * 16u + uint32_t(lane) * 16u;
+  switch (younger) {  // folded: f and younger are compile-time after unrolling
+    case 0: return ring_rd<0>(a);
+    case 1: return ring_rd<1>(a);
+    case 2: return ring_rd<2>(a);
+    case 3: return ring_rd<3>(a);
+    case 4: return ring_rd<4>(a);
+    case 5: return ring_rd<5>(a);
+    case 6: return ring_rd<6>(a);
+    case 7: return ring_rd<7>(a);
+    case 8: return ring_rd<8>(a);
+    case 9: return ring_rd<9>(a);
+    case 10: return ring_rd<10>(a);
+    case 11: return ring_rd<11>(a);
+    case 12: return ring_rd<12>(a);
+    case 13: return ring_rd<13>(a);
+    default: return ring_rd<14>(a);
+  }
+}
+
 // Copy-through stores of the fused compaction kernel: the payload bytes a lane
 // holds in registers go to the same position of the destination record
 // (dst = src + delta, delta a multiple of 4).  Written once, never re-read here.
@@ -435,10 +494,13 @@ __device__ __forceinline__ void store_bshift(uintptr_t chunk, uintptr_t own, con
 // NTS: non-temporal copy-through stores (product).  NOCRC (measurement only,
 // TFS_CRC_VARIANT=26: wrong CRCs): skip the payload steps, so the record kernel
 // runs its own load/store schedule without the table lookups.
-template <int RUN, int PF, bool NT, int LY, bool COPY = false, bool DPPSH = false, int NTS = 1, bool NOCRC = false>
+template <int RUN, int PF, bool NT, int LY, bool COPY = false, bool DPPSH = false, int NTS = 1, bool NOCRC = false,
+          bool LR = false>
 __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase& lb, const FileGeo<RUN>& g,
                                                const Head<RUN>& h, uint4 (&buf)[PF][RUN / 16], int lane,
-                                               uintptr_t junk, intptr_t delta = 0, bool copy_on = false) {
+                                               uintptr_t junk, intptr_t delta = 0, bool copy_on = false,
+                                               const LdsRing* ring = nullptr) {
+  static_assert(!LR || (RUN == 16 && PF <= 8), "LDS ring: one run per lane, counted waits up to 14");
   constexpr uint32_t kStripe = 64u * RUN;
   constexpr int kVec = RUN / 16;
   // Stripe 0: mask the bytes before `start` in the dword at A and inject the
@@ -498,9 +560,16 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
       }
     };
     uint32_t r = 1;
-    for (; r + PF <= g.nstripes; r += PF) {
+    // One full group of PF stripes.  LR (YC: 0 the first group, 1 later ones): slot
+    // f's refill has at least this many younger vector-memory ops when slot f is
+    // read -- first group: the PF - 1 other first loads and refills (PF - 1) and
+    // the f stripes' stores before it; later groups: the PF - 1 younger refills
+    // and the PF - 1 stripes' copy-through stores between them (every stripe of a
+    // full group issues at least one store instruction): 2 (PF - 1).
+    auto group = [&](auto yc) {  // (LR only)
 #pragma unroll
       for (int f = 0; f < PF; ++f) {
+        buf[f][0] = ring_slot<PF>(*ring, lane, f, decltype(yc)::value == 0 ? PF - 1 + f : 2 * (PF - 1));
         const uint32_t c_old = c;
         c = shift_stripe<LY>(T, c);
         if (f == 0) {
@@ -512,14 +581,43 @@ __device__ __forceinline__ uint32_t lane_chain(const uint32_t* T, const LaneBase
         c = (r + f == last && !lane_in_last) ? c_old : c;  // run past B16: not part of the chain
         if (COPY && copy_on) copy_stripe(r + f, buf[f][0]);
         const uintptr_t sb = stripe_base<RUN>(g, r + uint32_t(f) + uint32_t(PF), junk) + uintptr_t(lane) * RUN;
+        glds16(sb, ring->base + f * ring->stride);
+      }
+    };
+    if constexpr (LR) {
+      if (r + PF <= g.nstripes) {
+        group(std::integral_constant<int, 0>{});
+        r += PF;
+      }
+      for (; r + PF <= g.nstripes; r += PF) group(std::integral_constant<int, 1>{});
+    } else {
+      for (; r + PF <= g.nstripes; r += PF) {
 #pragma unroll
-        for (int v = 0; v < kVec; ++v) buf[f][v] = ld128s<NT>(sb + 16u * v);
+        for (int f = 0; f < PF; ++f) {
+          const uint32_t c_old = c;
+          c = shift_stripe<LY>(T, c);
+          if (f == 0) {
+            c ^= inj;  // XOR into the stripe's first dword == XOR into the register before its step
+            inj = 0;
+          }
+#pragma unroll
+          for (int v = 0; v < kVec; ++v) c = NOCRC ? c ^ buf[f][v].x : steps16(T, lb, c, buf[f][v]);
+          c = (r + f == last && !lane_in_last) ? c_old : c;  // run past B16: not part of the chain
+          if (COPY && copy_on) copy_stripe(r + f, buf[f][0]);
+          const uintptr_t sb = stripe_base<RUN>(g, r + uint32_t(f) + uint32_t(PF), junk) + uintptr_t(lane) * RUN;
+#pragma unroll
+          for (int v = 0; v < kVec; ++v) buf[f][v] = ld128s<NT>(sb + 16u * v);
+        }
       }
     }
-    // Remaining 0..PF-1 stripes are already in buf[0..].
+    // Remaining 0..PF-1 stripes are already in buf[0..] (LR: in ring slots 0.., the
+    // refills of slots f+1..PF-1 younger than slot f's).
 #pragma unroll
     for (int f = 0; f < PF - 1; ++f) {
       if (r + f < g.nstripes) {
+        // at least PF - 1 younger: the refills of slots f+1.. and the stores of the
+        // remaining stripes before it (or, with no full group, the first loads)
+        if constexpr (LR) buf[f][0] = ring_slot<PF>(*ring, lane, f, PF - 1);
         const uint32_t c_old = c;
         c = shift_stripe<LY>(T, c);
         if (f == 0) c ^= inj;
@@ -1723,8 +1821,9 @@ constexpr int kCompactDiag = 4 | 8;
 constexpr int kCompactHS = 2;
 // NW waves per workgroup, OCC workgroups per CU (LDS table layout LY must fit OCC
 // times in 160 KiB): the product is 16 waves, one workgroup, layout 1.
+// LR (measurement build): the stripes in flight in an LDS-DMA ring (LdsRing) instead of VGPRs.
 template <bool WIDE, bool VERIFY = false, int DIAG = kCompactDiag, int CPF = kPF, int CF = 1, int TS = 0,
-          bool SEG = false, int HS = 0, int NW = kBlock / kWave, int OCC = 1, int LY = kLY>
+          bool SEG = false, int HS = 0, int NW = kBlock / kWave, int OCC = 1, int LY = kLY, bool LR = false>
 __global__ void __launch_bounds__(NW * kWave, OCC * NW / 4) compact_pipe_kernel(
     const uint8_t* __restrict__ src, uint64_t src_len, const RawMeta* __restrict__ metas,
     const int32_t* __restrict__ flags, const int64_t* __restrict__ dest_off, const CompactJob* __restrict__ jobs,
@@ -1732,10 +1831,19 @@ __global__ void __launch_bounds__(NW * kWave, OCC * NW / 4) compact_pipe_kernel(
     uint32_t* n_bad, uint32_t* sched, CSegArgs cs) {
   constexpr bool DA = !VERIFY && (DIAG & 4) != 0;
   constexpr bool LNT = (DIAG & 8) && !VERIFY ? false : kNT;  // the verify form keeps the headline's loads
-  static_assert(OCC * LdsLayout<LY>::bytes <= 160u * 1024u, "OCC workgroups per CU must fit the LDS");
+  static_assert(OCC * (LdsLayout<LY>::bytes + (LR ? 1024u * NW * CPF : 0u)) <= 160u * 1024u,
+                "OCC workgroups per CU must fit the LDS");
   __shared__ uint32_t lds_tables[LdsLayout<LY>::bytes / 4];
   load_tables<kRun, kPAR, LY>(lds_tables, tg);
   const int lane = threadIdx.x & (kWave - 1);
+  LdsRing ring{nullptr, 0u, 0u};
+  if constexpr (LR) {  // slot f of wave w: lds_ring[(f * NW + w) * 64 ..] (no LDS object in the product)
+    __shared__ uint4 lds_ring[NW * CPF * kWave];
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    ring.base = lds_ring + w * kWave;
+    ring.addr = uint32_t(reinterpret_cast<uintptr_t>((lds_vp)(ring.base)));
+    ring.stride = NW * kWave;
+  }
   const LaneBase lb = lane_base_for<LY>(lane);
   const uint32_t wpb = NW;
   const uintptr_t junk = reinterpret_cast<uintptr_t>(tg->slice);
@@ -1766,21 +1874,23 @@ __global__ void __launch_bounds__(NW * kWave, OCC * NW / 4) compact_pipe_kernel(
     CRec cur = unit(f);
     CState st = issue_crec<DA>(cur, src, src_len, dst, lane, junk);
     uint4 buf[CPF][kRun / 16];
-    load_ring<kRun, CPF, LNT>(st.g, lane, buf, junk);
+    if constexpr (LR) load_ring_lds<kRun, CPF>(st.g, lane, ring, junk);
+    else load_ring<kRun, CPF, LNT>(st.g, lane, buf, junk);
     CRec nxt = fn < n ? unit(fn) : CRec{};
     uint32_t jv = !FC && fn < n ? tk.issue(lane) : 0u;
     for (;;) {
       const bool more = fn < n;
       const CRec ncur = nxt;
-      uint32_t c = st.g.nstripes ? lane_chain<kRun, CPF, LNT, LY, !VERIFY, true, 1, (DIAG & 2) != 0>(
-                                       lds_tables, lb, st.g, st.h, buf, lane, junk, st.delta, true)
+      uint32_t c = st.g.nstripes ? lane_chain<kRun, CPF, LNT, LY, !VERIFY, true, 1, (DIAG & 2) != 0, LR>(
+                                       lds_tables, lb, st.g, st.h, buf, lane, junk, st.delta, true, &ring)
                                  : 0u;
       // The next record's loads go out before this one is finished.
       CState ns = st;
       uint32_t fnn = n;
       if (more) {
         ns = issue_crec<DA>(ncur, src, src_len, dst, lane, junk);
-        load_ring<kRun, CPF, LNT>(ns.g, lane, buf, junk);
+        if constexpr (LR) load_ring_lds<kRun, CPF>(ns.g, lane, ring, junk);
+        else load_ring<kRun, CPF, LNT>(ns.g, lane, buf, junk);
         fnn = FC ? fc.take(lane) : tk.resolve(jv, lane);
         if (fnn < n) {
           nxt = unit(fnn);
@@ -2335,10 +2445,11 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
                        out_crc, out_status, n_bad);
     return hipGetLastError();
   }
-#define TFS_CJ(NW_, OCC_, LY_, PF_, DIAG_)                                                                           \
-  hipLaunchKernelGGL((compact_pipe_kernel<true, false, DIAG_, PF_, 1, 0, false, kCompactHS, NW_, OCC_, LY_>),        \
+#define TFS_CJR(NW_, OCC_, LY_, PF_, DIAG_, LR_)                                                                     \
+  hipLaunchKernelGGL((compact_pipe_kernel<true, false, DIAG_, PF_, 1, 0, false, kCompactHS, NW_, OCC_, LY_, LR_>),   \
                      dim3(grid_waves(n, NW_, ccap * OCC_)), dim3(NW_ * kWave), 0, stream, src, src_len, nullptr,       \
                      nullptr, nullptr, jobs, n, dst, tg, out_crc, out_status, n_bad, sched, CSegArgs{nullptr, 0u, 0u})
+#define TFS_CJ(NW_, OCC_, LY_, PF_, DIAG_) TFS_CJR(NW_, OCC_, LY_, PF_, DIAG_, false)
 #ifdef TFS_CRC_MEASURE
   // Measurement forms: 26 the product without the payload CRC steps
   // (its own load/store schedule; wrong CRCs); 67 / 68 the record list through the
@@ -2357,10 +2468,16 @@ hipError_t launch_compact_jobs(const uint8_t* src, uint64_t src_len, const Compa
   else if (variant == 97) TFS_CJ(16, 1, 2, kPF, kCompactDiag);
   else if (variant == 98) TFS_CJ(10, 2, 2, kPF, kCompactDiag);
   else if (variant == 99) TFS_CJ(16, 2, 2, 3, kCompactDiag);
+  // Round 6: the stripes in flight in an LDS-DMA ring
+  // (LdsRing) beside the 74 KiB tables -- 120: 16 waves x 5 slots (154 KiB of LDS;
+  // its VGPR-ring control is 97); 121: 8 waves x 8 slots (138 KiB).
+  else if (variant == 120) TFS_CJR(16, 1, 2, kPF, kCompactDiag, true);
+  else if (variant == 121) TFS_CJR(8, 1, 2, 8, kCompactDiag, true);
   else
 #endif
     TFS_CJ(16, 1, kLY, kPF, kCompactDiag);
 #undef TFS_CJ
+#undef TFS_CJR
   (void)variant;
   return hipGetLastError();
 }
