@@ -65,9 +65,11 @@ int tfs_crc32_set_resident(tfs_crc_ctx* ctx, int on);
 int tfs_crc32_resident_stats(tfs_crc_ctx* ctx, uint64_t* launches, uint64_t* files);
 /* Resident-path stamps (measurement build only, libtfs_crc_measure.so; the product
  * returns TFS_EXIT_PARAMETER_ERROR).  tfs_crc32_res_trace, before the context's
- * first resident call: `pinned` (page-locked, 4096 units x 4 u64) receives, per
+ * first resident call: `pinned` (page-locked, 4096 units x 8 u64) receives, per
  * ring unit, the GPU's 100 MHz wall-clock stamps of the poll issue that found the
- * unit published, that poll's return, the unit's words back and its CRC done.
+ * unit published, that poll's return, the unit's words back, the acquire fence
+ * done, wave 0's payload loads back and its CRC done (TFS_CRC_RES_NOFENCE=1 at
+ * that call: the kernel skips the fence, measurement only).
  * tfs_crc32_res_trace_last: the last synchronous call's host stamps (steady clock
  * ns) {enter, posted, result seen, return}, its first ring unit, whether it went
  * through the ring, and the wall-clock rate in kHz (tools/floor_probe.cpp). */

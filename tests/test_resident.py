@@ -365,3 +365,42 @@ def test_closes_beside_throughput_launches(oracle):
             b.free()
     finally:
         ctx.close()
+
+
+def test_lone_calls_fresh_bytes_every_length(monkeypatch, oracle):
+    """Round 6 (units polled by tag, tiny bodies read in one load): lone calls
+    through the ring with the content changing on every call -- the scalar drop-in
+    on pageable memory (every call through the same reused staging buffer, where
+    a stale cached line would show) and page-locked batch calls rewritten in place
+    -- lengths 0..70 (the tiny byte path below 32 and the stripe path above it),
+    then random up to 8 KiB, seeds random: every CRC equals the oracle's, and
+    every call went through the ring."""
+    import tfs_amd.crc as crc
+    L = crc.lib()
+    ctx = _ctx(monkeypatch, TFS_CRC_RESIDENT=1)
+    pin = crc.PinnedBuffer(ctx, 16384)
+    try:
+        rng = np.random.default_rng(606)
+        lens = list(range(0, 71)) + [int(x) for x in rng.integers(1, 8192, 200)]
+        assert L.tfs_crc32_bind_thread(ctx.handle) == 0
+        try:
+            for k, n in enumerate(lens):
+                data = synth_bytes(9000 + k, n + 16).tobytes()
+                seed = int(rng.integers(0, 2**32))
+                off = k % 13
+                assert L.tfs_crc32(seed, data[off:off + n], n) == ocrc(oracle, seed, data[off:off + n]), (k, n)
+        finally:
+            L.tfs_crc32_bind_thread(None)
+        for k, n in enumerate(lens):
+            pin.array[:n + 32] = synth_bytes(19000 + k, n + 32)   # rewritten in place every call
+            off = (k * 7) % 17
+            seed = int(rng.integers(0, 2**32))
+            got = ctx.batch(pin.array, [off], [n], [seed])[0]
+            assert int(got) == ocrc(oracle, seed, pin.array[off:off + n].tobytes()), (k, n)
+        st = ctx.stats()
+        nz = sum(1 for n in lens if n > 0)
+        assert st["resident_files"] == nz + len(lens), st   # the scalar calls of length 0 never reach the GPU
+        assert st["lone_calls"] == nz + len(lens), st
+    finally:
+        pin.free()
+        ctx.close()

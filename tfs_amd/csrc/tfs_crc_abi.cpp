@@ -5,6 +5,7 @@
 // There is deliberately no CPU CRC here: if a device call fails the error is
 // returned (TFS_CRC_EXIT_DEVICE_ERROR / TFS_CRC_EXIT_NO_DEVICE), never computed
 // on the host instead.
+#include <emmintrin.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -57,6 +58,7 @@ hipError_t launch_write_headers(uint8_t* image, const uint64_t* rec_off, const u
 hipError_t launch_write_packet_headers(uint8_t* base, const uint64_t* rec_off, const uint32_t* len, uint32_t n,
                                        int32_t pcode, int32_t version, uint64_t first_id, hipStream_t stream);
 #ifdef TFS_CRC_MEASURE
+hipError_t set_res_nofence(uint32_t v);
 hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, uint32_t n, uint64_t nbytes,
                            uint32_t* out, unsigned grid, hipStream_t stream);
 #endif
@@ -827,13 +829,16 @@ int resident_post(tfs_crc_ctx* ctx, Slot& s, int mode, const uint8_t* zb, const 
   void* zres = s.h_res.dev;
   if (!zres) return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "resident result words are not mapped");
   for (uint32_t i = 0; i < n; ++i) {
-    ResUnit& u = H->units[(P + i) % kResUnits];
-    u.addr = uint64_t(reinterpret_cast<uintptr_t>(zb + d[i].offset));
-    u.out = uint64_t(reinterpret_cast<uintptr_t>(zres)) + 8u * i;
-    u.len = d[i].len;
-    u.seed = mode == 0 ? d[i].aux : 0u;
-    u.seq = s.seq;
-    u.reserved = 0;
+    // each half in one 16-byte store (never torn for the kernel's 16-byte read)
+    ResUnit* u = &H->units[(P + i) % kResUnits];
+    const uint32_t tag = P + i + 1u;
+    const uint64_t addr = uint64_t(reinterpret_cast<uintptr_t>(zb + d[i].offset));
+    const uint64_t out = uint64_t(reinterpret_cast<uintptr_t>(zres)) + 8u * i;
+    _mm_store_si128(reinterpret_cast<__m128i*>(&u->addr),
+                    _mm_set_epi32(int(tag), int(d[i].len), int(uint32_t(addr >> 32)), int(uint32_t(addr))));
+    _mm_store_si128(reinterpret_cast<__m128i*>(&u->out),
+                    _mm_set_epi32(int(tag), int(mode == 0 ? d[i].aux : 0u), int(uint32_t(out >> 32)),
+                                  int(uint32_t(out))));
   }
   s.res_first = P;
   ctx->res_published = P + n;
@@ -849,7 +854,7 @@ int resident_post(tfs_crc_ctx* ctx, Slot& s, int mode, const uint8_t* zb, const 
 }
 
 // Completion of a resident batch: spin until every file's result word carries
-// this batch's seq; now and then check that the kernel is still there, and
+// its unit's tag; now and then check that the kernel is still there, and
 // relaunch it (under mu) when it left with this batch outstanding (idle or
 // lifetime exit racing the post).  Then the CRCs and verdicts go where
 // finish_slot reads them (the expected CRCs are in s.h_desc).
@@ -866,7 +871,7 @@ int wait_resident(tfs_crc_ctx* ctx, Slot& s, int mode, uint32_t n) {
   uint32_t i = 0, relaunches = 0;
   for (uint32_t spins = 1;; ++spins) {
     const uint32_t i0 = i;
-    while (i < n && uint32_t(res[i] >> 32) == s.seq) ++i;
+    while (i < n && uint32_t(res[i] >> 32) == s.res_first + i + 1u) ++i;  // {crc, unit tag}
     if (i == n) {
 #ifdef TFS_CRC_MEASURE
       ctx->tr_seen.store(now_ns(), std::memory_order_relaxed);
@@ -2553,6 +2558,10 @@ int tfs_crc32_res_trace(tfs_crc_ctx* ctx, void* pinned) {
   if (pinned && !host_dev_ptr(pinned, &dev)) return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "res_trace: not page-locked");
   ctx->res_trace_dev = static_cast<uint64_t*>(dev);
   HIP_TRY(ctx, hipDeviceGetAttribute(&ctx->tr_khz, hipDeviceAttributeWallClockRate, ctx->device));
+  // TFS_CRC_RES_NOFENCE=1: the resident kernel skips its acquire fence (its cost, measured)
+  const char* nf = getenv("TFS_CRC_RES_NOFENCE");
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  HIP_TRY(ctx, set_res_nofence(nf && atoi(nf) ? 1u : 0u));
   return TFS_SUCCESS;
 #else
   (void)pinned;

@@ -81,11 +81,18 @@ constexpr uint32_t kResExitLine = kResMaxGrid * kSchedStride;  // dstate: genera
 constexpr uint32_t kResLeftLine = kResExitLine + kSchedStride;  // dstate: workgroups of this launch that have left
 constexpr uint32_t kResStateBytes = (kResMaxGrid + 2u) * kSchedStride * 4u;  // a line per workgroup + 2
 constexpr uint32_t kResMaxPolls = 1u << 22;     // hard bound on one workgroup's idle polls
+// A unit is two 16-byte halves, each read by the kernel with one 16-byte load and
+// written by the host with one 16-byte store (an aligned 16-byte access is one
+// PCIe read and never torn), and both carry the unit's tag -- its index + 1,
+// wrapping (0 never matches the zeroed ring).  A workgroup polls its next unit
+// itself and takes it when both halves show the tag it expects: the unit comes
+// back with the poll that finds it, with no second round trip (round 6).  Its
+// result word is {crc, tag}.
 struct ResUnit {         // one file
   uint64_t addr;         // device-visible address of its first byte
+  uint32_t len, tag_a;
   uint64_t out;          // device-visible address of its result word
-  uint32_t len, seed;    // seed 0 for a verify (the host compares)
-  uint32_t seq, reserved;
+  uint32_t seed, tag_b;  // seed 0 for a verify (the host compares)
 };
 struct ResHost {
   uint64_t published;    // low 32 bits: units published (wrapping); high 32 bits: stop

@@ -1168,7 +1168,13 @@ __device__ __forceinline__ uintptr_t wg_run_addr(const FileGeo<16>& g, uint32_t 
 // words, and this wave's first kWgPF stripes.
 __device__ __forceinline__ void wg_issue(const FileGeo<16>& g, Head<16>& h, uint4 (&buf)[kWgPF], uint32_t wave, int lane,
                                          uintptr_t junk) {
-  if (wave == 0) h = load_head<16>(g, lane);
+  if (wave == 0) {
+    h = load_head<16>(g, lane);
+    // a tiny body (< kMinParallelLen bytes, no stripes): lane i loads byte i, all
+    // in one instruction (one PCIe round trip from host memory instead of one per
+    // byte); wg_file_crc takes them in order with readlane
+    if (g.nstripes == 0 && uint32_t(lane) < g.len) h.tb[0] = ld8(g.start + uint32_t(lane));
+  }
 #pragma unroll
   for (int k = 0; k < kWgPF; ++k) buf[k] = ld128s<true>(wg_run_addr(g, wave + 16u * uint32_t(k), lane, junk));
 }
@@ -1235,8 +1241,8 @@ __device__ __forceinline__ uint32_t wg_file_crc(const uint32_t* lds_tables, uint
     __syncthreads();
     if (wave == 0) {
       if (g.nstripes == 0) {  // tiny (< kMinParallelLen): the byte loop of func.cpp:429-433
-        crc = g.seed;
-        for (uint32_t i = 0; i < g.len; ++i) crc = step1(lds_tables, lb, crc, ld8(g.start + i));
+        crc = g.seed;         // over the bytes wg_issue loaded, byte i in lane i
+        for (uint32_t i = 0; i < g.len; ++i) crc = step1(lds_tables, lb, crc, __builtin_amdgcn_readlane(h.tb[0], i));
       } else {
         crc = 0;
 #pragma unroll
@@ -1306,11 +1312,13 @@ __global__ void __launch_bounds__(kBlock) crc_wg_kernel(const uint8_t* __restric
 // Resident form: the latency form's workgroup-per-file body in
 // a kernel that stays on the GPU and takes files from a page-locked ring that
 // the host appends to (ResHost), so a close batch costs no launch.  Unit u is
-// workgroup (u % grid)'s: thread 0 polls `published` (the host's count of
-// units, over PCIe) until its next unit is there, reads it (32 bytes, one round
-// trip) and the workgroup CRCs the file; thread 0 stores {crc, seq} as one
-// 8-byte system-scope store into the file's result word, which the host spins
-// on.  The kernel leaves when `published` has not moved for `idle_ticks` of the
+// workgroup (u % grid)'s: thread 0 polls its next unit itself (both 16-byte
+// halves, read together with `published`: one PCIe round trip per poll) until
+// the unit's tag shows it posted, and the workgroup CRCs the file; thread 0
+// stores {crc, tag} as one 8-byte system-scope store into the file's result
+// word, which the host spins on.  (Until round 5 the poll read `published` and
+// a second round trip read the unit: 1.6-1.9 us more per batch, DESIGN.md
+// section 5.5.)  The kernel leaves when `published` has not moved for `idle_ticks` of the
 // 100 MHz wall clock, after `life_ticks` in all, when the host sets `stop`, or
 // after kResMaxPolls polls: the first workgroup to decide so stores the launch's
 // generation into the exit line, and the others, which poll it, follow at once
@@ -1323,10 +1331,15 @@ __device__ __forceinline__ uint64_t ld_sys64(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+#ifdef TFS_CRC_MEASURE
+__device__ uint32_t g_res_nofence = 0;  // measurement: resident kernels skip the acquire fence
+hipError_t set_res_nofence(uint32_t v) { return hipMemcpyToSymbol(HIP_SYMBOL(g_res_nofence), &v, 4); }
+#endif
 // trace (measurement build only, tfs_crc32_res_trace; always null in the product):
-// per ring unit, four 100 MHz wall-clock stamps of the workgroup that took it --
-// the issue of the poll that found it published, that poll's return, the unit's
-// words back, its CRC done (just before the result store).
+// per ring unit, eight words of 100 MHz wall-clock stamps of the workgroup that
+// took it -- the issue of the poll that found it published, that poll's return,
+// the unit's words back, the acquire fence done, wave 0's payload loads back, its
+// CRC done (just before the result store).
 __global__ void __launch_bounds__(kBlock) crc_resident_kernel(const Tables* __restrict__ tg, const ResHost* hs,
                                                               uint32_t* dstate, uint32_t idle_ticks,
                                                               uint32_t life_ticks, uint32_t gen, uint64_t* trace) {
@@ -1338,7 +1351,7 @@ __global__ void __launch_bounds__(kBlock) crc_resident_kernel(const Tables* __re
   const LaneBase lb = lane_base_of(lane);
   const uintptr_t junk = reinterpret_cast<uintptr_t>(tg->slice);
   uint32_t* mine = &dstate[blockIdx.x * kSchedStride];
-  uint32_t done = 0, seq = 0;  // thread 0: units this workgroup has done (all launches)
+  uint32_t done = 0, tag = 0;  // thread 0: units this workgroup has done (all launches), the unit's tag
   if (threadIdx.x == 0) done = __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   load_wg_tables(lds_tables, tg);
   const uint64_t t0 = wall_clock64();
@@ -1346,29 +1359,48 @@ __global__ void __launch_bounds__(kBlock) crc_resident_kernel(const Tables* __re
   uint32_t seen = 0;  // thread 0: `published` when last looked
   if (threadIdx.x == 0) seen = uint32_t(ld_sys64(&hs->published));
 #ifdef TFS_CRC_MEASURE
-  uint64_t t_issue = 0, t_go = 0, t_unit = 0;
+  uint64_t t_issue = 0, t_go = 0, t_unit = 0, t_fence = 0, t_loaded = 0;
   uint32_t t_want = 0;
+  const uint32_t nofence = g_res_nofence;
 #else
   (void)trace;
 #endif
   for (;;) {
     if (threadIdx.x == 0) {
       const uint32_t want = blockIdx.x + done * gridDim.x;  // this workgroup's next unit
+      const uint32_t wtag = want + 1u;                       // its tag (tfs_crc_device.h ResUnit)
+      const ResUnit* up = &hs->units[want % kResUnits];
       uint32_t go = 0;
       for (uint32_t it = 0;; ++it) {
 #ifdef TFS_CRC_MEASURE
         const uint64_t ti = trace ? wall_clock64() : 0u;
 #endif
-        // Both loads in flight together: one PCIe round trip per poll.
-        const uint64_t ps = ld_sys64(&hs->published);  // published | stop << 32
+        // One PCIe round trip per poll: `published` (idle / stop) and both halves
+        // of this workgroup's next unit, all in flight together (system-coherent
+        // 8- and 16-byte loads), beside the exit line in device memory.
         const uint32_t ex = __hip_atomic_load(&dstate[kResExitLine], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (int32_t(uint32_t(ps) - want) > 0) {
+        uint64_t ps;
+        u32x4 ua, ub;
+        asm volatile(
+            "global_load_dwordx2 %0, %3, off sc0 sc1\n\t"
+            "global_load_dwordx4 %1, %4, off sc0 sc1\n\t"
+            "global_load_dwordx4 %2, %5, off sc0 sc1\n\t"
+            "s_waitcnt vmcnt(0)"
+            : "=&v"(ps), "=&v"(ua), "=&v"(ub)
+            : "v"(&hs->published), "v"(&up->addr), "v"(&up->out)
+            : "memory");
+        if (ua.w == wtag && ub.w == wtag) {  // the unit, whole, came back with this poll
           go = 1;
+          claim[1] = uint64_t(ua.x) | uint64_t(ua.y) << 32;  // addr
+          claim[2] = uint64_t(ub.x) | uint64_t(ub.y) << 32;  // out
+          claim[3] = uint64_t(ua.z) | uint64_t(ub.z) << 32;  // len | seed << 32
+          tag = wtag;
+          ++done;
 #ifdef TFS_CRC_MEASURE
           if (trace) {
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             t_issue = ti;
             t_go = wall_clock64();
+            t_unit = t_go;  // the unit arrives with the poll (no separate read)
             t_want = want;
           }
 #endif
@@ -1386,49 +1418,49 @@ __global__ void __launch_bounds__(kBlock) crc_resident_kernel(const Tables* __re
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      if (go) {
-        // The unit's four words are read in one PCIe round trip (all four loads
-        // issued before the first is used), not four.
-        const uint64_t* u = reinterpret_cast<const uint64_t*>(&hs->units[want % kResUnits]);
-        const uint64_t w0 = ld_sys64(u), w1 = ld_sys64(u + 1), w2 = ld_sys64(u + 2), w3 = ld_sys64(u + 3);
-        claim[1] = w0;
-        claim[2] = w1;
-        claim[3] = w2;
-        seq = uint32_t(w3);
-        ++done;
-#ifdef TFS_CRC_MEASURE
-        if (trace) {  // after the unit's words are back
-          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-          t_unit = wall_clock64();
-        }
-#endif
-      }
       claim[0] = go;
     }
     __syncthreads();
     if (!claim[0]) break;
     // The payload sits in page-locked memory the host rewrote since this
     // workgroup last looked: drop stale cached lines, as a launch would.
+#ifdef TFS_CRC_MEASURE
+    if (!nofence)  // measurement only: the fence's cost (tfs_crc32_res_trace)
+#endif
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+#ifdef TFS_CRC_MEASURE
+    if (trace && threadIdx.x == 0) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      t_fence = wall_clock64();
+    }
+#endif
     const FileGeo<16> g = make_geo<16>(reinterpret_cast<const uint8_t*>(uintptr_t(claim[1])), uint32_t(claim[3]),
                                        uint32_t(claim[3] >> 32));
     Head<16> h{};
     uint4 buf[kWgPF];
     wg_issue(g, h, buf, wave, lane, junk);
+#ifdef TFS_CRC_MEASURE
+    if (trace && threadIdx.x == 0) {  // wave 0's head and first stripe loads back
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      t_loaded = wall_clock64();
+    }
+#endif
     const uint32_t crc = wg_file_crc(lds_tables, part, lb, g, h, buf, wave, lane, junk);
 #ifdef TFS_CRC_MEASURE
     if (trace && threadIdx.x == 0) {  // vector stores to page-locked host memory
-      uint64_t* tr = trace + 4u * (t_want % kResUnits);
+      uint64_t* tr = trace + 8u * (t_want % kResUnits);
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       const uint64_t t_crc = wall_clock64();
       __hip_atomic_store(tr + 0, t_issue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(tr + 1, t_go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(tr + 2, t_unit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(tr + 3, t_crc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(tr + 3, t_fence, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(tr + 4, t_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(tr + 5, t_crc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 #endif
     if (threadIdx.x == 0)
-      __hip_atomic_store(reinterpret_cast<uint64_t*>(uintptr_t(claim[2])), uint64_t(crc) | uint64_t(seq) << 32,
+      __hip_atomic_store(reinterpret_cast<uint64_t*>(uintptr_t(claim[2])), uint64_t(crc) | uint64_t(tag) << 32,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __syncthreads();  // claim[] and part[] are rewritten for the next file
   }

@@ -4,14 +4,17 @@
 // synchronous path stamps the host side (tfs_crc32_res_trace_last).
 //   (no HIP headers needed)
 //   g++ -O2 -std=c++17 tools/floor_probe.cpp -Ltfs_amd -ltfs_crc_measure -Wl,-rpath,$PWD/tfs_amd -o tools/floor_probe
-//   tools/floor_probe [iters]   -> one JSON object on stdout
+//   tools/floor_probe [iters]   -> one JSON object on stdout (TFS_FLOOR_NOFENCE=1: a second
+//   pass with the resident kernel's acquire fence skipped, TFS_CRC_RES_NOFENCE)
 // Per call (a lone body through tfs_crc32_batch from page-locked memory, and the
 // scalar drop-in tfs_crc32 from pageable memory) it splits the host's wall time into
 //   host_pre     call entry -> the unit published (lock, slot, descriptor, staging copy)
 //   post_to_go   published -> the GPU's poll returns with it   (needs the clock offset)
 //   poll_rtt     the issue of that poll -> its return        (GPU clock: one PCIe read)
 //   unit_rtt     the unit's four words back                   (GPU clock: one PCIe read)
-//   body         payload read + CRC                           (GPU clock)
+//   fence        the kernel's acquire fence                   (GPU clock)
+//   payload_loads wave 0's payload loads back                 (GPU clock: one PCIe read)
+//   compute      the CRC (chains, wave and workgroup combine)  (GPU clock)
 //   crc_to_seen  result store -> the host sees it             (needs the clock offset)
 //   host_post    result seen -> the call returns
 // post_to_go + crc_to_seen is measured without any offset ((seen - posted) - (crc - go));
@@ -34,16 +37,22 @@ static double pct(std::vector<double> v, double p) {
   return v[std::min(v.size() - 1, size_t(p * double(v.size())))];
 }
 
-int main(int argc, char** argv) {
-  const int iters = argc > 1 ? atoi(argv[1]) : 400;
+struct Rec {
+  double total, host_pre, host_post, poll_rtt, unit_rtt, fence, loads, compute, legs, a, b;
+};
+
+// One pass over the forms and sizes on a fresh context (its resident kernel reads
+// TFS_CRC_RES_NOFENCE when tfs_crc32_res_trace arms the stamps).  crcs: every call's
+// result, in order (compared across passes).
+static int pass(int iters, std::string& out, const char* tag, std::vector<uint32_t>& crcs) {
   tfs_crc_ctx* ctx = nullptr;
   if (tfs_crc32_ctx_create(0, &ctx) != TFS_SUCCESS) {
     fprintf(stderr, "ctx: %s\n", ctx ? tfs_crc32_last_error(ctx) : "?");
     return 1;
   }
   void* trace = nullptr;
-  if (tfs_crc32_host_malloc_pinned(ctx, 4096 * 32, &trace) != TFS_SUCCESS) return 1;
-  memset(trace, 0, 4096 * 32);
+  if (tfs_crc32_host_malloc_pinned(ctx, 4096 * 64, &trace) != TFS_SUCCESS) return 1;
+  memset(trace, 0, 4096 * 64);
   if (tfs_crc32_res_trace(ctx, trace) != TFS_SUCCESS) {
     fprintf(stderr, "res_trace: %s\n", tfs_crc32_last_error(ctx));
     return 1;
@@ -56,12 +65,8 @@ int main(int argc, char** argv) {
   for (size_t i = 0; i < kBuf; ++i) pageable[i] = char(i * 2654435761u >> 13);
   memcpy(pinned, pageable.data(), kBuf);
   volatile uint64_t* tr = static_cast<volatile uint64_t*>(trace);
-  std::string out = "{\"tool\": \"floor_probe\", \"iters\": " + std::to_string(iters);
   for (int form = 0; form < 2; ++form) {
     for (uint32_t len : {32u, 1024u, 4096u}) {
-      struct Rec {
-        double total, host_pre, host_post, poll_rtt, unit_rtt, body, legs, a, b;
-      };
       std::vector<Rec> recs;
       int resident = 0, lost = 0;
       for (int it = -50; it < iters; ++it) {
@@ -75,21 +80,22 @@ int main(int argc, char** argv) {
           crc = tfs_crc32_e(0, pageable.data() + off, int32_t(len), &err);
           if (err) return 2;
         }
+        crcs.push_back(crc);
         uint64_t h[8];
         tfs_crc32_res_trace_last(ctx, h);
         if (it < 0) continue;
         if (!h[5]) continue;  // launched, not through the ring
         ++resident;
-        volatile uint64_t* u = tr + 4u * (h[4] % 4096u);
+        volatile uint64_t* u = tr + 8u * (h[4] % 4096u);
         // the stamps are stored just before the result: give them a moment to land
-        for (int spin = 0; spin < 100000 && u[3] == 0; ++spin) std::this_thread::yield();
-        if (u[3] == 0) {
+        for (int spin = 0; spin < 100000 && u[5] == 0; ++spin) std::this_thread::yield();
+        if (u[5] == 0) {
           ++lost;
           continue;
         }
         const double tick = 1e6 / double(h[6] ? h[6] : 100000);  // ns per wall-clock tick
         const double gi = double(u[0]) * tick, gg = double(u[1]) * tick, gu = double(u[2]) * tick,
-                     gc = double(u[3]) * tick;
+                     gf = double(u[3]) * tick, gl = double(u[4]) * tick, gc = double(u[5]) * tick;
         const double enter = double(h[0]), posted = double(h[1]), seen = double(h[2]), done = double(h[3]);
         Rec r;
         r.total = (done - enter) / 1e3;
@@ -97,43 +103,67 @@ int main(int argc, char** argv) {
         r.host_post = (done - seen) / 1e3;
         r.poll_rtt = (gg - gi) / 1e3;
         r.unit_rtt = (gu - gg) / 1e3;
-        r.body = (gc - gu) / 1e3;
+        r.fence = (gf - gu) / 1e3;
+        r.loads = (gl - gf) / 1e3;
+        r.compute = (gc - gl) / 1e3;
         r.legs = ((seen - posted) - (gc - gg)) / 1e3;
         r.a = (gg - posted) / 1e3;  // offset + up leg
         r.b = (seen - gc) / 1e3;    // down leg - offset
         recs.push_back(r);
-        u[0] = u[1] = u[2] = u[3] = 0;
+        for (int w = 0; w < 8; ++w) u[w] = 0;
       }
       double amin = 1e300, bmin = 1e300;
       for (auto& r : recs) amin = std::min(amin, r.a), bmin = std::min(bmin, r.b);
       const double off_us = (amin - bmin) / 2;  // the fastest up and down legs taken as equal
-      auto col = [&](auto f) {
+      auto p50 = [&](auto f) {
         std::vector<double> v;
         for (auto& r : recs) v.push_back(f(r));
-        return v;
+        return pct(v, 0.5);
       };
-      char b[1024];
+      std::vector<double> tot;
+      for (auto& r : recs) tot.push_back(r.total);
+      char b[1400];
       snprintf(b, sizeof b,
-               ", \"%s_%u\": {\"calls\": %zu, \"resident\": %d, \"stamps_lost\": %d, \"p50_us\": {\"total\": %.2f, "
-               "\"host_pre\": %.2f, \"post_to_go\": %.2f, \"poll_rtt\": %.2f, \"unit_rtt\": %.2f, \"body\": %.2f, "
-               "\"crc_to_seen\": %.2f, \"host_post\": %.2f, \"legs_offset_free\": %.2f}, \"p99_total_us\": %.2f, "
-               "\"min_legs_us\": %.2f}",
-               form == 0 ? "batch_pinned" : "scalar_pageable", len, recs.size(), resident, lost,
-               pct(col([](const Rec& r) { return r.total; }), 0.5), pct(col([](const Rec& r) { return r.host_pre; }), 0.5),
-               pct(col([&](const Rec& r) { return r.a - off_us; }), 0.5),
-               pct(col([](const Rec& r) { return r.poll_rtt; }), 0.5), pct(col([](const Rec& r) { return r.unit_rtt; }), 0.5),
-               pct(col([](const Rec& r) { return r.body; }), 0.5), pct(col([&](const Rec& r) { return r.b + off_us; }), 0.5),
-               pct(col([](const Rec& r) { return r.host_post; }), 0.5), pct(col([](const Rec& r) { return r.legs; }), 0.5),
-               pct(col([](const Rec& r) { return r.total; }), 0.99), pct(col([](const Rec& r) { return r.legs; }), 0.0));
+               ", \"%s%s_%u\": {\"calls\": %zu, \"resident\": %d, \"stamps_lost\": %d, \"p50_us\": {\"total\": %.2f, "
+               "\"host_pre\": %.2f, \"post_to_go\": %.2f, \"poll_rtt\": %.2f, \"unit_rtt\": %.2f, \"fence\": %.2f, "
+               "\"payload_loads\": %.2f, \"compute\": %.2f, \"crc_to_seen\": %.2f, \"host_post\": %.2f, "
+               "\"legs_offset_free\": %.2f}, \"p99_total_us\": %.2f}",
+               tag, form == 0 ? "batch_pinned" : "scalar_pageable", len, recs.size(), resident, lost,
+               p50([](const Rec& r) { return r.total; }), p50([](const Rec& r) { return r.host_pre; }),
+               p50([&](const Rec& r) { return r.a - off_us; }), p50([](const Rec& r) { return r.poll_rtt; }),
+               p50([](const Rec& r) { return r.unit_rtt; }), p50([](const Rec& r) { return r.fence; }),
+               p50([](const Rec& r) { return r.loads; }), p50([](const Rec& r) { return r.compute; }),
+               p50([&](const Rec& r) { return r.b + off_us; }), p50([](const Rec& r) { return r.host_post; }),
+               p50([](const Rec& r) { return r.legs; }), pct(tot, 0.99));
       out += b;
     }
   }
   tfs_crc32_bind_thread(nullptr);
-  out += "}";
-  printf("%s\n", out.c_str());
   // no unit is outstanding: the idle resident kernel writes no more stamps
   tfs_crc32_host_free_pinned(ctx, pinned);
   tfs_crc32_host_free_pinned(ctx, trace);
   tfs_crc32_ctx_destroy(ctx);
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? atoi(argv[1]) : 400;
+  std::string out = "{\"tool\": \"floor_probe\", \"iters\": " + std::to_string(iters);
+  std::vector<uint32_t> crcs;
+  if (int rc = pass(iters, out, "", crcs)) return rc;
+  // TFS_FLOOR_NOFENCE=1 (measurement build): a second pass with the kernel's acquire
+  // fence skipped -- its cost, and how many results change (a stale line would)
+  const char* nf = getenv("TFS_FLOOR_NOFENCE");
+  if (nf && atoi(nf)) {
+    std::vector<uint32_t> without;
+    setenv("TFS_CRC_RES_NOFENCE", "1", 1);
+    if (int rc = pass(iters, out, "nofence_", without)) return rc;
+    size_t diff = 0;
+    for (size_t i = 0; i < crcs.size() && i < without.size(); ++i) diff += crcs[i] != without[i];
+    out += ", \"nofence_results_differing\": " + std::to_string(diff) + ", \"calls_compared\": " +
+           std::to_string(std::min(crcs.size(), without.size()));
+  }
+  out += "}";
+  printf("%s\n", out.c_str());
   return 0;
 }
