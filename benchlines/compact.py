@@ -97,6 +97,12 @@ def bench_compact(args):
         "config": {"workload": "BASELINE configs[3]: %d fragmented blocks (%d distinct pinned images cycled)" % (
             nblocks, ndistinct), "live_bytes_per_block": live * rec,
             "pcie_bytes_per_block": pcie_block,
+            "distinct_note": "%d distinct page-locked source images (and destinations) are cycled over the %d blocks: "
+                             "4,096 distinct 64 MiB source images would need 256 GiB of page-locked host memory per GPU "
+                             "(512 GiB with their destinations) "
+                             "(the box allows ~270 GiB per command, all ranks together); the GPU keeps no copy of "
+                             "an image, so every live byte of every block still crosses PCIe each time, and %d MiB "
+                             "is far above every GPU cache" % (ndistinct, nblocks, ndistinct * blk_bytes >> 20),
             "transfer": "zero-copy: fused kernel reads live records from pinned host memory and writes the "
                         "new block to pinned host memory"},
         "pcie_GBs": float(world) * nblocks * pcie_block / el / 1e9,

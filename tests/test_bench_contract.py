@@ -57,13 +57,14 @@ def test_zipf_and_compact_lines_carry_cpu_baseline():
     assert 0 < e["value"] < z["value"] and e["pcie_GBs"] > 0 and e["n_buffers"] == 20 and e["inflight"] == 3
     assert e["roofline"]["bound"] == "pcie" and 0 < e["roofline"]["frac"] < 1.2
     assert e["parity"]["mismatches"] == 0 and e["parity"]["files_checked"] > 20 * 100
-    assert e["per_rank"]["pcie_GBs"]
+    assert e["per_rank"]["pcie_GBs"] and "cycled" in e["distinct_note"]
     s = _run(["--workload", "zipf_e2e", "--e2e-blocks", "8"])
     assert s["value"] > 0 and s["roofline"]["bound"] == "pcie" and s["parity"]["mismatches"] == 0
     c = _run(["--workload", "compact", "--compact-blocks", "16", "--cpu-seconds", "0.3"])
     assert c["value"] > 0 and c["cpu_baseline"]["kind"] == "port"
     assert c["unit"] == "GiB/s of live payload" and c["source_block_GiBs"] > c["value"]
     assert c["roofline"]["bound"] == "pcie" and 0 < c["roofline"]["frac"] < 1.2
+    assert "256 GiB" in c["config"]["distinct_note"]  # why distinct images are cycled, beside the number
     assert c["cpu_baseline"]["allcore"]["value"] > 0 and c["cpu_baseline"]["allcore"]["cores"] >= 1
 
 

@@ -1070,3 +1070,69 @@ def test_dynamic_tickets_verify_counts_each_file_once(oracle, variant, monkeypat
         assert np.array_equal(outc.download(np.uint32, n), exp)
     finally:
         ctx.close()
+
+
+def test_wide_pinned_calls_from_threads_overlap_and_agree(gpu_ctx, oracle):
+    """Round 6: each synchronous slot launches wide in-place batches on its own
+    stream, so calls from several threads run side by side (the configs[2]
+    receive-buffer leg: 3 caller threads).  Four threads x six calls each over
+    three distinct page-locked images with split files, compute with seeds and
+    verify with mismatches interleaved: every result equals the oracle's, and the
+    context's later single-threaded calls still agree."""
+    import threading
+    import tfs_amd.crc as crc
+    rng = np.random.default_rng(6006)
+    imgs = []
+    pins = []
+    try:
+        for k in range(3):
+            n = 400 + 50 * k
+            lens = rng.integers(1, 70000, n).astype(np.uint32)
+            lens[3] = 400 * 1024 + k          # split files
+            lens[n // 2] = (1 << 20) - 7
+            offs = np.zeros(n, np.uint64)
+            offs[1:] = np.cumsum(lens[:-1].astype(np.uint64) + rng.integers(0, 97, n - 1).astype(np.uint64))
+            size = int(offs[-1] + lens[-1]) + 64
+            pin = crc.PinnedBuffer(gpu_ctx, size)
+            pins.append(pin)
+            pin.array[:] = rng.integers(0, 256, size, dtype=np.uint8)
+            seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+            d = np.zeros(n, crc.DESC_DTYPE)
+            d["offset"], d["len"], d["aux"] = offs, lens, seeds
+            exp_s = np.zeros(n, np.uint32)
+            oracle.oracle_crc_batch(d.ctypes.data, n, pin.array.ctypes.data, exp_s.ctypes.data)
+            d["aux"] = 0
+            exp0 = np.zeros(n, np.uint32)
+            oracle.oracle_crc_batch(d.ctypes.data, n, pin.array.ctypes.data, exp0.ctypes.data)
+            imgs.append((pin, offs, lens, seeds, exp_s, exp0))
+        errors = []
+
+        def worker(t):
+            try:
+                for it in range(6):
+                    pin, offs, lens, seeds, exp_s, exp0 = imgs[(t + it) % 3]
+                    if (t + it) % 2:
+                        got = gpu_ctx.batch(pin.array, offs, lens, seeds)
+                        if not (got == exp_s).all():
+                            errors.append(("batch", t, it, int((got != exp_s).sum())))
+                    else:
+                        want = exp0.copy()
+                        want[it::97] ^= 1
+                        c, ok, nb, rc = gpu_ctx.verify(pin.array, offs, lens, want)
+                        nbad = len(range(it, len(want), 97))
+                        if not ((c == exp0).all() and nb == nbad and int((ok == 0).sum()) == nbad):
+                            errors.append(("verify", t, it, nb))
+            except Exception as e:  # reported below
+                errors.append(("exc", t, repr(e)))
+
+        ts = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert not errors, errors[:5]
+        pin, offs, lens, seeds, exp_s, exp0 = imgs[0]
+        assert (gpu_ctx.batch(pin.array, offs, lens, seeds) == exp_s).all()
+    finally:
+        for p in pins:
+            p.free()

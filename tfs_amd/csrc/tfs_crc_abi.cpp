@@ -179,6 +179,10 @@ struct Slot {
   PinBuf h_data, h_crc, h_ok, h_bad, h_desc, h_flag;
   PinBuf h_res;  // resident form: one {crc, seq} result word per file
   hipEvent_t done = nullptr;
+  // A synchronous slot's own stream for wide in-place launches (no copies): the
+  // launches of concurrent calls overlap, so the next buffer's waves fill the
+  // link while the last waves of the previous one drain (made on first use).
+  hipStream_t wide_stream = nullptr;
   bool busy = false;
   uint64_t ticket = 0;
   int status = TFS_SUCCESS;
@@ -199,6 +203,8 @@ struct Slot {
     h_res.release();
     if (done) (void)hipEventDestroy(done);
     done = nullptr;
+    if (wide_stream) (void)hipStreamDestroy(wide_stream);  // (synchronized by the caller)
+    wide_stream = nullptr;
   }
 };
 
@@ -240,8 +246,10 @@ constexpr uint32_t kOwnedSlots = kSchedSlots - kForeignSlots;
 constexpr int kVariantDmaCompact = 8;      // DMA staging for host compaction / block verify / small batches
 #ifdef TFS_CRC_MEASURE
 constexpr int kVariantStagedWide = 52;     // wide page-locked host batches staged by DMA (the round-4 form; A/B)
+constexpr int kVariantWideCtxStream = 53;  // wide in-place launches on the ctx stream (the round-5 form; A/B)
 #else
 constexpr int kVariantStagedWide = -1;
+constexpr int kVariantWideCtxStream = -1;
 #endif
 // A context that posted a close batch this recently keeps the resident kernel's
 // CUs out of its device's throughput launches even while the kernel is between
@@ -1050,11 +1058,25 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
     if (host_dev_ptr(static_cast<const uint8_t*>(base) + lo, &zb) && s.h_desc.dev && s.h_crc.dev && s.h_ok.dev) {
       memcpy(s.h_desc.p, d, size_t(n) * sizeof(Desc));
       s.count_bad = true;
-      if (const int rc2 = files_launch(ctx, st, mode, static_cast<const uint8_t*>(zb) - lo,
+      // Each slot launches on its own stream, so the launches of concurrent calls
+      // and submissions overlap: the next batch's waves fill the link while the
+      // last waves of the previous one drain (round 6).
+      hipStream_t wst = st;
+      if (ctx->variant != kVariantWideCtxStream) {
+        if (!s.wide_stream) {
+          HIP_TRY(ctx, hipStreamCreateWithFlags(&s.wide_stream, hipStreamNonBlocking));
+          if (bind_owned_stream(ctx, s.wide_stream) != hipSuccess) {
+            (void)hipStreamDestroy(s.wide_stream);
+            s.wide_stream = nullptr;
+          }
+        }
+        if (s.wide_stream) wst = s.wide_stream;
+      }
+      if (const int rc2 = files_launch(ctx, wst, mode, static_cast<const uint8_t*>(zb) - lo,
                                        static_cast<const Desc*>(s.h_desc.dev), n, static_cast<uint32_t*>(s.h_crc.dev),
                                        static_cast<uint8_t*>(s.h_ok.dev), nullptr, 0u, may_split))
         return rc2;
-      HIP_TRY(ctx, hipEventRecord(s.done, st));
+      HIP_TRY(ctx, hipEventRecord(s.done, wst));
       return TFS_SUCCESS;
     }
     (void)hipGetLastError();
@@ -1222,6 +1244,11 @@ int tfs_crc32_ctx_create(int device, tfs_crc_ctx** out) {
   live_add(ctx, ctx->id);
 #ifdef TFS_CRC_MEASURE
   if (const char* v = getenv("TFS_CRC_VARIANT")) ctx->variant = atoi(v);
+  // measurement: the synchronous slots stage pageable bytes in fine-grained
+  // (coherent) page-locked memory instead of the default (tools/floor_probe.cpp)
+  if (const char* v = getenv("TFS_CRC_STAGE_COHERENT"))
+    if (atoi(v))
+      for (Slot& x : ctx->sync_slots) x.h_data.coherent = true;
 #endif
   if (const char* v = getenv("TFS_CRC_COMPACT_SLOTS")) ctx->compact_slots = std::min(std::max(atoi(v), 1), kCompactSlots);
   if (const char* v = getenv("TFS_CRC_COMPACT_GROUP")) ctx->compact_group = uint32_t(std::min(std::max(atoi(v), 1), 256));
@@ -1282,8 +1309,14 @@ int tfs_crc32_ctx_destroy(tfs_crc_ctx* ctx) {
   resident_teardown(ctx);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->lat_stream) (void)hipStreamSynchronize(ctx->lat_stream);
-  for (auto& s : ctx->slots) s.release();
-  for (auto& s : ctx->sync_slots) s.release();
+  for (auto& s : ctx->slots) {
+    if (s.wide_stream) (void)hipStreamSynchronize(s.wide_stream);
+    s.release();
+  }
+  for (auto& s : ctx->sync_slots) {
+    if (s.wide_stream) (void)hipStreamSynchronize(s.wide_stream);
+    s.release();
+  }
   for (auto& cs : ctx->cslots) {
     if (cs.stream) (void)hipStreamSynchronize(cs.stream);
     cs.release();
@@ -2413,6 +2446,16 @@ int tfs_crc32_sync(tfs_crc_ctx* ctx) {
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   // the zero-copy small batches launched on the latency stream
   HIP_TRY(ctx, hipStreamSynchronize(ctx->lat_stream));
+  // and the wide in-place launches on the slots' own streams (round 6)
+  std::vector<hipStream_t> wide;
+  {
+    std::lock_guard<std::mutex> g(ctx->mu);
+    for (const Slot& x : ctx->slots)
+      if (x.wide_stream) wide.push_back(x.wide_stream);
+    for (const Slot& x : ctx->sync_slots)
+      if (x.wide_stream) wide.push_back(x.wide_stream);
+  }
+  for (hipStream_t w : wide) HIP_TRY(ctx, hipStreamSynchronize(w));
   return TFS_SUCCESS;
 }
 

@@ -1148,11 +1148,17 @@ __device__ __forceinline__ void load_wg_tables(uint32_t* T, const Tables* __rest
 }
 
 // shift(c, 16 * d) for d < 2^kWgLevels.
-__device__ __forceinline__ uint32_t wg_shift_runs(const uint32_t* T, uint32_t c, uint32_t d) {
+// dmax: a wave-uniform bound on d (the wave's lane 0 distance): the levels above
+// its highest bit are skipped -- a body of a few stripes needs 6-8 of the 11
+// (round 6: 5 dependent 7-lookup levels less per lone small call).
+__device__ __forceinline__ uint32_t wg_shift_runs(const uint32_t* T, uint32_t c, uint32_t d, uint32_t dmax) {
+  const uint32_t nlev = 32u - uint32_t(__builtin_clz(dmax | 1u));
 #pragma unroll
   for (int j = 0; j < kWgLevels; ++j) {
-    const uint32_t sh = shift5(T, kWgLevelOff + 1024u * uint32_t(j), c);
-    c = ((d >> j) & 1u) ? sh : c;
+    if (uint32_t(j) < nlev) {
+      const uint32_t sh = shift5(T, kWgLevelOff + 1024u * uint32_t(j), c);
+      c = ((d >> j) & 1u) ? sh : c;
+    }
   }
   return c;
 }
@@ -1234,7 +1240,7 @@ __device__ __forceinline__ uint32_t wg_file_crc(const uint32_t* lds_tables, uint
       slast -= 16u;
     }
     const uint32_t R = last * 64u + g.nvalid;
-    c = has ? wg_shift_runs(lds_tables, c, R - 1u - (slast * 64u + uint32_t(lane))) : 0u;
+    c = has ? wg_shift_runs(lds_tables, c, R - 1u - (slast * 64u + uint32_t(lane)), R - 1u - slast * 64u) : 0u;
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) c ^= __shfl_xor(c, m, kWave);
     if (lane == 0) part[wave] = c;

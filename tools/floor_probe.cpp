@@ -162,6 +162,18 @@ int main(int argc, char** argv) {
     for (size_t i = 0; i < crcs.size() && i < without.size(); ++i) diff += crcs[i] != without[i];
     out += ", \"nofence_results_differing\": " + std::to_string(diff) + ", \"calls_compared\": " +
            std::to_string(std::min(crcs.size(), without.size()));
+    // and the pageable bytes staged in fine-grained (coherent) memory, still without
+    // the fence: whether that staging can go without it
+    std::vector<uint32_t> coh;
+    setenv("TFS_CRC_STAGE_COHERENT", "1", 1);
+    if (int rc = pass(iters, out, "nofence_coherent_", coh)) return rc;
+    size_t dp = 0, np = 0;  // the pageable (staged) half of the calls only
+    const size_t half = crcs.size() / 2;
+    for (size_t i = half; i < crcs.size() && i < coh.size(); ++i, ++np) dp += crcs[i] != coh[i];
+    out += ", \"nofence_coherent_staged_results_differing\": " + std::to_string(dp) + ", \"staged_calls_compared\": " +
+           std::to_string(np);
+    unsetenv("TFS_CRC_STAGE_COHERENT");
+    unsetenv("TFS_CRC_RES_NOFENCE");
   }
   out += "}";
   printf("%s\n", out.c_str());

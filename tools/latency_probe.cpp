@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../include/tfs_crc.h"
+#include "../include/tfs_crc_testing.h"
 
 static double pct(std::vector<double> v, double p) {
   std::sort(v.begin(), v.end());
@@ -69,6 +70,15 @@ int main(int argc, char** argv) {
   };
   uint32_t nbad = 0;
   run("scalar_64k_pageable", [&] { return int(tfs_crc32(0, pageable.data(), kFile) != crc[0]); });
+  // lone small bodies (the drop-in's floor): 16 B (the tiny
+  // byte path), 32 B, 1 KiB, 4 KiB from pageable memory
+  for (uint32_t len : {16u, 32u, 1024u, 4096u}) {
+    uint32_t want = 0;
+    tfs_crc_desc d{0, len, 0};
+    tfs_crc32_batch(ctx, &d, 1, pageable.data(), len, &want);
+    const std::string s = "scalar_" + std::to_string(len) + "B_pageable";
+    run(s.c_str(), [&, len, want] { return int(tfs_crc32(0, pageable.data(), int32_t(len)) != want); });
+  }
   run("memset_sync", [&] { return tfs_crc32_memset_device(ctx, d_bad, 0, 4, nullptr) | tfs_crc32_sync(ctx); });
   for (uint32_t n : {1u, 8u, 64u}) {
     std::string s = "verify_pinned_n" + std::to_string(n);
