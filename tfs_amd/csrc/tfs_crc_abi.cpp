@@ -1058,11 +1058,14 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
     if (host_dev_ptr(static_cast<const uint8_t*>(base) + lo, &zb) && s.h_desc.dev && s.h_crc.dev && s.h_ok.dev) {
       memcpy(s.h_desc.p, d, size_t(n) * sizeof(Desc));
       s.count_bad = true;
-      // Each slot launches on its own stream, so the launches of concurrent calls
-      // and submissions overlap: the next batch's waves fill the link while the
-      // last waves of the previous one drain (round 6).
+      // A synchronous call launches on its slot's own stream, so the launches of
+      // concurrent calls overlap: the next batch's waves fill the link while the
+      // last waves of the previous one drain (round 6, DESIGN.md section 5.5:
+      // configs[2]'s receive-buffer leg 0.934 -> 0.965 of H2D).  Async submissions
+      // stay on the context stream in submission order (the same A/B on configs[4]'s
+      // block images: 0.964 / 0.965 on slot streams against 0.973 / 0.926).
       hipStream_t wst = st;
-      if (ctx->variant != kVariantWideCtxStream) {
+      if (job >= 0 && ctx->variant != kVariantWideCtxStream) {
         if (!s.wide_stream) {
           HIP_TRY(ctx, hipStreamCreateWithFlags(&s.wide_stream, hipStreamNonBlocking));
           if (bind_owned_stream(ctx, s.wide_stream) != hipSuccess) {

@@ -1181,8 +1181,13 @@ __device__ __forceinline__ void wg_issue(const FileGeo<16>& g, Head<16>& h, uint
     // byte); wg_file_crc takes them in order with readlane
     if (g.nstripes == 0 && uint32_t(lane) < g.len) h.tb[0] = ld8(g.start + uint32_t(lane));
   }
+  // Only the stripes the file has: a short body's waves issue nothing (no `junk`
+  // loads either -- right after the resident kernel's fence those miss to HBM).
 #pragma unroll
-  for (int k = 0; k < kWgPF; ++k) buf[k] = ld128s<true>(wg_run_addr(g, wave + 16u * uint32_t(k), lane, junk));
+  for (int k = 0; k < kWgPF; ++k) {
+    const uint32_t st = wave + 16u * uint32_t(k);  // (stripe 0 is the head: load_head)
+    if (st >= 1u && st < g.nstripes) buf[k] = ld128s<true>(wg_run_addr(g, st, lane, junk));
+  }
 }
 
 // One file by the whole workgroup (its loads issued by wg_issue): wave w's lane
