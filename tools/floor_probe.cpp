@@ -20,6 +20,8 @@
 // post_to_go + crc_to_seen is measured without any offset ((seen - posted) - (crc - go));
 // its split uses the offset estimate min(a) - min(b) over the calls, halved
 // (a = go - posted, b = seen - crc: the fastest up and down legs taken as equal).
+#include <sched.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -30,6 +32,34 @@
 
 #include "../include/tfs_crc.h"
 #include "../include/tfs_crc_testing.h"
+
+// Keep the probe's threads on the GPU's NUMA node (as bench.py's lines and the
+// device group's workers are): across the socket link every PCIe round trip is
+// longer, and an unbound probe lands on either side from run to run.
+static void bind_numa(int device) {
+  const int node = tfs_crc32_device_numa_node(device);
+  if (node < 0) return;
+  char path[96];
+  snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+  FILE* f = fopen(path, "r");
+  if (!f) return;
+  char buf[4096] = {0};
+  const size_t got = fread(buf, 1, sizeof buf - 1, f);
+  fclose(f);
+  buf[got] = 0;
+  cpu_set_t cur, want;
+  CPU_ZERO(&want);
+  if (sched_getaffinity(0, sizeof cur, &cur) != 0) return;
+  for (char* tok = strtok(buf, ",\n"); tok; tok = strtok(nullptr, ",\n")) {
+    int a = 0, b = 0;
+    const int k = sscanf(tok, "%d-%d", &a, &b);
+    if (k < 1) continue;
+    if (k == 1) b = a;
+    for (int c = a; c <= b && c < CPU_SETSIZE; ++c)
+      if (CPU_ISSET(c, &cur)) CPU_SET(c, &want);
+  }
+  if (CPU_COUNT(&want) > 0) sched_setaffinity(0, sizeof want, &want);
+}
 
 static double pct(std::vector<double> v, double p) {
   if (v.empty()) return 0;
@@ -148,6 +178,7 @@ static int pass(int iters, std::string& out, const char* tag, std::vector<uint32
 
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 400;
+  bind_numa(0);
   std::string out = "{\"tool\": \"floor_probe\", \"iters\": " + std::to_string(iters);
   std::vector<uint32_t> crcs;
   if (int rc = pass(iters, out, "", crcs)) return rc;

@@ -3,6 +3,8 @@
 // Build (CPU side, no HIP headers needed):
 //   g++ -O2 -std=c++17 tools/latency_probe.cpp -Ltfs_amd -ltfs_crc -Wl,-rpath,$PWD/tfs_amd -o tools/latency_probe
 // Prints one JSON object: p50/p99 microseconds per case.
+#include <sched.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -15,6 +17,34 @@
 #include "../include/tfs_crc.h"
 #include "../include/tfs_crc_testing.h"
 
+// Keep the probe's threads on the GPU's NUMA node (as bench.py's lines and the
+// device group's workers are): across the socket link every PCIe round trip is
+// longer, and an unbound probe lands on either side from run to run.
+static void bind_numa(int device) {
+  const int node = tfs_crc32_device_numa_node(device);
+  if (node < 0) return;
+  char path[96];
+  snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+  FILE* f = fopen(path, "r");
+  if (!f) return;
+  char buf[4096] = {0};
+  const size_t got = fread(buf, 1, sizeof buf - 1, f);
+  fclose(f);
+  buf[got] = 0;
+  cpu_set_t cur, want;
+  CPU_ZERO(&want);
+  if (sched_getaffinity(0, sizeof cur, &cur) != 0) return;
+  for (char* tok = strtok(buf, ",\n"); tok; tok = strtok(nullptr, ",\n")) {
+    int a = 0, b = 0;
+    const int k = sscanf(tok, "%d-%d", &a, &b);
+    if (k < 1) continue;
+    if (k == 1) b = a;
+    for (int c = a; c <= b && c < CPU_SETSIZE; ++c)
+      if (CPU_ISSET(c, &cur)) CPU_SET(c, &want);
+  }
+  if (CPU_COUNT(&want) > 0) sched_setaffinity(0, sizeof want, &want);
+}
+
 static double pct(std::vector<double> v, double p) {
   std::sort(v.begin(), v.end());
   return v[std::min(v.size() - 1, size_t(p * double(v.size())))];
@@ -22,6 +52,7 @@ static double pct(std::vector<double> v, double p) {
 
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 300;
+  bind_numa(0);
   tfs_crc_ctx* ctx = nullptr;
   if (tfs_crc32_ctx_create(0, &ctx) != TFS_SUCCESS) {
     fprintf(stderr, "ctx: %s\n", ctx ? tfs_crc32_last_error(ctx) : "?");
