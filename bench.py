@@ -71,6 +71,8 @@ def parse(argv=None):
     p.add_argument("--e2e-blocks", type=int, default=128,
                    help="blocks (receive buffers for zipf/zipf_e2e) per GPU for the end-to-end (H2D-inclusive) leg "
                         "of the default and zipf lines; 0 = off")
+    p.add_argument("--verify-threads", type=int, default=3,
+                   help="--workload block_verify: caller threads (the mirror / repair / checker call sites)")
     p.add_argument("--ec-mib", type=int, default=1536,
                    help="member size in MiB for --workload ec (< 2048: ErasureCode sizes are int)")
     p.add_argument("--workload", default="verify", choices=["verify"] + sorted(WORKLOADS),

@@ -1136,3 +1136,64 @@ def test_wide_pinned_calls_from_threads_overlap_and_agree(gpu_ctx, oracle):
     finally:
         for p in pins:
             p.free()
+
+
+def test_block_verify_in_place_from_threads(gpu_ctx, oracle):
+    """Round 6: tfs_block_verify of a page-locked image runs on a synchronous
+    slot's own stream with its wait outside the context lock, so verifies from
+    several threads (the mirror, repair and checker call sites) run side by side.
+    Four threads x five calls over three page-locked images with rejected records
+    (payload CRC, FileInfo id, FileInfo size, too short, past the image): every
+    call's statuses and CRCs equal the single-threaded call's, which the oracle
+    pins record by record."""
+    import ctypes
+    import threading
+    import tfs_amd.crc as crc
+    rng = np.random.default_rng(6116)
+    cases = []
+    pins = []
+    try:
+        for k in range(3):
+            sizes = [int(x) for x in rng.choice([1, 100, 4096, 65536, 70001, 200000], 40)]
+            img, metas = _block_image(oracle, sizes, seed=6200 + k)
+            img[int(metas[3]["offset"]) + 36 + 5] ^= 0x20        # payload CRC
+            metas[7]["file_id"] += 1                               # FileInfo id
+            img[int(metas[9]["offset"]) + 12] ^= 0x01             # FileInfo size
+            metas[11]["size"] = 36                                 # too short
+            metas[13]["offset"] = img.size - 10                    # past the image
+            pin = crc.PinnedBuffer(gpu_ctx, img.size)
+            pins.append(pin)
+            pin.array[:] = img
+            c, st, nb, rc = gpu_ctx.block_verify(pin.array, metas)
+            for i in range(len(sizes)):
+                oc = ctypes.c_uint32()
+                code = oracle.oracle_verify_file(pin.ptr, img.size, int(metas[i]["offset"]), int(metas[i]["size"]),
+                                                 ctypes.byref(oc))
+                if i == 7:
+                    assert st[i] == -8016
+                    continue
+                assert code == st[i], (k, i, code, st[i])
+                if code in (0, -1010):
+                    assert int(c[i]) == oc.value, (k, i)
+            cases.append((pin, metas, c.copy(), st.copy(), nb))
+        errors = []
+
+        def worker(t):
+            try:
+                for it in range(5):
+                    pin, metas, c0, st0, nb0 = cases[(t + it) % 3]
+                    c, st, nb, rc = gpu_ctx.block_verify(pin.array, metas)
+                    if not ((st == st0).all() and nb == nb0 and (c[st0 == 0] == c0[st0 == 0]).all()):
+                        errors.append((t, it))
+            except Exception as e:
+                errors.append(("exc", t, repr(e)))
+
+        ts = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert not errors, errors[:5]
+    finally:
+        for p in pins:
+            p.free()

@@ -1576,6 +1576,38 @@ int tfs_blocks_verify_device(tfs_crc_ctx* ctx, const void* d_src, uint64_t src_l
   return TFS_SUCCESS;
 }
 
+namespace {
+// (Caller holds ctx->mu.)  Launch the in-place verify of a page-locked image's
+// records on synchronous slot s's own stream, metas / CRCs / statuses in the
+// slot's page-locked words; s->done is recorded behind it.
+int block_verify_inplace_enqueue(tfs_crc_ctx* ctx, Slot* s, const uint8_t* d_base, uint64_t image_len,
+                                 const tfs_raw_meta* metas, uint32_t n) {
+  HIP_TRY(ctx, s->h_desc.reserve(size_t(n) * sizeof(RawMeta)));
+  HIP_TRY(ctx, s->h_crc.reserve(size_t(n) * 4));
+  HIP_TRY(ctx, s->h_ok.reserve(size_t(n) * 4));
+  if (!s->h_desc.dev || !s->h_crc.dev || !s->h_ok.dev)
+    return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "block_verify: page-locked words not mapped");
+  if (!s->wide_stream) {
+    HIP_TRY(ctx, hipStreamCreateWithFlags(&s->wide_stream, hipStreamNonBlocking));
+    if (bind_owned_stream(ctx, s->wide_stream) != hipSuccess) {
+      (void)hipStreamDestroy(s->wide_stream);
+      s->wide_stream = nullptr;
+      return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "block_verify: no scheduler slot for a stream");
+    }
+  }
+  if (!s->done) HIP_TRY(ctx, hipEventCreateWithFlags(&s->done, hipEventDisableTiming));
+  memcpy(s->h_desc.p, metas, size_t(n) * sizeof(RawMeta));
+  hipStream_t st = s->wide_stream;
+  SCHED_LAUNCH(ctx, st, "block_verify_pipe",
+               launch_block_verify_pipe(d_base, image_len, static_cast<const RawMeta*>(s->h_desc.dev), nullptr, n,
+                                        ctx->d_tables, static_cast<uint32_t*>(s->h_crc.dev),
+                                        static_cast<int32_t*>(s->h_ok.dev), nullptr, sched, st, ctx->variant,
+                                        throughput_cap(ctx)));
+  HIP_TRY(ctx, hipEventRecord(s->done, st));
+  return TFS_SUCCESS;
+}
+}  // namespace
+
 int tfs_block_verify(tfs_crc_ctx* ctx, const void* image, uint64_t image_len, const tfs_raw_meta* metas, uint32_t n,
                      uint32_t* out_crc, int32_t* out_status, uint32_t* n_bad) {
   if (!ctx || (n && (!image || !metas))) return TFS_EXIT_PARAMETER_ERROR;
@@ -1583,40 +1615,68 @@ int tfs_block_verify(tfs_crc_ctx* ctx, const void* image, uint64_t image_len, co
     if (n_bad) *n_bad = 0;
     return TFS_SUCCESS;
   }
+  // A page-locked image is read in place on a synchronous slot's own stream, the
+  // wait outside the context lock (round 6): verifies from several threads -- the
+  // mirror, repair and checker call sites -- run side by side, the next block's
+  // waves filling the link while the last waves of another drain.
+  void* zc = nullptr;
+  if (ctx->variant != kVariantDmaCompact && ctx->variant != kVariantStagedWide && is_pinned_host(image) &&
+      host_dev_ptr(image, &zc)) {
+    Slot* s = nullptr;
+    {
+      std::unique_lock<std::mutex> lk(ctx->mu);
+      if (const int f = injected_fault(ctx)) return f;
+      HIP_TRY(ctx, hipSetDevice(ctx->device));
+      for (;;) {
+        for (Slot& x : ctx->sync_slots)
+          if (!x.busy) {
+            s = &x;
+            break;
+          }
+        if (s) break;
+        ctx->sync_cv.wait(lk);
+      }
+      s->busy = true;
+      s->resident = false;
+      const int rc = block_verify_inplace_enqueue(ctx, s, static_cast<const uint8_t*>(zc), image_len, metas, n);
+      if (rc) {
+        s->busy = false;
+        ctx->sync_cv.notify_one();
+        return rc;
+      }
+    }
+    const hipError_t e = hipEventSynchronize(s->done);
+    int rc = TFS_SUCCESS;
+    uint32_t bad = 0;
+    if (e != hipSuccess) {
+      std::lock_guard<std::mutex> g(ctx->mu);
+      rc = set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "block_verify: %s", hipGetErrorString(e));
+    } else {
+      const int32_t* st = static_cast<const int32_t*>(s->h_ok.p);
+      for (uint32_t i = 0; i < n; ++i) bad += st[i] != TFS_SUCCESS ? 1u : 0u;
+      if (out_crc) memcpy(out_crc, s->h_crc.p, size_t(n) * 4);
+      if (out_status) memcpy(out_status, st, size_t(n) * 4);
+      if (n_bad) *n_bad = bad;
+      rc = bad ? TFS_EXIT_CHECK_CRC_ERROR : TFS_SUCCESS;
+    }
+    {
+      std::lock_guard<std::mutex> g(ctx->mu);
+      s->busy = false;
+    }
+    ctx->sync_cv.notify_one();
+    return rc;
+  }
+  (void)hipGetLastError();
   std::lock_guard<std::mutex> g(ctx->mu);
   if (const int f = injected_fault(ctx)) return f;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   Slot* s = free_slot(ctx);
   if (!s) return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "all %d slots busy", kSlots);
-  // A page-locked image is read in place (zero-copy): only the records the
-  // metas name cross PCIe -- a third of a fragmented block -- instead of a
-  // whole-block copy.  Pageable images are staged.
+  // Pageable images (and the measurement build's staged forms) are staged: one
+  // whole-image copy, then the launch on the context stream.
   const uint8_t* d_base = nullptr;
-  void* zc = nullptr;
-  if (ctx->variant != kVariantDmaCompact && is_pinned_host(image) && host_dev_ptr(image, &zc)) {
-    d_base = static_cast<const uint8_t*>(zc);
-    // Metas, CRCs and statuses through the slot's page-locked words too: one launch
-    // and a stream sync per block, no copy-engine work (five DMA set-ups less behind
-    // every ~0.4 ms block).  n_bad is counted from the statuses.
-    HIP_TRY(ctx, s->h_desc.reserve(size_t(n) * sizeof(RawMeta)));
-    HIP_TRY(ctx, s->h_crc.reserve(size_t(n) * 4));
-    HIP_TRY(ctx, s->h_ok.reserve(size_t(n) * 4));
-    if (ctx->variant != kVariantStagedWide && s->h_desc.dev && s->h_crc.dev && s->h_ok.dev) {
-      memcpy(s->h_desc.p, metas, size_t(n) * sizeof(RawMeta));
-      SCHED_LAUNCH(ctx, ctx->stream, "block_verify_pipe",
-                   launch_block_verify_pipe(d_base, image_len, static_cast<const RawMeta*>(s->h_desc.dev), nullptr, n,
-                                            ctx->d_tables, static_cast<uint32_t*>(s->h_crc.dev),
-                                            static_cast<int32_t*>(s->h_ok.dev), nullptr, sched, ctx->stream,
-                                            ctx->variant, throughput_cap(ctx)));
-      HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-      const int32_t* st = static_cast<const int32_t*>(s->h_ok.p);
-      uint32_t bad = 0;
-      for (uint32_t i = 0; i < n; ++i) bad += st[i] != TFS_SUCCESS ? 1u : 0u;
-      if (out_crc) memcpy(out_crc, s->h_crc.p, size_t(n) * 4);
-      if (out_status) memcpy(out_status, st, size_t(n) * 4);
-      if (n_bad) *n_bad = bad;
-      return bad ? TFS_EXIT_CHECK_CRC_ERROR : TFS_SUCCESS;
-    }
+  if (ctx->variant == kVariantStagedWide && is_pinned_host(image) && host_dev_ptr(image, &zc)) {
+    d_base = static_cast<const uint8_t*>(zc);  // the round-5 form: in place, copies through DMA
   } else {
     (void)hipGetLastError();
     const int rc = stage_span(ctx, *s, image, 0, image_len, &d_base);

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 6 closing pass 1: the driver's sequence on this tree (GPU suite, smoke,
+# the headline line with the driver's arguments) and the small-call floor.
+set -o pipefail
+O=gpurun_out/r06/final
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest -x -v --timeout 150 --timeout-method thread -m gpu tests > $O/gpu_tests.log 2>&1 &&
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 &&
+timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_default.json 2> $O/bench_default.err &&
+g++ -O2 -std=c++17 tools/floor_probe.cpp -Ltfs_amd -ltfs_crc_measure -Wl,-rpath,$PWD/tfs_amd -o tools/floor_probe &&
+timeout -k 10 120 tools/floor_probe 400 > $O/floor_probe.json 2> $O/floor_probe.err
