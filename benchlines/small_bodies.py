@@ -31,7 +31,7 @@ import numpy as np
 from benchlines.common import *  # noqa: F401,F403
 from benchlines.common import _ref_crc_fn
 
-SIZES = (32, 256, 1024, 4096, 16384, 65536)
+SIZES = (32, 80, 256, 1024, 4096, 16384, 65536)
 
 
 def _pcts(us):
@@ -120,9 +120,17 @@ def bench_small_bodies(args):
             raise SystemExit("small_bodies: reference CRC differs from the GPU's")
         rows[str(size)] = {"scalar_us": _pcts(us), "frame_us": _pcts(fus), "batch_us_per_frame": _pcts(bus),
                            "cpu_us": cpu_us}
-    # crossover: the body size at which the host loop costs one GPU round trip (linear in size)
+    # crossover: the body size at which the host loop (linear in size) costs as much as one
+    # GPU call, the call's p50 interpolated linearly between the measured sizes (bodies of up
+    # to 80 bytes ride in the resident ring's unit and cost less than the larger ones)
     per_byte = rows["65536"]["cpu_us"] / 65536
-    rt = rows["32"]["scalar_us"]["p50"]
+    cross = None
+    for a, b in zip(SIZES, SIZES[1:]):
+        ga, gb = rows[str(a)]["scalar_us"]["p50"], rows[str(b)]["scalar_us"]["p50"]
+        da, db = per_byte * a - ga, per_byte * b - gb  # host minus GPU at both ends
+        if da < 0 <= db:
+            cross = int(a + (b - a) * (-da) / (db - da))
+            break
     res = {
         "metric": "us per call, RPC body CRC (BasePacket::decode) through the drop-in, 32 B - 64 KiB bodies",
         "value": rows["4096"]["scalar_us"]["p50"], "unit": "us (p50, 4 KiB body, tfs_crc32_e)", "n_gpus": world,
@@ -131,7 +139,7 @@ def bench_small_bodies(args):
         "data": "synthetic bodies, seed TFS_PACKET_FLAG_V1", "config": {"workload": "small RPC bodies", "sizes": SIZES},
         "sizes": rows, "python_call_us": py_us,
         "cpu_kind": kind, "cpu_ns_per_byte": per_byte * 1e3,
-        "crossover_bytes": int(rt / per_byte),
+        "crossover_bytes": cross,
         "note": "scalar/frame/batch include ~python_call_us of ctypes per call; cpu_us is per call inside one C loop "
                 "on one core.  Below crossover_bytes a lone body is cheaper on the host loop than one GPU round "
                 "trip; batched reads (batch_us_per_frame) amortise the round trip over the frames of a read.",

@@ -372,16 +372,16 @@ def test_lone_calls_fresh_bytes_every_length(monkeypatch, oracle):
     through the ring with the content changing on every call -- the scalar drop-in
     on pageable memory (every call through the same reused staging buffer, where
     a stale cached line would show) and page-locked batch calls rewritten in place
-    -- lengths 0..70 (the tiny byte path below 32 and the stripe path above it),
-    then random up to 8 KiB, seeds random: every CRC equals the oracle's, and
-    every call went through the ring."""
+    -- lengths 0..100 (bodies of up to 80 bytes travel in the ring unit itself,
+    the stripe path above), then random up to 8 KiB, seeds random: every CRC
+    equals the oracle's, and every call went through the ring."""
     import tfs_amd.crc as crc
     L = crc.lib()
     ctx = _ctx(monkeypatch, TFS_CRC_RESIDENT=1)
     pin = crc.PinnedBuffer(ctx, 16384)
     try:
         rng = np.random.default_rng(606)
-        lens = list(range(0, 71)) + [int(x) for x in rng.integers(1, 8192, 200)]
+        lens = list(range(0, 101)) + [int(x) for x in rng.integers(1, 8192, 200)]
         assert L.tfs_crc32_bind_thread(ctx.handle) == 0
         try:
             for k, n in enumerate(lens):
@@ -404,3 +404,56 @@ def test_lone_calls_fresh_bytes_every_length(monkeypatch, oracle):
     finally:
         pin.free()
         ctx.close()
+
+
+def test_inline_bodies_mixed_batches_from_threads(monkeypatch, oracle):
+    """Bodies of at most 80 bytes travel in their ring unit (tfs_crc_device.h
+    kResInline): 8 threads of synchronous verifies, each batch mixing inline
+    bodies (0..80 bytes) with bodies read over PCIe (81..3000 bytes), rewritten in
+    place every call and with one wrong expected CRC per call, the ring's units
+    reused many times over (4,096 units): every CRC and verdict is checked."""
+    import tfs_amd.crc as crc
+    ctx = _ctx(monkeypatch, TFS_CRC_RESIDENT=1)
+    errors = []
+    nthreads, calls = 8, 400
+    try:
+        pins = [crc.PinnedBuffer(ctx, 8 * 4096 + 64) for _ in range(nthreads)]
+
+        def worker(t):
+            try:
+                rng = np.random.default_rng(7000 + t)
+                pin = pins[t]
+                for it in range(calls):
+                    n = int(rng.integers(1, 9))
+                    small = rng.random(n) < 0.7
+                    lens = np.where(small, rng.integers(0, 81, n), rng.integers(81, 3001, n)).astype(np.uint32)
+                    offs = np.arange(n, dtype=np.uint64) * 4096 + rng.integers(0, 16, n).astype(np.uint64)
+                    pin.array[:] = rng.integers(0, 256, pin.array.size, dtype=np.uint8)
+                    exp = _oracle_batch(oracle, pin.array, offs, lens, np.zeros(n, np.uint32))
+                    want = exp.copy()
+                    flip = it % n
+                    want[flip] ^= 1 << (it % 32)
+                    c, ok, nbad, rc = ctx.verify(pin.array, offs, lens, want)
+                    if not ((c == exp).all() and nbad == 1 and rc == -1010 and int(np.argmin(ok)) == flip):
+                        errors.append((t, it, n, lens.tolist()))
+                        return
+                    seeds = rng.integers(0, 2**32, n).astype(np.uint32)
+                    got = ctx.batch(pin.array, offs, lens, seeds)
+                    if not (got == _oracle_batch(oracle, pin.array, offs, lens, seeds)).all():
+                        errors.append((t, it, "batch", lens.tolist()))
+                        return
+            except Exception as e:  # noqa: BLE001
+                errors.append((t, repr(e)))
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(nthreads)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        launches, files = ctx.resident_stats()
+        for p in pins:
+            p.free()
+    finally:
+        ctx.close()
+    assert not errors, errors[:5]
+    assert files > 4096, files  # the ring wrapped

@@ -205,3 +205,65 @@ def test_split_threshold():
     assert split_units(KSPLIT, 5) is None and split_units(KSPLIT - 1, 5) is None
     assert len(split_units(KSPLIT + 1, 5)) == 2 and split_units(KSPLIT + 1, 5)[0][1] == 1
     assert len(split_units(3 * KSEG, 5)) == 3 and split_units(3 * KSEG, 5)[0][1] == KSEG
+
+
+# ---- bodies carried in the resident ring unit (tfs_crc_kernels.hip inline_crc) ----
+K_RES_INLINE = 8 + 6 * 12
+
+
+def pack_unit(body, tag):
+    """The 8 16-byte parts of a ring unit as the host writes them (tfs_crc_abi.cpp
+    resident_post): bytes 0..7 in part 0's address words, 12 bytes a part from part 2."""
+    w = list(int.from_bytes((bytes(body) + bytes(80))[4 * i:4 * i + 4], "little") for i in range(20))
+    parts = [[w[0], w[1], len(body), tag], [0, 0, 0, tag]]
+    for k in range(6):
+        parts.append([w[2 + 3 * k], w[3 + 3 * k], w[4 + 3 * k], tag if 8 + 12 * k < len(body) else 0])
+    return parts
+
+
+def emulate_inline(parts, ln, seed):
+    """inline_crc lane by lane: dword j's CRC from register 0, moved 4*(nd-1-j) bytes by
+    the bits of m (4, 8 bytes: zero-dword steps; 16, 32, 64: the level tables), XOR-reduced
+    over lanes 0..31, then the last ln % 4 bytes serially."""
+    nd = ln // 4
+    c = seed
+    if nd:
+        acc = 0
+        for j in range(32):
+            src = 0 if j < 2 else 2 + (j - 2) // 3
+            k = j if j < 2 else (j - 2) % 3
+            w = parts[src][k] if src < 8 else 0
+            if j == 0:
+                w ^= seed
+            x = step4(0, w)
+            m = nd - 1 - j if j < nd else 0
+            if m & 1:
+                x = step4(x, 0)
+            if m & 2:
+                x = step4(step4(x, 0), 0)
+            for bit in (2, 3, 4):
+                if (m >> bit) & 1:
+                    x = shift(x, 16 << (bit - 2))
+            acc ^= x if j < nd else 0
+        c = acc
+    if ln & 3:
+        j = nd
+        src = 0 if j < 2 else 2 + (j - 2) // 3
+        k = j if j < 2 else (j - 2) % 3
+        w = parts[src][k]
+        for i in range(ln & 3):
+            c = step1(c, (w >> (8 * i)) & 255)
+    return c
+
+
+def test_inline_body_decomposition_matches_oracle(oracle):
+    rng = random.Random(80)
+    for ln in range(0, K_RES_INLINE + 1):
+        for _ in range(4):
+            body = bytes(rng.randrange(256) for _ in range(ln))
+            seed = rng.randrange(1 << 32)
+            parts = pack_unit(body, 7)
+            # the kernel takes only the parts it needs: the two halves and ceil((ln - 8) / 12) body parts
+            need = 2 + (max(ln - 8, 0) + 11) // 12
+            assert all(p[3] == 7 for p in parts[:need]) and all(p[3] == 0 for p in parts[need:])
+            assert emulate_inline(parts, ln, seed) == ocrc(oracle, seed, body), (ln, seed)

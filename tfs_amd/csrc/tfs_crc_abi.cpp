@@ -822,12 +822,14 @@ int resident_ensure_running(tfs_crc_ctx* ctx, bool post = false) {
   return TFS_SUCCESS;
 }
 
-// (Caller holds ctx->mu.)  Post a zero-copy batch (device-visible base `zb`)
-// as units [P, P + n), one per file, each with its result word in s.h_res; then
-// `published`; the kernel is (re)launched if gone.  Returns 1 (nothing posted)
-// when the ring has no room: a unit of a batch still outstanding would be
-// rewritten.
-int resident_post(tfs_crc_ctx* ctx, Slot& s, int mode, const uint8_t* zb, const Desc* d, uint32_t n) {
+// (Caller holds ctx->mu.)  Post a zero-copy batch (device-visible base `zb`, the
+// same bytes host-readable at `hb`) as units [P, P + n), one per file, each with
+// its result word in s.h_res; then `published`; the kernel is (re)launched if
+// gone.  A body of at most kResInline bytes is copied into its unit (the kernel
+// reads no payload for it; `zb` may be null when every body is such).  Returns 1 (nothing posted) when the ring has no
+// room: a unit of a batch still outstanding would be rewritten.
+int resident_post(tfs_crc_ctx* ctx, Slot& s, int mode, const uint8_t* zb, const uint8_t* hb, const Desc* d,
+                  uint32_t n) {
   if (const int rc = resident_setup(ctx)) return rc;
   ResHost* H = ctx->res_host;
   const uint32_t P = ctx->res_published;
@@ -837,10 +839,20 @@ int resident_post(tfs_crc_ctx* ctx, Slot& s, int mode, const uint8_t* zb, const 
   void* zres = s.h_res.dev;
   if (!zres) return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "resident result words are not mapped");
   for (uint32_t i = 0; i < n; ++i) {
-    // each half in one 16-byte store (never torn for the kernel's 16-byte read)
+    // each part in one 16-byte store (never torn for the kernel's 16-byte read)
     ResUnit* u = &H->units[(P + i) % kResUnits];
     const uint32_t tag = P + i + 1u;
-    const uint64_t addr = uint64_t(reinterpret_cast<uintptr_t>(zb + d[i].offset));
+    uint64_t addr = 0;
+    if (d[i].len > kResInline) {
+      addr = uint64_t(reinterpret_cast<uintptr_t>(zb + d[i].offset));
+    } else {  // the body travels in the unit
+      alignas(16) uint32_t w[2 + 6 * 3] = {};
+      memcpy(w, hb + d[i].offset, d[i].len);
+      addr = uint64_t(w[0]) | uint64_t(w[1]) << 32;
+      for (uint32_t k = 0; 8u + 12u * k < d[i].len; ++k)
+        _mm_store_si128(reinterpret_cast<__m128i*>(u->body[k]),
+                        _mm_set_epi32(int(tag), int(w[2 + 3 * k + 2]), int(w[2 + 3 * k + 1]), int(w[2 + 3 * k])));
+    }
     const uint64_t out = uint64_t(reinterpret_cast<uintptr_t>(zres)) + 8u * i;
     _mm_store_si128(reinterpret_cast<__m128i*>(&u->addr),
                     _mm_set_epi32(int(tag), int(d[i].len), int(uint32_t(addr >> 32)), int(uint32_t(addr))));
@@ -988,6 +1000,29 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
   // A few files far apart in one page-locked buffer (a CloseBatcher batch of
   // leases in a LeaseBufferPool) are read in place too: only their bytes cross
   // PCIe, however wide the span.
+  // Bodies that all fit in their ring units (kResInline bytes or fewer: one
+  // scalar Func::crc of a small RPC body, a packet header check): the host copies
+  // them into the units from wherever they are -- no page-lock lookup, no staging
+  // copy, and the kernel reads no payload.
+  bool ring_full = false;
+  if (job >= 0 && ctx->resident && ctx->variant == 0 && n <= kWgMaxFiles) {
+    bool all_inline = true;
+    for (uint32_t i = 0; i < n && all_inline; ++i) all_inline = dd[i].len <= kResInline;
+    if (all_inline) {
+      HIP_TRY(ctx, s.h_desc.reserve(size_t(n) * sizeof(Desc)));
+      memcpy(s.h_desc.p, d, size_t(n) * sizeof(Desc));
+      const int rc = resident_post(ctx, s, mode, nullptr, static_cast<const uint8_t*>(base), dd, n);
+      if (rc < 0) return rc;
+      if (rc == 0) {
+        s.count_bad = true;
+        s.spin = true;
+        s.resident = true;
+        return TFS_SUCCESS;
+      }
+      ++ctx->res_ring_full;  // no room in the ring: the paths below launch it
+      ring_full = true;
+    }
+  }
   const bool wide = hi - lo > kZeroCopySpan;
   const bool pinned = ctx->variant != kVariantDmaCompact && (!wide || n <= kWgMaxFiles) && is_pinned_host(base);
   uint64_t wide_bytes = 0;
@@ -1011,8 +1046,9 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
     if (zb && zd && zcrc && zok && zflag) {
       s.seq = g_flag_seq.fetch_add(1) + 1u;
       if (s.seq == 0) s.seq = g_flag_seq.fetch_add(1) + 1u;  // 0 is the words' initial value
-      if (job >= 0 && ctx->resident && ctx->variant == 0 && n <= kWgMaxFiles) {
-        const int rc = resident_post(ctx, s, mode, static_cast<const uint8_t*>(zb) - lo, static_cast<const Desc*>(d), n);
+      if (job >= 0 && ctx->resident && ctx->variant == 0 && n <= kWgMaxFiles && !ring_full) {
+        const int rc = resident_post(ctx, s, mode, static_cast<const uint8_t*>(zb) - lo,
+                                     static_cast<const uint8_t*>(host_span) - lo, static_cast<const Desc*>(d), n);
         if (rc < 0) return rc;
         if (rc == 0) {
           s.count_bad = true;

@@ -81,18 +81,24 @@ constexpr uint32_t kResExitLine = kResMaxGrid * kSchedStride;  // dstate: genera
 constexpr uint32_t kResLeftLine = kResExitLine + kSchedStride;  // dstate: workgroups of this launch that have left
 constexpr uint32_t kResStateBytes = (kResMaxGrid + 2u) * kSchedStride * 4u;  // a line per workgroup + 2
 constexpr uint32_t kResMaxPolls = 1u << 22;     // hard bound on one workgroup's idle polls
-// A unit is two 16-byte halves, each read by the kernel with one 16-byte load and
-// written by the host with one 16-byte store (an aligned 16-byte access is one
-// PCIe read and never torn), and both carry the unit's tag -- its index + 1,
+// A unit is one 128-byte line of eight 16-byte parts, each read by the kernel with
+// one 16-byte load (lane p of the polling wave takes part p) and written by the
+// host with one 16-byte store (an aligned 16-byte access is one PCIe read and
+// never torn), and every part in use carries the unit's tag -- its index + 1,
 // wrapping (0 never matches the zeroed ring).  A workgroup polls its next unit
-// itself and takes it when both halves show the tag it expects: the unit comes
-// back with the poll that finds it, with no second round trip (round 6).  Its
-// result word is {crc, tag}.
+// itself and takes it when the parts show the tag it expects: the unit comes back
+// with the poll that finds it, with no second round trip (round 6).  Its result
+// word is {crc, tag}.
+// A body of at most kResInline bytes travels in the unit itself: its first 8
+// bytes in `addr`, the rest 12 to a part in body[] -- no payload read over PCIe
+// and no acquire fence for it.
+constexpr uint32_t kResInline = 8u + 6u * 12u;  // 80 bytes
 struct ResUnit {         // one file
-  uint64_t addr;         // device-visible address of its first byte
+  uint64_t addr;         // device-visible address of its first byte (inline: bytes 0..7)
   uint32_t len, tag_a;
   uint64_t out;          // device-visible address of its result word
   uint32_t seed, tag_b;  // seed 0 for a verify (the host compares)
+  uint32_t body[6][4];   // inline: bytes 8 + 12 k .. 19 + 12 k in [k][0..2], the tag in [k][3]
 };
 struct ResHost {
   uint64_t published;    // low 32 bits: units published (wrapping); high 32 bits: stop
@@ -102,7 +108,7 @@ struct ResHost {
   ResUnit units[kResUnits];
 };
 static_assert(sizeof(ResHost) == 256 + sizeof(ResUnit) * kResUnits, "resident ring header");
-static_assert(sizeof(ResUnit) == 32, "resident ring layout");
+static_assert(sizeof(ResUnit) == 128, "resident ring layout: one line per unit");
 
 // TFS status codes (src/common/error_msg.h)
 constexpr int32_t kSuccess = 0;

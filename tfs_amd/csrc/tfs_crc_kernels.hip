@@ -1323,13 +1323,15 @@ __global__ void __launch_bounds__(kBlock) crc_wg_kernel(const uint8_t* __restric
 // Resident form: the latency form's workgroup-per-file body in
 // a kernel that stays on the GPU and takes files from a page-locked ring that
 // the host appends to (ResHost), so a close batch costs no launch.  Unit u is
-// workgroup (u % grid)'s: thread 0 polls its next unit itself (both 16-byte
-// halves, read together with `published`: one PCIe round trip per poll) until
-// the unit's tag shows it posted, and the workgroup CRCs the file; thread 0
-// stores {crc, tag} as one 8-byte system-scope store into the file's result
-// word, which the host spins on.  (Until round 5 the poll read `published` and
-// a second round trip read the unit: 1.6-1.9 us more per batch, DESIGN.md
-// section 5.5.)  The kernel leaves when `published` has not moved for `idle_ticks` of the
+// workgroup (u % grid)'s: wave 0 polls its next unit itself (the unit's 128-byte
+// line, a 16-byte part per lane, read together with `published`: one PCIe round
+// trip per poll) until the unit's tag shows it posted, and the workgroup CRCs the
+// file -- wave 0 alone, from the unit's own words, for a body of at most
+// kResInline bytes; thread 0 stores {crc, tag} as one 8-byte system-scope store
+// into the file's result word, which the host spins on.  (Until round 5 the poll
+// read `published` and a second round trip read the unit: 1.6-1.9 us more per
+// batch; until the inline bodies every body was a third round trip after an
+// acquire fence)  The kernel leaves when `published` has not moved for `idle_ticks` of the
 // 100 MHz wall clock, after `life_ticks` in all, when the host sets `stop`, or
 // after kResMaxPolls polls: the first workgroup to decide so stores the launch's
 // generation into the exit line, and the others, which poll it, follow at once
@@ -1338,6 +1340,64 @@ __global__ void __launch_bounds__(kBlock) crc_wg_kernel(const uint8_t* __restric
 // next launch; the host relaunches the kernel when it finds it gone with work
 // pending.
 // ---------------------------------------------------------------------------
+// Dword j of an inline body as the polling wave holds it (tfs_crc_device.h
+// ResUnit): bytes 0..7 in part 0's first two words, then 12 bytes per part from
+// part 2 on.  j is wave-uniform.
+__device__ __forceinline__ uint32_t inline_word(const u32x4& u, uint32_t j) {
+  const uint32_t p = j < 2u ? 0u : 2u + (j - 2u) / 3u;
+  const uint32_t k = j < 2u ? j : (j - 2u) % 3u;
+  return uint32_t(__builtin_amdgcn_readlane(k == 0u ? u.x : (k == 1u ? u.y : u.z), p));
+}
+// Func::crc(seed, body) over an inline body (len <= kResInline), the byte loop of
+// func.cpp:429-433 restated by linearity, in wave 0: lane j < len / 4 takes dword j
+// (the seed folded into dword 0), its CRC from register 0 (one slice-by-4 step),
+// moved past the dwords after it -- 4 * m bytes, m = len / 4 - 1 - j, one table
+// step per bit of m (4 and 8 bytes by zero-dword steps, 16, 32 and 64 by the
+// level tables) -- and the lanes' values XOR-reduced; the last len % 4 bytes
+// then go one at a time.  Every lane of the wave returns the CRC.
+__device__ __forceinline__ uint32_t inline_crc(const uint32_t* T, const LaneBase& lb, const u32x4& u, uint32_t len,
+                                               uint32_t seed, int lane) {
+  const uint32_t nd = len / 4u;  // wave-uniform
+  uint32_t c = seed;
+  if (nd) {
+    const uint32_t j = uint32_t(lane);
+    const int src = j < 2u ? 0 : int(2u + (j - 2u) / 3u);
+    const uint32_t k = j < 2u ? j : (j - 2u) % 3u;
+    const uint32_t vx = uint32_t(__shfl(int(u.x), src, kWave)), vy = uint32_t(__shfl(int(u.y), src, kWave)),
+                   vz = uint32_t(__shfl(int(u.z), src, kWave));
+    uint32_t w = k == 0u ? vx : (k == 1u ? vy : vz);
+    w = j == 0u ? (w ^ seed) : w;
+    uint32_t x = step4(T, lb, 0u, w);
+    const uint32_t m = j < nd ? nd - 1u - j : 0u;
+    const uint32_t mmax = nd - 1u;
+    if (mmax >= 1u) {
+      const uint32_t t = step4(T, lb, x, 0u);
+      x = (m & 1u) ? t : x;
+    }
+    if (mmax >= 2u) {
+      const uint32_t t = step4(T, lb, step4(T, lb, x, 0u), 0u);
+      x = (m & 2u) ? t : x;
+    }
+#pragma unroll
+    for (uint32_t bit = 2; bit < 5; ++bit) {
+      if ((mmax >> bit) != 0u) {
+        const uint32_t t = shift5(T, kWgLevelOff + 1024u * (bit - 2u), x);  // 16 << (bit - 2) bytes
+        x = ((m >> bit) & 1u) ? t : x;
+      }
+    }
+    x = j < nd ? x : 0u;
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) x ^= uint32_t(__shfl_xor(int(x), o, kWave));  // nd <= 20 < 32 lanes
+    c = uint32_t(__builtin_amdgcn_readfirstlane(x));
+  }
+  const uint32_t nb = len & 3u;
+  if (nb) {
+    const uint32_t w = inline_word(u, nd);
+    for (uint32_t i = 0; i < nb; ++i) c = step1(T, lb, c, w >> (8u * i));
+  }
+  return c;
+}
+
 __device__ __forceinline__ uint64_t ld_sys64(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -1362,13 +1422,14 @@ __global__ void __launch_bounds__(kBlock) crc_resident_kernel(const Tables* __re
   const LaneBase lb = lane_base_of(lane);
   const uintptr_t junk = reinterpret_cast<uintptr_t>(tg->slice);
   uint32_t* mine = &dstate[blockIdx.x * kSchedStride];
-  uint32_t done = 0, tag = 0;  // thread 0: units this workgroup has done (all launches), the unit's tag
-  if (threadIdx.x == 0) done = __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // wave 0 (every lane the same): units this workgroup has done (all launches),
+  // the unit's tag, `published` when last looked
+  uint32_t done = 0, tag = 0, seen = 0;
+  if (wave == 0) done = __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   load_wg_tables(lds_tables, tg);
   const uint64_t t0 = wall_clock64();
   uint64_t last = t0;
-  uint32_t seen = 0;  // thread 0: `published` when last looked
-  if (threadIdx.x == 0) seen = uint32_t(ld_sys64(&hs->published));
+  if (wave == 0) seen = uint32_t(ld_sys64(&hs->published));
 #ifdef TFS_CRC_MEASURE
   uint64_t t_issue = 0, t_go = 0, t_unit = 0, t_fence = 0, t_loaded = 0;
   uint32_t t_want = 0;
@@ -1377,34 +1438,43 @@ __global__ void __launch_bounds__(kBlock) crc_resident_kernel(const Tables* __re
   (void)trace;
 #endif
   for (;;) {
-    if (threadIdx.x == 0) {
+    u32x4 u = {0u, 0u, 0u, 0u};  // wave 0, lane p < 8: part p of the unit (tfs_crc_device.h ResUnit)
+    if (wave == 0) {
       const uint32_t want = blockIdx.x + done * gridDim.x;  // this workgroup's next unit
-      const uint32_t wtag = want + 1u;                       // its tag (tfs_crc_device.h ResUnit)
+      const uint32_t wtag = want + 1u;                       // its tag
       const ResUnit* up = &hs->units[want % kResUnits];
+      const u32x4* part_p = reinterpret_cast<const u32x4*>(up) + (lane & 7);
       uint32_t go = 0;
       for (uint32_t it = 0;; ++it) {
 #ifdef TFS_CRC_MEASURE
         const uint64_t ti = trace ? wall_clock64() : 0u;
 #endif
-        // One PCIe round trip per poll: `published` (idle / stop) and both halves
-        // of this workgroup's next unit, all in flight together (system-coherent
-        // 8- and 16-byte loads), beside the exit line in device memory.
+        // One PCIe round trip per poll: `published` (idle / stop) and the unit's
+        // line, a 16-byte part per lane, all in flight together (system-coherent
+        // loads), beside the exit line in device memory.
         const uint32_t ex = __hip_atomic_load(&dstate[kResExitLine], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        uint64_t ps;
-        u32x4 ua, ub;
-        asm volatile(
-            "global_load_dwordx2 %0, %3, off sc0 sc1\n\t"
-            "global_load_dwordx4 %1, %4, off sc0 sc1\n\t"
-            "global_load_dwordx4 %2, %5, off sc0 sc1\n\t"
-            "s_waitcnt vmcnt(0)"
-            : "=&v"(ps), "=&v"(ua), "=&v"(ub)
-            : "v"(&hs->published), "v"(&up->addr), "v"(&up->out)
-            : "memory");
-        if (ua.w == wtag && ub.w == wtag) {  // the unit, whole, came back with this poll
+        uint64_t ps = 0;
+        if (lane < 8) {
+          asm volatile(
+              "global_load_dwordx2 %0, %2, off sc0 sc1\n\t"
+              "global_load_dwordx4 %1, %3, off sc0 sc1\n\t"
+              "s_waitcnt vmcnt(0)"
+              : "=&v"(ps), "=&v"(u)
+              : "v"(&hs->published), "v"(part_p)
+              : "memory");
+        }
+        // the parts in use: the two halves, and an inline body's parts
+        const uint32_t len0 = __builtin_amdgcn_readlane(u.z, 0);
+        const uint32_t nparts = 2u + (len0 <= kResInline && len0 > 8u ? (len0 - 8u + 11u) / 12u : 0u);
+        const bool stale = uint32_t(lane) < nparts && u.w != wtag;
+        if (__builtin_amdgcn_ballot_w64(stale) == 0) {  // the unit, whole, came back with this poll
           go = 1;
-          claim[1] = uint64_t(ua.x) | uint64_t(ua.y) << 32;  // addr
-          claim[2] = uint64_t(ub.x) | uint64_t(ub.y) << 32;  // out
-          claim[3] = uint64_t(ua.z) | uint64_t(ub.z) << 32;  // len | seed << 32
+          if (lane == 0) {
+            claim[1] = uint64_t(u.x) | uint64_t(u.y) << 32;  // addr
+            claim[2] = uint64_t(uint32_t(__builtin_amdgcn_readlane(u.x, 1))) |
+                       uint64_t(uint32_t(__builtin_amdgcn_readlane(u.y, 1))) << 32;  // out
+            claim[3] = uint64_t(len0) | uint64_t(uint32_t(__builtin_amdgcn_readlane(u.z, 1))) << 32;  // len | seed << 32
+          }
           tag = wtag;
           ++done;
 #ifdef TFS_CRC_MEASURE
@@ -1419,44 +1489,56 @@ __global__ void __launch_bounds__(kBlock) crc_resident_kernel(const Tables* __re
         }
         if (ex == gen) break;
         const uint64_t now = wall_clock64();
-        if (uint32_t(ps) != seen) {  // units posted (to any workgroup): not idle
-          seen = uint32_t(ps);
+        const uint64_t ps0 = uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(ps)))) |
+                             uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(ps >> 32)))) << 32;
+        if (uint32_t(ps0) != seen) {  // units posted (to any workgroup): not idle
+          seen = uint32_t(ps0);
           last = now;
         }
-        if (uint32_t(ps >> 32) || now - last > idle_ticks || now - t0 > life_ticks || it >= kResMaxPolls) {
-          __hip_atomic_store(&dstate[kResExitLine], gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (uint32_t(ps0 >> 32) || now - last > idle_ticks || now - t0 > life_ticks || it >= kResMaxPolls) {
+          if (lane == 0) __hip_atomic_store(&dstate[kResExitLine], gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      claim[0] = go;
+      if (lane == 0) claim[0] = go;
     }
     __syncthreads();
     if (!claim[0]) break;
-    // The payload sits in page-locked memory the host rewrote since this
-    // workgroup last looked: drop stale cached lines, as a launch would.
+    const uint32_t len = uint32_t(claim[3]), seed = uint32_t(claim[3] >> 32);
+    uint32_t crc = 0;
+    if (len <= kResInline) {
+      // The body came with the unit: wave 0 computes its CRC from the unit's
+      // words (no payload read, so no fence).
 #ifdef TFS_CRC_MEASURE
-    if (!nofence)  // measurement only: the fence's cost (tfs_crc32_res_trace)
+      if (trace && threadIdx.x == 0) t_fence = t_loaded = wall_clock64();
 #endif
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      if (wave == 0) crc = inline_crc(lds_tables, lb, u, len, seed, lane);
+    } else {
+      // The payload sits in page-locked memory the host rewrote since this
+      // workgroup last looked: drop stale cached lines, as a launch would.
 #ifdef TFS_CRC_MEASURE
-    if (trace && threadIdx.x == 0) {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      t_fence = wall_clock64();
+      if (!nofence)  // measurement only: the fence's cost (tfs_crc32_res_trace)
+#endif
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+#ifdef TFS_CRC_MEASURE
+      if (trace && threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        t_fence = wall_clock64();
+      }
+#endif
+      const FileGeo<16> g = make_geo<16>(reinterpret_cast<const uint8_t*>(uintptr_t(claim[1])), len, seed);
+      Head<16> h{};
+      uint4 buf[kWgPF];
+      wg_issue(g, h, buf, wave, lane, junk);
+#ifdef TFS_CRC_MEASURE
+      if (trace && threadIdx.x == 0) {  // wave 0's head and first stripe loads back
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        t_loaded = wall_clock64();
+      }
+#endif
+      crc = wg_file_crc(lds_tables, part, lb, g, h, buf, wave, lane, junk);
     }
-#endif
-    const FileGeo<16> g = make_geo<16>(reinterpret_cast<const uint8_t*>(uintptr_t(claim[1])), uint32_t(claim[3]),
-                                       uint32_t(claim[3] >> 32));
-    Head<16> h{};
-    uint4 buf[kWgPF];
-    wg_issue(g, h, buf, wave, lane, junk);
-#ifdef TFS_CRC_MEASURE
-    if (trace && threadIdx.x == 0) {  // wave 0's head and first stripe loads back
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      t_loaded = wall_clock64();
-    }
-#endif
-    const uint32_t crc = wg_file_crc(lds_tables, part, lb, g, h, buf, wave, lane, junk);
 #ifdef TFS_CRC_MEASURE
     if (trace && threadIdx.x == 0) {  // vector stores to page-locked host memory
       uint64_t* tr = trace + 8u * (t_want % kResUnits);

@@ -96,7 +96,7 @@ static int pass(int iters, std::string& out, const char* tag, std::vector<uint32
   memcpy(pinned, pageable.data(), kBuf);
   volatile uint64_t* tr = static_cast<volatile uint64_t*>(trace);
   for (int form = 0; form < 2; ++form) {
-    for (uint32_t len : {32u, 1024u, 4096u}) {
+    for (uint32_t len : {32u, 80u, 96u, 1024u, 4096u}) {
       std::vector<Rec> recs;
       int resident = 0, lost = 0;
       for (int it = -50; it < iters; ++it) {
