@@ -34,15 +34,18 @@ def _random_batch(rng, n, maxlen=70000, seed=0):
 
 def test_resident_batches_match_oracle(monkeypatch, oracle):
     """Compute with seeds and verify (with mismatches) through the ring, batch sizes
-    1..256, pageable and page-locked; the same calls with the ring off agree."""
+    1..256, pageable and page-locked; the same calls with the ring off agree.  The
+    batches that read more than 1 MiB over PCIe (bodies over 80 bytes; the shorter
+    ones travel in the ring unit) take the bulk form: fence, non-temporal stripes."""
     import tfs_amd.crc as crc
     ctx = _ctx(monkeypatch, TFS_CRC_RESIDENT=1)
     try:
         rng = np.random.default_rng(31)
-        ring_files = 0
+        ring_files = bulk = 0
         for it, n in enumerate((1, 2, 3, 8, 17, 64, 200, 256)):
             buf, offs, lens = _random_batch(rng, n, maxlen=70000 if n <= 64 else 30000, seed=500 + n)
             ring_files += 3 * n  # spans <= 8 MiB: read in place, so through the ring
+            bulk += int(lens[lens > 80].sum()) > 1 << 20
             seeds = rng.integers(0, 2**32, n).astype(np.uint32)
             exp = _oracle_batch(oracle, buf, offs, lens, seeds)
             assert (ctx.batch(buf, offs, lens, seeds) == exp).all(), n
@@ -59,7 +62,7 @@ def test_resident_batches_match_oracle(monkeypatch, oracle):
             finally:
                 pin.free()
         launches, files = ctx.resident_stats()
-        assert launches >= 1 and files == ring_files, (launches, files, ring_files)
+        assert launches >= 1 and files == ring_files and bulk >= 2, (launches, files, ring_files, bulk)
         ctx.set_resident(False)
         buf, offs, lens = _random_batch(rng, 40, seed=77)
         seeds = rng.integers(0, 2**32, 40).astype(np.uint32)

@@ -58,7 +58,7 @@ hipError_t launch_write_headers(uint8_t* image, const uint64_t* rec_off, const u
 hipError_t launch_write_packet_headers(uint8_t* base, const uint64_t* rec_off, const uint32_t* len, uint32_t n,
                                        int32_t pcode, int32_t version, uint64_t first_id, hipStream_t stream);
 #ifdef TFS_CRC_MEASURE
-hipError_t set_res_nofence(uint32_t v);
+hipError_t set_res_fence(uint32_t v);
 hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, uint32_t n, uint64_t nbytes,
                            uint32_t* out, unsigned grid, hipStream_t stream);
 #endif
@@ -838,6 +838,10 @@ int resident_post(tfs_crc_ctx* ctx, Slot& s, int mode, const uint8_t* zb, const 
   HIP_TRY(ctx, s.h_res.reserve(size_t(n) * 8));
   void* zres = s.h_res.dev;
   if (!zres) return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "resident result words are not mapped");
+  uint64_t pcie_bytes = 0;  // what the kernel reads over PCIe for this batch
+  for (uint32_t i = 0; i < n; ++i) pcie_bytes += d[i].len > kResInline ? d[i].len : 0u;
+  const uint32_t bulk = pcie_bytes > kResBulkBytes ? kResBulk : 0u;  // tfs_crc_device.h
+
   for (uint32_t i = 0; i < n; ++i) {
     // each part in one 16-byte store (never torn for the kernel's 16-byte read)
     ResUnit* u = &H->units[(P + i) % kResUnits];
@@ -855,7 +859,8 @@ int resident_post(tfs_crc_ctx* ctx, Slot& s, int mode, const uint8_t* zb, const 
     }
     const uint64_t out = uint64_t(reinterpret_cast<uintptr_t>(zres)) + 8u * i;
     _mm_store_si128(reinterpret_cast<__m128i*>(&u->addr),
-                    _mm_set_epi32(int(tag), int(d[i].len), int(uint32_t(addr >> 32)), int(uint32_t(addr))));
+                    _mm_set_epi32(int(tag), int(d[i].len | (d[i].len > kResInline ? bulk : 0u)),
+                                  int(uint32_t(addr >> 32)), int(uint32_t(addr))));
     _mm_store_si128(reinterpret_cast<__m128i*>(&u->out),
                     _mm_set_epi32(int(tag), int(mode == 0 ? d[i].aux : 0u), int(uint32_t(out >> 32)),
                                   int(uint32_t(out))));
@@ -2700,10 +2705,11 @@ int tfs_crc32_res_trace(tfs_crc_ctx* ctx, void* pinned) {
   if (pinned && !host_dev_ptr(pinned, &dev)) return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "res_trace: not page-locked");
   ctx->res_trace_dev = static_cast<uint64_t*>(dev);
   HIP_TRY(ctx, hipDeviceGetAttribute(&ctx->tr_khz, hipDeviceAttributeWallClockRate, ctx->device));
-  // TFS_CRC_RES_NOFENCE=1: the resident kernel skips its acquire fence (its cost, measured)
-  const char* nf = getenv("TFS_CRC_RES_NOFENCE");
+  // TFS_CRC_RES_FENCE=1: the resident kernel also fences before each payload read
+  // over PCIe, as it did before its system-coherent loads (the A/B of round 6)
+  const char* fe = getenv("TFS_CRC_RES_FENCE");
   HIP_TRY(ctx, hipSetDevice(ctx->device));
-  HIP_TRY(ctx, set_res_nofence(nf && atoi(nf) ? 1u : 0u));
+  HIP_TRY(ctx, set_res_fence(fe && atoi(fe) ? 1u : 0u));
   return TFS_SUCCESS;
 #else
   (void)pinned;

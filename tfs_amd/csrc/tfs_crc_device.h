@@ -93,6 +93,14 @@ constexpr uint32_t kResMaxPolls = 1u << 22;     // hard bound on one workgroup's
 // bytes in `addr`, the rest 12 to a part in body[] -- no payload read over PCIe
 // and no acquire fence for it.
 constexpr uint32_t kResInline = 8u + 6u * 12u;  // 80 bytes
+// The ring's workgroups read bodies with system-coherent loads and no fence:
+// 0.6-1.2 us less per lone call, but ~10 % less rate than non-temporal loads once
+// 16 workgroups stream together (64 files of 64 KiB: 92.8 against 84.4 us fenced,
+// DESIGN.md section 5.5).  The units of a batch that reads more than
+// kResBulkBytes over PCIe carry kResBulk in their length word: fence, then
+// non-temporal stripes.
+constexpr uint32_t kResBulk = 0x80000000u;
+constexpr uint64_t kResBulkBytes = 1u << 20;
 struct ResUnit {         // one file
   uint64_t addr;         // device-visible address of its first byte (inline: bytes 0..7)
   uint32_t len, tag_a;

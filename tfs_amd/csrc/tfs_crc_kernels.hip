@@ -1170,23 +1170,92 @@ __device__ __forceinline__ uintptr_t wg_run_addr(const FileGeo<16>& g, uint32_t 
   return (s >= 1u && s < g.nstripes ? g.sb0 + uintptr_t(s) * 1024u : junk) + uintptr_t(lane) * 16u;
 }
 
+// Where the latency form reads a file from.  SYS = false (crc_wg_kernel): global
+// loads, payload stripes non-temporal, ring refills past the file from `junk`.
+// SYS = true (crc_resident_kernel): buffer loads with the system-coherent policy
+// (sc0 sc1) off a wave-uniform resource at the file's stripe base -- a payload
+// the host rewrote since the workgroup last looked is never served from a stale
+// cached line, so no acquire fence per file -- and every load the file does not
+// need (ring refills past its end, masked head lanes) is out of the resource's
+// range: it returns 0 and moves no bytes.
+struct WgSrc {
+  __amdgpu_buffer_rsrc_t r;
+  uintptr_t base;
+  bool bulk;  // stripes by non-temporal loads (the caller fenced): a bulk batch, kResBulk
+};
+constexpr uint32_t kWgOOR = 0xFFFFFFF0u;           // an offset past every resource's range
+constexpr int kSysPolicy = 1 | 16;                 // sc0 | sc1 (system scope)
+constexpr int kNtPolicy = 2;                       // nt (streaming)
+__device__ __forceinline__ WgSrc wg_src(const FileGeo<16>& g, bool bulk) {
+  const uintptr_t base = g.nstripes ? g.sb0 : g.start;
+  return WgSrc{__builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), 0, 0x7fffffff, 0x00020000), base,
+               bulk};
+}
+__device__ __forceinline__ int wg_off(const WgSrc& src, bool ok, uintptr_t a) {
+  return int(ok ? uint32_t(a - src.base) : kWgOOR);
+}
+// A payload stripe: system-coherent, or (bulk) non-temporal -- one load either way
+// (a wave-uniform branch).
+__device__ __forceinline__ uint4 sys128(const WgSrc& src, bool ok, uintptr_t a) {
+  const int off = wg_off(src, ok, a);
+  u32x4 v;
+  if (src.bulk) v = __builtin_amdgcn_raw_buffer_load_b128(src.r, off, 0, kNtPolicy);
+  else v = __builtin_amdgcn_raw_buffer_load_b128(src.r, off, 0, kSysPolicy);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t sys32(const WgSrc& src, bool ok, uintptr_t a) {
+  return __builtin_amdgcn_raw_buffer_load_b32(src.r, wg_off(src, ok, a), 0, kSysPolicy);
+}
+__device__ __forceinline__ uint32_t sys8(const WgSrc& src, bool ok, uintptr_t a) {
+  return __builtin_amdgcn_raw_buffer_load_b8(src.r, wg_off(src, ok, a), 0, kSysPolicy);
+}
+// load_head<16> through the resource (same words, same zeros).
+__device__ __forceinline__ Head<16> load_head_sys(const FileGeo<16>& g, const WgSrc& src, int lane) {
+  Head<16> h;
+  const uintptr_t lo = g.sb0 + uintptr_t(lane) * 16u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uintptr_t q = lo + 4u * i;
+    h.w[i] = sys32(src, g.nstripes && q >= g.A && q < g.B16, q);
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) h.tw[i] = sys32(src, g.nstripes && g.B16 + 4u * i + 4u <= g.end, g.B16 + 4u * i);
+  const uintptr_t B = g.nstripes ? (g.end & ~uintptr_t(3)) : g.start;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) h.tb[i] = sys8(src, g.nstripes && B + i < g.end, B + i);
+  return h;
+}
+// Stripe st's run of this lane (junk / out of range past the file).
+template <bool SYS>
+__device__ __forceinline__ uint4 wg_run_load(const FileGeo<16>& g, const WgSrc& src, uint32_t st, int lane,
+                                             uintptr_t junk) {
+  if constexpr (SYS) return sys128(src, st >= 1u && st < g.nstripes, g.sb0 + uintptr_t(st) * 1024u + uintptr_t(lane) * 16u);
+  return ld128s<true>(wg_run_addr(g, st, lane, junk));
+}
+
 // Issue one file's loads for the latency form: (wave 0) the head stripe and tail
 // words, and this wave's first kWgPF stripes.
-__device__ __forceinline__ void wg_issue(const FileGeo<16>& g, Head<16>& h, uint4 (&buf)[kWgPF], uint32_t wave, int lane,
-                                         uintptr_t junk) {
+template <bool SYS>
+__device__ __forceinline__ void wg_issue(const FileGeo<16>& g, const WgSrc& src, Head<16>& h, uint4 (&buf)[kWgPF],
+                                         uint32_t wave, int lane, uintptr_t junk) {
   if (wave == 0) {
-    h = load_head<16>(g, lane);
+    if constexpr (SYS) h = load_head_sys(g, src, lane);
+    else h = load_head<16>(g, lane);
     // a tiny body (< kMinParallelLen bytes, no stripes): lane i loads byte i, all
     // in one instruction (one PCIe round trip from host memory instead of one per
     // byte); wg_file_crc takes them in order with readlane
-    if (g.nstripes == 0 && uint32_t(lane) < g.len) h.tb[0] = ld8(g.start + uint32_t(lane));
+    if constexpr (SYS) {
+      if (g.nstripes == 0) h.tb[0] = sys8(src, uint32_t(lane) < g.len, g.start + uint32_t(lane));
+    } else {
+      if (g.nstripes == 0 && uint32_t(lane) < g.len) h.tb[0] = ld8(g.start + uint32_t(lane));
+    }
   }
   // Only the stripes the file has: a short body's waves issue nothing (no `junk`
-  // loads either -- right after the resident kernel's fence those miss to HBM).
+  // loads either -- right after a fence those miss to HBM).
 #pragma unroll
   for (int k = 0; k < kWgPF; ++k) {
     const uint32_t st = wave + 16u * uint32_t(k);  // (stripe 0 is the head: load_head)
-    if (st >= 1u && st < g.nstripes) buf[k] = ld128s<true>(wg_run_addr(g, st, lane, junk));
+    if (st >= 1u && st < g.nstripes) buf[k] = wg_run_load<SYS>(g, src, st, lane, junk);
   }
 }
 
@@ -1195,9 +1264,10 @@ __device__ __forceinline__ void wg_issue(const FileGeo<16>& g, Head<16>& h, uint
 // the wave and across waves through `part`.  The CRC is returned in wave 0
 // (undefined in the other waves); `part` must not be rewritten before the
 // caller's next __syncthreads.
+template <bool SYS>
 __device__ __forceinline__ uint32_t wg_file_crc(const uint32_t* lds_tables, uint32_t* part, const LaneBase& lb,
-                                                const FileGeo<16>& g, const Head<16>& h, uint4 (&buf)[kWgPF],
-                                                uint32_t wave, int lane, uintptr_t junk) {
+                                                const FileGeo<16>& g, const WgSrc& src, const Head<16>& h,
+                                                uint4 (&buf)[kWgPF], uint32_t wave, int lane, uintptr_t junk) {
   uint32_t crc = 0;
   {
     // ---- this wave's lane chains over stripes wave, wave+16, ...
@@ -1232,7 +1302,7 @@ __device__ __forceinline__ uint32_t wg_file_crc(const uint32_t* lds_tables, uint
             c = steps16(lds_tables, lb, c ^ (st == 1u ? inj : 0u), buf[fi]);
           }
           c = (st == last && !lane_in_last) ? c_old : c;  // run past B16: not part of the chain
-          buf[fi] = ld128s<true>(wg_run_addr(g, st + 16u * kWgPF, lane, junk));
+          buf[fi] = wg_run_load<SYS>(g, src, st + 16u * kWgPF, lane, junk);
         }
       }
     }
@@ -1292,7 +1362,7 @@ __global__ void __launch_bounds__(kBlock) crc_wg_kernel(const uint8_t* __restric
   auto issue = [&](uint32_t ff) {
     cur = desc[ff];
     g = make_geo<16>(base + cur.offset, cur.len, MODE == 0 ? cur.aux : vseed);
-    wg_issue(g, h, buf, wave, lane, junk);
+    wg_issue<false>(g, WgSrc{}, h, buf, wave, lane, junk);
   };
   // The first file's loads are in flight while the tables are staged.
   if (f < n) issue(f);
@@ -1300,7 +1370,7 @@ __global__ void __launch_bounds__(kBlock) crc_wg_kernel(const uint8_t* __restric
   __syncthreads();
   uint32_t bad = 0;
   while (f < n) {
-    const uint32_t crc = wg_file_crc(lds_tables, part, lb, g, h, buf, wave, lane, junk);
+    const uint32_t crc = wg_file_crc<false>(lds_tables, part, lb, g, WgSrc{}, h, buf, wave, lane, junk);
     if (wave == 0 && lane == 0) {
       if (out_crc) out_crc[f] = crc;
       if (MODE == 1) {
@@ -1403,8 +1473,8 @@ __device__ __forceinline__ uint64_t ld_sys64(const uint64_t* p) {
 }
 
 #ifdef TFS_CRC_MEASURE
-__device__ uint32_t g_res_nofence = 0;  // measurement: resident kernels skip the acquire fence
-hipError_t set_res_nofence(uint32_t v) { return hipMemcpyToSymbol(HIP_SYMBOL(g_res_nofence), &v, 4); }
+__device__ uint32_t g_res_fence = 0;  // measurement: resident kernels fence before each payload (the pre-round-6 form)
+hipError_t set_res_fence(uint32_t v) { return hipMemcpyToSymbol(HIP_SYMBOL(g_res_fence), &v, 4); }
 #endif
 // trace (measurement build only, tfs_crc32_res_trace; always null in the product):
 // per ring unit, eight words of 100 MHz wall-clock stamps of the workgroup that
@@ -1433,7 +1503,7 @@ __global__ void __launch_bounds__(kBlock) crc_resident_kernel(const Tables* __re
 #ifdef TFS_CRC_MEASURE
   uint64_t t_issue = 0, t_go = 0, t_unit = 0, t_fence = 0, t_loaded = 0;
   uint32_t t_want = 0;
-  const uint32_t nofence = g_res_nofence;
+  const uint32_t fence_ab = g_res_fence;
 #else
   (void)trace;
 #endif
@@ -1505,7 +1575,9 @@ __global__ void __launch_bounds__(kBlock) crc_resident_kernel(const Tables* __re
     }
     __syncthreads();
     if (!claim[0]) break;
-    const uint32_t len = uint32_t(claim[3]), seed = uint32_t(claim[3] >> 32);
+    const uint32_t lw = uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(claim[3])));  // wave-uniform
+    const uint32_t len = lw & ~kResBulk, seed = uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(claim[3] >> 32)));
+    const bool bulk = (lw & kResBulk) != 0u;
     uint32_t crc = 0;
     if (len <= kResInline) {
       // The body came with the unit: wave 0 computes its CRC from the unit's
@@ -1516,28 +1588,37 @@ __global__ void __launch_bounds__(kBlock) crc_resident_kernel(const Tables* __re
       if (wave == 0) crc = inline_crc(lds_tables, lb, u, len, seed, lane);
     } else {
       // The payload sits in page-locked memory the host rewrote since this
-      // workgroup last looked: drop stale cached lines, as a launch would.
+      // workgroup last looked.  A lone or small batch's body is read with
+      // system-coherent loads (wg_src), never from a stale cached line, so no
+      // acquire fence (round 6; before, a fence per file as a launch has: 0.6 us);
+      // a bulk batch's (kResBulk) stripes stream with non-temporal loads (the
+      // link's full rate) after the fence drops stale lines.
 #ifdef TFS_CRC_MEASURE
-      if (!nofence)  // measurement only: the fence's cost (tfs_crc32_res_trace)
+      if (bulk || fence_ab)  // fence_ab: measurement only, the fenced form for A/B
+#else
+      if (bulk)
 #endif
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 #ifdef TFS_CRC_MEASURE
       if (trace && threadIdx.x == 0) {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         t_fence = wall_clock64();
       }
 #endif
-      const FileGeo<16> g = make_geo<16>(reinterpret_cast<const uint8_t*>(uintptr_t(claim[1])), len, seed);
+      const uint64_t addr = uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(claim[1])))) |
+                            uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(uint32_t(claim[1] >> 32)))) << 32;
+      const FileGeo<16> g = make_geo<16>(reinterpret_cast<const uint8_t*>(uintptr_t(addr)), len, seed);
+      const WgSrc src = wg_src(g, bulk);  // wave-uniform: the resource in SGPRs
       Head<16> h{};
       uint4 buf[kWgPF];
-      wg_issue(g, h, buf, wave, lane, junk);
+      wg_issue<true>(g, src, h, buf, wave, lane, junk);
 #ifdef TFS_CRC_MEASURE
       if (trace && threadIdx.x == 0) {  // wave 0's head and first stripe loads back
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         t_loaded = wall_clock64();
       }
 #endif
-      crc = wg_file_crc(lds_tables, part, lb, g, h, buf, wave, lane, junk);
+      crc = wg_file_crc<true>(lds_tables, part, lb, g, src, h, buf, wave, lane, junk);
     }
 #ifdef TFS_CRC_MEASURE
     if (trace && threadIdx.x == 0) {  // vector stores to page-locked host memory

@@ -4,8 +4,8 @@
 // synchronous path stamps the host side (tfs_crc32_res_trace_last).
 //   (no HIP headers needed)
 //   g++ -O2 -std=c++17 tools/floor_probe.cpp -Ltfs_amd -ltfs_crc_measure -Wl,-rpath,$PWD/tfs_amd -o tools/floor_probe
-//   tools/floor_probe [iters]   -> one JSON object on stdout (TFS_FLOOR_NOFENCE=1: a second
-//   pass with the resident kernel's acquire fence skipped, TFS_CRC_RES_NOFENCE)
+//   tools/floor_probe [iters]   -> one JSON object on stdout (TFS_FLOOR_FENCE=1: a second
+//   pass with the resident kernel's acquire fence before each payload, TFS_CRC_RES_FENCE)
 // Per call (a lone body through tfs_crc32_batch from page-locked memory, and the
 // scalar drop-in tfs_crc32 from pageable memory) it splits the host's wall time into
 //   host_pre     call entry -> the unit published (lock, slot, descriptor, staging copy)
@@ -72,7 +72,7 @@ struct Rec {
 };
 
 // One pass over the forms and sizes on a fresh context (its resident kernel reads
-// TFS_CRC_RES_NOFENCE when tfs_crc32_res_trace arms the stamps).  crcs: every call's
+// TFS_CRC_RES_FENCE when tfs_crc32_res_trace arms the stamps).  crcs: every call's
 // result, in order (compared across passes).
 static int pass(int iters, std::string& out, const char* tag, std::vector<uint32_t>& crcs) {
   tfs_crc_ctx* ctx = nullptr;
@@ -182,29 +182,19 @@ int main(int argc, char** argv) {
   std::string out = "{\"tool\": \"floor_probe\", \"iters\": " + std::to_string(iters);
   std::vector<uint32_t> crcs;
   if (int rc = pass(iters, out, "", crcs)) return rc;
-  // TFS_FLOOR_NOFENCE=1 (measurement build): a second pass with the kernel's acquire
-  // fence skipped -- its cost, and how many results change (a stale line would)
-  const char* nf = getenv("TFS_FLOOR_NOFENCE");
-  if (nf && atoi(nf)) {
-    std::vector<uint32_t> without;
-    setenv("TFS_CRC_RES_NOFENCE", "1", 1);
-    if (int rc = pass(iters, out, "nofence_", without)) return rc;
+  // TFS_FLOOR_FENCE=1 (measurement build): a second pass with the kernel's acquire
+  // fence before each payload read (the form before its system-coherent loads) --
+  // the fence's cost, and that no result changes
+  const char* fe = getenv("TFS_FLOOR_FENCE");
+  if (fe && atoi(fe)) {
+    std::vector<uint32_t> fenced;
+    setenv("TFS_CRC_RES_FENCE", "1", 1);
+    if (int rc = pass(iters, out, "fenced_", fenced)) return rc;
     size_t diff = 0;
-    for (size_t i = 0; i < crcs.size() && i < without.size(); ++i) diff += crcs[i] != without[i];
-    out += ", \"nofence_results_differing\": " + std::to_string(diff) + ", \"calls_compared\": " +
-           std::to_string(std::min(crcs.size(), without.size()));
-    // and the pageable bytes staged in fine-grained (coherent) memory, still without
-    // the fence: whether that staging can go without it
-    std::vector<uint32_t> coh;
-    setenv("TFS_CRC_STAGE_COHERENT", "1", 1);
-    if (int rc = pass(iters, out, "nofence_coherent_", coh)) return rc;
-    size_t dp = 0, np = 0;  // the pageable (staged) half of the calls only
-    const size_t half = crcs.size() / 2;
-    for (size_t i = half; i < crcs.size() && i < coh.size(); ++i, ++np) dp += crcs[i] != coh[i];
-    out += ", \"nofence_coherent_staged_results_differing\": " + std::to_string(dp) + ", \"staged_calls_compared\": " +
-           std::to_string(np);
-    unsetenv("TFS_CRC_STAGE_COHERENT");
-    unsetenv("TFS_CRC_RES_NOFENCE");
+    for (size_t i = 0; i < crcs.size() && i < fenced.size(); ++i) diff += crcs[i] != fenced[i];
+    out += ", \"fenced_results_differing\": " + std::to_string(diff) + ", \"calls_compared\": " +
+           std::to_string(std::min(crcs.size(), fenced.size()));
+    unsetenv("TFS_CRC_RES_FENCE");
   }
   out += "}";
   printf("%s\n", out.c_str());

@@ -111,7 +111,7 @@ int main(int argc, char** argv) {
     run(s.c_str(), [&, len, want] { return int(tfs_crc32(0, pageable.data(), int32_t(len)) != want); });
   }
   run("memset_sync", [&] { return tfs_crc32_memset_device(ctx, d_bad, 0, 4, nullptr) | tfs_crc32_sync(ctx); });
-  for (uint32_t n : {1u, 8u, 64u}) {
+  for (uint32_t n : {1u, 8u, 16u, 32u, 64u}) {
     std::string s = "verify_pinned_n" + std::to_string(n);
     run(s.c_str(), [&, n] {
       return tfs_crc32_verify(ctx, vd.data(), n, pinned, size_t(kMax) * kFile, crc.data(), ok.data(), &nbad);
