@@ -63,6 +63,11 @@ int tfs_crc32_debug_poison_resident(tfs_crc_ctx* ctx, uint32_t done);
  * Stats: kernel launches made and files taken through the ring so far. */
 int tfs_crc32_set_resident(tfs_crc_ctx* ctx, int on);
 int tfs_crc32_resident_stats(tfs_crc_ctx* ctx, uint64_t* launches, uint64_t* files);
+/* Where the context's resident ring lives: 1 = fine-grained device memory the host
+ * writes through the PCIe BAR (the default on a large-BAR device), 0 = page-locked
+ * host memory (no large BAR, or TFS_CRC_RESIDENT_VRAM=0 when the context was
+ * made), -1 = not set up yet (no resident call so far). */
+int tfs_crc32_resident_ring_in_device_memory(tfs_crc_ctx* ctx);
 /* Resident-path stamps (measurement build only, libtfs_crc_measure.so; the product
  * returns TFS_EXIT_PARAMETER_ERROR).  tfs_crc32_res_trace, before the context's
  * first resident call: `pinned` (page-locked, 4096 units x 8 u64) receives, per

@@ -370,7 +370,17 @@ def test_closes_beside_throughput_launches(oracle):
         ctx.close()
 
 
-def test_lone_calls_fresh_bytes_every_length(monkeypatch, oracle):
+def _vram_check(ctx, vram):
+    """After the context's first resident call: the ring is where it was asked for
+    (device memory needs a large-BAR device; skip when there is none)."""
+    where = ctx.resident_ring_in_device_memory()
+    if vram and where == 0:
+        pytest.skip("no large-BAR device: the ring stays in host memory")
+    assert where == vram, where
+
+
+@pytest.mark.parametrize("vram", [0, 1])
+def test_lone_calls_fresh_bytes_every_length(monkeypatch, oracle, vram):
     """Round 6 (units polled by tag, tiny bodies read in one load): lone calls
     through the ring with the content changing on every call -- the scalar drop-in
     on pageable memory (every call through the same reused staging buffer, where
@@ -380,7 +390,7 @@ def test_lone_calls_fresh_bytes_every_length(monkeypatch, oracle):
     equals the oracle's, and every call went through the ring."""
     import tfs_amd.crc as crc
     L = crc.lib()
-    ctx = _ctx(monkeypatch, TFS_CRC_RESIDENT=1)
+    ctx = _ctx(monkeypatch, TFS_CRC_RESIDENT=1, TFS_CRC_RESIDENT_VRAM=vram)
     pin = crc.PinnedBuffer(ctx, 16384)
     try:
         rng = np.random.default_rng(606)
@@ -400,6 +410,7 @@ def test_lone_calls_fresh_bytes_every_length(monkeypatch, oracle):
             seed = int(rng.integers(0, 2**32))
             got = ctx.batch(pin.array, [off], [n], [seed])[0]
             assert int(got) == ocrc(oracle, seed, pin.array[off:off + n].tobytes()), (k, n)
+        _vram_check(ctx, vram)
         st = ctx.stats()
         nz = sum(1 for n in lens if n > 0)
         assert st["resident_files"] == nz + len(lens), st   # the scalar calls of length 0 never reach the GPU
@@ -409,14 +420,15 @@ def test_lone_calls_fresh_bytes_every_length(monkeypatch, oracle):
         ctx.close()
 
 
-def test_inline_bodies_mixed_batches_from_threads(monkeypatch, oracle):
+@pytest.mark.parametrize("vram", [0, 1])
+def test_inline_bodies_mixed_batches_from_threads(monkeypatch, oracle, vram):
     """Bodies of at most 80 bytes travel in their ring unit (tfs_crc_device.h
     kResInline): 8 threads of synchronous verifies, each batch mixing inline
     bodies (0..80 bytes) with bodies read over PCIe (81..3000 bytes), rewritten in
     place every call and with one wrong expected CRC per call, the ring's units
     reused many times over (4,096 units): every CRC and verdict is checked."""
     import tfs_amd.crc as crc
-    ctx = _ctx(monkeypatch, TFS_CRC_RESIDENT=1)
+    ctx = _ctx(monkeypatch, TFS_CRC_RESIDENT=1, TFS_CRC_RESIDENT_VRAM=vram)
     errors = []
     nthreads, calls = 8, 400
     try:
@@ -454,9 +466,13 @@ def test_inline_bodies_mixed_batches_from_threads(monkeypatch, oracle):
         for x in th:
             x.join()
         launches, files = ctx.resident_stats()
+        where = ctx.resident_ring_in_device_memory()
         for p in pins:
             p.free()
     finally:
         ctx.close()
     assert not errors, errors[:5]
     assert files > 4096, files  # the ring wrapped
+    if vram and where == 0:
+        pytest.skip("no large-BAR device: the ring stayed in host memory")
+    assert where == vram, where

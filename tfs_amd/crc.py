@@ -70,7 +70,7 @@ EXPORTED = [
     "tfs_crc32_event_elapsed_ms", "tfs_crc32_event_destroy",
     "tfs_crc32_stream", "tfs_crc32_sync", "tfs_crc32_stream_create", "tfs_crc32_stream_sync",
     "tfs_crc32_stream_destroy", "tfs_crc32_inject_device_error", "tfs_crc32_set_resident",
-    "tfs_crc32_resident_stats", "tfs_crc32_stats", "tfs_crc32_res_trace", "tfs_crc32_res_trace_last", "tfs_crc32_error_count", "tfs_crc32_set_default_ctx", "tfs_crc32_bind_thread",
+    "tfs_crc32_resident_stats", "tfs_crc32_resident_ring_in_device_memory", "tfs_crc32_stats", "tfs_crc32_res_trace", "tfs_crc32_res_trace_last", "tfs_crc32_error_count", "tfs_crc32_set_default_ctx", "tfs_crc32_bind_thread",
     "tfs_crc32_default_ctx", "tfs_crc32_set_cu_reserve", "tfs_crc32_throughput_grid", "tfs_crc32_sched_stats", "tfs_crc32_plan_stats",
     "tfs_crc32_debug_state", "tfs_crc32_debug_poison_resident",
     "tfs_crc32_set_split", "tfs_crc32_split_stats", "tfs_crc32_set_compact_segment",
@@ -170,6 +170,7 @@ def lib(measure=False):
             "tfs_crc32_set_resident": (ctypes.c_int, [vp, ctypes.c_int]),
             "tfs_crc32_resident_stats": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64),
                                                         ctypes.POINTER(ctypes.c_uint64)]),
+            "tfs_crc32_resident_ring_in_device_memory": (ctypes.c_int, [vp]),
             "tfs_crc32_stats": (ctypes.c_int, [vp, vp]),
             "tfs_crc32_res_trace": (ctypes.c_int, [vp, vp]),
             "tfs_crc32_res_trace_last": (ctypes.c_int, [vp, vp]),
@@ -315,6 +316,11 @@ class Context:
         a, b = ctypes.c_uint64(), ctypes.c_uint64()
         self._check(self.L.tfs_crc32_resident_stats(self.handle, ctypes.byref(a), ctypes.byref(b)), "resident_stats")
         return a.value, b.value
+
+    def resident_ring_in_device_memory(self):
+        """1: the resident ring is in device memory written through the BAR; 0: in
+        page-locked host memory; -1: not set up yet."""
+        return int(self.L.tfs_crc32_resident_ring_in_device_memory(self.handle))
 
     def stats(self):
         """tfs_crc32_stats as a dict: host calls, lone (one-body) calls and those under

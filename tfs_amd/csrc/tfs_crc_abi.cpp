@@ -62,7 +62,8 @@ hipError_t set_res_fence(uint32_t v);
 hipError_t launch_membench(int pattern, const uint8_t* base, const Desc* desc, uint32_t n, uint64_t nbytes,
                            uint32_t* out, unsigned grid, hipStream_t stream);
 #endif
-hipError_t launch_resident(const Tables* tg, const ResHost* hs, uint32_t* dstate, unsigned grid, uint32_t idle_ticks,
+hipError_t launch_resident(const Tables* tg, const ResHost* hs, uint32_t* left, uint32_t* dstate, unsigned grid,
+                           uint32_t idle_ticks,
                            uint32_t life_ticks, uint32_t gen, hipStream_t stream, uint64_t* trace);
 }  // namespace tfscrc
 
@@ -329,6 +330,17 @@ struct tfs_crc_ctx {
   uint32_t res_idle_us = 200, res_life_us = 10000;  // TFS_CRC_RESIDENT_IDLE_US / _LIFE_US
   ResHost* res_host = nullptr;
   ResHost* res_host_d = nullptr;  // its device-visible address
+  // The ring in device memory the host writes through the PCIe BAR (fine-grained,
+  // CPU-mapped, on a large-BAR device): the workgroups poll
+  // HBM instead of host memory (0.44 against 1.48 us a poll), and bodies of up to
+  // kResLandMax bytes land there too.  `left` (GPU-written, host-read) stays in
+  // host memory.  Without a large BAR the ring is in page-locked host memory.
+  bool res_vram = false;
+  bool res_vram_want = true;  // TFS_CRC_RESIDENT_VRAM=0: the ring in page-locked host memory
+  void* res_left_block = nullptr;  // the page-locked ResHost holding `left` (and the ring, unless res_vram)
+  uint8_t* res_land = nullptr;     // landing slots in device memory (res_vram only), kResUnits x kResLandMax
+  uint32_t* res_left = nullptr;    // host address of the `left` word
+  uint32_t* res_left_d = nullptr;  // its device-visible address
   uint32_t* res_state = nullptr;
   hipStream_t res_stream = nullptr;
   hipEvent_t res_event = nullptr;
@@ -560,7 +572,7 @@ int sched_release(tfs_crc_ctx* ctx, hipStream_t st, const SchedLease& L, hipErro
 bool resident_live(const tfs_crc_ctx* c, int64_t now) {
   if (!c->res_ring.load(std::memory_order_acquire)) return false;
   const uint32_t gen = c->res_gen.load(std::memory_order_acquire);
-  const bool alive = gen != 0 && __atomic_load_n(&c->res_host->left, __ATOMIC_ACQUIRE) != gen;
+  const bool alive = gen != 0 && __atomic_load_n(c->res_left, __ATOMIC_ACQUIRE) != gen;
   return alive || now - c->res_last_post_ns.load(std::memory_order_relaxed) < kResRecentNs;
 }
 
@@ -601,7 +613,8 @@ void resident_atexit() {
     if (!H || !c->res_running) continue;
     const uint32_t gen = uint32_t(c->res_launches);
     __atomic_store_n(&H->published, uint64_t(c->res_published) | (uint64_t(1) << 32), __ATOMIC_RELEASE);
-    for (int i = 0; i < 200000 && __atomic_load_n(&H->left, __ATOMIC_ACQUIRE) != gen; ++i) __builtin_ia32_pause();
+    _mm_sfence();  // a ring in device memory: the store leaves the write-combining buffer now
+    for (int i = 0; i < 200000 && __atomic_load_n(c->res_left, __ATOMIC_ACQUIRE) != gen; ++i) __builtin_ia32_pause();
   }
 }
 
@@ -623,6 +636,24 @@ int resident_setup(tfs_crc_ctx* ctx) {
     (void)hipHostFree(h);
     return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "resident ring: hipHostGetDevicePointer failed");
   }
+  ctx->res_left = &static_cast<ResHost*>(h)->left;
+  ctx->res_left_d = &static_cast<ResHost*>(hd)->left;
+  // The ring itself in fine-grained device memory the CPU writes through the BAR
+  // (a large-BAR device only: every byte of device memory CPU-mapped).
+  void* dv = nullptr;
+  int large_bar = 0;
+  if (ctx->res_vram_want && hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, ctx->device) == hipSuccess &&
+      large_bar) {
+    void* land = nullptr;
+    if (hipExtMallocWithFlags(&dv, sizeof(ResHost), hipDeviceMallocFinegrained) != hipSuccess ||
+        hipExtMallocWithFlags(&land, size_t(kResUnits) * kResLandMax, hipDeviceMallocFinegrained) != hipSuccess) {
+      (void)hipGetLastError();
+      if (dv) (void)hipFree(dv);
+      dv = nullptr;
+    } else {
+      ctx->res_land = static_cast<uint8_t*>(land);
+    }
+  }
   void* st = nullptr;
   // The device state (done counts, exit line) is zeroed on the kernel's own stream
   // and waited for: a recycled allocation may hold a previous context's counts,
@@ -633,15 +664,22 @@ int resident_setup(tfs_crc_ctx* ctx) {
       hipStreamCreateWithPriority(&ctx->res_stream, hipStreamNonBlocking, ctx->lat_prio) != hipSuccess ||
       hipMemsetAsync(st, 0, kResStateBytes, ctx->res_stream) != hipSuccess ||
       hipStreamSynchronize(ctx->res_stream) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->res_event, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&ctx->res_event, hipEventDisableTiming) != hipSuccess ||
+      (dv && (hipMemsetAsync(dv, 0, sizeof(ResHost), ctx->res_stream) != hipSuccess ||
+              hipStreamSynchronize(ctx->res_stream) != hipSuccess))) {
     (void)hipHostFree(h);
+    if (dv) (void)hipFree(dv);
+    if (ctx->res_land) (void)hipFree(ctx->res_land);
+    ctx->res_land = nullptr;
     if (st) (void)hipFree(st);
     if (ctx->res_stream) (void)hipStreamDestroy(ctx->res_stream);
     ctx->res_stream = nullptr;
     return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "resident ring: device state allocation failed");
   }
-  ctx->res_host = static_cast<ResHost*>(h);
-  ctx->res_host_d = static_cast<ResHost*>(hd);
+  ctx->res_vram = dv != nullptr;
+  ctx->res_host = static_cast<ResHost*>(dv ? dv : h);  // the ring the host posts into
+  ctx->res_host_d = static_cast<ResHost*>(dv ? dv : hd);
+  ctx->res_left_block = h;
   ctx->res_state = static_cast<uint32_t*>(st);
   ctx->res_published = 0;
   std::lock_guard<std::mutex> g(g_res_mu);
@@ -804,7 +842,7 @@ int cseg_prepare(tfs_crc_ctx* ctx, hipStream_t st, uint32_t k, uint32_t n, uint3
 // still found by wait_resident's periodic event query.
 int resident_ensure_running(tfs_crc_ctx* ctx, bool post = false) {
   if (ctx->res_running && post &&
-      __atomic_load_n(&ctx->res_host->left, __ATOMIC_ACQUIRE) != ctx->res_gen.load(std::memory_order_relaxed))
+      __atomic_load_n(ctx->res_left, __ATOMIC_ACQUIRE) != ctx->res_gen.load(std::memory_order_relaxed))
     return TFS_SUCCESS;
   if (ctx->res_running) {
     const hipError_t e = hipEventQuery(ctx->res_event);
@@ -813,8 +851,8 @@ int resident_ensure_running(tfs_crc_ctx* ctx, bool post = false) {
     ctx->res_running = false;
   }
   const uint32_t gen = uint32_t(ctx->res_launches + 1u);
-  HIP_TRY(ctx, launch_resident(ctx->d_tables, ctx->res_host_d, ctx->res_state, ctx->res_grid, ctx->res_idle_ticks,
-                               ctx->res_life_ticks, gen, ctx->res_stream, ctx->res_trace_dev));
+  HIP_TRY(ctx, launch_resident(ctx->d_tables, ctx->res_host_d, ctx->res_left_d, ctx->res_state, ctx->res_grid,
+                               ctx->res_idle_ticks, ctx->res_life_ticks, gen, ctx->res_stream, ctx->res_trace_dev));
   HIP_TRY(ctx, hipEventRecord(ctx->res_event, ctx->res_stream));
   ctx->res_running = true;
   ++ctx->res_launches;
@@ -838,8 +876,25 @@ int resident_post(tfs_crc_ctx* ctx, Slot& s, int mode, const uint8_t* zb, const 
   HIP_TRY(ctx, s.h_res.reserve(size_t(n) * 8));
   void* zres = s.h_res.dev;
   if (!zres) return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "resident result words are not mapped");
+  // Bodies landed in device memory (ring in device memory, up to kResLandMax bytes)
+  // and bodies in the unit are not read over PCIe.
+  // (at most kResBulkBytes landed per batch: a larger batch's bodies are read over PCIe)
+  auto landable = [&](uint32_t len) { return ctx->res_land && len > kResInline && len <= kResLandMax; };
+  uint64_t land_total = 0;
+  for (uint32_t i = 0; i < n; ++i) land_total += landable(d[i].len) ? d[i].len : 0u;
+  const bool land_ok = land_total <= kResBulkBytes;
+  auto landed = [&](uint32_t len) { return land_ok && landable(len); };
   uint64_t pcie_bytes = 0;  // what the kernel reads over PCIe for this batch
-  for (uint32_t i = 0; i < n; ++i) pcie_bytes += d[i].len > kResInline ? d[i].len : 0u;
+  for (uint32_t i = 0; i < n; ++i) pcie_bytes += d[i].len > kResInline && !landed(d[i].len) ? d[i].len : 0u;
+  // Landed bodies go through the BAR first, then one store fence, so the device
+  // memory holds them before any unit naming them leaves the write-combining buffers.
+  bool any_landed = false;
+  for (uint32_t i = 0; i < n; ++i)
+    if (landed(d[i].len)) {
+      memcpy(ctx->res_land + size_t((P + i) % kResUnits) * kResLandMax, hb + d[i].offset, d[i].len);
+      any_landed = true;
+    }
+  if (any_landed) _mm_sfence();
   const uint32_t bulk = pcie_bytes > kResBulkBytes ? kResBulk : 0u;  // tfs_crc_device.h
 
   for (uint32_t i = 0; i < n; ++i) {
@@ -847,7 +902,9 @@ int resident_post(tfs_crc_ctx* ctx, Slot& s, int mode, const uint8_t* zb, const 
     ResUnit* u = &H->units[(P + i) % kResUnits];
     const uint32_t tag = P + i + 1u;
     uint64_t addr = 0;
-    if (d[i].len > kResInline) {
+    if (landed(d[i].len)) {  // copied into the unit's landing slot above
+      addr = uint64_t(reinterpret_cast<uintptr_t>(ctx->res_land + size_t((P + i) % kResUnits) * kResLandMax));
+    } else if (d[i].len > kResInline) {
       addr = uint64_t(reinterpret_cast<uintptr_t>(zb + d[i].offset));
     } else {  // the body travels in the unit
       alignas(16) uint32_t w[2 + 6 * 3] = {};
@@ -869,7 +926,9 @@ int resident_post(tfs_crc_ctx* ctx, Slot& s, int mode, const uint8_t* zb, const 
   ctx->res_published = P + n;
   ctx->res_files += n;
   ctx->res_last_post_ns.store(now_ns(), std::memory_order_relaxed);
+  if (ctx->res_vram) _mm_sfence();  // the units' write-combined stores leave before `published`
   __atomic_store_n(&H->published, uint64_t(ctx->res_published), __ATOMIC_RELEASE);
+  if (ctx->res_vram) _mm_sfence();  // and `published` leaves now
   const int rc = resident_ensure_running(ctx, true);
   // A launch that fails leaves units published that no kernel may ever take (or
   // one taking them late, into result words since reused): the context stops
@@ -911,7 +970,7 @@ int wait_resident(tfs_crc_ctx* ctx, Slot& s, int mode, uint32_t n) {
       // event queries: 38 ns alone, 2.3 us each from 8 threads at once,
       // tools/hipcall_cost.cpp); a faulted launch, which never signs out, is
       // still found by the query every 65,536 spins.
-      if (__atomic_load_n(&ctx->res_host->left, __ATOMIC_ACQUIRE) != ctx->res_gen.load(std::memory_order_acquire) &&
+      if (__atomic_load_n(ctx->res_left, __ATOMIC_ACQUIRE) != ctx->res_gen.load(std::memory_order_acquire) &&
           (spins & 65535u) != 0)
         continue;
       const hipError_t e = hipEventQuery(ctx->res_event);
@@ -947,12 +1006,19 @@ void resident_teardown(tfs_crc_ctx* ctx) {
     ctx->res_ring.store(false, std::memory_order_release);
   }
   __atomic_store_n(&ctx->res_host->published, uint64_t(ctx->res_published) | (uint64_t(1) << 32), __ATOMIC_RELEASE);
+  _mm_sfence();
   if (ctx->res_stream) (void)hipStreamSynchronize(ctx->res_stream);
   if (ctx->res_event) (void)hipEventDestroy(ctx->res_event);
   if (ctx->res_stream) (void)hipStreamDestroy(ctx->res_stream);
   if (ctx->res_state) (void)hipFree(ctx->res_state);
-  (void)hipHostFree(ctx->res_host);
+  if (ctx->res_vram) (void)hipFree(ctx->res_host);
+  if (ctx->res_land) (void)hipFree(ctx->res_land);
+  ctx->res_land = nullptr;
+  (void)hipHostFree(ctx->res_left_block);
   ctx->res_host = ctx->res_host_d = nullptr;
+  ctx->res_left = ctx->res_left_d = nullptr;
+  ctx->res_left_block = nullptr;
+  ctx->res_vram = false;
   ctx->res_state = nullptr;
   ctx->res_stream = nullptr;
   ctx->res_event = nullptr;
@@ -1011,9 +1077,17 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
   // copy, and the kernel reads no payload.
   bool ring_full = false;
   if (job >= 0 && ctx->resident && ctx->variant == 0 && n <= kWgMaxFiles) {
+    // (with the ring in device memory, bodies of up to kResLandMax bytes too: they
+    // are copied into landing slots there)
+    if (const int rc = resident_setup(ctx)) return rc;
+    const uint32_t host_copied = ctx->res_land ? kResLandMax : kResInline;
     bool all_inline = true;
-    for (uint32_t i = 0; i < n && all_inline; ++i) all_inline = dd[i].len <= kResInline;
-    if (all_inline) {
+    uint64_t copied = 0;
+    for (uint32_t i = 0; i < n && all_inline; ++i) {
+      all_inline = dd[i].len <= host_copied;
+      copied += dd[i].len;
+    }
+    if (all_inline && copied <= kResBulkBytes) {
       HIP_TRY(ctx, s.h_desc.reserve(size_t(n) * sizeof(Desc)));
       memcpy(s.h_desc.p, d, size_t(n) * sizeof(Desc));
       const int rc = resident_post(ctx, s, mode, nullptr, static_cast<const uint8_t*>(base), dd, n);
@@ -1297,6 +1371,7 @@ int tfs_crc32_ctx_create(int device, tfs_crc_ctx** out) {
   if (const char* v = getenv("TFS_CRC_COMPACT_SLOTS")) ctx->compact_slots = std::min(std::max(atoi(v), 1), kCompactSlots);
   if (const char* v = getenv("TFS_CRC_COMPACT_GROUP")) ctx->compact_group = uint32_t(std::min(std::max(atoi(v), 1), 256));
   if (const char* v = getenv("TFS_CRC_RESIDENT")) ctx->resident = atoi(v) != 0;
+  if (const char* v = getenv("TFS_CRC_RESIDENT_VRAM")) ctx->res_vram_want = atoi(v) != 0;
   if (const char* v = getenv("TFS_CRC_RESIDENT_WGS")) ctx->res_grid = unsigned(std::min(std::max(atoi(v), 1), 256));
   if (const char* v = getenv("TFS_CRC_RESIDENT_IDLE_US")) ctx->res_idle_us = uint32_t(std::min(std::max(atoi(v), 1), 1000000));
   if (const char* v = getenv("TFS_CRC_RESIDENT_LIFE_US")) ctx->res_life_us = uint32_t(std::min(std::max(atoi(v), 1), 10000000));
@@ -2755,6 +2830,13 @@ int tfs_crc32_resident_stats(tfs_crc_ctx* ctx, uint64_t* launches, uint64_t* fil
   if (launches) *launches = ctx->res_launches;
   if (files) *files = ctx->res_files;
   return TFS_SUCCESS;
+}
+
+int tfs_crc32_resident_ring_in_device_memory(tfs_crc_ctx* ctx) {
+  if (!ctx) return TFS_EXIT_PARAMETER_ERROR;
+  std::lock_guard<std::mutex> g(ctx->mu);
+  if (!ctx->res_host) return -1;
+  return ctx->res_vram ? 1 : 0;
 }
 
 int tfs_crc32_stream_create(tfs_crc_ctx* ctx, void** stream) {

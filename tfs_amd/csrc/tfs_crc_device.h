@@ -100,6 +100,12 @@ constexpr uint32_t kResInline = 8u + 6u * 12u;  // 80 bytes
 // kResBulkBytes over PCIe carry kResBulk in their length word: fence, then
 // non-temporal stripes.
 constexpr uint32_t kResBulk = 0x80000000u;
+// With the ring in device memory (large BAR), a body of kResInline..kResLandMax
+// bytes is copied by the host through the BAR into unit i's landing slot (slot
+// i % kResUnits, kResLandMax bytes each) before the unit is written: the workgroup
+// reads it from HBM instead of over PCIe.  PCIe keeps the host's posted writes in
+// order, so the body lands before the unit that names it.
+constexpr uint32_t kResLandMax = 16384;
 constexpr uint64_t kResBulkBytes = 1u << 20;
 struct ResUnit {         // one file
   uint64_t addr;         // device-visible address of its first byte (inline: bytes 0..7)

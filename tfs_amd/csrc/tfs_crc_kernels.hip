@@ -1482,7 +1482,7 @@ hipError_t set_res_fence(uint32_t v) { return hipMemcpyToSymbol(HIP_SYMBOL(g_res
 // the unit's words back, the acquire fence done, wave 0's payload loads back, its
 // CRC done (just before the result store).
 __global__ void __launch_bounds__(kBlock) crc_resident_kernel(const Tables* __restrict__ tg, const ResHost* hs,
-                                                              uint32_t* dstate, uint32_t idle_ticks,
+                                                              uint32_t* left, uint32_t* dstate, uint32_t idle_ticks,
                                                               uint32_t life_ticks, uint32_t gen, uint64_t* trace) {
   __shared__ uint32_t lds_tables[kWgLdsBytes / 4];
   __shared__ uint32_t part[kWgWaves];
@@ -1644,7 +1644,7 @@ __global__ void __launch_bounds__(kBlock) crc_resident_kernel(const Tables* __re
     // without HIP calls, tfs_crc_abi.cpp resident_atexit).
     if (atomicAdd(&dstate[kResLeftLine], 1u) + 1u == gridDim.x) {
       atomicExch(&dstate[kResLeftLine], 0u);
-      __hip_atomic_store(const_cast<uint32_t*>(&hs->left), gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(left, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -2577,10 +2577,10 @@ hipError_t launch_crc_files(int mode, const uint8_t* base, const Desc* desc, uin
                            cap, split);
 }
 
-hipError_t launch_resident(const Tables* tg, const ResHost* hs, uint32_t* dstate, unsigned grid, uint32_t idle_ticks,
-                           uint32_t life_ticks, uint32_t gen, hipStream_t stream, uint64_t* trace) {
-  hipLaunchKernelGGL(crc_resident_kernel, dim3(grid), dim3(kBlock), 0, stream, tg, hs, dstate, idle_ticks, life_ticks,
-                     gen, trace);
+hipError_t launch_resident(const Tables* tg, const ResHost* hs, uint32_t* left, uint32_t* dstate, unsigned grid,
+                           uint32_t idle_ticks, uint32_t life_ticks, uint32_t gen, hipStream_t stream, uint64_t* trace) {
+  hipLaunchKernelGGL(crc_resident_kernel, dim3(grid), dim3(kBlock), 0, stream, tg, hs, left, dstate, idle_ticks,
+                     life_ticks, gen, trace);
   return hipGetLastError();
 }
 

@@ -103,7 +103,7 @@ int main(int argc, char** argv) {
   run("scalar_64k_pageable", [&] { return int(tfs_crc32(0, pageable.data(), kFile) != crc[0]); });
   // lone small bodies (the drop-in's floor): 16-80 B (in the
   // ring unit itself since round 6), 96 B, 1 KiB, 4 KiB from pageable memory
-  for (uint32_t len : {16u, 32u, 64u, 80u, 96u, 1024u, 4096u}) {
+  for (uint32_t len : {16u, 32u, 64u, 80u, 96u, 1024u, 4096u, 16384u}) {
     uint32_t want = 0;
     tfs_crc_desc d{0, len, 0};
     tfs_crc32_batch(ctx, &d, 1, pageable.data(), len, &want);
