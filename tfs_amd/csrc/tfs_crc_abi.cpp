@@ -338,6 +338,7 @@ struct tfs_crc_ctx {
   bool res_vram = false;
   bool res_vram_want = true;  // TFS_CRC_RESIDENT_VRAM=0: the ring in page-locked host memory
   void* res_left_block = nullptr;  // the page-locked ResHost holding `left` (and the ring, unless res_vram)
+  int64_t res_bar_ns = -1;         // 4 KiB written through the BAR at setup (calibration), -1: not tried
   uint8_t* res_land = nullptr;     // landing slots in device memory (res_vram only), kResUnits x kResLandMax
   uint32_t* res_left = nullptr;    // host address of the `left` word
   uint32_t* res_left_d = nullptr;  // its device-visible address
@@ -618,6 +619,10 @@ void resident_atexit() {
   }
 }
 
+// A BAR the host writes slower than this (4 KiB, write-combined: ~100 ns) is not
+// used for the ring.
+constexpr int64_t kResBarMaxNs = 2000;
+
 // (Caller holds ctx->mu.)  Ring, device state, stream and event, made on first use.
 int resident_setup(tfs_crc_ctx* ctx) {
   if (ctx->res_host) return TFS_SUCCESS;
@@ -675,6 +680,27 @@ int resident_setup(tfs_crc_ctx* ctx) {
     if (ctx->res_stream) (void)hipStreamDestroy(ctx->res_stream);
     ctx->res_stream = nullptr;
     return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "resident ring: device state allocation failed");
+  }
+  // Calibrate the host's writes through the BAR: 4 KiB of zeros over the (zeroed)
+  // ring, best of three.  Write-combined, that is ~0.1 us; a box whose BAR the
+  // CPU maps uncached takes microseconds per 16-byte store (one such mapping was
+  // seen, 96-byte calls 2.5 us slower), and the ring then stays in host memory.
+  if (dv) {
+    alignas(64) static const uint8_t zeros[4096] = {};
+    int64_t best = INT64_MAX;
+    for (int k = 0; k < 3; ++k) {
+      const int64_t t0 = now_ns();
+      memcpy(static_cast<ResHost*>(dv)->units, zeros, sizeof zeros);
+      _mm_sfence();
+      best = std::min(best, now_ns() - t0);
+    }
+    ctx->res_bar_ns = best;
+    if (best > kResBarMaxNs) {
+      (void)hipFree(dv);
+      if (ctx->res_land) (void)hipFree(ctx->res_land);
+      dv = nullptr;
+      ctx->res_land = nullptr;
+    }
   }
   ctx->res_vram = dv != nullptr;
   ctx->res_host = static_cast<ResHost*>(dv ? dv : h);  // the ring the host posts into
