@@ -143,11 +143,11 @@ tfs_crc_ctx* tfs_crc32_default_ctx(void);
 /* Per-context call counters, monotonic from the context's creation, so an
  * integration can see callers that should batch.  A lone host call (one body)
  * shorter than TFS_CRC_LONE_CROSSOVER bytes costs one GPU round trip over PCIe
- * (~4 us up to 80 bytes, ~7 us above), longer than the reference's host loop takes on
+ * (~4 us up to 80 bytes, 5-7 us above), longer than the reference's host loop takes on
  * it (1.6 ns/byte): such a caller -- a small RPC body checked alone,
  * base_packet.cpp:141 -- should gather its bodies into one tfs_crc32_batch /
  * tfs_packet_verify call.  Scalar calls count on the context they run on. */
-#define TFS_CRC_LONE_CROSSOVER 4400 /* round 6: 4,437 B measured on the closing tree (bench.py --workload small_bodies) */
+#define TFS_CRC_LONE_CROSSOVER 3500 /* round 6: 3,452 B measured on the closing tree with the ring in device memory, 4,437 with it in host memory (bench.py --workload small_bodies) */
 typedef struct tfs_crc_stats {
   uint64_t host_calls;         /* synchronous host-memory calls: scalar, get_crc, batch, verify, small packet sets */
   uint64_t host_files;         /* bodies they carried */

@@ -98,7 +98,7 @@ class CrcStats(ctypes.Structure):
         "resident_files", "resident_ring_full")]
 
 
-LONE_CROSSOVER = 4400  # TFS_CRC_LONE_CROSSOVER
+LONE_CROSSOVER = 3500  # TFS_CRC_LONE_CROSSOVER
 
 
 class TfsCrcError(RuntimeError):

@@ -904,11 +904,11 @@ int resident_post(tfs_crc_ctx* ctx, Slot& s, int mode, const uint8_t* zb, const 
   if (!zres) return set_err(ctx, TFS_CRC_EXIT_DEVICE_ERROR, "resident result words are not mapped");
   // Bodies landed in device memory (ring in device memory, up to kResLandMax bytes)
   // and bodies in the unit are not read over PCIe.
-  // (at most kResBulkBytes landed per batch: a larger batch's bodies are read over PCIe)
+  // (at most kResLandBatch landed per batch: a larger batch's bodies are read over PCIe)
   auto landable = [&](uint32_t len) { return ctx->res_land && len > kResInline && len <= kResLandMax; };
   uint64_t land_total = 0;
   for (uint32_t i = 0; i < n; ++i) land_total += landable(d[i].len) ? d[i].len : 0u;
-  const bool land_ok = land_total <= kResBulkBytes;
+  const bool land_ok = land_total <= kResLandBatch;
   auto landed = [&](uint32_t len) { return land_ok && landable(len); };
   uint64_t pcie_bytes = 0;  // what the kernel reads over PCIe for this batch
   for (uint32_t i = 0; i < n; ++i) pcie_bytes += d[i].len > kResInline && !landed(d[i].len) ? d[i].len : 0u;
@@ -1113,7 +1113,7 @@ int enqueue_host_batch(tfs_crc_ctx* ctx, Slot& s, int mode, const void* d, uint3
       all_inline = dd[i].len <= host_copied;
       copied += dd[i].len;
     }
-    if (all_inline && copied <= kResBulkBytes) {
+    if (all_inline && (!ctx->res_land || copied <= kResLandBatch)) {
       HIP_TRY(ctx, s.h_desc.reserve(size_t(n) * sizeof(Desc)));
       memcpy(s.h_desc.p, d, size_t(n) * sizeof(Desc));
       const int rc = resident_post(ctx, s, mode, nullptr, static_cast<const uint8_t*>(base), dd, n);
