@@ -911,7 +911,13 @@ int resident_post(tfs_crc_ctx* ctx, Slot& s, int mode, const uint8_t* zb, const 
   const bool land_ok = land_total <= kResLandBatch;
   auto landed = [&](uint32_t len) { return land_ok && landable(len); };
   uint64_t pcie_bytes = 0;  // what the kernel reads over PCIe for this batch
-  for (uint32_t i = 0; i < n; ++i) pcie_bytes += d[i].len > kResInline && !landed(d[i].len) ? d[i].len : 0u;
+  for (uint32_t i = 0; i < n; ++i)
+    if (d[i].len > kResInline && !landed(d[i].len)) {
+      // (the caller's fast path passes no device-visible base: every body must then be
+      // in the unit or landed -- enqueue_host_batch's rule, checked here too)
+      if (!zb) return set_err(ctx, TFS_EXIT_PARAMETER_ERROR, "resident ring: a body to read over PCIe has no device address");
+      pcie_bytes += d[i].len;
+    }
   // Landed bodies go through the BAR first, then one store fence, so the device
   // memory holds them before any unit naming them leaves the write-combining buffers.
   bool any_landed = false;
