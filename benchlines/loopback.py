@@ -171,7 +171,9 @@ def bench_loopback(args):
     # resident kernel over this whole line: launches (first + relaunches after
     # idle or lifetime exits) against the files it took
     launches, rfiles = ctx.resident_stats()
-    res["resident_kernel"] = {"launches": int(launches), "files": int(rfiles)}
+    res["resident_kernel"] = {"launches": int(launches), "files": int(rfiles),
+                              "ring": {1: "device memory", 0: "host memory"}.get(ctx.resident_ring_in_device_memory(),
+                                                                                 "not set up")}
     # PCIe bytes of one loopback: every payload crosses once for the close check
     # (zero-copy reads of the lease buffers) and once for the whole-block verify.
     pcie_bytes = 2.0 * n * L

@@ -140,6 +140,8 @@ def bench_small_bodies(args):
         "sizes": rows, "python_call_us": py_us,
         "cpu_kind": kind, "cpu_ns_per_byte": per_byte * 1e3,
         "crossover_bytes": cross,
+        # where the resident ring (and the bodies of up to 16 KiB) lived for these calls
+        "resident_ring": {1: "device memory", 0: "host memory"}.get(ctx.resident_ring_in_device_memory(), "not set up"),
         "note": "scalar/frame/batch include ~python_call_us of ctypes per call; cpu_us is per call inside one C loop "
                 "on one core.  Below crossover_bytes a lone body is cheaper on the host loop than one GPU round "
                 "trip; batched reads (batch_us_per_frame) amortise the round trip over the frames of a read.",

@@ -107,6 +107,21 @@ def test_block_verify_device_and_loopback_lines():
     for k in ("scalar_tfs_crc32_64KiB", "close_1_leases", "close_8_leases", "close_64_leases"):
         assert 0 < lb["latency"][k]["p50_us"] <= lb["latency"][k]["p99_us"], k
     assert lb["cpu_baseline"]["allcore"]["value"] > 0
+    assert lb["resident_kernel"]["ring"] in ("device memory", "host memory")
+
+
+@pytest.mark.gpu
+def test_small_bodies_line():
+    """Per-call latency of lone bodies: every size, the reference loop beside it, the
+    crossover between them, and where the resident ring lived."""
+    sb = _run(["--workload", "small_bodies", "--steps", "4"])
+    assert set(sb["sizes"]) == {"32", "80", "256", "1024", "4096", "16384", "65536"}
+    for k, row in sb["sizes"].items():
+        assert 0 < row["scalar_us"]["p50"] <= row["scalar_us"]["p99"], k
+        assert row["cpu_us"] > 0 and row["batch_us_per_frame"]["p50"] > 0, k
+    assert sb["higher_is_better"] is False and sb["cpu_kind"] in ("reference", "port")
+    assert 80 < sb["crossover_bytes"] < 65536
+    assert sb["resident_ring"] in ("device memory", "host memory")
 
 
 @pytest.mark.gpu
