@@ -213,8 +213,8 @@ def bench_block_verify_device(args):
     el, kms = timed(ctx, step)
     algo_per_rec = FILEINFO + FILE_SIZE + 40 + 4 + 4   # header + payload + job read, crc + status written
     achieved = nfiles * algo_per_rec / (kms / 1e3) / 1e9
-    bv_traffic, bv_src = _pmc_traffic("profiles/r05/final/block_verify_device/pmc_summary.json",
-                                      "compact_pipe_kernel<true, true, 12, 5, 4, 3, false, 0, 16, 1, 1>", nblocks == 1024)
+    bv_traffic, bv_src = _pmc_traffic("profiles/r06/pmc/block_verify_device/pmc_summary.json",
+                                      "compact_pipe_kernel<true, true, 12, 5, 4, 3", nblocks == 1024)
     res = {
         "metric": "GiB/s payload verified on read from device-resident block images (FileInfo checks + re-CRC)",
         "value": world * args.steps * nfiles * FILE_SIZE / el / 2**30, "unit": "GiB/s", "n_gpus": world,

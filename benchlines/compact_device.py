@@ -111,8 +111,8 @@ def bench_compact_device(args):
     live_bytes = float(nlive) * rec
     algo = 2 * live_bytes + nlive * (40 + 4)  # read + write live records, 40 B CompactJob + 4 B status
     live_payload = float(nlive) * FILE_SIZE
-    cd_traffic, cd_src = _pmc_traffic("profiles/r05/compact/pmc_summary.json",
-                                      "compact_pipe_kernel<true, false, 12, 5, 1, 0, false, 2, 16, 1, 1>", nblocks == 1024)
+    cd_traffic, cd_src = _pmc_traffic("profiles/r06/pmc/compact_device/pmc_summary.json",
+                                      "compact_pipe_kernel<true, false, 12, 5, 1, 0, false, 2", nblocks == 1024)
     res = {
         "metric": "GiB/s of live payload compacted on the device (re-CRC + repack of live files)",
         "value": world * args.steps * live_payload / el / 2**30, "unit": "GiB/s of live payload", "n_gpus": world,

@@ -60,7 +60,7 @@ def bench_ec(args):
         kms = e0.elapsed_ms(e1) / args.steps
         out[name] = {"ms": kms, "GiBs_data": world * args.steps * k * size / el / 2**30,
                      "hbm_GBs": (rd + wr) * size / (kms / 1e3) / 1e9}
-    e_traffic, e_src = _pmc_traffic("profiles/r05/final/ec/pmc_summary.json", "ec_apply_kernel<3>", args.ec_mib == 1536)
+    e_traffic, e_src = _pmc_traffic("profiles/r06/pmc/ec/pmc_summary.json", "ec_apply_kernel<3", args.ec_mib == 1536)
     res = {
         "metric": "GiB/s of data encoded (ErasureCode k=5 m=3, Cauchy bitmatrix w=8 ps=128), device-resident",
         "value": out["encode"]["GiBs_data"], "unit": "GiB/s", "n_gpus": world, "steps": args.steps,

@@ -67,7 +67,7 @@ def bench_packet(args):
     # the frame (24-B header + body) and its 16-B PacketDesc read, the 4-B crc and
     # 4-B status written; the wave that checksums the body parses the header itself.
     algo = n * (float(frame) + 16 + 4 + 4)
-    p_traffic, p_src = _pmc_traffic("profiles/r05/final/packet/pmc_summary.json", PACKET_KERNEL, n == 1048576)
+    p_traffic, p_src = _pmc_traffic("profiles/r06/pmc/packet/pmc_summary.json", PACKET_KERNEL, n == 1048576)
     res = {
         "metric": "GiB/s packet bytes CRC-verified (BasePacket::decode), device-resident V1 frames",
         "value": world * args.steps * n * frame / el / 2**30, "unit": "GiB/s", "n_gpus": world,

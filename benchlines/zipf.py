@@ -9,7 +9,7 @@ import numpy as np
 
 from benchlines.common import *  # noqa: F401,F403
 
-ZIPF_PROFILE = "profiles/r05/final/zipf/pmc_summary.json"
+ZIPF_PROFILE = "profiles/r06/pmc/zipf/pmc_summary.json"
 
 
 def build(ctx, nblocks, seed):
